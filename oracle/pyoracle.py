@@ -1,0 +1,130 @@
+"""ctypes bindings for the oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module (as the checker). The product (imagecodecs_amd) never does.
+
+  decode(jpeg)            -> (code, w, h, ncomp, bytes)   oracle/liboracle.so  (CPU restatement)
+  decode_trace(jpeg)      -> (code, coef[int16 n,64], dc[int32 n])
+  tje_encode(q, w, h, c, rgb) -> bytes | None            oracle/liboracle.so
+  ref_decode / ref_tje_encode                             oracle/_ref/libref_jpeg.so (the
+                                                         reference itself; container only)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+
+def build(ref: bool = False) -> None:
+    subprocess.run(["make", "-s", "-C", _HERE, "all"] + (["ref"] if ref else []), check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.or_nj_decode.restype = C.c_int
+        L.or_nj_decode.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_int),
+                                   C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p]
+        L.or_tje_encode.restype = C.c_int
+        L.or_tje_encode.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                    C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.or_free.argtypes = [C.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+class _Trace(C.Structure):
+    _fields_ = [("nblocks", C.c_int32), ("coef", C.c_void_p), ("dc", C.c_void_p), ("cap_blocks", C.c_int32)]
+
+
+def _decode(data: bytes, trace=None):
+    L = lib()
+    buf = C.create_string_buffer(bytes(data), len(data))
+    out = C.c_void_p()
+    w, h, n = C.c_int(), C.c_int(), C.c_int()
+    code = L.or_nj_decode(buf, len(data), C.byref(out), C.byref(w), C.byref(h), C.byref(n),
+                          C.byref(trace) if trace is not None else None)
+    pix = b""
+    if out.value:
+        pix = C.string_at(out.value, w.value * h.value * n.value)
+        L.or_free(out)
+    return code, w.value, h.value, n.value, pix
+
+
+def decode(data: bytes):
+    """NanoJPEG-equivalent decode -> (code, w, h, ncomp, pixel bytes)."""
+    return _decode(data)
+
+
+def decode_trace(data: bytes, cap_blocks: int = 1 << 20):
+    coef = np.zeros((cap_blocks, 64), np.int16)
+    dc = np.zeros(cap_blocks, np.int32)
+    t = _Trace(0, coef.ctypes.data, dc.ctypes.data, cap_blocks)
+    code = _decode(data, t)[0]
+    n = min(t.nblocks, cap_blocks)
+    return code, coef[:n].copy(), dc[:n].copy()
+
+
+def tje_encode(quality: int, w: int, h: int, comps: int, rgb: bytes):
+    L = lib()
+    src = C.create_string_buffer(bytes(rgb), max(1, len(rgb)))
+    out = C.c_void_p()
+    n = C.c_int64()
+    ok = L.or_tje_encode(quality, w, h, comps, src, C.byref(out), C.byref(n))
+    if not ok:
+        return None
+    res = C.string_at(out.value, n.value)
+    L.or_free(out)
+    return res
+
+
+# ---- the reference itself (oracle/_ref, built from /root/reference in place) ----
+def ref_available() -> bool:
+    return os.path.exists(os.path.join(_HERE, "_ref", "libref_jpeg.so"))
+
+
+def ref():
+    global _REF
+    if _REF is None:
+        L = C.CDLL(os.path.join(_HERE, "_ref", "libref_jpeg.so"))
+        L.ref_nj_decode.restype = C.c_int
+        L.ref_nj_decode.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_int), C.c_void_p, C.c_longlong]
+        L.ref_tje_encode.restype = C.c_int
+        L.ref_tje_encode.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                     C.c_longlong, C.POINTER(C.c_longlong)]
+        _REF = L
+    return _REF
+
+
+def ref_decode(data: bytes, cap: int = 1 << 28):
+    L = ref()
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    out = C.create_string_buffer(cap)
+    w, h, n = C.c_int(), C.c_int(), C.c_int()
+    code = L.ref_nj_decode(src, len(data), C.byref(w), C.byref(h), C.byref(n), out, cap)
+    if code != 0:
+        return code, 0, 0, 0, b""
+    return code, w.value, h.value, n.value, out.raw[: w.value * h.value * n.value]
+
+
+def ref_tje_encode(quality: int, w: int, h: int, comps: int, rgb: bytes, cap: int = 1 << 28):
+    L = ref()
+    src = C.create_string_buffer(bytes(rgb), max(1, len(rgb)))
+    out = C.create_string_buffer(cap)
+    n = C.c_longlong()
+    ok = L.ref_tje_encode(quality, w, h, comps, src, out, cap, C.byref(n))
+    if ok != 1:
+        return None
+    return out.raw[: n.value]
