@@ -1,0 +1,300 @@
+"""imagecodecs_amd -- MI355X-native JPEG codec behind ImageCodecs' codecs.h API.
+
+The product is the C-ABI library ``imagecodecs_amd/lib/libicx.so`` (include/icx.h): hand-
+written gfx950 HIP kernels for the NanoJPEG-exact decode path and the tiny_jpeg-exact
+encode path. This module is the host-side mirror of the reference interface for Python
+callers (tests, bench): it binds the C ABI with ctypes and offers
+
+  * ``Context``                   -- one device + stream (icx_create)
+  * ``Context.nj_decode`` & co.   -- njInit/njDecode/njGet* semantics (jpeg_dec.h:117-171)
+  * ``Context.decode``            -- Image::readJpg's one-shot decode (codecs.cpp:821-849)
+  * ``Batch``                     -- device-resident batched decode (the throughput path)
+  * ``Image``                     -- ImageCodecs::Image (codecs.h:16-103) for .jpg/.jpeg
+
+There is deliberately no CPU fallback: if libicx.so is missing or no GPU is visible every
+entry point raises ``ICXError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+__all__ = ["ICXError", "Context", "Batch", "Image", "lib", "build", "LIB_PATH",
+           "OK", "NO_JPEG", "UNSUPPORTED", "OUT_OF_MEM", "INTERNAL_ERR", "SYNTAX_ERROR"]
+
+OK, NO_JPEG, UNSUPPORTED, OUT_OF_MEM, INTERNAL_ERR, SYNTAX_ERROR = range(6)  # nj_result_t
+RESULT_NAMES = ["NJ_OK", "NJ_NO_JPEG", "NJ_UNSUPPORTED", "NJ_OUT_OF_MEM", "NJ_INTERNAL_ERR", "NJ_SYNTAX_ERROR"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libicx.so")
+_LIB = None
+
+
+class ICXError(RuntimeError):
+    pass
+
+
+def build() -> str:
+    """Compile libicx.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+_vp, _i32, _i64, _u64, _sz = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_size_t
+_SIGS = {
+    "icx_version": (C.c_char_p, []),
+    "icx_last_error": (C.c_char_p, [_vp]),
+    "icx_create": (_vp, [_i32]),
+    "icx_destroy": (None, [_vp]),
+    "icx_free": (None, [_vp]),
+    "icx_jpeg_probe": (_i32, [_vp, _sz, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
+    "icx_nj_init": (None, [_vp]),
+    "icx_nj_done": (None, [_vp]),
+    "icx_nj_decode": (_i32, [_vp, _vp, _i32]),
+    "icx_nj_get_width": (_i32, [_vp]),
+    "icx_nj_get_height": (_i32, [_vp]),
+    "icx_nj_is_color": (_i32, [_vp]),
+    "icx_nj_get_image": (_vp, [_vp]),
+    "icx_nj_get_image_size": (_i32, [_vp]),
+    "icx_jpeg_decode": (_i32, [_vp, _vp, _sz, C.POINTER(_vp), C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
+    "icx_batch_create": (_vp, [_vp, _i32, _i32, _i32, _i32]),
+    "icx_batch_destroy": (None, [_vp]),
+    "icx_jpeg_batch_decode": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "icx_jpeg_batch_decode_host": (_i32, [_vp, _i32, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "icx_batch_stage_times": (_i32, [_vp, _vp, _vp, _i32]),
+    "icx_tje_encode_with_func": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
+    "icx_tje_encode_to_file_at_quality": (_i32, [_vp, C.c_char_p, _i32, _i32, _i32, _i32, _vp]),
+    "icx_tje_encode_to_file": (_i32, [_vp, C.c_char_p, _i32, _i32, _i32, _vp]),
+}
+
+WRITE_FUNC = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
+
+
+def lib():
+    """Load libicx.so (raises ICXError if it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ICXError(f"{LIB_PATH} not built: run `make -C imagecodecs_amd` (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _err(ctx_ptr) -> str:
+    msg = lib().icx_last_error(ctx_ptr)
+    return msg.decode() if msg else ""
+
+
+class Context:
+    """icx_create(device): a device + HIP stream; also holds njDecode-style state."""
+
+    def __init__(self, device: int = 0):
+        self._p = lib().icx_create(device)
+        if not self._p:
+            raise ICXError("icx_create failed: " + _err(None))
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().icx_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def ptr(self):
+        return self._p
+
+    # ---- NanoJPEG-compatible state API (jpeg_dec.h:130-171)
+    def nj_init(self):
+        lib().icx_nj_init(self._p)
+
+    def nj_done(self):
+        lib().icx_nj_done(self._p)
+
+    def nj_decode(self, jpeg: bytes) -> int:
+        buf = C.create_string_buffer(bytes(jpeg), max(1, len(jpeg)))
+        return lib().icx_nj_decode(self._p, buf, len(jpeg))
+
+    def nj_get_width(self) -> int:
+        return lib().icx_nj_get_width(self._p)
+
+    def nj_get_height(self) -> int:
+        return lib().icx_nj_get_height(self._p)
+
+    def nj_is_color(self) -> int:
+        return lib().icx_nj_is_color(self._p)
+
+    def nj_get_image_size(self) -> int:
+        return lib().icx_nj_get_image_size(self._p)
+
+    def nj_get_image(self) -> bytes:
+        p = lib().icx_nj_get_image(self._p)
+        return C.string_at(p, self.nj_get_image_size()) if p else b""
+
+    # ---- one-shot decode (Image::readJpg)
+    def decode(self, jpeg: bytes):
+        """-> (code, width, height, ncomp, pixel bytes)."""
+        buf = C.create_string_buffer(bytes(jpeg), max(1, len(jpeg)))
+        out = C.c_void_p()
+        w, h, n = C.c_int(), C.c_int(), C.c_int()
+        code = lib().icx_jpeg_decode(self._p, buf, len(jpeg), C.byref(out), C.byref(w), C.byref(h), C.byref(n))
+        pix = b""
+        if out.value:
+            pix = C.string_at(out.value, w.value * h.value * n.value)
+            lib().icx_free(out)
+        if code == INTERNAL_ERR and _err(self._p):
+            raise ICXError(_err(self._p))
+        return code, w.value, h.value, n.value, pix
+
+    # ---- encode (tiny_jpeg, jpeg_enc.h:114-160)
+    def tje_encode(self, quality: int, width: int, height: int, comps: int, src: bytes):
+        """tje_encode_with_func into memory -> bytes, or None on error (tje returns 0)."""
+        chunks = []
+
+        @WRITE_FUNC
+        def sink(_ctx, data, size):
+            chunks.append(C.string_at(data, size))
+
+        buf = C.create_string_buffer(bytes(src), max(1, len(src)))
+        ok = lib().icx_tje_encode_with_func(self._p, sink, None, quality, width, height, comps, buf)
+        return b"".join(chunks) if ok == 1 else None
+
+
+def probe(jpeg: bytes):
+    """Host header walk (njDecode through SOS) -> (code, width, height, ncomp)."""
+    w, h, n = C.c_int(), C.c_int(), C.c_int()
+    buf = C.create_string_buffer(bytes(jpeg), max(1, len(jpeg)))
+    code = lib().icx_jpeg_probe(buf, len(jpeg), C.byref(w), C.byref(h), C.byref(n))
+    return code, w.value, h.value, n.value
+
+
+class Batch:
+    """Device-resident batched decode (icx_jpeg_batch_*). Inputs/outputs are device pointers
+    (ints) -- e.g. torch CUDA tensors' data_ptr() -- on the context's device."""
+
+    def __init__(self, ctx: Context, max_images: int, max_width: int, max_height: int, group: int = 0):
+        self.ctx = ctx
+        self._p = lib().icx_batch_create(ctx.ptr, max_images, max_width, max_height, group)
+        if not self._p:
+            raise ICXError("icx_batch_create failed: " + _err(ctx.ptr))
+        self.max_images, self.max_width, self.max_height = max_images, max_width, max_height
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().icx_batch_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+    def decode_device(self, n, d_data, d_offsets, d_sizes, d_out, out_stride, d_status, d_dims, stream=0):
+        rc = lib().icx_jpeg_batch_decode(self._p, n, d_data, d_offsets, d_sizes, d_out, out_stride,
+                                         d_status, d_dims, stream or None)
+        if rc != OK:
+            raise ICXError(f"icx_jpeg_batch_decode -> {rc}: {_err(self.ctx.ptr)}")
+
+    def decode_host(self, jpegs, out_stride=None):
+        """Decode a list of bytes objects -> list of (code, w, h, ncomp, np.ndarray|None)."""
+        n = len(jpegs)
+        out_stride = out_stride or self.max_width * self.max_height * 3
+        bufs = [C.create_string_buffer(bytes(j), max(1, len(j))) for j in jpegs]
+        ptrs = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in bufs])
+        sizes = (C.c_size_t * n)(*[len(j) for j in jpegs])
+        outs_np = [np.empty(out_stride, np.uint8) for _ in range(n)]
+        outs = (C.c_void_p * n)(*[o.ctypes.data for o in outs_np])
+        status = np.zeros(n, np.int32)
+        dims = np.zeros((n, 3), np.int32)
+        rc = lib().icx_jpeg_batch_decode_host(self._p, n, ptrs, sizes, outs, out_stride,
+                                              status.ctypes.data, dims.ctypes.data)
+        if rc != OK:
+            raise ICXError(f"icx_jpeg_batch_decode_host -> {rc}: {_err(self.ctx.ptr)}")
+        res = []
+        for i in range(n):
+            w, h, c = (int(x) for x in dims[i])
+            pix = outs_np[i][: w * h * c].reshape(h, w, c) if status[i] == OK else None
+            res.append((int(status[i]), w, h, c, pix))
+        return res
+
+    def stage_times(self) -> dict:
+        names = (C.c_char_p * 16)()
+        ms = (C.c_float * 16)()
+        k = lib().icx_batch_stage_times(self._p, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+
+class Image:
+    """ImageCodecs::Image (codecs.h:16-103) for the JPEG hot path.
+
+    read()/write() dispatch on the lower-cased extension like Image::read/write
+    (codecs.cpp:53-122); only .jpg/.jpeg are on this path -- other extensions raise
+    ValueError (the reference's std::invalid_argument for unknown types)."""
+
+    _ctx = None
+
+    def __init__(self):
+        self.h_ = self.w_ = self.d_ = 0
+        self.pixels_ = None
+
+    @classmethod
+    def context(cls):
+        if cls._ctx is None:
+            cls._ctx = Context(0)
+        return cls._ctx
+
+    def read(self, filepath: str):
+        ext = os.path.splitext(filepath)[1].lower()
+        if ext not in (".jpg", ".jpeg"):
+            raise ValueError("Cannot parse filetype")
+        data = open(filepath, "rb").read()
+        code, w, h, n, pix = self.context().decode(data)
+        if code != OK:
+            raise RuntimeError("Error decoding the input file.\n")  # codecs.cpp:836
+        self.w_, self.h_, self.d_ = w, h, n
+        self.pixels_ = np.frombuffer(pix, np.uint8).copy()
+
+    def write(self, filepath: str):
+        ext = os.path.splitext(filepath)[1].lower()
+        if ext not in (".jpg", ".jpeg"):
+            raise ValueError("Cannot parse filetype")
+        out = self.context().tje_encode(3, self.w_, self.h_, self.d_, self.pixels_.tobytes())  # codecs.cpp:853
+        with open(filepath, "wb") as f:
+            if out is not None:
+                f.write(out)
+
+    def load(self, pixels, w: int, h: int, channels: int):
+        self.pixels_ = np.ascontiguousarray(pixels, np.uint8).reshape(-1)
+        self.w_, self.h_, self.d_ = w, h, channels
+
+    def rows(self):
+        return self.h_
+
+    def cols(self):
+        return self.w_
+
+    def channels(self):
+        return self.d_
+
+    def empty(self):
+        return self.h_ == 0 or self.w_ == 0 or self.d_ == 0 or self.pixels_ is None
+
+    def totalBytes(self):
+        return self.w_ * self.h_ * self.d_
+
+    def data(self):
+        return self.pixels_

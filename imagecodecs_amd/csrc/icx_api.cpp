@@ -1,0 +1,381 @@
+// icx_api.cpp -- host side of libicx.so: the C ABI declared in include/icx.h.
+//
+// Contexts own a HIP stream and the NanoJPEG-style single-image state; batches own the
+// device workspace of one image group. No CPU decode path exists: every decode runs the
+// HIP kernels in icx_decode.hip, and a missing/unusable GPU is reported as an error.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/icx.h"
+#include "icx_internal.h"
+
+using namespace icx;
+
+struct icx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // njDecode-style state (jpeg_dec.h:313-330 equivalent, per context)
+    std::vector<uint8_t> nj_image;
+    int nj_w = 0, nj_h = 0, nj_color = 0, nj_size = 0;
+    icx_batch* single = nullptr;  // cached workspace for one-image calls
+    // staging for one-image calls
+    uint8_t* d_in = nullptr;
+    size_t d_in_cap = 0;
+};
+
+struct EventHook;
+
+struct icx_batch {
+    icx_ctx* ctx = nullptr;
+    int max_images = 0;
+    GroupWs ws;
+    uint8_t* d_hin = nullptr;  // staging for icx_jpeg_batch_decode_host
+    size_t d_hin_cap = 0;
+    std::unique_ptr<EventHook> hook;
+};
+
+static std::string g_create_err;
+
+static thread_local char g_msg[512];
+
+#define ICX_HIP(ctx, call, ret)                                                             \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            std::snprintf(g_msg, sizeof g_msg, "%s failed: %s", #call, hipGetErrorString(e_)); \
+            if (ctx) (ctx)->err = g_msg;                                                    \
+            return ret;                                                                     \
+        }                                                                                   \
+    } while (0)
+
+// Brackets every pipeline stage with HIP events on the launch stream.
+struct EventHook : StageHook {
+    struct Rec { Stage s; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void reset() { recs.clear(); used = 0; }
+    void begin(Stage s, hipStream_t st) override {
+        hipEvent_t a = get(), b = get();
+        if (!a || !b) return;
+        (void)hipEventRecord(a, st);
+        recs.push_back({s, a, b});
+    }
+    void end(Stage s, hipStream_t st) override {
+        for (auto it = recs.rbegin(); it != recs.rend(); ++it)
+            if (it->s == s) { (void)hipEventRecord(it->b, st); return; }
+    }
+    ~EventHook() override {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+extern "C" {
+
+const char* icx_version(void) { return "icx 0.1.0 gfx950"; }
+
+const char* icx_last_error(const icx_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
+
+icx_ctx* icx_create(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        g_create_err = "no HIP device available (libicx has no CPU decode path)";
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        g_create_err = "device ordinal out of range";
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        g_create_err = "hipSetDevice failed";
+        return nullptr;
+    }
+    auto* c = new icx_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        g_create_err = "hipStreamCreate failed";
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void icx_batch_destroy(icx_batch* b);
+
+void icx_destroy(icx_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->single) icx_batch_destroy(c->single);
+    if (c->d_in) (void)hipFree(c->d_in);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void icx_free(void* p) { std::free(p); }
+
+int icx_jpeg_probe(const uint8_t* jpeg, size_t size, int* w, int* h, int* ncomp) {
+    if (w) *w = 0;
+    if (h) *h = 0;
+    if (ncomp) *ncomp = 0;
+    if (!jpeg) return ICX_NO_JPEG;
+    auto d = std::make_unique<Desc>();
+    int st = parse_headers(jpeg, (int64_t)std::min<size_t>(size, 0x7FFFFFFF), *d);
+    if (st != kPending) return st;
+    if (w) *w = d->W;
+    if (h) *h = d->H;
+    if (ncomp) *ncomp = d->nc == 1 ? 1 : 3;
+    return ICX_OK;
+}
+
+// ----------------------------------------------------------------------------- batches
+icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, int group) {
+    if (!ctx || max_images <= 0 || max_w <= 0 || max_h <= 0 || max_w > 65535 || max_h > 65535) {
+        if (ctx) ctx->err = "icx_batch_create: bad arguments";
+        return nullptr;
+    }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), nullptr);
+    auto b = std::make_unique<icx_batch>();
+    b->ctx = ctx;
+    b->max_images = max_images;
+    GroupWs& ws = b->ws;
+    ws.max_w = max_w;
+    ws.max_h = max_h;
+    ws.coef_cap = ws_coef_cap(max_w, max_h);
+    ws.plane_cap = ws_plane_cap(max_w, max_h);
+    ws.tmp_cap = ws_tmp_cap(max_w, max_h);
+    const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc);
+    if (group <= 0) {
+        const int64_t budget = (int64_t)8 << 30;  // auto: ~8 GiB of workspace
+        group = (int)std::max<int64_t>(1, std::min<int64_t>(max_images, budget / per_slot));
+    }
+    group = std::min(group, max_images);
+    ws.slots = group;
+    ICX_HIP(ctx, hipMalloc(&ws.desc, sizeof(Desc) * group), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)ws.coef_cap * 64 * 2 * group), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)ws.coef_cap * 4 * group), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.planes, (size_t)ws.plane_cap * group), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), nullptr);
+    b->hook = std::make_unique<EventHook>();
+    return b.release();
+}
+
+void icx_batch_destroy(icx_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->ctx->device);
+    (void)hipFree(b->ws.desc);
+    (void)hipFree(b->ws.ac);
+    (void)hipFree(b->ws.dc);
+    (void)hipFree(b->ws.planes);
+    (void)hipFree(b->ws.tmp);
+    if (b->d_hin) (void)hipFree(b->d_hin);
+    delete b;
+}
+
+int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_size,
+                          uint8_t* d_out, uint64_t out_stride, int32_t* d_status, int32_t* d_dims, void* stream) {
+    if (!b) return ICX_INTERNAL_ERR;
+    icx_ctx* ctx = b->ctx;
+    if (n < 0 || n > b->max_images) { ctx->err = "icx_jpeg_batch_decode: n exceeds batch capacity"; return ICX_INTERNAL_ERR; }
+    if (n == 0) return ICX_OK;
+    if (!d_data || !d_off || !d_size || !d_out || !d_status || !d_dims) { ctx->err = "null pointer"; return ICX_INTERNAL_ERR; }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    b->hook->reset();
+    for (int g0 = 0; g0 < n; g0 += b->ws.slots) {
+        const int gn = std::min(b->ws.slots, n - g0);
+        launch_decode_group(b->ws, gn, d_data, d_off + g0, d_size + g0, d_out + (uint64_t)g0 * out_stride, out_stride,
+                            d_status + g0, d_dims + 3 * g0, st, b->hook.get());
+    }
+    ICX_HIP(ctx, hipGetLastError(), ICX_INTERNAL_ERR);
+    return ICX_OK;
+}
+
+int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int cap) {
+    if (!b) return 0;
+    float acc[kStCount] = {0};
+    for (auto& r : b->hook->recs) {
+        float t = 0;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) acc[r.s] += t;
+    }
+    int k = 0;
+    for (int s = 0; s < kStCount && k < cap; ++s, ++k) {
+        if (names) names[k] = kStageNames[s];
+        if (ms) ms[k] = acc[s];
+    }
+    return kStCount;
+}
+
+int icx_jpeg_batch_decode_host(icx_batch* b, int n, const uint8_t* const* jpegs, const size_t* sizes,
+                               uint8_t* const* outs, uint64_t out_stride, int32_t* status, int32_t* dims) {
+    if (!b) return ICX_INTERNAL_ERR;
+    icx_ctx* ctx = b->ctx;
+    if (n <= 0) return n == 0 ? ICX_OK : ICX_INTERNAL_ERR;
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
+    std::vector<uint64_t> off(n), sz(n);
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) { off[i] = total; sz[i] = sizes[i]; total += (sizes[i] + 15) & ~uint64_t(15); }
+    const size_t meta = (size_t)n * (8 + 8 + 4 + 12);
+    const size_t need = total + meta + (size_t)n * out_stride + 256;
+    if (need > b->d_hin_cap) {
+        if (b->d_hin) (void)hipFree(b->d_hin);
+        b->d_hin = nullptr;
+        b->d_hin_cap = 0;
+        ICX_HIP(ctx, hipMalloc(&b->d_hin, need), ICX_OUT_OF_MEM);
+        b->d_hin_cap = need;
+    }
+    uint8_t* base = b->d_hin;
+    uint8_t* d_data = base;
+    uint64_t* d_off = reinterpret_cast<uint64_t*>(base + ((total + 15) & ~uint64_t(15)));
+    uint64_t* d_sz = d_off + n;
+    int32_t* d_st = reinterpret_cast<int32_t*>(d_sz + n);
+    int32_t* d_dm = d_st + n;
+    uint8_t* d_out = reinterpret_cast<uint8_t*>(((uintptr_t)(d_dm + 3 * n) + 255) & ~uintptr_t(255));
+    hipStream_t st = ctx->stream;
+    for (int i = 0; i < n; ++i)
+        if (sz[i]) ICX_HIP(ctx, hipMemcpyAsync(d_data + off[i], jpegs[i], sz[i], hipMemcpyHostToDevice, st), ICX_INTERNAL_ERR);
+    ICX_HIP(ctx, hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, st), ICX_INTERNAL_ERR);
+    ICX_HIP(ctx, hipMemcpyAsync(d_sz, sz.data(), 8 * n, hipMemcpyHostToDevice, st), ICX_INTERNAL_ERR);
+    int rc = icx_jpeg_batch_decode(b, n, d_data, d_off, d_sz, d_out, out_stride, d_st, d_dm, st);
+    if (rc) return rc;
+    ICX_HIP(ctx, hipMemcpyAsync(status, d_st, 4 * n, hipMemcpyDeviceToHost, st), ICX_INTERNAL_ERR);
+    ICX_HIP(ctx, hipMemcpyAsync(dims, d_dm, 12 * n, hipMemcpyDeviceToHost, st), ICX_INTERNAL_ERR);
+    ICX_HIP(ctx, hipStreamSynchronize(st), ICX_INTERNAL_ERR);
+    for (int i = 0; i < n; ++i) {
+        const size_t bytes = (size_t)dims[3 * i] * dims[3 * i + 1] * dims[3 * i + 2];
+        if (status[i] == ICX_OK && bytes)
+            ICX_HIP(ctx, hipMemcpyAsync(outs[i], d_out + (uint64_t)i * out_stride, bytes, hipMemcpyDeviceToHost, st),
+                    ICX_INTERNAL_ERR);
+    }
+    ICX_HIP(ctx, hipStreamSynchronize(st), ICX_INTERNAL_ERR);
+    return ICX_OK;
+}
+
+// ------------------------------------------------------------------- one-image decode
+// Image::readJpg's path (codecs.cpp:821-849): probe on the host for the allocation size,
+// then the full GPU pipeline on a cached one-slot workspace.
+static int decode_one(icx_ctx* ctx, const uint8_t* jpeg, size_t size, std::vector<uint8_t>& out, int& w, int& h,
+                      int& color) {
+    w = h = color = 0;
+    out.clear();
+    if (!ctx) return ICX_INTERNAL_ERR;
+    int pw = 0, ph = 0, pc = 0;
+    const int probe = icx_jpeg_probe(jpeg, size, &pw, &ph, &pc);
+    if (probe != ICX_OK) return probe;  // header-level result is final (no entropy data reached)
+    if (!ctx->single || ctx->single->ws.max_w < pw || ctx->single->ws.max_h < ph) {
+        if (ctx->single) icx_batch_destroy(ctx->single);
+        ctx->single = icx_batch_create(ctx, 1, std::max(pw, 1), std::max(ph, 1), 1);
+        if (!ctx->single) return ICX_OUT_OF_MEM;
+    }
+    const uint8_t* in[1] = {jpeg};
+    size_t sizes[1] = {std::min<size_t>(size, 0x7FFFFFFF)};
+    out.resize(std::max<size_t>((size_t)pw * ph * 3, 1));
+    uint8_t* outs[1] = {out.data()};
+    int32_t st = 0, dims[3] = {0, 0, 0};
+    int rc = icx_jpeg_batch_decode_host(ctx->single, 1, in, sizes, outs, out.size(), &st, dims);
+    if (rc) return rc;
+    if (st != ICX_OK) { out.clear(); return st; }
+    w = dims[0];
+    h = dims[1];
+    color = dims[2] == 3;
+    out.resize((size_t)w * h * dims[2]);
+    return ICX_OK;
+}
+
+int icx_jpeg_decode(icx_ctx* ctx, const uint8_t* jpeg, size_t size, uint8_t** out, int* w, int* h, int* ncomp) {
+    if (out) *out = nullptr;
+    std::vector<uint8_t> buf;
+    int W = 0, H = 0, color = 0;
+    int rc = decode_one(ctx, jpeg, size, buf, W, H, color);
+    if (w) *w = W;
+    if (h) *h = H;
+    if (ncomp) *ncomp = rc == ICX_OK ? (color ? 3 : 1) : 0;
+    if (rc == ICX_OK && out && !buf.empty()) {
+        *out = static_cast<uint8_t*>(std::malloc(buf.size()));
+        if (!*out) return ICX_OUT_OF_MEM;
+        std::memcpy(*out, buf.data(), buf.size());
+    }
+    return rc;
+}
+
+// ------------------------------------------------------- NanoJPEG-compatible state API
+void icx_nj_init(icx_ctx* ctx) {
+    if (!ctx) return;
+    ctx->nj_image.clear();
+    ctx->nj_w = ctx->nj_h = ctx->nj_color = ctx->nj_size = 0;
+}
+void icx_nj_done(icx_ctx* ctx) { icx_nj_init(ctx); }
+
+int icx_nj_decode(icx_ctx* ctx, const void* jpeg, int size) {
+    if (!ctx) return ICX_INTERNAL_ERR;
+    icx_nj_init(ctx);  // njDecode starts with njDone (jpeg_dec.h:881)
+    int W = 0, H = 0, color = 0;
+    int rc = decode_one(ctx, static_cast<const uint8_t*>(jpeg), (size_t)(size & 0x7FFFFFFF), ctx->nj_image, W, H, color);
+    if (rc == ICX_OK) {
+        ctx->nj_w = W;
+        ctx->nj_h = H;
+        ctx->nj_color = color;
+        ctx->nj_size = (int)ctx->nj_image.size();
+    }
+    return rc;
+}
+int icx_nj_get_width(const icx_ctx* ctx) { return ctx ? ctx->nj_w : 0; }
+int icx_nj_get_height(const icx_ctx* ctx) { return ctx ? ctx->nj_h : 0; }
+int icx_nj_is_color(const icx_ctx* ctx) { return ctx ? ctx->nj_color : 0; }
+unsigned char* icx_nj_get_image(icx_ctx* ctx) {
+    return (ctx && !ctx->nj_image.empty()) ? ctx->nj_image.data() : nullptr;
+}
+int icx_nj_get_image_size(const icx_ctx* ctx) { return ctx ? ctx->nj_size : 0; }
+
+// ------------------------------------------------------------------ encode (tiny_jpeg)
+int icx_tje_encode_with_func(icx_ctx* ctx, icx_write_func* func, void* context, int quality, int width, int height,
+                             int num_components, const unsigned char* src) {
+    if (!ctx || !func) return 0;
+    if (quality < 1 || quality > 3) { ctx->err = "quality must be 1, 2 or 3"; return 0; }   // jpeg_enc.h:1223
+    if (num_components != 3 && num_components != 4) { ctx->err = "num_components must be 3 or 4"; return 0; }  // :954
+    if (width > 0xFFFF || height > 0xFFFF || width < 0 || height < 0) { ctx->err = "image too large"; return 0; }  // :958
+    if ((int64_t)width * height > 0 && !src) { ctx->err = "null source"; return 0; }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), 0);
+    std::vector<uint8_t> file;
+    if (!tje_encode_gpu(ctx->stream, quality, width, height, num_components, src, file)) {
+        ctx->err = "HIP failure in tje_encode_gpu";
+        return 0;
+    }
+    // tje hands the sink buffered chunks of TJEI_BUFFER_SIZE-1 bytes (jpeg_enc.h:474-496)
+    for (size_t o = 0; o < file.size(); o += 1023)
+        func(context, file.data() + o, (int)std::min<size_t>(1023, file.size() - o));
+    return 1;
+}
+
+static void file_sink(void* ctx, void* data, int size) { std::fwrite(data, (size_t)size, 1, (FILE*)ctx); }
+
+int icx_tje_encode_to_file_at_quality(icx_ctx* ctx, const char* dest_path, int quality, int width, int height,
+                                      int num_components, const unsigned char* src) {
+    FILE* fd = std::fopen(dest_path, "wb");  // jpeg_enc.h:1194-1213
+    if (!fd) { if (ctx) ctx->err = "could not open file for writing"; return 0; }
+    int result = icx_tje_encode_with_func(ctx, file_sink, fd, quality, width, height, num_components, src);
+    result |= 0 == std::fclose(fd);  // the reference's own (lossy) success rule, :1210
+    return result;
+}
+
+int icx_tje_encode_to_file(icx_ctx* ctx, const char* dest_path, int width, int height, int num_components,
+                           const unsigned char* src) {
+    return icx_tje_encode_to_file_at_quality(ctx, dest_path, 3, width, height, num_components, src);  // :1177-1185
+}
+
+}  // extern "C"

@@ -1,0 +1,311 @@
+// icx_decode.hip -- gfx950 kernels for batched JPEG decode (NanoJPEG-exact).
+//
+// Pipeline per group of images (one slot per image, all kernels cover the whole group):
+//   k_parse          header walk per image on the GPU            (jpeg_dec.h:880-903)
+//   k_entropy_seq    sequential Huffman decode, one lane/image   (jpeg_dec.h:643-718)
+//   k_idct           dequant + integer IDCT, 8 lanes per block   (jpeg_dec.h:343-442,658-676)
+//   k_upsample       one bicubic doubling pass per launch        (jpeg_dec.h:736-791,817-833)
+//   k_convert        YCbCr->RGB / gray stride removal            (jpeg_dec.h:834-865)
+// All integer math reproduces the reference bit for bit (icx_jpeg.h).
+#include <hip/hip_runtime.h>
+
+#include "icx_internal.h"
+
+namespace icx {
+
+const char* const kStageNames[kStCount] = {"parse", "entropy", "idct", "upsample", "convert"};
+
+int64_t ws_coef_cap(int w, int h) {  // any power-of-two sampling: MCU <= 64 px
+    int64_t wp = ((int64_t)w + 63) / 64 * 64, hp = ((int64_t)h + 63) / 64 * 64;
+    return 3 * (wp / 8) * (hp / 8);
+}
+int64_t ws_plane_cap(int w, int h) { return ws_coef_cap(w, h) * 64; }
+int64_t ws_tmp_cap(int w, int h) { return ((int64_t)w + 8) * ((int64_t)h + 8); }
+
+// ------------------------------------------------------------------------------ parse
+__global__ void k_parse(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                        const uint64_t* __restrict__ size, Desc* __restrict__ desc, int max_w, int max_h,
+                        uint64_t out_stride) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Desc& d = desc[i];
+    int st = parse_headers(data + off[i], (int64_t)size[i], d);
+    if (st == kPending) {
+        // capacity of this batch's workspace / output slot (the reference allocates here, :568-572)
+        const int64_t out_bytes = (int64_t)d.W * d.H * (d.nc == 1 ? 1 : d.nc);
+        if (d.W > max_w || d.H > max_h || out_bytes > (int64_t)out_stride) d.status = kOutOfMem;
+    }
+}
+
+// ---------------------------------------------------------------- entropy (sequential)
+// One lane walks one image's entropy-coded segment exactly like njDecodeScan. Used for
+// every image in this first slice; later slices keep it as the verified fallback.
+__global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                              Desc* __restrict__ desc, int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
+                              int64_t coef_cap) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Desc& d = desc[i];
+    if (d.status != kPending) return;
+    RawBits b{data + off[i] + d.scan_off, d.size - d.scan_off, 0u, 0, 0};
+    int16_t* A = ac + (int64_t)i * coef_cap * 64;
+    int32_t* D = dcv + (int64_t)i * coef_cap;
+    int32_t pred[3] = {0, 0, 0};
+    int left = d.restart, expect = 0;
+    const int64_t nmcu = (int64_t)d.mbw * d.mbh;
+    int64_t blk = 0;
+    int err = 0;
+    for (int64_t m = 0; m < (nmcu > 0 ? nmcu : 1) && !err; ++m) {
+        for (int r = 0; r < d.bpm && !err; ++r, ++blk) {
+            int sbx, sby;
+            const int ci = mcu_block_comp(d, r, sbx, sby);
+            const Comp& c = d.c[ci];
+            int16_t* row = A + blk * 64;
+            for (int k = 0; k < 64; k += 8) *reinterpret_cast<int4*>(row + k) = make_int4(0, 0, 0, 0);
+            // DC (jpeg_dec.h:662-663)
+            int sym = 0;
+            int len = huff_lookup(d.huff[c.dc_tab], rb_peek(b, 16), sym);
+            if (!len) { err = kSyntaxError; break; }
+            rb_drop(b, len);
+            int nb = sym & 15;
+            int32_t v = 0;
+            if (nb) { v = extend((int32_t)rb_peek(b, nb), nb); rb_drop(b, nb); }
+            pred[ci] = wadd(pred[ci], v);
+            D[blk] = pred[ci];
+            // AC (jpeg_dec.h:664-671)
+            int k = 0;
+            do {
+                len = huff_lookup(d.huff[c.ac_tab], rb_peek(b, 16), sym);
+                if (!len) { err = kSyntaxError; break; }
+                rb_drop(b, len);
+                if (!sym) break;  // EOB
+                if (!(sym & 0x0F) && sym != 0xF0) { err = kSyntaxError; break; }
+                nb = sym & 15;
+                v = 0;
+                if (nb) { v = extend((int32_t)rb_peek(b, nb), nb); rb_drop(b, nb); }
+                k += (sym >> 4) + 1;
+                if (k > 63) { err = kSyntaxError; break; }
+                row[nat_of_zig(k)] = (int16_t)v;
+            } while (k < 63);
+            if (b.err) err = b.err;
+        }
+        if (err) break;
+        if (d.restart && m + 1 < nmcu && !(--left)) {  // jpeg_dec.h:707-715
+            b.nacc &= 0xF8;
+            const int mk = (int)rb_peek(b, 16);
+            rb_drop(b, 16);
+            if ((mk & 0xFFF8) != 0xFFD0 || (mk & 7) != expect) { err = kSyntaxError; break; }
+            expect = (expect + 1) & 7;
+            left = d.restart;
+            pred[0] = pred[1] = pred[2] = 0;
+        }
+    }
+    d.status = err ? kSyntaxError : kOk;
+}
+
+// ----------------------------------------------------------------------- plane layout
+__device__ __forceinline__ int64_t comp_plane_off(const Desc& d, int ci) {
+    int64_t o = 0;
+    for (int j = 0; j < ci; ++j) o += (int64_t)d.c[j].stride * ((int64_t)d.mbh * d.c[j].vs * 8);
+    return o;
+}
+
+// --------------------------------------------------------------------------------- IDCT
+// 256 lanes = 32 blocks x 8 rows. Lane (b, r) dequantizes and row-transforms row r of block
+// b, then column-transforms column r, then stores row r of the 8x8 pixel tile (8 bytes).
+__global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                              const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
+                                              int64_t coef_cap, int64_t plane_cap) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (d.status != kOk) return;
+    __shared__ int32_t qn[3][64];        // natural-order dequant table per component
+    __shared__ int32_t rows[32][8][9];   // row-pass output, padded
+    __shared__ uint8_t pix[32][8][8];
+    const int t = threadIdx.x;
+    if (t < 3 * 64) {
+        const int ci = t >> 6, n = t & 63;
+        qn[ci][n] = ci < d.nc ? d.q[d.c[ci].tq][kZigOfNat[n]] : 0;
+    }
+    __syncthreads();
+    const int64_t nblocks = (int64_t)d.mbw * d.mbh * d.bpm;
+    const int lb = t >> 3, r = t & 7;
+    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
+    const int32_t* D = dcv + (int64_t)img * coef_cap;
+    uint8_t* P = planes + (int64_t)img * plane_cap;
+    for (int64_t base = (int64_t)blockIdx.x * 32; base < nblocks; base += (int64_t)gridDim.x * 32) {
+        const int64_t n = base + lb;
+        const bool live = n < nblocks;
+        int ci = 0, sbx = 0, sby = 0;
+        int64_t mcu = 0;
+        if (live) {
+            mcu = n / d.bpm;
+            ci = mcu_block_comp(d, (int)(n - mcu * d.bpm), sbx, sby);
+            const int4 raw = *reinterpret_cast<const int4*>(A + n * 64 + r * 8);
+            const int16_t* s = reinterpret_cast<const int16_t*>(&raw);
+            int32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = wmul(s[j], qn[ci][r * 8 + j]);
+            if (r == 0) v[0] = wmul(D[n], qn[ci][0]);
+            idct_row(v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rows[lb][r][j] = v[j];
+        }
+        __syncthreads();
+        if (live) {
+            int32_t col[8];
+            uint8_t o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) col[j] = rows[lb][j][r];
+            idct_col(col, o);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pix[lb][j][r] = o[j];
+        }
+        __syncthreads();
+        if (live) {
+            const Comp& c = d.c[ci];
+            const int64_t mby = mcu / d.mbw, mbx = mcu - mby * d.mbw;
+            const int64_t y = (mby * c.vs + sby) * 8 + r, x = (mbx * c.hs + sbx) * 8;
+            uint8_t* dst = P + comp_plane_off(d, ci) + y * c.stride + x;
+            *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(&pix[lb][r][0]);
+        }
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------------- upsample
+// The doubling program of one component: njConvert's loop (jpeg_dec.h:822-827).
+struct Plane {
+    const uint8_t* p;
+    int w, h, stride;
+};
+__device__ __forceinline__ int comp_program(const Desc& d, int ci, uint8_t (&ops)[6]) {
+    int w = d.c[ci].w, h = d.c[ci].h, n = 0;
+    while ((w < d.W || h < d.H) && n < 6) {
+        if (w < d.W) { ops[n++] = 'H'; w <<= 1; }
+        if (h < d.H && n < 6) { ops[n++] = 'V'; h <<= 1; }
+    }
+    return n;
+}
+// Buffer holding the output of pass p (p < 0: the IDCT plane) of component ci.
+__device__ __forceinline__ Plane pass_plane(const Desc& d, int ci, int p, const uint8_t* plane_slot,
+                                            const uint8_t* tmp_slot, int64_t tmp_cap, const uint8_t (&ops)[6]) {
+    const Comp& c = d.c[ci];
+    Plane pl{plane_slot + comp_plane_off(d, ci), c.w, c.h, c.stride};
+    for (int k = 0; k <= p; ++k) {
+        if (ops[k] == 'H') pl.w <<= 1; else pl.h <<= 1;
+        pl.stride = pl.w;
+        pl.p = tmp_slot + ((int64_t)ci * 2 + (k & 1)) * tmp_cap;
+    }
+    return pl;
+}
+
+// grid: (x: pixel tiles, y: slot*3 + comp). Pass `p` of every component that has one.
+__global__ __launch_bounds__(256) void k_upsample(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
+                                                  uint8_t* __restrict__ tmp, int64_t plane_cap, int64_t tmp_cap, int p) {
+    const int img = blockIdx.y / 3, ci = blockIdx.y % 3;
+    const Desc& d = desc[img];
+    if (d.status != kOk || ci >= d.nc) return;
+    uint8_t ops[6];
+    const int nops = comp_program(d, ci, ops);
+    if (p >= nops) return;
+    const uint8_t* pslot = planes + (int64_t)img * plane_cap;
+    uint8_t* tslot = tmp + (int64_t)img * 3 * 2 * tmp_cap;
+    const Plane in = pass_plane(d, ci, p - 1, pslot, tslot, tmp_cap, ops);
+    const Plane out = pass_plane(d, ci, p, pslot, tslot, tmp_cap, ops);
+    uint8_t* o = const_cast<uint8_t*>(out.p);
+    const int64_t total = (int64_t)out.w * out.h;
+    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+        const int y = (int)(idx / out.w), x = (int)(idx - (int64_t)y * out.w);
+        uint8_t v;
+        if (ops[p] == 'H') {
+            const uint8_t* row = in.p + (int64_t)y * in.stride;
+            v = double_tap(x, in.w, [&](int i) { return (int)row[i]; },
+                           [&](int j) { return (int)row[in.stride - j]; });
+        } else {
+            const uint8_t* col = in.p + x;
+            v = double_tap(y, in.h, [&](int i) { return (int)col[(int64_t)i * in.stride]; },
+                           [&](int j) { return (int)col[(int64_t)(in.h - j) * in.stride]; });
+        }
+        o[idx] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------ convert
+__global__ __launch_bounds__(256) void k_convert(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
+                                                 const uint8_t* __restrict__ tmp, int64_t plane_cap, int64_t tmp_cap,
+                                                 uint8_t* __restrict__ out, uint64_t out_stride) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (d.status != kOk) return;
+    const uint8_t* pslot = planes + (int64_t)img * plane_cap;
+    const uint8_t* tslot = tmp + (int64_t)img * 3 * 2 * tmp_cap;
+    Plane pl[3];
+    for (int ci = 0; ci < d.nc; ++ci) {
+        uint8_t ops[6];
+        const int nops = comp_program(d, ci, ops);
+        pl[ci] = pass_plane(d, ci, nops - 1, pslot, tslot, tmp_cap, ops);
+    }
+    uint8_t* o = out + (int64_t)img * out_stride;
+    const int64_t total = (int64_t)d.W * d.H;
+    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+        const int y = (int)(idx / d.W), x = (int)(idx - (int64_t)y * d.W);
+        if (d.nc == 3) {
+            ycc_to_rgb(pl[0].p[(int64_t)y * pl[0].stride + x], pl[1].p[(int64_t)y * pl[1].stride + x],
+                       pl[2].p[(int64_t)y * pl[2].stride + x], o + idx * 3);
+        } else {
+            o[idx] = pl[0].p[(int64_t)y * pl[0].stride + x];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------- finalize
+__global__ void k_finalize(int n, const Desc* __restrict__ desc, int32_t* __restrict__ status,
+                           int32_t* __restrict__ dims) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Desc& d = desc[i];
+    const int st = d.status == kPending ? kInternalErr : d.status;
+    status[i] = st;
+    dims[3 * i + 0] = st == kOk ? d.W : 0;
+    dims[3 * i + 1] = st == kOk ? d.H : 0;
+    dims[3 * i + 2] = st == kOk ? (d.nc == 1 ? 1 : 3) : 0;
+}
+
+// ---------------------------------------------------------------------------- launcher
+void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
+                         const uint64_t* d_size, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
+                         int32_t* d_dims, hipStream_t st, StageHook* hook) {
+    if (n <= 0) return;
+    auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
+    auto E = [&](Stage s) { if (hook) hook->end(s, st); };
+    const int tb = 64, nb = (n + tb - 1) / tb;
+    B(kStParse);
+    hipLaunchKernelGGL(k_parse, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
+                       out_stride);
+    E(kStParse);
+    B(kStEntropy);
+    hipLaunchKernelGGL(k_entropy_seq, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc,
+                       ws.coef_cap);
+    E(kStEntropy);
+    B(kStIdct);
+    const int64_t maxblk = ws.coef_cap;
+    const int gx = (int)std::min<int64_t>((maxblk + 31) / 32, 4096);
+    hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
+                       ws.plane_cap);
+    E(kStIdct);
+    B(kStUpsample);
+    const int ux = (int)std::min<int64_t>((ws.tmp_cap + 255) / 256, 4096);
+    for (int p = 0; p < 6; ++p)
+        hipLaunchKernelGGL(k_upsample, dim3(ux, n * 3), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
+                           ws.tmp_cap, p);
+    E(kStUpsample);
+    B(kStConvert);
+    const int cx = (int)std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
+                       ws.tmp_cap, d_out, out_stride);
+    hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(tb), 0, st, n, ws.desc, d_status, d_dims);
+    E(kStConvert);
+}
+
+}  // namespace icx

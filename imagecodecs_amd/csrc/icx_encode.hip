@@ -1,0 +1,397 @@
+// icx_encode.hip -- gfx950 tiny_jpeg-exact encoder (jpeg_enc.h:786-1175).
+//
+//   k_enc_units   gather + float RGB->YCbCr + AAN float FDCT + quantize, one lane per
+//                 (8x8 block, component) unit                 (jpeg_enc.h:1094-1126, 656-817)
+//   k_enc_count   Huffman bit length of every unit            (jpeg_enc.h:831-887)
+//   (scan)        exclusive prefix sum of unit bit lengths -> bit offsets (hipCUB)
+//   k_enc_emit    pack each unit's codes at its bit offset    (jpeg_enc.h:613-643)
+//   k_stuff_*     FF -> FF 00 byte stuffing by count/scan/copy (jpeg_enc.h:634-638)
+// Built with -ffp-contract=off: every float op rounds exactly like the reference build.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <vector>
+
+#include "icx_internal.h"
+
+namespace icx {
+
+struct EncTables {
+    float pq[2][64];          // 1/(8*aan[x]*aan[y]*q), natural order (jpeg_enc.h:980-986)
+    uint16_t code[4][256];    // 0 luma DC, 1 luma AC, 2 chroma DC, 3 chroma AC
+    uint8_t len[4][256];
+};
+
+__constant__ static const uint8_t kZigOfNatE[64] = {
+    0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43,
+    9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+    21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+// AAN float FDCT on 8 samples at stride S (tjei_fdct, jpeg_enc.h:667-712), in registers.
+template <int S>
+__device__ __forceinline__ void fdct8(float* p) {
+    const float t0 = p[0] + p[7 * S], t7 = p[0] - p[7 * S];
+    const float t1 = p[S] + p[6 * S], t6 = p[S] - p[6 * S];
+    const float t2 = p[2 * S] + p[5 * S], t5 = p[2 * S] - p[5 * S];
+    const float t3 = p[3 * S] + p[4 * S], t4 = p[3 * S] - p[4 * S];
+    const float e10 = t0 + t3, e13 = t0 - t3, e11 = t1 + t2, e12 = t1 - t2;
+    p[0] = e10 + e11;
+    p[4 * S] = e10 - e11;
+    const float z1 = (e12 + e13) * ((float)0.707106781);
+    p[2 * S] = e13 + z1;
+    p[6 * S] = e13 - z1;
+    const float o10 = t4 + t5, o11 = t5 + t6, o12 = t6 + t7;
+    const float z5 = (o10 - o12) * ((float)0.382683433);
+    const float z2 = ((float)0.541196100) * o10 + z5;
+    const float z4 = ((float)1.306562965) * o12 + z5;
+    const float z3 = o11 * ((float)0.707106781);
+    const float z11 = t7 + z3, z13 = t7 - z3;
+    p[5 * S] = z13 + z2;
+    p[3 * S] = z13 - z2;
+    p[S] = z11 + z4;
+    p[7 * S] = z11 - z4;
+}
+
+__global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ src, int w, int h, int comps,
+                                                   int bw, int64_t nunits, const EncTables* __restrict__ T,
+                                                   int16_t* __restrict__ zz) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nunits) return;
+    const int64_t blk = u / 3;
+    const int c = (int)(u - blk * 3);
+    const int bx = (int)(blk % bw), by = (int)(blk / bw);
+    float f[64];
+#pragma unroll
+    for (int oy = 0; oy < 8; ++oy) {
+        const int row = min(by * 8 + oy, h - 1);  // edge clamp (jpeg_enc.h:1106-1111)
+#pragma unroll
+        for (int ox = 0; ox < 8; ++ox) {
+            const int col = min(bx * 8 + ox, w - 1);
+            const uint8_t* p = src + ((int64_t)row * w + col) * comps;
+            const uint8_t r = p[0], g = p[1], b = p[2];
+            float v;  // jpeg_enc.h:1118-1120, evaluated left to right
+            if (c == 0) v = 0.299f * r + 0.587f * g + 0.114f * b - 128;
+            else if (c == 1) v = -0.1687f * r - 0.3313f * g + 0.5f * b;
+            else v = 0.5f * r - 0.4187f * g - 0.0813f * b;
+            f[oy * 8 + ox] = v;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) fdct8<1>(f + 8 * r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) fdct8<8>(f + k);
+    const float* pq = T->pq[c ? 1 : 0];
+    int16_t* o = zz + u * 64;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {  // jpeg_enc.h:806-817
+        float v = f[i];
+        v *= pq[i];
+        v = floorf(v + 1024 + 0.5f);
+        v -= 1024;
+        o[kZigOfNatE[i]] = (int16_t)(int)v;
+    }
+}
+
+__device__ __forceinline__ void vli(int v, int& nb, uint32_t& bits) {  // jpeg_enc.h:598-610
+    int mag = v < 0 ? -v : v;
+    if (v < 0) --v;
+    nb = mag ? 32 - __clz(mag) : 1;
+    bits = (uint32_t)v & ((1u << nb) - 1u);
+}
+
+// Visit every (length, bits) code of one unit in stream order (jpeg_enc.h:831-887).
+template <class F>
+__device__ __forceinline__ void unit_codes(const int16_t* zz, int pred, const EncTables* T, int c, F&& put) {
+    const int td = c ? 2 : 0, ta = c ? 3 : 1;
+    int nb;
+    uint32_t bits;
+    const int diff = zz[0] - pred;
+    if (diff) {
+        vli(diff, nb, bits);
+        put(T->len[td][nb], T->code[td][nb]);
+        put(nb, bits);
+    } else {
+        put(T->len[td][0], T->code[td][0]);
+    }
+    int last = 0;
+    for (int i = 63; i > 0; --i)
+        if (zz[i]) { last = i; break; }
+    for (int i = 1; i <= last; ++i) {
+        int run = 0;
+        while (zz[i] == 0) {
+            ++run;
+            ++i;
+            if (run == 16) { put(T->len[ta][0xF0], T->code[ta][0xF0]); run = 0; }
+        }
+        vli(zz[i], nb, bits);
+        const int sym = (run << 4) | nb;
+        put(T->len[ta][sym], T->code[ta][sym]);
+        put(nb, bits);
+    }
+    if (last != 63) put(T->len[ta][0], T->code[ta][0]);
+}
+
+__global__ __launch_bounds__(256) void k_enc_count(const int16_t* __restrict__ zz, int64_t nunits,
+                                                   const EncTables* __restrict__ T, uint64_t* __restrict__ nbits) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nunits) return;
+    const int c = (int)(u % 3);
+    const int pred = u >= 3 ? zz[(u - 3) * 64] : 0;  // DC predictor never resets (:834-835)
+    uint64_t total = 0;
+    unit_codes(zz + u * 64, pred, T, c, [&](int n, uint32_t) { total += (uint64_t)n; });
+    nbits[u] = total;
+}
+
+// Stream words hold bits MSB-first: word k covers stream bits [32k, 32k+32).
+__global__ __launch_bounds__(256) void k_enc_emit(const int16_t* __restrict__ zz, int64_t nunits,
+                                                  const EncTables* __restrict__ T, const uint64_t* __restrict__ off,
+                                                  uint32_t* __restrict__ words) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nunits) return;
+    const int c = (int)(u % 3);
+    const int pred = u >= 3 ? zz[(u - 3) * 64] : 0;
+    uint64_t pos = off[u];
+    uint64_t wi = pos >> 5;
+    uint32_t acc = 0;
+    unit_codes(zz + u * 64, pred, T, c, [&](int n, uint32_t v) {
+        if (!n) return;
+        v &= (n == 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+        while (n > 0) {
+            const int o = (int)(pos & 31);
+            const int take = min(n, 32 - o);
+            const uint32_t part = (v >> (n - take)) & ((take == 32) ? 0xFFFFFFFFu : ((1u << take) - 1u));
+            acc |= part << (32 - o - take);
+            pos += take;
+            n -= take;
+            if ((pos & 31) == 0) {
+                atomicOr(&words[wi], acc);
+                acc = 0;
+                ++wi;
+            }
+        }
+    });
+    if (pos & 31) atomicOr(&words[wi], acc);
+}
+
+__device__ __forceinline__ uint8_t stream_byte(const uint32_t* words, uint64_t b) {
+    return (uint8_t)(words[b >> 2] >> (24 - 8 * (b & 3)));
+}
+
+constexpr int kStuffChunk = 64;  // stream bytes per lane
+
+__global__ __launch_bounds__(256) void k_stuff_count(const uint32_t* __restrict__ words, uint64_t nbytes,
+                                                     uint32_t* __restrict__ cnt, int64_t nchunks) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nchunks) return;
+    const uint64_t b0 = (uint64_t)t * kStuffChunk, b1 = min<uint64_t>(b0 + kStuffChunk, nbytes);
+    uint32_t n = 0;
+    for (uint64_t b = b0; b < b1; ++b) n += stream_byte(words, b) == 0xFF;
+    cnt[t] = n;
+}
+
+__global__ __launch_bounds__(256) void k_stuff_write(const uint32_t* __restrict__ words, uint64_t nbytes,
+                                                     const uint32_t* __restrict__ base, int64_t nchunks,
+                                                     uint8_t* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nchunks) return;
+    const uint64_t b0 = (uint64_t)t * kStuffChunk, b1 = min<uint64_t>(b0 + kStuffChunk, nbytes);
+    uint64_t o = b0 + base[t];
+    for (uint64_t b = b0; b < b1; ++b) {
+        const uint8_t v = stream_byte(words, b);
+        out[o++] = v;
+        if (v == 0xFF) out[o++] = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------ host
+static const uint8_t kLumaQ[64] = {
+    16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55, 14, 13, 16, 24, 40, 57, 69, 56,
+    14, 17, 22, 29, 51, 87, 80, 62, 18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+    49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};  // jpeg_enc.h:266-276
+static const uint8_t kChromaQ[64] = {
+    16, 12, 14, 14, 18, 24, 49, 72, 11, 10, 16, 24, 40, 51, 61, 12, 13, 17, 22, 35, 64, 92, 14, 16,
+    22, 37, 55, 78, 95, 19, 24, 29, 56, 64, 87, 98, 26, 40, 51, 68, 81, 103, 112, 58, 57, 87, 109, 104,
+    121, 100, 60, 69, 80, 103, 113, 120, 103, 55, 56, 62, 77, 92, 101, 99};  // jpeg_enc.h:294-305
+static const uint8_t kDcLB[16] = {0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+static const uint8_t kDcCB[16] = {0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+static const uint8_t kDcV[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+static const uint8_t kAcLB[16] = {0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d};
+static const uint8_t kAcCB[16] = {0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77};
+static const uint8_t kAcLV[162] = {  // jpeg_enc.h:336-349
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61, 0x07, 0x22, 0x71,
+    0x14, 0x32, 0x81, 0x91, 0xA1, 0x08, 0x23, 0x42, 0xB1, 0xC1, 0x15, 0x52, 0xD1, 0xF0, 0x24, 0x33, 0x62, 0x72,
+    0x82, 0x09, 0x0A, 0x16, 0x17, 0x18, 0x19, 0x1A, 0x25, 0x26, 0x27, 0x28, 0x29, 0x2A, 0x34, 0x35, 0x36, 0x37,
+    0x38, 0x39, 0x3A, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4A, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59,
+    0x5A, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6A, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7A, 0x83,
+    0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8A, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9A, 0xA2, 0xA3,
+    0xA4, 0xA5, 0xA6, 0xA7, 0xA8, 0xA9, 0xAA, 0xB2, 0xB3, 0xB4, 0xB5, 0xB6, 0xB7, 0xB8, 0xB9, 0xBA, 0xC2, 0xC3,
+    0xC4, 0xC5, 0xC6, 0xC7, 0xC8, 0xC9, 0xCA, 0xD2, 0xD3, 0xD4, 0xD5, 0xD6, 0xD7, 0xD8, 0xD9, 0xDA, 0xE1, 0xE2,
+    0xE3, 0xE4, 0xE5, 0xE6, 0xE7, 0xE8, 0xE9, 0xEA, 0xF1, 0xF2, 0xF3, 0xF4, 0xF5, 0xF6, 0xF7, 0xF8, 0xF9, 0xFA};
+static const uint8_t kAcCV[162] = {  // jpeg_enc.h:355-368
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61, 0x71, 0x13, 0x22,
+    0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xA1, 0xB1, 0xC1, 0x09, 0x23, 0x33, 0x52, 0xF0, 0x15, 0x62, 0x72, 0xD1,
+    0x0A, 0x16, 0x24, 0x34, 0xE1, 0x25, 0xF1, 0x17, 0x18, 0x19, 0x1A, 0x26, 0x27, 0x28, 0x29, 0x2A, 0x35, 0x36,
+    0x37, 0x38, 0x39, 0x3A, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4A, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58,
+    0x59, 0x5A, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6A, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7A,
+    0x82, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8A, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9A,
+    0xA2, 0xA3, 0xA4, 0xA5, 0xA6, 0xA7, 0xA8, 0xA9, 0xAA, 0xB2, 0xB3, 0xB4, 0xB5, 0xB6, 0xB7, 0xB8, 0xB9, 0xBA,
+    0xC2, 0xC3, 0xC4, 0xC5, 0xC6, 0xC7, 0xC8, 0xC9, 0xCA, 0xD2, 0xD3, 0xD4, 0xD5, 0xD6, 0xD7, 0xD8, 0xD9, 0xDA,
+    0xE2, 0xE3, 0xE4, 0xE5, 0xE6, 0xE7, 0xE8, 0xE9, 0xEA, 0xF2, 0xF3, 0xF4, 0xF5, 0xF6, 0xF7, 0xF8, 0xF9, 0xFA};
+static const uint8_t kZigOfNatH[64] = {
+    0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43,
+    9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+    21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+static void huff_codes(uint16_t* code, uint8_t* len, const uint8_t* bits, const uint8_t* vals) {  // C.2
+    unsigned cd = 0;
+    int k = 0;
+    for (int L = 1; L <= 16; ++L) {
+        for (int i = 0; i < bits[L - 1]; ++i, ++k) { code[vals[k]] = (uint16_t)cd++; len[vals[k]] = (uint8_t)L; }
+        cd <<= 1;
+    }
+}
+
+// Header bytes of tje_encode_main (jpeg_enc.h:989-1077) for quality tables ql/qc.
+static void tje_header(std::vector<uint8_t>& o, int w, int h, const uint8_t* ql, const uint8_t* qc) {
+    auto u8 = [&](int v) { o.push_back((uint8_t)v); };
+    auto be = [&](int v) { u8(v >> 8); u8(v & 255); };
+    static const uint8_t jfif[] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0,
+                                   0x01, 0x02, 0x01, 0x00, 0x60, 0x00, 0x60, 0x00, 0x00};
+    o.insert(o.end(), jfif, jfif + sizeof jfif);
+    static const char com[] = "Created by Tiny JPEG Encoder";
+    be(0xFFFE);
+    be(2 + (int)sizeof(com) - 1);
+    o.insert(o.end(), com, com + sizeof(com) - 1);
+    be(0xFFDB); be(0x43); u8(0); o.insert(o.end(), ql, ql + 64);
+    be(0xFFDB); be(0x43); u8(1); o.insert(o.end(), qc, qc + 64);
+    be(0xFFC0); be(17); u8(8); be(h); be(w); u8(3);
+    for (int i = 0; i < 3; ++i) { u8(i + 1); u8(0x11); u8(i ? 1 : 0); }
+    const uint8_t* hb[4] = {kDcLB, kAcLB, kDcCB, kAcCB};
+    const uint8_t* hv[4] = {kDcV, kAcLV, kDcV, kAcCV};
+    const int id[4] = {0x00, 0x10, 0x01, 0x11};
+    for (int t = 0; t < 4; ++t) {
+        int n = 0;
+        for (int i = 0; i < 16; ++i) n += hb[t][i];
+        be(0xFFC4); be(2 + 1 + 16 + n); u8(id[t]);
+        o.insert(o.end(), hb[t], hb[t] + 16);
+        o.insert(o.end(), hv[t], hv[t] + n);
+    }
+    be(0xFFDA); be(12); u8(3);
+    u8(1); u8(0x00); u8(2); u8(0x11); u8(3); u8(0x11);
+    u8(0); u8(63); u8(0);
+}
+
+#define ENC_HIP(call)                               \
+    do {                                            \
+        if ((call) != hipSuccess) { ok = false; goto done; } \
+    } while (0)
+
+// Encode on the GPU; returns false on a HIP failure. `out` receives the whole file.
+bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const uint8_t* src,
+                    std::vector<uint8_t>& out) {
+    uint8_t ql[64], qc[64];
+    for (int i = 0; i < 64; ++i) {  // jpeg_enc.h:1231-1256
+        if (quality == 3) { ql[i] = qc[i] = 1; continue; }
+        const int div = quality == 2 ? 10 : 1;
+        ql[i] = (uint8_t)(kLumaQ[i] / div);
+        if (!ql[i]) ql[i] = 1;
+        qc[i] = (uint8_t)(kChromaQ[i] / div);
+        if (!qc[i]) qc[i] = 1;
+    }
+    EncTables T;
+    std::memset(&T, 0, sizeof T);
+    static const float aan[8] = {1.0f, 1.387039845f, 1.306562965f, 1.175875602f,
+                                 1.0f, 0.785694958f, 0.541196100f, 0.275899379f};
+    for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) {
+            const int i = y * 8 + x;
+            T.pq[0][i] = 1.0f / (8 * aan[x] * aan[y] * ql[kZigOfNatH[i]]);
+            T.pq[1][i] = 1.0f / (8 * aan[x] * aan[y] * qc[kZigOfNatH[i]]);
+        }
+    huff_codes(T.code[0], T.len[0], kDcLB, kDcV);
+    huff_codes(T.code[1], T.len[1], kAcLB, kAcLV);
+    huff_codes(T.code[2], T.len[2], kDcCB, kDcV);
+    huff_codes(T.code[3], T.len[3], kAcCB, kAcCV);
+    out.clear();
+    tje_header(out, w, h, ql, qc);
+
+    const int bw = (w + 7) / 8, bh = (h + 7) / 8;
+    const int64_t nunits = (int64_t)bw * bh * 3;
+    const size_t srcb = (size_t)w * h * comps;
+    bool ok = true;
+    uint8_t *d_src = nullptr, *d_out = nullptr;
+    EncTables* d_T = nullptr;
+    int16_t* d_zz = nullptr;
+    uint64_t *d_nb = nullptr, *d_off = nullptr;
+    uint32_t *d_words = nullptr, *d_cnt = nullptr, *d_base = nullptr;
+    void* d_tmp = nullptr;
+    size_t tmp_b = 0, tmp_b2 = 0;
+    uint64_t last_off = 0, last_nb = 0, total_bits = 0, nbytes = 0, nff = 0;
+    uint32_t last_cnt = 0, last_base = 0;
+    int64_t nchunks = 0;
+    const int TB = 256;
+    const int gu = (int)((nunits + TB - 1) / TB);
+    if (nunits == 0) {  // empty image: headers + EOI only
+        out.push_back(0xFF);
+        out.push_back(0xD9);
+        return true;
+    }
+    ENC_HIP(hipMalloc(&d_src, srcb));
+    ENC_HIP(hipMalloc(&d_T, sizeof T));
+    ENC_HIP(hipMalloc(&d_zz, (size_t)nunits * 64 * 2));
+    ENC_HIP(hipMalloc(&d_nb, (size_t)nunits * 8));
+    ENC_HIP(hipMalloc(&d_off, (size_t)nunits * 8));
+    ENC_HIP(hipMemcpyAsync(d_src, src, srcb, hipMemcpyHostToDevice, st));
+    ENC_HIP(hipMemcpyAsync(d_T, &T, sizeof T, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_enc_units, dim3(gu), dim3(TB), 0, st, d_src, w, h, comps, bw, nunits, d_T, d_zz);
+    hipLaunchKernelGGL(k_enc_count, dim3(gu), dim3(TB), 0, st, d_zz, nunits, d_T, d_nb);
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, d_nb, d_off, (int)nunits, st));
+    ENC_HIP(hipMalloc(&d_tmp, tmp_b));
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_b, d_nb, d_off, (int)nunits, st));
+    ENC_HIP(hipMemcpyAsync(&last_off, d_off + nunits - 1, 8, hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipMemcpyAsync(&last_nb, d_nb + nunits - 1, 8, hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipStreamSynchronize(st));
+    total_bits = last_off + last_nb;
+    nbytes = (total_bits + 7) / 8;  // final partial byte zero-padded (jpeg_enc.h:1161-1165)
+    ENC_HIP(hipMalloc(&d_words, ((nbytes + 3) / 4 + 1) * 4));
+    ENC_HIP(hipMemsetAsync(d_words, 0, ((nbytes + 3) / 4 + 1) * 4, st));
+    hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, d_zz, nunits, d_T, d_off, d_words);
+    nchunks = (int64_t)((nbytes + kStuffChunk - 1) / kStuffChunk);
+    if (nchunks > 0) {
+        ENC_HIP(hipMalloc(&d_cnt, (size_t)nchunks * 4));
+        ENC_HIP(hipMalloc(&d_base, (size_t)nchunks * 4));
+        const int gc = (int)((nchunks + TB - 1) / TB);
+        hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, d_words, nbytes, d_cnt, nchunks);
+        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, d_cnt, d_base, (int)nchunks, st));
+        if (tmp_b2 > tmp_b) {
+            ENC_HIP(hipFree(d_tmp));
+            d_tmp = nullptr;
+            ENC_HIP(hipMalloc(&d_tmp, tmp_b2));
+            tmp_b = tmp_b2;
+        }
+        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_b, d_cnt, d_base, (int)nchunks, st));
+        ENC_HIP(hipMemcpyAsync(&last_cnt, d_cnt + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
+        ENC_HIP(hipMemcpyAsync(&last_base, d_base + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
+        ENC_HIP(hipStreamSynchronize(st));
+        nff = (uint64_t)last_cnt + last_base;
+        ENC_HIP(hipMalloc(&d_out, nbytes + nff));
+        hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, d_words, nbytes, d_base, nchunks, d_out);
+        {
+            const size_t h0 = out.size();
+            out.resize(h0 + nbytes + nff);
+            ENC_HIP(hipMemcpyAsync(out.data() + h0, d_out, nbytes + nff, hipMemcpyDeviceToHost, st));
+        }
+    }
+    ENC_HIP(hipStreamSynchronize(st));
+    ENC_HIP(hipGetLastError());
+    out.push_back(0xFF);
+    out.push_back(0xD9);
+done:
+    for (void* p : {(void*)d_src, (void*)d_T, (void*)d_zz, (void*)d_nb, (void*)d_off, (void*)d_words, (void*)d_cnt,
+                    (void*)d_base, d_tmp, (void*)d_out})
+        if (p) (void)hipFree(p);
+    return ok;
+}
+
+}  // namespace icx

@@ -1,0 +1,121 @@
+/*
+ * icx.h -- C ABI of libicx.so, the MI355X-native JPEG codec behind ImageCodecs' codecs.h.
+ *
+ * Plain pointers and sizes only (no torch / HIP types in signatures). Every function is
+ * extern "C", never throws, and is reentrant per icx_ctx. Each entry point names the
+ * reference interface it replaces (paths relative to the jstrom2002/ImageCodecs tree):
+ *
+ *   NanoJPEG (jpeg_dec.h:117-171): njInit/njDecode/njGetWidth/njGetHeight/njIsColor/
+ *       njGetImage/njGetImageSize/njDone  -> icx_nj_* below, with the decoder state held
+ *       in an icx_ctx instead of NanoJPEG's process-global `nj` (jpeg_dec.h:332).
+ *   tiny_jpeg (jpeg_enc.h:114-160): tje_encode_to_file/_at_quality/tje_encode_with_func
+ *       -> icx_tje_* below (same quality 1..3 contract and byte stream).
+ *   Image::readJpg (codecs.cpp:821-849) -> icx_jpeg_decode (one call, host in/host out).
+ *   Batch decode (new) -> icx_jpeg_batch_* (device-resident in and out).
+ *
+ * Result codes are NanoJPEG's nj_result_t values (jpeg_dec.h:117-125).
+ */
+#ifndef ICX_H
+#define ICX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum icx_result {
+    ICX_OK = 0,              /* NJ_OK            */
+    ICX_NO_JPEG = 1,         /* NJ_NO_JPEG       */
+    ICX_UNSUPPORTED = 2,     /* NJ_UNSUPPORTED   */
+    ICX_OUT_OF_MEM = 3,      /* NJ_OUT_OF_MEM    */
+    ICX_INTERNAL_ERR = 4,    /* NJ_INTERNAL_ERR  */
+    ICX_SYNTAX_ERROR = 5     /* NJ_SYNTAX_ERROR  */
+};
+
+typedef struct icx_ctx icx_ctx;
+
+/* ---- context ------------------------------------------------------------------- */
+/* One context per (device, HIP stream). `device` is a HIP device ordinal. Returns NULL
+ * if the device cannot be opened (see icx_last_error(NULL)). */
+icx_ctx* icx_create(int device);
+void icx_destroy(icx_ctx* ctx);
+/* Last error message for this context (or the last icx_create failure when ctx==NULL). */
+const char* icx_last_error(const icx_ctx* ctx);
+/* Library version string, e.g. "icx 0.1.0 gfx950". */
+const char* icx_version(void);
+
+/* ---- header probe (host only; no device work) ------------------------------------ */
+/* Parses markers up to the first SOS exactly as njDecode does (jpeg_dec.h:880-903).
+ * Returns ICX_OK when the stream is well-formed up to the entropy-coded data (decode may
+ * still fail later) and fills width/height/ncomp (ncomp: 1 gray, 3 colour); otherwise the
+ * code njDecode would return. */
+int icx_jpeg_probe(const uint8_t* jpeg, size_t size, int* width, int* height, int* ncomp);
+
+/* ---- NanoJPEG-compatible stateful API (jpeg_dec.h:130-171) ------------------------- */
+/* njInit (jpeg_dec.h:130) / njDone (:171): reset the context's decoder state. */
+void icx_nj_init(icx_ctx* ctx);
+void icx_nj_done(icx_ctx* ctx);
+/* njDecode (jpeg_dec.h:138): decodes on the GPU; returns an icx_result. */
+int icx_nj_decode(icx_ctx* ctx, const void* jpeg, int size);
+int icx_nj_get_width(const icx_ctx* ctx);         /* njGetWidth     (:142) */
+int icx_nj_get_height(const icx_ctx* ctx);        /* njGetHeight    (:146) */
+int icx_nj_is_color(const icx_ctx* ctx);          /* njIsColor      (:151) */
+unsigned char* icx_nj_get_image(icx_ctx* ctx);    /* njGetImage     (:160) host memory owned by ctx */
+int icx_nj_get_image_size(const icx_ctx* ctx);    /* njGetImageSize (:165) */
+
+/* ---- one-shot decode (Image::readJpg, codecs.cpp:821-849) ------------------------- */
+/* Decodes on the GPU; *out receives a malloc()'d W*H*ncomp buffer (free with icx_free).
+ * ncomp is 3 for colour and 1 for gray (the reference adapter's d=3-for-gray over-read,
+ * codecs.cpp:840-844, is not reproduced). */
+int icx_jpeg_decode(icx_ctx* ctx, const uint8_t* jpeg, size_t size, uint8_t** out, int* width,
+                    int* height, int* ncomp);
+void icx_free(void* p);
+
+/* ---- batch decode, device-resident (the throughput path) ------------------------- */
+typedef struct icx_batch icx_batch;
+
+/* Workspace for up to `max_images` images per call, each at most max_width x max_height
+ * (any sampling NanoJPEG accepts). Images are processed in groups of `group` (0 = auto)
+ * that reuse one workspace. Returns NULL on allocation failure. */
+icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_width, int max_height, int group);
+void icx_batch_destroy(icx_batch* b);
+
+/* Decode n images. All pointers are DEVICE pointers on the context's device:
+ *   d_data      concatenated JPEG files; image i is d_data[d_offsets[i] .. + d_sizes[i])
+ *   d_out       output; image i is written at d_out + i*out_stride, packed W*H*ncomp bytes
+ *   d_status    n int32 icx_result codes (per image; one bad image never fails the batch)
+ *   d_dims      n*3 int32 {width, height, ncomp} (ncomp 3 colour / 1 gray; 0s on error)
+ * An image larger than the batch limits, or whose pixels exceed out_stride, gets
+ * ICX_OUT_OF_MEM. Work is enqueued on `stream` (a hipStream_t; NULL = the context's
+ * stream); the call returns without synchronizing. Returns ICX_OK or a call-level error. */
+int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint64_t* d_offsets,
+                          const uint64_t* d_sizes, uint8_t* d_out, uint64_t out_stride,
+                          int32_t* d_status, int32_t* d_dims, void* stream);
+
+/* Host-buffer convenience: copies inputs to the device, decodes, copies results back.
+ * outs[i] must hold out_stride bytes. */
+int icx_jpeg_batch_decode_host(icx_batch* b, int n, const uint8_t* const* jpegs, const size_t* sizes,
+                               uint8_t* const* outs, uint64_t out_stride, int32_t* status, int32_t* dims);
+
+/* Per-stage timings (ms) of the most recent batch call, measured with HIP events on the
+ * stream the kernels ran on. Fills up to `cap` entries; returns the number of stages. */
+int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int cap);
+
+/* ---- encode (tiny_jpeg, jpeg_enc.h:114-160) --------------------------------------- */
+typedef void icx_write_func(void* context, void* data, int size); /* = tje_write_func */
+
+/* tje_encode_with_func (jpeg_enc.h:154): quality 1..3, comps 3 (RGB) or 4 (RGBA);
+ * returns 1 on success, 0 on error. The byte stream is identical to tiny_jpeg's. */
+int icx_tje_encode_with_func(icx_ctx* ctx, icx_write_func* func, void* context, int quality,
+                             int width, int height, int num_components, const unsigned char* src);
+/* tje_encode_to_file_at_quality (jpeg_enc.h:137) / tje_encode_to_file (:114, quality 3). */
+int icx_tje_encode_to_file_at_quality(icx_ctx* ctx, const char* dest_path, int quality, int width,
+                                      int height, int num_components, const unsigned char* src);
+int icx_tje_encode_to_file(icx_ctx* ctx, const char* dest_path, int width, int height,
+                           int num_components, const unsigned char* src);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICX_H */

@@ -1,0 +1,113 @@
+"""GPU parity tests (tier 2/3 of SURVEY.md §4): the HIP decode path through the C ABI vs the
+oracle / the reference's golden vectors. Bit-exact for every byte (integer path)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+import imagecodecs_amd as icx
+from oracle import pyoracle as O
+from tools import synthpy as S
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = json.load(open(os.path.join(GOLDEN, "decode_manifest.json")))
+SYNTH = json.load(open(os.path.join(GOLDEN, "synth_manifest.json")))
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = icx.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_decode_golden(ctx, name):
+    exp = MANIFEST[name]
+    data = open(os.path.join(GOLDEN, name), "rb").read()
+    code, w, h, n, pix = ctx.decode(data)
+    assert code == exp["code"], (code, exp["code"])
+    if code == icx.OK:
+        assert (w, h, n) == (exp["w"], exp["h"], exp["ncomp"])
+        assert sha(pix) == exp["sha256"]
+
+
+def test_nanojpeg_state_api(ctx):
+    data = open(os.path.join(GOLDEN, "test.jpg"), "rb").read()
+    ctx.nj_init()
+    assert ctx.nj_decode(data) == 0
+    assert (ctx.nj_get_width(), ctx.nj_get_height(), ctx.nj_is_color()) == (499, 289, 1)
+    assert ctx.nj_get_image_size() == 499 * 289 * 3
+    assert sha(ctx.nj_get_image()) == MANIFEST["test.jpg"]["sha256"]
+    ctx.nj_done()
+    assert ctx.nj_get_image_size() == 0 and ctx.nj_get_image() == b""
+
+
+def test_batch_mixed_goldens(ctx):
+    """One batch holding every golden (sizes, samplings, DRI, corrupt files): per-image status,
+    one bad image never fails the batch."""
+    names = sorted(MANIFEST)
+    jpegs = [open(os.path.join(GOLDEN, n), "rb").read() for n in names]
+    b = icx.Batch(ctx, len(jpegs), 512, 512)
+    res = b.decode_host(jpegs)
+    for name, (code, w, h, n, pix) in zip(names, res):
+        exp = MANIFEST[name]
+        assert code == exp["code"], name
+        if code == icx.OK:
+            assert (w, h, n) == (exp["w"], exp["h"], exp["ncomp"]), name
+            assert sha(pix.tobytes()) == exp["sha256"], name
+    b.close()
+
+
+@pytest.mark.parametrize("key", sorted(SYNTH))
+def test_synth_large(ctx, key):
+    e = SYNTH[key]
+    data = S.synth_jpeg(e["seed"], e["w"], e["h"], e["sampling"], e["quality"], e["restart"])
+    assert sha(data) == e["jpeg_sha256"]
+    code, w, h, n, pix = ctx.decode(data)
+    assert code == e["code"] == 0 and (w, h) == (e["w"], e["h"])
+    assert sha(pix) == e["sha256"]
+
+
+def test_batch_out_of_capacity_is_oom(ctx):
+    small = S.synth_jpeg(1, 64, 64)
+    big = S.synth_jpeg(2, 200, 100)
+    b = icx.Batch(ctx, 2, 128, 128)
+    res = b.decode_host([small, big])
+    assert res[0][0] == icx.OK and res[1][0] == icx.OUT_OF_MEM
+    assert res[0][4].tobytes() == O.decode(small)[4]
+
+
+def test_device_resident_batch_torch(ctx):
+    """The throughput API: device pointers in, device pointers out, per-image statuses."""
+    import torch
+    dev = torch.device("cuda", 0)
+    jpegs = [S.synth_jpeg(100 + i, 96 + 8 * i, 80 - 4 * i, ["420", "444", "422", "gray"][i % 4], 80, i % 2)
+             for i in range(8)]
+    sizes = [len(j) for j in jpegs]
+    offs = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
+    data = torch.from_numpy(np.frombuffer(b"".join(jpegs), np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_sz = torch.from_numpy(np.array(sizes, np.int64)).to(dev)
+    stride = 160 * 96 * 3
+    out = torch.zeros(len(jpegs) * stride, dtype=torch.uint8, device=dev)
+    st = torch.full((len(jpegs),), -1, dtype=torch.int32, device=dev)
+    dims = torch.zeros((len(jpegs), 3), dtype=torch.int32, device=dev)
+    b = icx.Batch(ctx, len(jpegs), 160, 96)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    b.decode_device(len(jpegs), data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), out.data_ptr(), stride,
+                    st.data_ptr(), dims.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    st, dims, out = st.cpu().numpy(), dims.cpu().numpy(), out.cpu().numpy()
+    for i, j in enumerate(jpegs):
+        code, w, h, n, pix = O.decode(j)
+        assert st[i] == code == 0 and tuple(dims[i]) == (w, h, n)
+        assert out[i * stride: i * stride + w * h * n].tobytes() == pix
