@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: batched JPEG decode on MI355X (BASELINE.json metric: megapixels/s JPEG decode of
+synthetic RGB batches at 1/2/4/8 GPUs, plus % of HBM roofline).
+
+A "step" = one call of the device-resident batch decode (icx_jpeg_batch_decode) over this
+rank's shard of images, compressed input already resident in HBM, RGB output written to HBM.
+Workloads:
+  c3   (default) per GPU: 512 synthetic 4096x4096 baseline JPEGs, 4:2:0, q90 -- config C3's
+       per-GPU shard (C3 = 4096 images on 8 GPUs). Weak scaling: every rank decodes its own
+       512 images; the only collective is the final gather of per-image statuses (RCCL).
+  c2   per GPU: 1024 synthetic 1024x1024 4:2:0 q90 JPEGs (config C2).
+Images come from a pool of --pool distinct synthetic images (tools/synth.c, seeded per rank)
+cycled to fill the batch.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run
+(one rank per GPU; RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the env). Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    "c3": dict(n=512, w=4096, h=4096, sampling="420", quality=90,
+               desc="C3 per-GPU shard: 512 x 4096x4096 4:2:0 q90 baseline JPEG (C3 = 4096 images / 8 GPUs)"),
+    "c2": dict(n=1024, w=1024, h=1024, sampling="420", quality=90,
+               desc="C2: 1024 x 1024x1024 4:2:0 q90 baseline JPEG"),
+}
+
+
+def _gen(args):
+    seed, w, h, sampling, quality = args
+    from tools import synthpy
+    return synthpy.synth_jpeg(seed, w, h, sampling, quality, 0)
+
+
+def make_pool(seeds, w, h, sampling, quality, procs):
+    jobs = [(s, w, h, sampling, quality) for s in seeds]
+    if procs <= 1 or len(jobs) == 1:
+        return [_gen(j) for j in jobs]
+    with mp.get_context("fork").Pool(procs) as p:
+        return p.map(_gen, jobs)
+
+
+def _oracle_decode(data):
+    from oracle import pyoracle
+    t = time.perf_counter()
+    code, w, h, n, pix = pyoracle.decode(data)
+    return time.perf_counter() - t, code, hashlib.sha256(pix).hexdigest(), w * h
+
+
+def cpu_baseline(pool, target_s, cores):
+    """Time the oracle (bit-exact CPU restatement of NanoJPEG; the reference is not on the GPU
+    box) on a bounded sample of the same pool: one image per worker process."""
+    probe_t, _, _, px = _oracle_decode(pool[0])
+    per_core = max(1, int(target_s / max(probe_t, 1e-3)))
+    sample = [pool[i % len(pool)] for i in range(per_core * cores)]
+    t0 = time.perf_counter()
+    if cores > 1:
+        with mp.get_context("fork").Pool(cores) as p:
+            res = p.map(_oracle_decode, sample)
+    else:
+        res = [_oracle_decode(s) for s in sample]
+    wall = time.perf_counter() - t0
+    mpx = sum(r[3] for r in res) / 1e6
+    hashes = {}
+    for s, r in zip(sample, res):
+        hashes[hashlib.sha256(s).hexdigest()] = r[2]
+    return {"value": round(mpx / wall, 2), "unit": "megapixels/s", "cores": cores, "kind": "port",
+            "sample": f"{len(sample)} images of the same pool ({len(sample) // cores} per core), oracle/ "
+                      f"NanoJPEG restatement, {wall:.1f} s wall"}, hashes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--images", type=int, default=0, help="override images per GPU")
+    ap.add_argument("--pool", type=int, default=16, help="distinct images per rank")
+    ap.add_argument("--group", type=int, default=0, help="images per workspace group (0=auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0)")
+    ap.add_argument("--cpu-cores", type=int, default=8)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    wl = dict(WORKLOADS[args.workload])
+    n = args.images or wl["n"]
+    W, H = wl["w"], wl["h"]
+
+    # inputs first (CPU only, before any GPU init so fork() is safe)
+    seeds = [1234 + rank * 100000 + i for i in range(min(args.pool, n))]
+    t = time.perf_counter()
+    pool = make_pool(seeds, W, H, wl["sampling"], wl["quality"], procs=min(16, len(seeds)))
+    gen_s = time.perf_counter() - t
+    cpu = None
+    cpu_hashes = {}
+    if rank == 0 and not args.no_cpu:
+        cpu, cpu_hashes = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores)
+
+    import torch
+    import imagecodecs_amd as icx
+
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    jpegs = [pool[i % len(pool)] for i in range(n)]
+    sizes = np.array([len(j) for j in jpegs], np.int64)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum((sizes[:-1] + 15) // 16 * 16)
+    blob = np.zeros(int(offs[-1] + sizes[-1]), np.uint8)
+    for i, j in enumerate(jpegs):
+        blob[offs[i]: offs[i] + sizes[i]] = np.frombuffer(j, np.uint8)
+    d_data = torch.from_numpy(blob).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_sz = torch.from_numpy(sizes).to(dev)
+    stride = W * H * 3
+    d_out = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+    d_st = torch.empty(n, dtype=torch.int32, device=dev)
+    d_dims = torch.empty((n, 3), dtype=torch.int32, device=dev)
+    gathered = [torch.empty_like(d_st) for _ in range(world)] if world > 1 else None
+
+    ctx = icx.Context(local)
+    batch = icx.Batch(ctx, n, W, H, args.group)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out.data_ptr(), stride,
+                            d_st.data_ptr(), d_dims.data_ptr(), stream.cuda_stream)
+        if world > 1:  # final gather of per-image statuses over RCCL/xGMI
+            dist.all_gather(gathered, d_st)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    stages = batch.stage_times()  # HIP events on this stream, last step
+    paths = batch.path_stats()
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # correctness of the measured run: every image OK; pool images bit-exact vs the oracle
+    st = d_st.cpu().numpy()
+    ok_all = bool((st == 0).all())
+    checked = 0
+    mismatches = 0
+    if rank == 0 and cpu_hashes:
+        for i in range(min(len(pool), n)):
+            key = hashlib.sha256(pool[i]).hexdigest()
+            if key in cpu_hashes:
+                got = hashlib.sha256(d_out[i * stride: i * stride + W * H * 3].cpu().numpy().tobytes()).hexdigest()
+                checked += 1
+                mismatches += got != cpu_hashes[key]
+
+    comp_bytes = float(sizes.sum())
+    alg_bytes = comp_bytes + n * W * H * 3.0  # compressed + W*H*3 per image
+    mpx = n * W * H / 1e6
+    ms_step = elapsed / args.steps * 1e3
+    value = world * mpx / (elapsed / args.steps)
+    dom = max((k for k in stages if stages[k] > 0), key=lambda k: stages[k], default=None)
+    roof = None
+    if dom:
+        achieved = alg_bytes / (stages[dom] * 1e-3) / 1e9
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            tj = json.load(open(tpath))
+            if tj.get("workload") == args.workload and tj.get("kernel_stage") == dom:
+                traffic = tj.get("bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": f"{dom} stage", "stage_ms": {k: round(v, 3) for k, v in stages.items()},
+                "pipeline_frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    out = {
+        "metric": "megapixels/s JPEG decode, 4096x4096 RGB batch" if args.workload == "c3"
+        else "megapixels/s JPEG decode, 1024x1024 RGB batch",
+        "value": round(value, 2), "unit": "megapixels/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (tools/synth.c, seeded)",
+        "config": {"workload": wl["desc"], "images_per_gpu": n, "pool": len(pool), "width": W, "height": H,
+                   "bytes_per_pixel_compressed": round(comp_bytes / (n * W * H), 4),
+                   "parallelism": f"dp{world} (images sharded; RCCL gather of statuses)"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
+        "entropy_paths": paths,
+        "gen_seconds": round(gen_s, 1),
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

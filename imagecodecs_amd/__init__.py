@@ -65,6 +65,7 @@ _SIGS = {
     "icx_jpeg_batch_decode": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "icx_jpeg_batch_decode_host": (_i32, [_vp, _i32, _vp, _vp, _vp, _u64, _vp, _vp]),
     "icx_batch_stage_times": (_i32, [_vp, _vp, _vp, _i32]),
+    "icx_batch_path_stats": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "icx_tje_encode_with_func": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "icx_tje_encode_to_file_at_quality": (_i32, [_vp, C.c_char_p, _i32, _i32, _i32, _i32, _vp]),
     "icx_tje_encode_to_file": (_i32, [_vp, C.c_char_p, _i32, _i32, _i32, _vp]),
@@ -73,12 +74,29 @@ _SIGS = {
 WRITE_FUNC = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
 
 
+def _share_hip_runtime_with_torch() -> None:
+    """PyTorch-ROCm ships its own libamdhip64/libhsa-runtime64 and loads them by file name
+    (RPATH $ORIGIN). Preloading exactly those files first makes libicx's DT_NEEDED
+    (libamdhip64.so.7 / libhsa-runtime64.so.1, matched by SONAME) bind to the same runtime,
+    so device pointers, streams and RCCL are shared whatever the import order."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    tlib = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        path = os.path.join(tlib, name)
+        if os.path.exists(path):
+            C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
 def lib():
     """Load libicx.so (raises ICXError if it has not been built)."""
     global _LIB
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise ICXError(f"{LIB_PATH} not built: run `make -C imagecodecs_amd` (hipcc, gfx950)")
+        _share_hip_runtime_with_torch()
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)
@@ -230,6 +248,11 @@ class Batch:
             pix = outs_np[i][: w * h * c].reshape(h, w, c) if status[i] == OK else None
             res.append((int(status[i]), w, h, c, pix))
         return res
+
+    def path_stats(self) -> dict:
+        a, b, c = C.c_int(), C.c_int(), C.c_int()
+        lib().icx_batch_path_stats(self._p, C.byref(a), C.byref(b), C.byref(c))
+        return {"parallel": a.value, "fallback": b.value, "sequential": c.value}
 
     def stage_times(self) -> dict:
         names = (C.c_char_p * 16)()

@@ -159,7 +159,11 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     ws.coef_cap = ws_coef_cap(max_w, max_h);
     ws.plane_cap = ws_plane_cap(max_w, max_h);
     ws.tmp_cap = ws_tmp_cap(max_w, max_h);
-    const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc);
+    ws.ucap = ((int64_t)max_w * max_h + 4095) / 4096 * 4096;  // 1 B/px of entropy data (q90 ~0.4)
+    const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
+    const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
+    const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) +
+                             ws.ucap + tiles_per_slot * 20 + lanes_per_slot * (8 + 20 + 24);
     if (group <= 0) {
         const int64_t budget = (int64_t)8 << 30;  // auto: ~8 GiB of workspace
         group = (int)std::max<int64_t>(1, std::min<int64_t>(max_images, budget / per_slot));
@@ -171,6 +175,19 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)ws.coef_cap * 4 * group), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.planes, (size_t)ws.plane_cap * group), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), nullptr);
+    ws.tiles_cap = tiles_per_slot * group;
+    ws.lanes_cap = lanes_per_slot * group;
+    ICX_HIP(ctx, hipMalloc(&ws.spec, sizeof(SpecImg) * group), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.tilepre, sizeof(int32_t) * (group + 1)), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.wgpre, sizeof(int32_t) * (group + 1)), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.totals, sizeof(int32_t) * 4), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.tiles, sizeof(TileRec) * ws.tiles_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.tile_obase, sizeof(int32_t) * ws.tiles_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.ucap * group), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.X, sizeof(uint64_t) * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.sub, sizeof(SubRec) * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.ent, sizeof(LaneEntry) * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.stats, sizeof(int32_t) * 4), nullptr);
     b->hook = std::make_unique<EventHook>();
     return b.release();
 }
@@ -183,6 +200,10 @@ void icx_batch_destroy(icx_batch* b) {
     (void)hipFree(b->ws.dc);
     (void)hipFree(b->ws.planes);
     (void)hipFree(b->ws.tmp);
+    for (void* p : {(void*)b->ws.spec, (void*)b->ws.tilepre, (void*)b->ws.wgpre, (void*)b->ws.totals,
+                    (void*)b->ws.tiles, (void*)b->ws.tile_obase, (void*)b->ws.U, (void*)b->ws.X,
+                    (void*)b->ws.sub, (void*)b->ws.ent, (void*)b->ws.stats})
+        if (p) (void)hipFree(p);
     if (b->d_hin) (void)hipFree(b->d_hin);
     delete b;
 }
@@ -197,12 +218,23 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     b->hook->reset();
+    ICX_HIP(ctx, hipMemsetAsync(b->ws.stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
     for (int g0 = 0; g0 < n; g0 += b->ws.slots) {
         const int gn = std::min(b->ws.slots, n - g0);
         launch_decode_group(b->ws, gn, d_data, d_off + g0, d_size + g0, d_out + (uint64_t)g0 * out_stride, out_stride,
                             d_status + g0, d_dims + 3 * g0, st, b->hook.get());
     }
     ICX_HIP(ctx, hipGetLastError(), ICX_INTERNAL_ERR);
+    return ICX_OK;
+}
+
+int icx_batch_path_stats(const icx_batch* b, int32_t* parallel, int32_t* fallback, int32_t* sequential) {
+    if (!b) return ICX_INTERNAL_ERR;
+    int32_t h[4] = {0, 0, 0, 0};
+    ICX_HIP(b->ctx, hipMemcpy(h, b->ws.stats, sizeof h, hipMemcpyDeviceToHost), ICX_INTERNAL_ERR);
+    if (parallel) *parallel = h[0];
+    if (fallback) *fallback = h[1];
+    if (sequential) *sequential = h[2];
     return ICX_OK;
 }
 

@@ -38,8 +38,9 @@ __global__ void k_parse(int n, const uint8_t* __restrict__ data, const uint64_t*
 }
 
 // ---------------------------------------------------------------- entropy (sequential)
-// One lane walks one image's entropy-coded segment exactly like njDecodeScan. Used for
-// every image in this first slice; later slices keep it as the verified fallback.
+// One lane walks one image's entropy-coded segment exactly like njDecodeScan. It takes
+// every image the parallel path (icx_spec.hip) does not finish: restart-interval streams,
+// exotic sampling, oversized scans, and chains that failed verification.
 __global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                               Desc* __restrict__ desc, int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                               int64_t coef_cap) {
@@ -285,6 +286,7 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
                        out_stride);
     E(kStParse);
     B(kStEntropy);
+    launch_spec_entropy(ws, n, d_data, d_off, st);
     hipLaunchKernelGGL(k_entropy_seq, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc,
                        ws.coef_cap);
     E(kStEntropy);

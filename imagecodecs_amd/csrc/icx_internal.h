@@ -10,6 +10,28 @@
 
 namespace icx {
 
+// ---- speculative parallel entropy decode (icx_spec.hip) ----
+constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16 B)
+constexpr int kSubBytes = 256;     // unstuffed bytes per decode lane (subsequence)
+constexpr int kLanes = 256;        // lanes per decode workgroup
+constexpr int kSpecMaxBpm = 16;    // blocks per MCU handled by the parallel path
+enum : int32_t { kSpecSyntax = 1, kSpecGiveUp = 2 };
+
+struct SpecImg {
+    int32_t mode;          // 0 not on this path, 1 active, 2 fall back to the sequential kernel
+    int32_t err;           // kSpecSyntax | kSpecGiveUp (atomicOr)
+    int32_t ntiles, tile_base;
+    int32_t nwg, wg_base;  // 256-lane decode groups, flat numbering over the batch group
+    int32_t nsub, pad;
+    int64_t scan_len;      // raw entropy-coded bytes (file end - scan start)
+    int64_t ulen;          // unstuffed data bytes before FF D9 / end of file / bad marker
+    int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)
+    int64_t total_blocks;
+};
+struct TileRec { int32_t kept, end_err; int64_t end_at; };
+struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };
+struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
+
 // Device workspace for one group of images processed together (slot i = image i of the
 // group). Capacities are per slot and cover any sampling NanoJPEG accepts at max_w x max_h.
 struct GroupWs {
@@ -23,7 +45,24 @@ struct GroupWs {
     int32_t* dc = nullptr;   // [slots][coef_cap] absolute quantized DC per block
     uint8_t* planes = nullptr;  // [slots][plane_cap]
     uint8_t* tmp = nullptr;     // [slots][3 comps][2 buffers][tmp_cap]
+    // parallel entropy decode
+    int64_t ucap = 0;           // unstuffed bytes per slot
+    int64_t tiles_cap = 0;      // flat tile records for the whole group
+    int64_t lanes_cap = 0;      // flat lane records for the whole group
+    SpecImg* spec = nullptr;    // [slots]
+    int32_t* tilepre = nullptr; // [slots+1]
+    int32_t* wgpre = nullptr;   // [slots+1]
+    int32_t* totals = nullptr;  // [2]: tiles, lane groups
+    TileRec* tiles = nullptr;
+    int32_t* tile_obase = nullptr;
+    uint8_t* U = nullptr;       // [slots][ucap]
+    uint64_t* X = nullptr;      // [lanes_cap] exit states
+    SubRec* sub = nullptr;      // [lanes_cap]
+    LaneEntry* ent = nullptr;   // [lanes_cap]
+    int32_t* stats = nullptr;   // [4] path counters, accumulated over a batch call
 };
+
+void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st);
 
 int64_t ws_coef_cap(int w, int h);
 int64_t ws_plane_cap(int w, int h);

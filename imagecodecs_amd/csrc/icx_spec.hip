@@ -1,0 +1,576 @@
+// icx_spec.hip -- massively parallel, bit-exact Huffman decode of baseline JPEG on gfx950.
+//
+// NanoJPEG decodes the entropy-coded segment with one serial bit reader
+// (njDecodeScan, jpeg_dec.h:678-718). Here every image is cut into subsequences of
+// kSubBytes unstuffed bytes, one lane each, and decoded speculatively; JPEG's Huffman
+// codes self-synchronise, so a lane that starts at a guessed state soon lands on the
+// true symbol/block boundaries. Correctness never depends on that luck: every lane's
+// exit state is re-derived from its predecessor's and compared, and an image with an
+// unresolved disagreement falls back to the sequential kernel (k_entropy_seq).
+//
+//   k_spec_plan     which images take this path; flat tile / lane-group numbering
+//   k_ustf_count    NanoJPEG's marker rules (jpeg_dec.h:447-482) per 4 KiB tile:
+//   k_ustf_scan       FF00/FFFF -> FF, FFDn kept, FFD9 / bad marker ends the data;
+//   k_ustf_write      writes the unstuffed stream U (reads past its end give 0xFF)
+//   k_spec_guess    lane j decodes subsequence j from a guessed state -> exit state X[j]
+//   k_spec_count    lane j re-decodes from X[j-1]: blocks started, DC-diff sums, and
+//                   whether its exit state reproduces X[j]
+//   k_spec_scan     per image: block index + DC predictor at every lane entry;
+//                   picks the fallback for images whose chain does not verify
+//   k_spec_write    lane j decodes the blocks that START in its range (whole blocks),
+//                   writes quantized coefficients; true-path errors flag the image
+// A lane's state is (bit position in U, block-in-MCU b, coefficient cursor z).
+#include <hip/hip_runtime.h>
+
+#include "icx_internal.h"
+
+namespace icx {
+
+__device__ __forceinline__ uint64_t pack_state(int64_t pos, int b, int z) {
+    return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)z;
+}
+__device__ __forceinline__ int64_t st_pos(uint64_t s) { return (int64_t)(s >> 16); }
+__device__ __forceinline__ int st_b(uint64_t s) { return (int)((s >> 8) & 0xFF); }
+__device__ __forceinline__ int st_z(uint64_t s) { return (int)(s & 0xFF); }
+
+// ------------------------------------------------------------------------------- plan
+__device__ int block_exclusive_scan(int v, int* sh) {  // blockDim.x <= 1024, returns exclusive
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
+        const int x = t >= o ? sh[t - o] : 0;
+        __syncthreads();
+        sh[t] += x;
+        __syncthreads();
+    }
+    const int incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                    int32_t* __restrict__ tilepre, int32_t* __restrict__ wgpre,
+                                                    int32_t* __restrict__ totals, int64_t ucap) {
+    __shared__ int sh[1024];
+    int carry_t = 0, carry_w = 0;
+    for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+        const int i = i0 + threadIdx.x;
+        int nt = 0, nw = 0;
+        if (i < n) {
+            const Desc& d = desc[i];
+            SpecImg& s = spec[i];
+            s.mode = 0;
+            s.err = 0;
+            const int64_t scan_len = d.size - d.scan_off;
+            const bool ok = d.status == kPending && d.restart == 0 && d.nc >= 1 && d.bpm <= kSpecMaxBpm &&
+                            scan_len > 0 && scan_len <= ucap;
+            if (ok) {
+                s.mode = 1;
+                s.scan_len = scan_len;
+                s.total_blocks = (int64_t)d.mbw * d.mbh * d.bpm;
+                nt = (int)((scan_len + kTileBytes - 1) / kTileBytes);
+                const int64_t nsub = (scan_len + kSubBytes - 1) / kSubBytes;
+                nw = (int)((nsub + kLanes - 1) / kLanes);
+            }
+            s.ntiles = nt;
+            s.nwg = nw;
+        }
+        const int et = block_exclusive_scan(nt, sh);
+        const int ew = block_exclusive_scan(nw, sh);
+        if (i < n) {
+            tilepre[i] = carry_t + et;
+            wgpre[i] = carry_w + ew;
+            spec[i].tile_base = carry_t + et;
+            spec[i].wg_base = carry_w + ew;
+        }
+        __shared__ int last_t, last_w;
+        if (threadIdx.x == blockDim.x - 1) { last_t = et + nt; last_w = ew + nw; }
+        __syncthreads();
+        carry_t += last_t;
+        carry_w += last_w;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        tilepre[n] = carry_t;
+        wgpre[n] = carry_w;
+        totals[0] = carry_t;
+        totals[1] = carry_w;
+    }
+}
+
+// image owning flat item x, given exclusive prefix pre[0..n] (pre[n] = total)
+__device__ __forceinline__ int find_image(const int32_t* pre, int n, int x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------- unstuff
+// Per-lane marker automaton over kChunk raw bytes. Returns kept-byte count before the
+// first end event; *end_at = raw offset of the FF that ends the data (or -1), *end_err =
+// whether that end is a syntax error (bad marker / FF at EOF) rather than FF D9.
+constexpr int kChunk = kTileBytes / 256;
+
+__device__ __forceinline__ bool carry_after_ff(const uint8_t* R, int64_t a, int32_t* giveup) {
+    int k = 0;
+    while (a - 1 - k >= 0 && R[a - 1 - k] == 0xFF) {
+        if (++k > 4096) { *giveup = 1; break; }  // pathological FF run: image goes sequential
+    }
+    return k & 1;
+}
+
+template <bool WRITE>
+__device__ __forceinline__ int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, int* end_err,
+                                          uint8_t* out, int32_t* giveup) {
+    *end_at = -1;
+    *end_err = 0;
+    if (a >= L) return 0;
+    bool after_ff = carry_after_ff(R, a, giveup);
+    int kept = 0;
+    const int64_t b = a + kChunk < L ? a + kChunk : L;
+    for (int64_t p = a; p < b; ++p) {
+        if (after_ff) { after_ff = false; continue; }  // marker byte, consumed with its FF
+        const uint8_t c = R[p];
+        if (c != 0xFF) {
+            if (WRITE) out[kept] = c;
+            ++kept;
+            continue;
+        }
+        if (p + 1 >= L) { *end_at = p; *end_err = 1; break; }  // FF ends the file (:477-478)
+        const uint8_t m = R[p + 1];
+        if (m == 0x00 || m == 0xFF) {  // :465-467
+            if (WRITE) out[kept] = 0xFF;
+            ++kept;
+            after_ff = true;
+        } else if ((m & 0xF8) == 0xD0) {  // RSTn: both bytes enter the bit buffer (:472-475)
+            if (WRITE) { out[kept] = 0xFF; out[kept + 1] = m; }
+            kept += 2;
+            after_ff = true;
+        } else {  // D9 ends the data (:468); anything else is a syntax error (:470-471)
+            *end_at = p;
+            *end_err = m != 0xD9;
+            break;
+        }
+    }
+    return kept;
+}
+
+__global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __restrict__ data,
+                                                    const uint64_t* __restrict__ off, const Desc* __restrict__ desc,
+                                                    SpecImg* __restrict__ spec, const int32_t* __restrict__ tilepre,
+                                                    const int32_t* __restrict__ totals, TileRec* __restrict__ tiles) {
+    __shared__ int sh[256];
+    __shared__ int64_t s_end;
+    __shared__ int s_err;
+    const int total = totals[0];
+    for (int t = blockIdx.x; t < total; t += gridDim.x) {
+        const int i = find_image(tilepre, n, t);
+        const Desc& d = desc[i];
+        const uint8_t* R = data + off[i] + d.scan_off;
+        const int64_t L = spec[i].scan_len;
+        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)threadIdx.x * kChunk;
+        int64_t end_at;
+        int end_err;
+        int32_t giveup = 0;
+        const int kept = ustf_chunk<false>(R, L, a, &end_at, &end_err, nullptr, &giveup);
+        if (giveup) atomicOr(&spec[i].err, kSpecGiveUp);
+        if (threadIdx.x == 0) { s_end = INT64_MAX; s_err = 0; }
+        __syncthreads();
+        if (end_at >= 0) atomicMin((unsigned long long*)&s_end, (unsigned long long)end_at);
+        __syncthreads();
+        const int64_t tend = s_end;
+        if (end_at >= 0 && end_at == tend) s_err = end_err;  // the unique lane owning that FF
+        // kept bytes before the tile's first end event
+        const bool before = end_at >= 0 ? end_at <= tend : a < tend;
+        const int ex = block_exclusive_scan(before ? kept : 0, sh);
+        if (threadIdx.x == 255) {
+            TileRec r;
+            r.kept = ex + (before ? kept : 0);
+            r.end_at = tend == INT64_MAX ? -1 : tend;
+            r.end_err = s_err;
+            tiles[t] = r;
+        }
+        __syncthreads();
+    }
+}
+
+// Per image: exclusive prefix of kept bytes over tiles, data length, error position.
+__global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ spec, TileRec* __restrict__ tiles,
+                                                   int32_t* __restrict__ tile_obase) {
+    __shared__ int sh[256];
+    __shared__ int s_first_end;
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    SpecImg& s = spec[i];
+    if (s.mode != 1) return;
+    if (threadIdx.x == 0) s_first_end = INT32_MAX;
+    __syncthreads();
+    for (int t = threadIdx.x; t < s.ntiles; t += blockDim.x)
+        if (tiles[s.tile_base + t].end_at >= 0) atomicMin(&s_first_end, t);
+    __syncthreads();
+    const int fe = s_first_end;
+    int64_t carry = 0;
+    for (int t0 = 0; t0 < s.ntiles; t0 += blockDim.x) {
+        const int t = t0 + threadIdx.x;
+        const int k = (t < s.ntiles && t <= fe) ? tiles[s.tile_base + t].kept : 0;
+        const int ex = block_exclusive_scan(k, sh);
+        if (t < s.ntiles) tile_obase[s.tile_base + t] = (int32_t)(carry + ex);
+        __shared__ int s_sum;
+        if (threadIdx.x == blockDim.x - 1) s_sum = ex + k;
+        __syncthreads();
+        carry += s_sum;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        s.ulen = carry;
+        s.errpos = (fe != INT32_MAX && tiles[s.tile_base + fe].end_err) ? carry : INT64_MAX;
+        const int64_t nsub = carry > 0 ? (carry + kSubBytes - 1) / kSubBytes : 1;
+        s.nsub = (int32_t)nsub;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __restrict__ data,
+                                                    const uint64_t* __restrict__ off, const Desc* __restrict__ desc,
+                                                    const SpecImg* __restrict__ spec, const int32_t* __restrict__ tilepre,
+                                                    const int32_t* __restrict__ totals, const TileRec* __restrict__ tiles,
+                                                    const int32_t* __restrict__ tile_obase, uint8_t* __restrict__ U,
+                                                    int64_t ucap) {
+    __shared__ int sh[256];
+    const int total = totals[0];
+    for (int t = blockIdx.x; t < total; t += gridDim.x) {
+        const int i = find_image(tilepre, n, t);
+        const SpecImg& s = spec[i];
+        const int64_t tend = tiles[t].end_at;
+        const int64_t obase = tile_obase[t];  // == ulen for every tile past the first end event
+        const Desc& d = desc[i];
+        const uint8_t* R = data + off[i] + d.scan_off;
+        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)threadIdx.x * kChunk;
+        int64_t end_at;
+        int end_err;
+        int32_t giveup = 0;
+        const bool live = obase < s.ulen;
+        const int kept = live ? ustf_chunk<false>(R, s.scan_len, a, &end_at, &end_err, nullptr, &giveup) : 0;
+        const bool before = live && (end_at >= 0 ? (tend < 0 || end_at <= tend) : (tend < 0 || a < tend));
+        const int ex = block_exclusive_scan(before ? kept : 0, sh);
+        if (before && kept) {
+            const int64_t o = obase + ex;
+            if (o + kept <= s.ulen)
+                ustf_chunk<true>(R, s.scan_len, a, &end_at, &end_err, U + (int64_t)i * ucap + o, &giveup);
+        }
+        __syncthreads();
+    }
+}
+
+// -------------------------------------------------------------------- entropy lanes
+struct LdsTables {
+    Huff huff[4];
+    int8_t comp_of[kSpecMaxBpm];
+    int8_t dc_of[3], ac_of[3];
+};
+
+__device__ __forceinline__ void load_tables(LdsTables& T, const Desc& d) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&d.huff[0]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&T.huff[0]);
+    for (int k = threadIdx.x; k < (int)(sizeof(Huff) * 4 / 4); k += blockDim.x) dst[k] = src[k];
+    if (threadIdx.x < kSpecMaxBpm) {
+        int sbx, sby;
+        T.comp_of[threadIdx.x] = threadIdx.x < d.bpm ? (int8_t)mcu_block_comp(d, threadIdx.x, sbx, sby) : 0;
+    }
+    if (threadIdx.x < 3) {
+        T.dc_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].dc_tab;
+        T.ac_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].ac_tab;
+    }
+}
+
+// MSB-first reader over U; bytes at or past ulen read as 0xFF (jpeg_dec.h:451-455).
+struct Reader {
+    const uint8_t* u;
+    int64_t ulen;
+    uint64_t buf;
+    int nb;
+    int64_t widx;
+    __device__ __forceinline__ uint32_t word(int64_t w) const {
+        const int64_t b = w * 4;
+        if (b + 4 <= ulen) return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(u + b));
+        uint32_t v = 0;
+        for (int i = 0; i < 4; ++i) v = (v << 8) | (b + i < ulen ? u[b + i] : 0xFFu);
+        return v;
+    }
+    __device__ __forceinline__ void refill() {
+        if (nb <= 32) {
+            buf |= (uint64_t)word(widx++) << (32 - nb);
+            nb += 32;
+        }
+    }
+    __device__ __forceinline__ void init(const uint8_t* u_, int64_t ulen_, int64_t bitpos) {
+        u = u_;
+        ulen = ulen_;
+        widx = bitpos >> 5;
+        nb = 0;
+        buf = 0;
+        refill();
+        refill();
+        const int skip = (int)(bitpos & 31);
+        buf <<= skip;
+        nb -= skip;
+    }
+    __device__ __forceinline__ int64_t pos() const { return widx * 32 - nb; }
+    __device__ __forceinline__ uint32_t peek16() const { return (uint32_t)(buf >> 48); }
+    __device__ __forceinline__ uint32_t take(int n) {
+        const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
+        buf <<= n;
+        nb -= n;
+        return v;
+    }
+};
+
+enum : int { kUnitOk = 0, kUnitErr = 1 };
+
+// One Huffman code + magnitude bits in the state (b, z); z == 0 expects the DC code.
+// On return: *coef = coefficient index written (0 = DC, 1..63 AC, -1 none), *val = value.
+// Errors (jpeg_dec.h:646, 667, 669) end the block deterministically so speculative lanes
+// keep going; on the true path any error makes the image NJ_SYNTAX_ERROR.
+__device__ __forceinline__ int decode_unit(Reader& r, const LdsTables& T, int bpm, int& b, int& z, int& coef,
+                                           int32_t& val) {
+    const int ci = T.comp_of[b];
+    const Huff& H = T.huff[z == 0 ? T.dc_of[ci] : T.ac_of[ci]];
+    r.refill();
+    int sym = 0;
+    const int len = huff_lookup(H, r.peek16(), sym);
+    coef = -1;
+    val = 0;
+    auto end_block = [&]() { z = 0; b = (b + 1 == bpm) ? 0 : b + 1; };
+    if (!len) { r.take(1); end_block(); return kUnitErr; }
+    r.take(len);
+    const int nbx = sym & 15;
+    const int32_t v = nbx ? extend((int32_t)r.take(nbx), nbx) : 0;
+    if (z == 0) { z = 1; coef = 0; val = v; return kUnitOk; }
+    if (sym == 0) { end_block(); return kUnitOk; }  // EOB
+    if (!nbx && sym != 0xF0) { end_block(); return kUnitErr; }
+    const int c = z + (sym >> 4);
+    if (c > 63) { end_block(); return kUnitErr; }
+    coef = c;
+    val = v;
+    if (c == 63) end_block(); else z = c + 1;
+    return kUnitOk;
+}
+
+__device__ __forceinline__ int wg_image_setup(const int32_t* wgpre, int n, int wg, int& cur, LdsTables& T,
+                                              const Desc* desc) {
+    const int i = find_image(wgpre, n, wg);
+    if (i != cur) {
+        __syncthreads();
+        load_tables(T, desc[i]);
+        __syncthreads();
+        cur = i;
+    }
+    return i;
+}
+
+__global__ __launch_bounds__(256) void k_spec_guess(int n, const Desc* __restrict__ desc,
+                                                    const SpecImg* __restrict__ spec, const int32_t* __restrict__ wgpre,
+                                                    const int32_t* __restrict__ totals, const uint8_t* __restrict__ U,
+                                                    int64_t ucap, uint64_t* __restrict__ X) {
+    __shared__ LdsTables T;
+    int cur = -1;
+    const int total = totals[1];
+    for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
+        const SpecImg& s = spec[i];
+        const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
+        if (j >= s.nsub - 1) continue;  // the last lane's exit is never needed
+        const int bpm = desc[i].bpm;
+        Reader r;
+        r.init(U + (int64_t)i * ucap, s.ulen, j * kSubBytes * 8);
+        int b = 0, z = 0, coef;
+        int32_t val;
+        const int64_t end = (j + 1) * kSubBytes * 8;
+        while (r.pos() < end) decode_unit(r, T, bpm, b, z, coef, val);
+        X[(int64_t)s.wg_base * kLanes + j] = pack_state(r.pos(), b, z);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_spec_count(int n, const Desc* __restrict__ desc,
+                                                    const SpecImg* __restrict__ spec, const int32_t* __restrict__ wgpre,
+                                                    const int32_t* __restrict__ totals, const uint8_t* __restrict__ U,
+                                                    int64_t ucap, const uint64_t* __restrict__ X,
+                                                    SubRec* __restrict__ sub) {
+    __shared__ LdsTables T;
+    int cur = -1;
+    const int total = totals[1];
+    for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
+        const SpecImg& s = spec[i];
+        const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
+        if (j >= s.nsub - 1) continue;
+        const int bpm = desc[i].bpm;
+        const int64_t base = (int64_t)s.wg_base * kLanes;
+        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[base + j - 1];
+        Reader r;
+        r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
+        int b = st_b(entry), z = st_z(entry), coef;
+        int32_t val, cnt = 0, ds[3] = {0, 0, 0};
+        const int64_t end = (j + 1) * kSubBytes * 8;
+        while (r.pos() < end) {
+            const int ci = T.comp_of[b];
+            const bool dc = z == 0;
+            decode_unit(r, T, bpm, b, z, coef, val);
+            if (dc) {
+                ++cnt;
+                ds[ci] = wadd(ds[ci], val);
+            }
+        }
+        SubRec rec;
+        rec.cnt = cnt;
+        rec.ds0 = ds[0];
+        rec.ds1 = ds[1];
+        rec.ds2 = ds[2];
+        rec.mism = pack_state(r.pos(), b, z) != X[base + j];
+        sub[base + j] = rec;
+    }
+}
+
+// Per image: block index and DC predictors at every lane entry; chain verification.
+__global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ spec, SubRec* __restrict__ sub,
+                                                   LaneEntry* __restrict__ ent) {
+    __shared__ int sh[256];
+    __shared__ int s_cnt, s_d0, s_d1, s_d2;
+    __shared__ int64_t s_bad;
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    SpecImg& s = spec[i];
+    if (s.mode != 1) return;
+    if (threadIdx.x == 0) s_bad = INT64_MAX;
+    const int64_t base = (int64_t)s.wg_base * kLanes;
+    int64_t G = 0;
+    int32_t P0 = 0, P1 = 0, P2 = 0;
+    for (int64_t j0 = 0; j0 < s.nsub; j0 += blockDim.x) {
+        const int64_t j = j0 + threadIdx.x;
+        const bool live = j < s.nsub - 1;
+        const SubRec rec = live ? sub[base + j] : SubRec{0, 0, 0, 0, 0};
+        // int32 prefix sums (wrap-around adds commute, matching dcpred += diff)
+        const int e = block_exclusive_scan(rec.cnt, sh);
+        const int e0 = block_exclusive_scan(rec.ds0, sh);
+        const int e1 = block_exclusive_scan(rec.ds1, sh);
+        const int e2 = block_exclusive_scan(rec.ds2, sh);
+        if (j < s.nsub) {
+            LaneEntry le;
+            le.G = G + e;
+            le.p0 = wadd(P0, e0);
+            le.p1 = wadd(P1, e1);
+            le.p2 = wadd(P2, e2);
+            ent[base + j] = le;
+            // a disagreement only matters if the true decode still has blocks to place after it
+            if (live && rec.mism && le.G + rec.cnt < s.total_blocks)
+                atomicMin((unsigned long long*)&s_bad, (unsigned long long)j);
+        }
+        if (threadIdx.x == blockDim.x - 1) {
+            s_cnt = e + rec.cnt;
+            s_d0 = wadd(e0, rec.ds0);
+            s_d1 = wadd(e1, rec.ds1);
+            s_d2 = wadd(e2, rec.ds2);
+        }
+        __syncthreads();
+        G += s_cnt;
+        P0 = wadd(P0, s_d0);
+        P1 = wadd(P1, s_d1);
+        P2 = wadd(P2, s_d2);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && (s_bad != INT64_MAX || (s.err & kSpecGiveUp))) s.mode = 2;  // -> sequential
+}
+
+__global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                    const int32_t* __restrict__ wgpre, const int32_t* __restrict__ totals,
+                                                    const uint8_t* __restrict__ U, int64_t ucap,
+                                                    const uint64_t* __restrict__ X, const LaneEntry* __restrict__ ent,
+                                                    int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
+                                                    int64_t coef_cap) {
+    __shared__ LdsTables T;
+    __shared__ int32_t blk[kLanes][33];  // one 64 x int16 block per lane (+1 word: no bank conflicts)
+    int cur = -1;
+    const int total = totals[1];
+    for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
+        SpecImg& s = spec[i];
+        if (s.mode != 1) continue;
+        const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
+        if (j >= s.nsub) continue;
+        const int bpm = desc[i].bpm;
+        const int64_t base = (int64_t)s.wg_base * kLanes;
+        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[base + j - 1];
+        const bool last = j == s.nsub - 1;
+        const int64_t limit = last ? INT64_MAX : st_pos(X[base + j]);
+        const LaneEntry le = ent[base + j];
+        Reader r;
+        r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
+        int b = st_b(entry), z = st_z(entry), coef;
+        int32_t val;
+        // the block in progress at entry belongs to the previous lane
+        while (z != 0) decode_unit(r, T, bpm, b, z, coef, val);
+        int32_t pred[3] = {le.p0, le.p1, le.p2};
+        const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
+        int16_t* A = ac + (int64_t)i * coef_cap * 64;
+        int32_t* D = dcv + (int64_t)i * coef_cap;
+        int16_t* mine = reinterpret_cast<int16_t*>(&blk[threadIdx.x][0]);
+        bool bad = false;
+        for (int64_t bi = le.G; bi < s.total_blocks && r.pos() < limit && !bad; ++bi) {
+            const int ci = T.comp_of[b];
+            for (int k = 0; k < 32; ++k) blk[threadIdx.x][k] = 0;
+            do {
+                // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
+                if (r.pos() + 16 > errbits) bad = true;
+                const int rc = decode_unit(r, T, bpm, b, z, coef, val);
+                if (rc != kUnitOk || r.pos() > errbits) bad = true;
+                if (coef == 0) {
+                    pred[ci] = wadd(pred[ci], val);
+                    D[bi] = pred[ci];
+                } else if (coef > 0) {
+                    mine[nat_of_zig(coef)] = (int16_t)val;
+                }
+            } while (z != 0 && !bad);
+            int4* dst = reinterpret_cast<int4*>(A + bi * 64);
+            const int32_t* src = &blk[threadIdx.x][0];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dst[q] = make_int4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
+        }
+        if (bad) atomicOr(&s.err, kSpecSyntax);
+    }
+}
+
+__global__ void k_spec_finish(int n, Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
+                              int32_t* __restrict__ stats) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SpecImg& s = spec[i];
+    if (s.mode == 1) desc[i].status = (s.err & kSpecSyntax) ? kSyntaxError : kOk;
+    // path statistics: [0] parallel path, [1] parallel -> sequential fallback, [2] sequential only
+    if (s.mode == 1) atomicAdd(&stats[0], 1);
+    else if (s.mode == 2) atomicAdd(&stats[1], 1);
+    else if (desc[i].status == kPending) atomicAdd(&stats[2], 1);
+}
+
+void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st) {
+    const int g = 2048;  // grid-stride launches: >> 256 CUs
+    hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.totals,
+                       ws.ucap);
+    hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
+                       ws.totals, ws.tiles);
+    hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase);
+    hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
+                       ws.totals, ws.tiles, ws.tile_obase, ws.U, ws.ucap);
+    hipLaunchKernelGGL(k_spec_guess, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
+                       ws.ucap, ws.X);
+    hipLaunchKernelGGL(k_spec_count, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
+                       ws.ucap, ws.X, ws.sub);
+    hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
+    hipLaunchKernelGGL(k_spec_write, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
+                       ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);
+    hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
+}
+
+}  // namespace icx

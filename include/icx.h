@@ -102,6 +102,12 @@ int icx_jpeg_batch_decode_host(icx_batch* b, int n, const uint8_t* const* jpegs,
  * stream the kernels ran on. Fills up to `cap` entries; returns the number of stages. */
 int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int cap);
 
+/* Which entropy path the images of the most recent batch call took: the parallel
+ * self-synchronising decoder, the parallel decoder falling back to the sequential one
+ * (unverified chain), or the sequential decoder only (restart intervals, exotic sampling).
+ * Synchronizes with the device. */
+int icx_batch_path_stats(const icx_batch* b, int32_t* parallel, int32_t* fallback, int32_t* sequential);
+
 /* ---- encode (tiny_jpeg, jpeg_enc.h:114-160) --------------------------------------- */
 typedef void icx_write_func(void* context, void* data, int size); /* = tje_write_func */
 

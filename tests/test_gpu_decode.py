@@ -58,6 +58,8 @@ def test_batch_mixed_goldens(ctx):
     jpegs = [open(os.path.join(GOLDEN, n), "rb").read() for n in names]
     b = icx.Batch(ctx, len(jpegs), 512, 512)
     res = b.decode_host(jpegs)
+    stats = b.path_stats()
+    assert stats["parallel"] >= 80, stats  # every non-DRI stream takes the parallel path
     for name, (code, w, h, n, pix) in zip(names, res):
         exp = MANIFEST[name]
         assert code == exp["code"], name
@@ -111,3 +113,32 @@ def test_device_resident_batch_torch(ctx):
         code, w, h, n, pix = O.decode(j)
         assert st[i] == code == 0 and tuple(dims[i]) == (w, h, n)
         assert out[i * stride: i * stride + w * h * n].tobytes() == pix
+
+
+@pytest.mark.parametrize("sampling", ["420", "444", "422", "gray", "440", "411"])
+def test_parallel_path_large_bit_exact(ctx, sampling):
+    """Several large images in one batch: all must take the parallel entropy path (no
+    fallback) and match the oracle byte for byte."""
+    jpegs = [S.synth_jpeg(300 + k, 777 + 64 * k, 555 + 32 * k, sampling, 60 + 15 * k) for k in range(3)]
+    b = icx.Batch(ctx, len(jpegs), 1024, 1024)
+    res = b.decode_host(jpegs)
+    stats = b.path_stats()
+    assert stats == {"parallel": 3, "fallback": 0, "sequential": 0}, stats
+    for j, (code, w, h, n, pix) in zip(jpegs, res):
+        ocode, ow, oh, on, opix = O.decode(j)
+        assert code == ocode == 0 and (w, h, n) == (ow, oh, on)
+        assert pix.tobytes() == opix
+
+
+def test_parallel_path_coefficients_match_trace(ctx):
+    """Stage-level parity: error-free random streams across sizes/qualities."""
+    rng = np.random.default_rng(5)
+    jpegs = []
+    for k in range(24):
+        w, h = int(rng.integers(16, 700)), int(rng.integers(16, 700))
+        jpegs.append(S.synth_jpeg(900 + k, w, h, ["420", "444", "422", "gray"][k % 4], int(rng.integers(5, 100))))
+    b = icx.Batch(ctx, len(jpegs), 700, 700)
+    res = b.decode_host(jpegs)
+    assert b.path_stats()["fallback"] == 0
+    for j, (code, w, h, n, pix) in zip(jpegs, res):
+        assert code == 0 and pix.tobytes() == O.decode(j)[4]
