@@ -163,7 +163,8 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
     const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) +
-                             ws.ucap + tiles_per_slot * 20 + lanes_per_slot * (8 + 20 + 24);
+                             ws.ucap + tiles_per_slot * 20 +
+                             lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
     if (group <= 0) {
         const int64_t budget = (int64_t)8 << 30;  // auto: ~8 GiB of workspace
         group = (int)std::max<int64_t>(1, std::min<int64_t>(max_images, budget / per_slot));
@@ -188,6 +189,11 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     ICX_HIP(ctx, hipMalloc(&ws.sub, sizeof(SubRec) * ws.lanes_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.ent, sizeof(LaneEntry) * ws.lanes_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.stats, sizeof(int32_t) * 4), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.Y, sizeof(uint64_t) * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.rec, sizeof(RecState) * kRec * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.nrec, sizeof(int32_t) * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.guess_cnt, sizeof(int32_t) * 4 * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.repair, sizeof(int32_t) * kMaxRepair * group), nullptr);
     b->hook = std::make_unique<EventHook>();
     return b.release();
 }
@@ -202,7 +208,8 @@ void icx_batch_destroy(icx_batch* b) {
     (void)hipFree(b->ws.tmp);
     for (void* p : {(void*)b->ws.spec, (void*)b->ws.tilepre, (void*)b->ws.wgpre, (void*)b->ws.totals,
                     (void*)b->ws.tiles, (void*)b->ws.tile_obase, (void*)b->ws.U, (void*)b->ws.X,
-                    (void*)b->ws.sub, (void*)b->ws.ent, (void*)b->ws.stats})
+                    (void*)b->ws.sub, (void*)b->ws.ent, (void*)b->ws.stats, (void*)b->ws.Y,
+                    (void*)b->ws.rec, (void*)b->ws.nrec, (void*)b->ws.guess_cnt, (void*)b->ws.repair})
         if (p) (void)hipFree(p);
     if (b->d_hin) (void)hipFree(b->d_hin);
     delete b;

@@ -62,7 +62,7 @@ __global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uin
             const int ci = mcu_block_comp(d, r, sbx, sby);
             const Comp& c = d.c[ci];
             int16_t* row = A + blk * 64;
-            for (int k = 0; k < 64; k += 8) *reinterpret_cast<int4*>(row + k) = make_int4(0, 0, 0, 0);
+            __builtin_memset(row, 0, 64 * sizeof(int16_t));
             // DC (jpeg_dec.h:662-663)
             int sym = 0;
             int len = huff_lookup(d.huff[c.dc_tab], rb_peek(b, 16), sym);
@@ -142,8 +142,8 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
         if (live) {
             mcu = n / d.bpm;
             ci = mcu_block_comp(d, (int)(n - mcu * d.bpm), sbx, sby);
-            const int4 raw = *reinterpret_cast<const int4*>(A + n * 64 + r * 8);
-            const int16_t* s = reinterpret_cast<const int16_t*>(&raw);
+            int16_t s[8];
+            __builtin_memcpy(s, A + n * 64 + r * 8, sizeof s);
             int32_t v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = wmul(s[j], qn[ci][r * 8 + j]);
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
             const int64_t mby = mcu / d.mbw, mbx = mcu - mby * d.mbw;
             const int64_t y = (mby * c.vs + sby) * 8 + r, x = (mbx * c.hs + sbx) * 8;
             uint8_t* dst = P + comp_plane_off(d, ci) + y * c.stride + x;
-            *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(&pix[lb][r][0]);
+            __builtin_memcpy(dst, &pix[lb][r][0], 8);
         }
         __syncthreads();
     }

@@ -12,7 +12,9 @@ namespace icx {
 
 // ---- speculative parallel entropy decode (icx_spec.hip) ----
 constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16 B)
-constexpr int kSubBytes = 256;     // unstuffed bytes per decode lane (subsequence)
+constexpr int kSubBytes = 2048;    // unstuffed bytes per decode lane (subsequence)
+constexpr int kRec = 16;           // block-start states a guess lane records for resync
+constexpr int kMaxRepair = 1024;   // unsynchronised lanes repaired per image before giving up
 constexpr int kLanes = 256;        // lanes per decode workgroup
 constexpr int kSpecMaxBpm = 16;    // blocks per MCU handled by the parallel path
 enum : int32_t { kSpecSyntax = 1, kSpecGiveUp = 2 };
@@ -22,7 +24,7 @@ struct SpecImg {
     int32_t err;           // kSpecSyntax | kSpecGiveUp (atomicOr)
     int32_t ntiles, tile_base;
     int32_t nwg, wg_base;  // 256-lane decode groups, flat numbering over the batch group
-    int32_t nsub, pad;
+    int32_t nsub, nrepair;   // lanes; unsynchronised lanes queued for repair
     int64_t scan_len;      // raw entropy-coded bytes (file end - scan start)
     int64_t ulen;          // unstuffed data bytes before FF D9 / end of file / bad marker
     int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)
@@ -30,6 +32,9 @@ struct SpecImg {
 };
 struct TileRec { int32_t kept, end_err; int64_t end_at; };
 struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };
+// A block-start state seen by a guess lane: bit offset from the lane start, block-in-MCU,
+// DC codes decoded before it, and the per-component DC-diff sums before it.
+struct RecState { uint32_t rel; int32_t b, cnt; int32_t ds[3]; };
 struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
 
 // Device workspace for one group of images processed together (slot i = image i of the
@@ -56,7 +61,12 @@ struct GroupWs {
     TileRec* tiles = nullptr;
     int32_t* tile_obase = nullptr;
     uint8_t* U = nullptr;       // [slots][ucap]
-    uint64_t* X = nullptr;      // [lanes_cap] exit states
+    uint64_t* X = nullptr;      // [lanes_cap] exit states (guess pass; repaired in place)
+    uint64_t* Y = nullptr;      // [lanes_cap] exit states re-derived by the count pass
+    RecState* rec = nullptr;    // [lanes_cap][kRec]
+    int32_t* nrec = nullptr;    // [lanes_cap]
+    int32_t* guess_cnt = nullptr;  // [lanes_cap][4]: DC codes and DC sums over the whole guess lane
+    int32_t* repair = nullptr;  // [slots][kMaxRepair] lanes whose chain needs a serial repair
     SubRec* sub = nullptr;      // [lanes_cap]
     LaneEntry* ent = nullptr;   // [lanes_cap]
     int32_t* stats = nullptr;   // [4] path counters, accumulated over a batch call

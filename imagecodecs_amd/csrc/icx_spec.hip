@@ -22,16 +22,9 @@
 // A lane's state is (bit position in U, block-in-MCU b, coefficient cursor z).
 #include <hip/hip_runtime.h>
 
-#include "icx_internal.h"
+#include "icx_spec_core.h"
 
 namespace icx {
-
-__device__ __forceinline__ uint64_t pack_state(int64_t pos, int b, int z) {
-    return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)z;
-}
-__device__ __forceinline__ int64_t st_pos(uint64_t s) { return (int64_t)(s >> 16); }
-__device__ __forceinline__ int st_b(uint64_t s) { return (int)((s >> 8) & 0xFF); }
-__device__ __forceinline__ int st_z(uint64_t s) { return (int)(s & 0xFF); }
 
 // ------------------------------------------------------------------------------- plan
 __device__ int block_exclusive_scan(int v, int* sh) {  // blockDim.x <= 1024, returns exclusive
@@ -62,6 +55,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ de
             SpecImg& s = spec[i];
             s.mode = 0;
             s.err = 0;
+            s.nrepair = 0;
             const int64_t scan_len = d.size - d.scan_off;
             const bool ok = d.status == kPending && d.restart == 0 && d.nc >= 1 && d.bpm <= kSpecMaxBpm &&
                             scan_len > 0 && scan_len <= ucap;
@@ -110,55 +104,6 @@ __device__ __forceinline__ int find_image(const int32_t* pre, int n, int x) {
 }
 
 // ---------------------------------------------------------------------------- unstuff
-// Per-lane marker automaton over kChunk raw bytes. Returns kept-byte count before the
-// first end event; *end_at = raw offset of the FF that ends the data (or -1), *end_err =
-// whether that end is a syntax error (bad marker / FF at EOF) rather than FF D9.
-constexpr int kChunk = kTileBytes / 256;
-
-__device__ __forceinline__ bool carry_after_ff(const uint8_t* R, int64_t a, int32_t* giveup) {
-    int k = 0;
-    while (a - 1 - k >= 0 && R[a - 1 - k] == 0xFF) {
-        if (++k > 4096) { *giveup = 1; break; }  // pathological FF run: image goes sequential
-    }
-    return k & 1;
-}
-
-template <bool WRITE>
-__device__ __forceinline__ int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, int* end_err,
-                                          uint8_t* out, int32_t* giveup) {
-    *end_at = -1;
-    *end_err = 0;
-    if (a >= L) return 0;
-    bool after_ff = carry_after_ff(R, a, giveup);
-    int kept = 0;
-    const int64_t b = a + kChunk < L ? a + kChunk : L;
-    for (int64_t p = a; p < b; ++p) {
-        if (after_ff) { after_ff = false; continue; }  // marker byte, consumed with its FF
-        const uint8_t c = R[p];
-        if (c != 0xFF) {
-            if (WRITE) out[kept] = c;
-            ++kept;
-            continue;
-        }
-        if (p + 1 >= L) { *end_at = p; *end_err = 1; break; }  // FF ends the file (:477-478)
-        const uint8_t m = R[p + 1];
-        if (m == 0x00 || m == 0xFF) {  // :465-467
-            if (WRITE) out[kept] = 0xFF;
-            ++kept;
-            after_ff = true;
-        } else if ((m & 0xF8) == 0xD0) {  // RSTn: both bytes enter the bit buffer (:472-475)
-            if (WRITE) { out[kept] = 0xFF; out[kept + 1] = m; }
-            kept += 2;
-            after_ff = true;
-        } else {  // D9 ends the data (:468); anything else is a syntax error (:470-471)
-            *end_at = p;
-            *end_err = m != 0xD9;
-            break;
-        }
-    }
-    return kept;
-}
-
 __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __restrict__ data,
                                                     const uint64_t* __restrict__ off, const Desc* __restrict__ desc,
                                                     SpecImg* __restrict__ spec, const int32_t* __restrict__ tilepre,
@@ -266,12 +211,6 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
 }
 
 // -------------------------------------------------------------------- entropy lanes
-struct LdsTables {
-    Huff huff[4];
-    int8_t comp_of[kSpecMaxBpm];
-    int8_t dc_of[3], ac_of[3];
-};
-
 __device__ __forceinline__ void load_tables(LdsTables& T, const Desc& d) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&d.huff[0]);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&T.huff[0]);
@@ -284,79 +223,6 @@ __device__ __forceinline__ void load_tables(LdsTables& T, const Desc& d) {
         T.dc_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].dc_tab;
         T.ac_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].ac_tab;
     }
-}
-
-// MSB-first reader over U; bytes at or past ulen read as 0xFF (jpeg_dec.h:451-455).
-struct Reader {
-    const uint8_t* u;
-    int64_t ulen;
-    uint64_t buf;
-    int nb;
-    int64_t widx;
-    __device__ __forceinline__ uint32_t word(int64_t w) const {
-        const int64_t b = w * 4;
-        if (b + 4 <= ulen) return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(u + b));
-        uint32_t v = 0;
-        for (int i = 0; i < 4; ++i) v = (v << 8) | (b + i < ulen ? u[b + i] : 0xFFu);
-        return v;
-    }
-    __device__ __forceinline__ void refill() {
-        if (nb <= 32) {
-            buf |= (uint64_t)word(widx++) << (32 - nb);
-            nb += 32;
-        }
-    }
-    __device__ __forceinline__ void init(const uint8_t* u_, int64_t ulen_, int64_t bitpos) {
-        u = u_;
-        ulen = ulen_;
-        widx = bitpos >> 5;
-        nb = 0;
-        buf = 0;
-        refill();
-        refill();
-        const int skip = (int)(bitpos & 31);
-        buf <<= skip;
-        nb -= skip;
-    }
-    __device__ __forceinline__ int64_t pos() const { return widx * 32 - nb; }
-    __device__ __forceinline__ uint32_t peek16() const { return (uint32_t)(buf >> 48); }
-    __device__ __forceinline__ uint32_t take(int n) {
-        const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
-        buf <<= n;
-        nb -= n;
-        return v;
-    }
-};
-
-enum : int { kUnitOk = 0, kUnitErr = 1 };
-
-// One Huffman code + magnitude bits in the state (b, z); z == 0 expects the DC code.
-// On return: *coef = coefficient index written (0 = DC, 1..63 AC, -1 none), *val = value.
-// Errors (jpeg_dec.h:646, 667, 669) end the block deterministically so speculative lanes
-// keep going; on the true path any error makes the image NJ_SYNTAX_ERROR.
-__device__ __forceinline__ int decode_unit(Reader& r, const LdsTables& T, int bpm, int& b, int& z, int& coef,
-                                           int32_t& val) {
-    const int ci = T.comp_of[b];
-    const Huff& H = T.huff[z == 0 ? T.dc_of[ci] : T.ac_of[ci]];
-    r.refill();
-    int sym = 0;
-    const int len = huff_lookup(H, r.peek16(), sym);
-    coef = -1;
-    val = 0;
-    auto end_block = [&]() { z = 0; b = (b + 1 == bpm) ? 0 : b + 1; };
-    if (!len) { r.take(1); end_block(); return kUnitErr; }
-    r.take(len);
-    const int nbx = sym & 15;
-    const int32_t v = nbx ? extend((int32_t)r.take(nbx), nbx) : 0;
-    if (z == 0) { z = 1; coef = 0; val = v; return kUnitOk; }
-    if (sym == 0) { end_block(); return kUnitOk; }  // EOB
-    if (!nbx && sym != 0xF0) { end_block(); return kUnitErr; }
-    const int c = z + (sym >> 4);
-    if (c > 63) { end_block(); return kUnitErr; }
-    coef = c;
-    val = v;
-    if (c == 63) end_block(); else z = c + 1;
-    return kUnitOk;
 }
 
 __device__ __forceinline__ int wg_image_setup(const int32_t* wgpre, int n, int wg, int& cur, LdsTables& T,
@@ -374,7 +240,8 @@ __device__ __forceinline__ int wg_image_setup(const int32_t* wgpre, int n, int w
 __global__ __launch_bounds__(256) void k_spec_guess(int n, const Desc* __restrict__ desc,
                                                     const SpecImg* __restrict__ spec, const int32_t* __restrict__ wgpre,
                                                     const int32_t* __restrict__ totals, const uint8_t* __restrict__ U,
-                                                    int64_t ucap, uint64_t* __restrict__ X) {
+                                                    int64_t ucap, uint64_t* __restrict__ X, RecState* __restrict__ rec,
+                                                    int32_t* __restrict__ nrec, int32_t* __restrict__ gtot) {
     __shared__ LdsTables T;
     int cur = -1;
     const int total = totals[1];
@@ -383,68 +250,88 @@ __global__ __launch_bounds__(256) void k_spec_guess(int n, const Desc* __restric
         const SpecImg& s = spec[i];
         const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
         if (j >= s.nsub - 1) continue;  // the last lane's exit is never needed
-        const int bpm = desc[i].bpm;
-        Reader r;
-        r.init(U + (int64_t)i * ucap, s.ulen, j * kSubBytes * 8);
-        int b = 0, z = 0, coef;
-        int32_t val;
-        const int64_t end = (j + 1) * kSubBytes * 8;
-        while (r.pos() < end) decode_unit(r, T, bpm, b, z, coef, val);
-        X[(int64_t)s.wg_base * kLanes + j] = pack_state(r.pos(), b, z);
+        const int64_t f = (int64_t)s.wg_base * kLanes + j;
+        const int64_t sb = (int64_t)kSubBytes * 8;
+        X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, desc[i].bpm, j * sb, (j + 1) * sb, 0, rec + f * kRec,
+                          nrec + f, gtot + 4 * f);
     }
 }
 
-__global__ __launch_bounds__(256) void k_spec_count(int n, const Desc* __restrict__ desc,
-                                                    const SpecImg* __restrict__ spec, const int32_t* __restrict__ wgpre,
-                                                    const int32_t* __restrict__ totals, const uint8_t* __restrict__ U,
-                                                    int64_t ucap, const uint64_t* __restrict__ X,
-                                                    SubRec* __restrict__ sub) {
+__global__ __launch_bounds__(256) void k_spec_count(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                    const int32_t* __restrict__ wgpre, const int32_t* __restrict__ totals,
+                                                    const uint8_t* __restrict__ U, int64_t ucap,
+                                                    const uint64_t* __restrict__ X, uint64_t* __restrict__ Y,
+                                                    const RecState* __restrict__ rec, const int32_t* __restrict__ nrec,
+                                                    const int32_t* __restrict__ gtot, SubRec* __restrict__ sub,
+                                                    int32_t* __restrict__ repair) {
     __shared__ LdsTables T;
     int cur = -1;
     const int total = totals[1];
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
-        const SpecImg& s = spec[i];
+        SpecImg& s = spec[i];
         const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
         if (j >= s.nsub - 1) continue;
-        const int bpm = desc[i].bpm;
-        const int64_t base = (int64_t)s.wg_base * kLanes;
-        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[base + j - 1];
-        Reader r;
-        r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
-        int b = st_b(entry), z = st_z(entry), coef;
-        int32_t val, cnt = 0, ds[3] = {0, 0, 0};
-        const int64_t end = (j + 1) * kSubBytes * 8;
-        while (r.pos() < end) {
-            const int ci = T.comp_of[b];
-            const bool dc = z == 0;
-            decode_unit(r, T, bpm, b, z, coef, val);
-            if (dc) {
-                ++cnt;
-                ds[ci] = wadd(ds[ci], val);
-            }
+        const int64_t base = (int64_t)s.wg_base * kLanes, f = base + j;
+        const int64_t sb = (int64_t)kSubBytes * 8;
+        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
+        SubRec out;
+        bool synced;
+        Y[f] = lane_count(U + (int64_t)i * ucap, s.ulen, T, desc[i].bpm, entry, j * sb, (j + 1) * sb, rec + f * kRec,
+                          nrec[f], gtot + 4 * f, X[f], out, synced);
+        sub[f] = out;
+        if (out.mism) {  // queue for the serial repair walk
+            const int q = atomicAdd(&s.nrepair, 1);
+            if (q < kMaxRepair) repair[(int64_t)i * kMaxRepair + q] = (int32_t)j;
         }
-        SubRec rec;
-        rec.cnt = cnt;
-        rec.ds0 = ds[0];
-        rec.ds1 = ds[1];
-        rec.ds2 = ds[2];
-        rec.mism = pack_state(r.pos(), b, z) != X[base + j];
-        sub[base + j] = rec;
     }
 }
 
-// Per image: block index and DC predictors at every lane entry; chain verification.
+// One workgroup per image with queued lanes; lane 0 walks them in order (they are rare:
+// a guess lane that never resynchronised inside its 2 KiB).
+__global__ __launch_bounds__(64) void k_spec_repair(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                    const uint8_t* __restrict__ U, int64_t ucap, uint64_t* __restrict__ X,
+                                                    const uint64_t* __restrict__ Y, const RecState* __restrict__ rec,
+                                                    const int32_t* __restrict__ nrec, const int32_t* __restrict__ gtot,
+                                                    SubRec* __restrict__ sub, int32_t* __restrict__ repair) {
+    __shared__ LdsTables T;
+    const int i = blockIdx.x;
+    SpecImg& s = spec[i];
+    if (s.mode != 1 || s.nrepair == 0) return;
+    load_tables(T, desc[i]);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    if (s.nrepair > kMaxRepair) { s.mode = 2; return; }
+    int32_t* q = repair + (int64_t)i * kMaxRepair;
+    const int nq = s.nrepair;
+    for (int a = 1; a < nq; ++a) {  // insertion sort (short list)
+        const int32_t v = q[a];
+        int c = a - 1;
+        while (c >= 0 && q[c] > v) { q[c + 1] = q[c]; --c; }
+        q[c + 1] = v;
+    }
+    const int64_t base = (int64_t)s.wg_base * kLanes;
+    int64_t done = -1;
+    for (int a = 0; a < nq; ++a) {
+        const int64_t j = q[a];
+        if (j <= done) continue;  // re-derived by an earlier walk
+        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, desc[i].bpm, j, s.nsub, (int64_t)kSubBytes * 8, X + base,
+                           Y + base, rec + base * kRec, nrec + base, gtot + 4 * base, sub + base, 64);
+        if (done < 0) { s.mode = 2; return; }  // pathological stream: sequential decode
+    }
+}
+
+// Per image: block index and DC predictors at every lane entry (after repair all lane
+// chains agree, so these are the true values).
 __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ spec, SubRec* __restrict__ sub,
                                                    LaneEntry* __restrict__ ent) {
     __shared__ int sh[256];
     __shared__ int s_cnt, s_d0, s_d1, s_d2;
-    __shared__ int64_t s_bad;
     const int i = blockIdx.x;
     if (i >= n) return;
     SpecImg& s = spec[i];
     if (s.mode != 1) return;
-    if (threadIdx.x == 0) s_bad = INT64_MAX;
+    if (s.err & kSpecGiveUp) { if (threadIdx.x == 0) s.mode = 2; return; }
     const int64_t base = (int64_t)s.wg_base * kLanes;
     int64_t G = 0;
     int32_t P0 = 0, P1 = 0, P2 = 0;
@@ -464,9 +351,6 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
             le.p1 = wadd(P1, e1);
             le.p2 = wadd(P2, e2);
             ent[base + j] = le;
-            // a disagreement only matters if the true decode still has blocks to place after it
-            if (live && rec.mism && le.G + rec.cnt < s.total_blocks)
-                atomicMin((unsigned long long*)&s_bad, (unsigned long long)j);
         }
         if (threadIdx.x == blockDim.x - 1) {
             s_cnt = e + rec.cnt;
@@ -481,7 +365,6 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
         P2 = wadd(P2, s_d2);
         __syncthreads();
     }
-    if (threadIdx.x == 0 && (s_bad != INT64_MAX || (s.err & kSpecGiveUp))) s.mode = 2;  // -> sequential
 }
 
 __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
@@ -491,7 +374,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                     int64_t coef_cap) {
     __shared__ LdsTables T;
-    __shared__ int32_t blk[kLanes][33];  // one 64 x int16 block per lane (+1 word: no bank conflicts)
+    __shared__ int16_t blk[kLanes][66];  // one 64 x int16 block per lane (+1 word: no bank conflicts)
     int cur = -1;
     const int total = totals[1];
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
@@ -516,11 +399,11 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
         int16_t* A = ac + (int64_t)i * coef_cap * 64;
         int32_t* D = dcv + (int64_t)i * coef_cap;
-        int16_t* mine = reinterpret_cast<int16_t*>(&blk[threadIdx.x][0]);
+        int16_t* mine = &blk[threadIdx.x][0];
         bool bad = false;
         for (int64_t bi = le.G; bi < s.total_blocks && r.pos() < limit && !bad; ++bi) {
             const int ci = T.comp_of[b];
-            for (int k = 0; k < 32; ++k) blk[threadIdx.x][k] = 0;
+            __builtin_memset(mine, 0, 128);
             do {
                 // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
                 if (r.pos() + 16 > errbits) bad = true;
@@ -533,10 +416,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                     mine[nat_of_zig(coef)] = (int16_t)val;
                 }
             } while (z != 0 && !bad);
-            int4* dst = reinterpret_cast<int4*>(A + bi * 64);
-            const int32_t* src = &blk[threadIdx.x][0];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) dst[q] = make_int4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
+            __builtin_memcpy(A + bi * 64, mine, 128);  // type-safe copy of the whole block
         }
         if (bad) atomicOr(&s.err, kSpecSyntax);
     }
@@ -564,9 +444,11 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles, ws.tile_obase, ws.U, ws.ucap);
     hipLaunchKernelGGL(k_spec_guess, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
-                       ws.ucap, ws.X);
+                       ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt);
     hipLaunchKernelGGL(k_spec_count, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
-                       ws.ucap, ws.X, ws.sub);
+                       ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+    hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.U, ws.ucap, ws.X, ws.Y, ws.rec,
+                       ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
     hipLaunchKernelGGL(k_spec_write, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
                        ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);

@@ -1,0 +1,247 @@
+// icx_spec_core.h -- per-lane logic of the parallel entropy decoder (icx_spec.hip), kept
+// __host__ __device__ so the very same code also runs in the CPU emulator used by the
+// tests (tests/emu/spec_emu.cpp). No kernels here.
+#pragma once
+#include "icx_internal.h"
+
+namespace icx {
+
+ICX_HD uint64_t pack_state(int64_t pos, int b, int z) {
+    return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)z;
+}
+ICX_HD int64_t st_pos(uint64_t s) { return (int64_t)(s >> 16); }
+ICX_HD int st_b(uint64_t s) { return (int)((s >> 8) & 0xFF); }
+ICX_HD int st_z(uint64_t s) { return (int)(s & 0xFF); }
+
+// Per-lane marker automaton over kChunk raw bytes. Returns kept-byte count before the
+// first end event; *end_at = raw offset of the FF that ends the data (or -1), *end_err =
+// whether that end is a syntax error (bad marker / FF at EOF) rather than FF D9.
+constexpr int kChunk = kTileBytes / 256;
+
+ICX_HD bool carry_after_ff(const uint8_t* R, int64_t a, int32_t* giveup) {
+    int k = 0;
+    while (a - 1 - k >= 0 && R[a - 1 - k] == 0xFF) {
+        if (++k > 4096) { *giveup = 1; break; }  // pathological FF run: image goes sequential
+    }
+    return k & 1;
+}
+
+template <bool WRITE>
+ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, int* end_err,
+                                          uint8_t* out, int32_t* giveup) {
+    *end_at = -1;
+    *end_err = 0;
+    if (a >= L) return 0;
+    bool after_ff = carry_after_ff(R, a, giveup);
+    int kept = 0;
+    const int64_t b = a + kChunk < L ? a + kChunk : L;
+    for (int64_t p = a; p < b; ++p) {
+        if (after_ff) { after_ff = false; continue; }  // marker byte, consumed with its FF
+        const uint8_t c = R[p];
+        if (c != 0xFF) {
+            if (WRITE) out[kept] = c;
+            ++kept;
+            continue;
+        }
+        if (p + 1 >= L) { *end_at = p; *end_err = 1; break; }  // FF ends the file (:477-478)
+        const uint8_t m = R[p + 1];
+        if (m == 0x00 || m == 0xFF) {  // :465-467
+            if (WRITE) out[kept] = 0xFF;
+            ++kept;
+            after_ff = true;
+        } else if ((m & 0xF8) == 0xD0) {  // RSTn: both bytes enter the bit buffer (:472-475)
+            if (WRITE) { out[kept] = 0xFF; out[kept + 1] = m; }
+            kept += 2;
+            after_ff = true;
+        } else {  // D9 ends the data (:468); anything else is a syntax error (:470-471)
+            *end_at = p;
+            *end_err = m != 0xD9;
+            break;
+        }
+    }
+    return kept;
+}
+
+struct LdsTables {
+    Huff huff[4];
+    int8_t comp_of[kSpecMaxBpm];
+    int8_t dc_of[3], ac_of[3];
+};
+
+// MSB-first reader over U; bytes at or past ulen read as 0xFF (jpeg_dec.h:451-455).
+struct Reader {
+    const uint8_t* u;
+    int64_t ulen;
+    uint64_t buf;
+    int nb;
+    int64_t widx;
+    ICX_HD uint32_t word(int64_t w) const {
+        const int64_t b = w * 4;
+        if (b + 4 <= ulen) return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(u + b));
+        uint32_t v = 0;
+        for (int i = 0; i < 4; ++i) v = (v << 8) | (b + i < ulen ? u[b + i] : 0xFFu);
+        return v;
+    }
+    ICX_HD void refill() {
+        if (nb <= 32) {
+            buf |= (uint64_t)word(widx++) << (32 - nb);
+            nb += 32;
+        }
+    }
+    ICX_HD void init(const uint8_t* u_, int64_t ulen_, int64_t bitpos) {
+        u = u_;
+        ulen = ulen_;
+        widx = bitpos >> 5;
+        nb = 0;
+        buf = 0;
+        refill();
+        refill();
+        const int skip = (int)(bitpos & 31);
+        buf <<= skip;
+        nb -= skip;
+    }
+    ICX_HD int64_t pos() const { return widx * 32 - nb; }
+    ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
+    ICX_HD uint32_t take(int n) {
+        const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
+        buf <<= n;
+        nb -= n;
+        return v;
+    }
+};
+
+enum : int { kUnitOk = 0, kUnitErr = 1 };
+
+// One Huffman code + magnitude bits in the state (b, z); z == 0 expects the DC code.
+// On return: *coef = coefficient index written (0 = DC, 1..63 AC, -1 none), *val = value.
+// Errors (jpeg_dec.h:646, 667, 669) end the block deterministically so speculative lanes
+// keep going; on the true path any error makes the image NJ_SYNTAX_ERROR.
+ICX_HD int decode_unit(Reader& r, const LdsTables& T, int bpm, int& b, int& z, int& coef,
+                                           int32_t& val) {
+    const int ci = T.comp_of[b];
+    const Huff& H = T.huff[z == 0 ? T.dc_of[ci] : T.ac_of[ci]];
+    r.refill();
+    int sym = 0;
+    const int len = huff_lookup(H, r.peek16(), sym);
+    coef = -1;
+    val = 0;
+    auto end_block = [&]() { z = 0; b = (b + 1 == bpm) ? 0 : b + 1; };
+    if (!len) { r.take(1); end_block(); return kUnitErr; }
+    r.take(len);
+    const int nbx = sym & 15;
+    const int32_t v = nbx ? extend((int32_t)r.take(nbx), nbx) : 0;
+    if (z == 0) { z = 1; coef = 0; val = v; return kUnitOk; }
+    if (sym == 0) { end_block(); return kUnitOk; }  // EOB
+    if (!nbx && sym != 0xF0) { end_block(); return kUnitErr; }
+    const int c = z + (sym >> 4);
+    if (c > 63) { end_block(); return kUnitErr; }
+    coef = c;
+    val = v;
+    if (c == 63) end_block(); else z = c + 1;
+    return kUnitOk;
+}
+
+// ------------------------------------------------------------------------ lane logic
+// Guess lane: decode [start, end) from the block-start guess (b0, z=0). Records the first
+// kRec MCU-start states (b == 0, z == 0) it passes through (rec, *nrec) and its totals tot = {DC codes,
+// DC-diff sums per component} over the whole lane. Returns the exit state: the first code
+// boundary at or after `end`.
+ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, int bpm, int64_t start, int64_t end,
+                           int b0, RecState* rec, int32_t* nrec, int32_t* tot) {
+    Reader r;
+    r.init(U, ulen, start);
+    int b = b0, z = 0, coef;
+    int32_t val, cnt = 0, ds[3] = {0, 0, 0};
+    int nr = 0;
+    while (r.pos() < end) {
+        if (z == 0 && b == 0 && nr < kRec) {  // MCU starts: the true path passes one per MCU
+            RecState& e = rec[nr++];
+            e.rel = (uint32_t)(r.pos() - start);
+            e.b = b;
+            e.cnt = cnt;
+            e.ds[0] = ds[0];
+            e.ds[1] = ds[1];
+            e.ds[2] = ds[2];
+        }
+        const int ci = T.comp_of[b];
+        const bool dc = z == 0;
+        decode_unit(r, T, bpm, b, z, coef, val);
+        if (dc) {
+            ++cnt;
+            ds[ci] = wadd(ds[ci], val);
+        }
+    }
+    *nrec = nr;
+    tot[0] = cnt;
+    tot[1] = ds[0];
+    tot[2] = ds[1];
+    tot[3] = ds[2];
+    return pack_state(r.pos(), b, z);
+}
+
+// Count lane: decode from the (verified) entry state; as soon as a block-start state equals
+// one the guess lane recorded, both decodes coincide from there on, so the lane's totals are
+// spliced from the guess lane's and its exit is the guess exit (synced = true). Otherwise the
+// whole lane is decoded and its own exit returned.
+ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, int bpm, uint64_t entry, int64_t start,
+                           int64_t end, const RecState* rec, int nrec, const int32_t* tot, uint64_t guess_exit,
+                           SubRec& out, bool& synced) {
+    Reader r;
+    r.init(U, ulen, st_pos(entry));
+    int b = st_b(entry), z = st_z(entry), coef;
+    int32_t val, cnt = 0, ds[3] = {0, 0, 0};
+    int m = 0;
+    synced = false;
+    while (r.pos() < end) {
+        if (z == 0 && b == 0 && m < nrec) {
+            const int64_t rel = r.pos() - start;
+            while (m < nrec && (int64_t)rec[m].rel < rel) ++m;
+            if (m < nrec && (int64_t)rec[m].rel == rel) {
+                out.cnt = cnt + tot[0] - rec[m].cnt;
+                out.ds0 = wadd(ds[0], wsub(tot[1], rec[m].ds[0]));
+                out.ds1 = wadd(ds[1], wsub(tot[2], rec[m].ds[1]));
+                out.ds2 = wadd(ds[2], wsub(tot[3], rec[m].ds[2]));
+                out.mism = 0;
+                synced = true;
+                return guess_exit;
+            }
+        }
+        const int ci = T.comp_of[b];
+        const bool dc = z == 0;
+        decode_unit(r, T, bpm, b, z, coef, val);
+        if (dc) {
+            ++cnt;
+            ds[ci] = wadd(ds[ci], val);
+        }
+    }
+    const uint64_t ex = pack_state(r.pos(), b, z);
+    out.cnt = cnt;
+    out.ds0 = ds[0];
+    out.ds1 = ds[1];
+    out.ds2 = ds[2];
+    out.mism = ex != guess_exit;
+    return ex;
+}
+
+// Serial repair of one unsynchronised lane j (its count pass derived the true exit Y[j]):
+// adopt it and re-derive the following lanes until one's exit agrees with its guess exit.
+// Returns the last lane touched, or -1 if the walk exceeded `max_walk` lanes.
+ICX_HD int64_t repair_walk(const uint8_t* U, int64_t ulen, const LdsTables& T, int bpm, int64_t j, int64_t nsub,
+                           int64_t sub_bits, uint64_t* X, const uint64_t* Y, const RecState* rec, const int32_t* nrec,
+                           const int32_t* tot, SubRec* sub, int max_walk) {
+    X[j] = Y[j];
+    int64_t k = j + 1;
+    for (int steps = 0; k < nsub - 1; ++k, ++steps) {
+        if (steps >= max_walk) return -1;
+        bool synced;
+        SubRec out;
+        const uint64_t ex = lane_count(U, ulen, T, bpm, X[k - 1], k * sub_bits, (k + 1) * sub_bits, rec + k * kRec,
+                                       nrec[k], tot + 4 * k, X[k], out, synced);
+        sub[k] = out;
+        if (ex == X[k]) break;
+        X[k] = ex;
+    }
+    return k;
+}
+
+}  // namespace icx

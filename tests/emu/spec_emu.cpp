@@ -1,0 +1,221 @@
+// spec_emu.cpp -- TEST-ONLY CPU emulator of the parallel entropy decoder (icx_spec.hip).
+// It runs the kernels' per-lane logic (imagecodecs_amd/csrc/icx_spec_core.h, the same
+// __host__ __device__ code the GPU executes) lane by lane on the host, mirroring each
+// kernel's bookkeeping, so the algorithm can be checked on a machine without a GPU.
+// Never linked into libicx.so.
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../imagecodecs_amd/csrc/icx_spec_core.h"
+
+using namespace icx;
+
+extern "C" {
+
+// Returns: 0 parallel path finished (status in *status), 1 image would fall back to the
+// sequential kernel, 2 not eligible for the parallel path (status = header result).
+// coef: nblocks*64 int16 natural order; dc: nblocks int32 absolute. *nblocks = total blocks.
+int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* coef, int32_t* dc,
+                    int64_t cap_blocks, int64_t* nblocks, int32_t* status, int64_t* stats /*[4]*/) {
+    auto dp = std::make_unique<Desc>();
+    Desc& d = *dp;
+    *status = parse_headers(file, size, d);
+    *nblocks = 0;
+    const int64_t scan_len = d.size - d.scan_off;
+    if (!(d.status == kPending && d.restart == 0 && d.nc >= 1 && d.bpm <= kSpecMaxBpm && scan_len > 0)) return 2;
+    const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
+    *nblocks = total;
+    if (total > cap_blocks) return 2;
+    const uint8_t* R = file + d.scan_off;
+    // ---- unstuff (k_ustf_count / k_ustf_scan / k_ustf_write)
+    const int64_t ntiles = (scan_len + kTileBytes - 1) / kTileBytes;
+    std::vector<TileRec> tiles(ntiles);
+    int32_t giveup = 0;
+    for (int64_t t = 0; t < ntiles; ++t) {
+        int64_t tend = INT64_MAX;
+        int terr = 0;
+        std::vector<int> kept(256);
+        std::vector<int64_t> ends(256);
+        std::vector<int> errs(256);
+        for (int l = 0; l < 256; ++l) {
+            const int64_t a = t * kTileBytes + (int64_t)l * kChunk;
+            kept[l] = ustf_chunk<false>(R, scan_len, a, &ends[l], &errs[l], nullptr, &giveup);
+            if (ends[l] >= 0 && ends[l] < tend) { tend = ends[l]; terr = errs[l]; }
+        }
+        int sum = 0;
+        for (int l = 0; l < 256; ++l) {
+            const int64_t a = t * kTileBytes + (int64_t)l * kChunk;
+            const bool before = ends[l] >= 0 ? ends[l] <= tend : a < tend;
+            if (before) sum += kept[l];
+        }
+        tiles[t].kept = sum;
+        tiles[t].end_at = tend == INT64_MAX ? -1 : tend;
+        tiles[t].end_err = terr;
+    }
+    int64_t fe = -1;
+    for (int64_t t = 0; t < ntiles; ++t)
+        if (tiles[t].end_at >= 0) { fe = t; break; }
+    std::vector<int64_t> obase(ntiles);
+    int64_t ulen = 0;
+    for (int64_t t = 0; t < ntiles; ++t) {
+        obase[t] = ulen;
+        if (fe < 0 || t <= fe) ulen += tiles[t].kept;
+    }
+    const int64_t errpos = (fe >= 0 && tiles[fe].end_err) ? ulen : INT64_MAX;
+    std::vector<uint8_t> U(ulen + 8, 0);
+    for (int64_t t = 0; t < ntiles; ++t) {
+        if (obase[t] >= ulen) continue;
+        const int64_t tend = tiles[t].end_at;
+        int64_t o = obase[t];
+        for (int l = 0; l < 256; ++l) {
+            const int64_t a = t * kTileBytes + (int64_t)l * kChunk;
+            int64_t e;
+            int er;
+            const int k = ustf_chunk<false>(R, scan_len, a, &e, &er, nullptr, &giveup);
+            const bool before = e >= 0 ? (tend < 0 || e <= tend) : (tend < 0 || a < tend);
+            if (!before) continue;
+            if (k && o + k <= ulen) ustf_chunk<true>(R, scan_len, a, &e, &er, U.data() + o, &giveup);
+            o += k;
+        }
+    }
+    if (giveup) { stats[1]++; return 1; }
+    // ---- tables
+    auto Tp = std::make_unique<LdsTables>();
+    LdsTables& T = *Tp;
+    std::memcpy(T.huff, d.huff, sizeof(T.huff));
+    for (int b = 0; b < kSpecMaxBpm; ++b) {
+        int sx, sy;
+        T.comp_of[b] = b < d.bpm ? (int8_t)mcu_block_comp(d, b, sx, sy) : 0;
+    }
+    for (int c = 0; c < 3; ++c) { T.dc_of[c] = (int8_t)d.c[c].dc_tab; T.ac_of[c] = (int8_t)d.c[c].ac_tab; }
+    const int64_t S = sub_bytes;
+    const int64_t nsub = ulen > 0 ? (ulen + S - 1) / S : 1;
+    const int bpm = d.bpm;
+    // ---- guess (k_spec_guess)
+    const int64_t sb = S * 8;
+    std::vector<uint64_t> X(nsub, 0), Y(nsub, 0);
+    std::vector<RecState> rec(nsub * kRec);
+    std::vector<int32_t> nrec(nsub, 0), tot(nsub * 4, 0);
+    for (int64_t j = 0; j + 1 < nsub; ++j)
+        X[j] = lane_guess(U.data(), ulen, T, bpm, j * sb, (j + 1) * sb, 0, rec.data() + j * kRec, &nrec[j], &tot[4 * j]);
+    // ---- count (k_spec_count)
+    std::vector<SubRec> sub(nsub, SubRec{0, 0, 0, 0, 0});
+    std::vector<int32_t> queue;
+    int64_t synced_lanes = 0;
+    for (int64_t j = 0; j + 1 < nsub; ++j) {
+        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[j - 1];
+        bool synced;
+        Y[j] = lane_count(U.data(), ulen, T, bpm, entry, j * sb, (j + 1) * sb, rec.data() + j * kRec, nrec[j],
+                          &tot[4 * j], X[j], sub[j], synced);
+        synced_lanes += synced;
+        if (sub[j].mism) queue.push_back((int32_t)j);
+    }
+    stats[2] += (int64_t)queue.size();
+    stats[3] += synced_lanes;
+    // ---- repair (k_spec_repair)
+    if ((int)queue.size() > kMaxRepair) { stats[1]++; return 1; }
+    int64_t done = -1;
+    for (int32_t j : queue) {
+        if (j <= done) continue;
+        done = repair_walk(U.data(), ulen, T, bpm, j, nsub, sb, X.data(), Y.data(), rec.data(), nrec.data(), tot.data(),
+                           sub.data(), 64);
+        if (done < 0) { stats[1]++; return 1; }
+    }
+    // ---- scan (k_spec_scan)
+    std::vector<LaneEntry> ent(nsub);
+    int64_t G = 0;
+    int32_t P[3] = {0, 0, 0};
+    for (int64_t j = 0; j < nsub; ++j) {
+        ent[j] = LaneEntry{G, P[0], P[1], P[2], 0};
+        if (j + 1 < nsub) {
+            G += sub[j].cnt;
+            P[0] = wadd(P[0], sub[j].ds0);
+            P[1] = wadd(P[1], sub[j].ds1);
+            P[2] = wadd(P[2], sub[j].ds2);
+        }
+    }
+    // ---- write (k_spec_write)
+    bool anybad = false;
+    std::memset(coef, 0, sizeof(int16_t) * 64 * total);
+    for (int64_t j = 0; j < nsub; ++j) {
+        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[j - 1];
+        const bool last = j == nsub - 1;
+        const int64_t limit = last ? INT64_MAX : st_pos(X[j]);
+        Reader r;
+        r.init(U.data(), ulen, st_pos(entry));
+        int b = st_b(entry), z = st_z(entry), coefi;
+        int32_t val;
+        while (z != 0) decode_unit(r, T, bpm, b, z, coefi, val);
+        int32_t pred[3] = {ent[j].p0, ent[j].p1, ent[j].p2};
+        const int64_t errbits = errpos == INT64_MAX ? INT64_MAX : errpos * 8;
+        bool bad = false;
+        for (int64_t bi = ent[j].G; bi < total && r.pos() < limit && !bad; ++bi) {
+            const int ci = T.comp_of[b];
+            int16_t blk[64];
+            std::memset(blk, 0, sizeof blk);
+            do {
+                if (r.pos() + 16 > errbits) bad = true;
+                const int rc = decode_unit(r, T, bpm, b, z, coefi, val);
+                if (rc != kUnitOk || r.pos() > errbits) bad = true;
+                if (coefi == 0) { pred[ci] = wadd(pred[ci], val); dc[bi] = pred[ci]; }
+                else if (coefi > 0) blk[nat_of_zig(coefi)] = (int16_t)val;
+            } while (z != 0 && !bad);
+            std::memcpy(coef + bi * 64, blk, sizeof blk);
+        }
+        anybad |= bad;
+    }
+    *status = anybad ? kSyntaxError : kOk;
+    stats[0]++;
+    return 0;
+}
+}
+
+#include <unordered_map>
+extern "C" {
+// Sync-distance study: for `nstarts` evenly spaced start bits, decode from a guessed state
+// (b = guess_b, z = 0) and report the bits consumed until the lane's state equals the true
+// decoder's state at the same position (-1 if not within `maxbits`).
+int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, int64_t maxbits, int64_t* out) {
+    auto dp = std::make_unique<Desc>();
+    Desc& d = *dp;
+    if (parse_headers(file, size, d) != kPending || d.restart || d.bpm > kSpecMaxBpm) return -1;
+    const uint8_t* R = file + d.scan_off;
+    const int64_t L = d.size - d.scan_off;
+    std::vector<uint8_t> U(L + 8);
+    int64_t e; int er; int32_t gu = 0;
+    int64_t ulen = 0;
+    for (int64_t a = 0; a < L; a += kChunk) {
+        int k = ustf_chunk<true>(R, L, a, &e, &er, U.data() + ulen, &gu);
+        ulen += k;
+        if (e >= 0) break;
+    }
+    auto Tp = std::make_unique<LdsTables>();
+    LdsTables& T = *Tp;
+    std::memcpy(T.huff, d.huff, sizeof(T.huff));
+    for (int b = 0; b < kSpecMaxBpm; ++b) { int sx, sy; T.comp_of[b] = b < d.bpm ? (int8_t)mcu_block_comp(d, b, sx, sy) : 0; }
+    for (int c = 0; c < 3; ++c) { T.dc_of[c] = (int8_t)d.c[c].dc_tab; T.ac_of[c] = (int8_t)d.c[c].ac_tab; }
+    std::unordered_map<int64_t, int> truth;  // pos -> (b<<8|z)
+    {
+        Reader r; r.init(U.data(), ulen, 0);
+        int b = 0, z = 0, c; int32_t v;
+        const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
+        int64_t blocks = 0;
+        truth[0] = 0;
+        while (blocks < total) { bool dc = z == 0; decode_unit(r, T, d.bpm, b, z, c, v); if (dc) ++blocks; truth[r.pos()] = (b << 8) | z; }
+    }
+    for (int s = 0; s < nstarts; ++s) {
+        const int64_t start = (ulen * 8) * s / nstarts;
+        Reader r; r.init(U.data(), ulen, start);
+        int b = guess_b, z = 0, c; int32_t v;
+        out[s] = -1;
+        while (r.pos() - start < maxbits) {
+            decode_unit(r, T, d.bpm, b, z, c, v);
+            auto it = truth.find(r.pos());
+            if (it != truth.end() && it->second == ((b << 8) | z)) { out[s] = r.pos() - start; break; }
+        }
+    }
+    return 0;
+}
+}

@@ -59,7 +59,7 @@ def test_batch_mixed_goldens(ctx):
     b = icx.Batch(ctx, len(jpegs), 512, 512)
     res = b.decode_host(jpegs)
     stats = b.path_stats()
-    assert stats["parallel"] >= 80, stats  # every non-DRI stream takes the parallel path
+    assert stats["parallel"] >= 40 and stats["fallback"] == 0, stats  # non-DRI streams: parallel path
     for name, (code, w, h, n, pix) in zip(names, res):
         exp = MANIFEST[name]
         assert code == exp["code"], name

@@ -1,0 +1,107 @@
+"""CPU tests of the parallel entropy-decode ALGORITHM (icx_spec.hip) without a GPU.
+
+tests/emu/spec_emu.cpp runs the kernels' per-lane code (imagecodecs_amd/csrc/icx_spec_core.h,
+compiled __host__ __device__) lane by lane on the CPU: unstuff, speculative guess, count/verify,
+scan, whole-block write. Its quantized coefficients and DC values must equal the oracle's
+NanoJPEG trace block for block, for every subsequence size tried."""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from oracle import pyoracle as O
+from tools import synthpy as S
+
+EMU_DIR = os.path.join(ROOT, "tests", "emu")
+MANIFEST = json.load(open(os.path.join(GOLDEN, "decode_manifest.json")))
+_L = None
+
+
+def emu_lib():
+    global _L
+    if _L is None:
+        subprocess.run(["make", "-s", "-C", EMU_DIR], check=True)
+        import imagecodecs_amd
+        imagecodecs_amd._share_hip_runtime_with_torch()
+        L = C.CDLL(os.path.join(EMU_DIR, "libspecemu.so"))
+        L.emu_spec_decode.restype = C.c_int
+        L.emu_spec_decode.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_int64,
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.c_void_p]
+        _L = L
+    return _L
+
+
+def emu(data: bytes, sub_bytes: int = 256, cap: int = 1 << 17):
+    coef = np.zeros((cap, 64), np.int16)
+    dc = np.zeros(cap, np.int32)
+    nb, st = C.c_int64(), C.c_int32()
+    stats = np.zeros(4, np.int64)
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    mode = emu_lib().emu_spec_decode(buf, len(data), sub_bytes, coef.ctypes.data, dc.ctypes.data, cap,
+                                     C.byref(nb), C.byref(st), stats.ctypes.data)
+    return mode, st.value, coef[: nb.value], dc[: nb.value]
+
+
+def check(data, sub_bytes, allow_fallback=False):
+    mode, st, coef, dc = emu(data, sub_bytes)
+    if mode == 2:
+        return mode
+    if mode == 1:
+        assert allow_fallback, "parallel chain failed to verify"
+        return mode
+    oc, ocoef, odc = O.decode_trace(data)
+    assert st == (0 if oc == 0 else 5), (st, oc)
+    if oc == 0:
+        assert np.array_equal(coef, ocoef) and np.array_equal(dc, odc)
+    return mode
+
+
+@pytest.mark.parametrize("sub_bytes", [64, 256, 2048])
+def test_emulated_parallel_decode_goldens(sub_bytes):
+    """Every non-DRI golden finishes on the parallel path (repair walks included)."""
+    modes = [check(open(os.path.join(GOLDEN, n), "rb").read(), sub_bytes, allow_fallback=False) for n in sorted(MANIFEST)]
+    assert modes.count(0) >= 40 and modes.count(1) == 0
+
+
+@pytest.mark.parametrize("sampling", ["420", "444", "422", "gray", "440", "411"])
+def test_emulated_parallel_decode_synthetic(sampling):
+    rng = np.random.default_rng(hash(sampling) % 1000)
+    for k in range(3):
+        w, h = int(rng.integers(40, 400)), int(rng.integers(40, 400))
+        data = S.synth_jpeg(4000 + k, w, h, sampling, int(rng.integers(20, 100)))
+        for sub in (32, 256, 2048):  # tiny lanes may exceed the 64-lane repair walk -> fallback
+            assert check(data, sub, allow_fallback=sub < 256) in ((0, 1) if sub < 256 else (0,))
+
+
+def test_emulated_parallel_decode_corrupt_streams_status():
+    rng = np.random.default_rng(11)
+    base = bytearray(S.synth_jpeg(77, 200, 150, "420", 85))
+    sos = base.index(b"\xff\xda")
+    start = sos + 2 + ((base[sos + 2] << 8) | base[sos + 3])
+    for t in range(40):
+        d = bytearray(base)
+        for _ in range(1 + t % 4):
+            d[int(rng.integers(start, len(d) - 2))] = int(rng.integers(0, 256))
+        check(bytes(d), [32, 256, 2048][t % 3], allow_fallback=True)
+
+
+def test_emulated_resync_statistics_4k():
+    """At the production lane size (2 KiB) a 4:2:0 q90 4096x1024 image resyncs inside almost
+    every lane; the repair walk covers the rest (bit-exact either way)."""
+    data = S.synth_jpeg(4242, 4096, 1024, "420", 90)
+    coef = np.zeros((1 << 17, 64), np.int16)
+    dc = np.zeros(1 << 17, np.int32)
+    nb, st = C.c_int64(), C.c_int32()
+    stats = np.zeros(4, np.int64)
+    buf = C.create_string_buffer(data, len(data))
+    mode = emu_lib().emu_spec_decode(buf, len(data), 2048, coef.ctypes.data, dc.ctypes.data, 1 << 17, C.byref(nb),
+                                     C.byref(st), stats.ctypes.data)
+    assert mode == 0 and st.value == 0
+    oc, ocoef, odc = O.decode_trace(data)
+    assert np.array_equal(coef[: nb.value], ocoef) and np.array_equal(dc[: nb.value], odc)
+    lanes = (len(data) + 2047) // 2048
+    assert stats[3] >= 0.97 * (lanes - 1), stats  # lanes spliced at a recorded state
