@@ -165,8 +165,10 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) +
                              ws.ucap + tiles_per_slot * 20 +
                              lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
-    if (group <= 0) {
-        const int64_t budget = (int64_t)8 << 30;  // auto: ~8 GiB of workspace
+    if (group <= 0) {  // auto: up to 40% of the free HBM (288 GB per MI355X), at least one image
+        size_t free_b = 0, total_b = 0;
+        ICX_HIP(ctx, hipMemGetInfo(&free_b, &total_b), nullptr);
+        const int64_t budget = (int64_t)(0.4 * (double)free_b);
         group = (int)std::max<int64_t>(1, std::min<int64_t>(max_images, budget / per_slot));
     }
     group = std::min(group, max_images);

@@ -23,18 +23,28 @@ int64_t ws_plane_cap(int w, int h) { return ws_coef_cap(w, h) * 64; }
 int64_t ws_tmp_cap(int w, int h) { return ((int64_t)w + 8) * ((int64_t)h + 8); }
 
 // ------------------------------------------------------------------------------ parse
-__global__ void k_parse(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
-                        const uint64_t* __restrict__ size, Desc* __restrict__ desc, int max_w, int max_h,
-                        uint64_t out_stride) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// One 64-lane workgroup per image: zero the descriptor together, lane 0 walks the markers,
+// then all lanes fill the four 2048-entry fast Huffman tables.
+__global__ __launch_bounds__(64) void k_parse(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                              const uint64_t* __restrict__ size, Desc* __restrict__ desc, int max_w,
+                                              int max_h, uint64_t out_stride) {
+    const int i = blockIdx.x;
     if (i >= n) return;
     Desc& d = desc[i];
-    int st = parse_headers(data + off[i], (int64_t)size[i], d);
-    if (st == kPending) {
-        // capacity of this batch's workspace / output slot (the reference allocates here, :568-572)
-        const int64_t out_bytes = (int64_t)d.W * d.H * (d.nc == 1 ? 1 : d.nc);
-        if (d.W > max_w || d.H > max_h || out_bytes > (int64_t)out_stride) d.status = kOutOfMem;
+    uint32_t* raw = reinterpret_cast<uint32_t*>(&d);
+    for (size_t k = threadIdx.x; k < sizeof(Desc) / 4; k += blockDim.x) raw[k] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int st = parse_headers(data + off[i], (int64_t)size[i], d, false);
+        if (st == kPending) {
+            // capacity of this batch's workspace / output slot (the reference allocates here, :568-572)
+            const int64_t out_bytes = (int64_t)d.W * d.H * (d.nc == 1 ? 1 : d.nc);
+            if (d.W > max_w || d.H > max_h || out_bytes > (int64_t)out_stride) d.status = kOutOfMem;
+        }
     }
+    __syncthreads();
+    if (d.status != kPending) return;
+    for (int t = 0; t < 4; ++t) huff_fill_fast(d.huff[t], threadIdx.x, blockDim.x);
 }
 
 // ---------------------------------------------------------------- entropy (sequential)
@@ -282,7 +292,7 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     const int tb = 64, nb = (n + tb - 1) / tb;
     B(kStParse);
-    hipLaunchKernelGGL(k_parse, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
+    hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
                        out_stride);
     E(kStParse);
     B(kStEntropy);
@@ -292,18 +302,19 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     E(kStEntropy);
     B(kStIdct);
     const int64_t maxblk = ws.coef_cap;
-    const int gx = (int)std::min<int64_t>((maxblk + 31) / 32, 4096);
+    // ~16K workgroups per launch in total; every kernel grid-strides over its image's work
+    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 31) / 32, 16384 / n));
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap);
     E(kStIdct);
     B(kStUpsample);
-    const int ux = (int)std::min<int64_t>((ws.tmp_cap + 255) / 256, 4096);
+    const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, 16384 / (3 * n)));
     for (int p = 0; p < 6; ++p)
         hipLaunchKernelGGL(k_upsample, dim3(ux, n * 3), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
                            ws.tmp_cap, p);
     E(kStUpsample);
     B(kStConvert);
-    const int cx = (int)std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 4096);
+    const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 16384 / n));
     hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
                        ws.tmp_cap, d_out, out_stride);
     hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(tb), 0, st, n, ws.desc, d_status, d_dims);

@@ -54,13 +54,13 @@ ICX_HD uint8_t clip8(int32_t v) { return v < 0 ? 0 : (v > 255 ? 255 : (uint8_t)v
 // a 16-bit window v has code length L = min{L : v < bound[L]}, symbol index
 // first[L] + ((v - bound[L-1]) >> (16-L)); v >= bound[16] is an invalid code (bits == 0).
 // fast[] resolves lengths <= kFastBits with one lookup.
-constexpr int kFastBits = 9;
+constexpr int kFastBits = 11;
 struct Huff {
     uint16_t fast[1 << kFastBits];  // (len << 8) | sym, 0 = not resolvable in kFastBits
     uint32_t bound[17];
     int16_t first[17];
     uint8_t sym[256];
-    uint8_t pad[14];
+    uint8_t pad[2];
 };
 
 ICX_HD void huff_finalize(Huff& t, const uint8_t* count /*[17], count[0]=0*/) {
@@ -74,12 +74,16 @@ ICX_HD void huff_finalize(Huff& t, const uint8_t* count /*[17], count[0]=0*/) {
         idx += count[L];
         t.bound[L] = edge;
     }
-    for (int p = 0; p < (1 << kFastBits); ++p) {
-        uint32_t v = (uint32_t)p << (16 - kFastBits);
+}
+
+// fast[p] for p = lane, lane+step, ... (the GPU fills a table with a whole workgroup).
+ICX_HD void huff_fill_fast(Huff& t, int lane, int step) {
+    for (int p = lane; p < (1 << kFastBits); p += step) {
+        const uint32_t v = (uint32_t)p << (16 - kFastBits);
         uint16_t e = 0;
         for (int L = 1; L <= kFastBits; ++L)
             if (v < t.bound[L]) {
-                int s = t.sym[t.first[L] + (int)((v - t.bound[L - 1]) >> (16 - L))];
+                const int s = t.sym[t.first[L] + (int)((v - t.bound[L - 1]) >> (16 - L))];
                 e = (uint16_t)((L << 8) | s);
                 break;
             }
@@ -250,9 +254,11 @@ ICX_HD int parse_sos(Cursor& cu, Desc& d) {  // njDecodeScan header :678-695
     return cu.err;
 }
 
-// Zero-initialised descriptor + header walk. `d` must be writable; returns d.status.
-ICX_HD int parse_headers(const uint8_t* file, int64_t size, Desc& d) {
-    {
+// Header walk into a descriptor; returns d.status. With zero = false the caller has already
+// zeroed `d` (njInit, jpeg_dec.h:868-870). The fast[] lookup tables are NOT filled here: call
+// huff_fill_fast on each table before decoding (k_parse does it with a whole workgroup).
+ICX_HD int parse_headers(const uint8_t* file, int64_t size, Desc& d, bool zero = true) {
+    if (zero) {
         uint8_t* raw = reinterpret_cast<uint8_t*>(&d);
         for (size_t i = 0; i < sizeof(Desc); ++i) raw[i] = 0;  // njInit :868-870
     }

@@ -219,6 +219,7 @@ __device__ __forceinline__ void load_tables(LdsTables& T, const Desc& d) {
         int sbx, sby;
         T.comp_of[threadIdx.x] = threadIdx.x < d.bpm ? (int8_t)mcu_block_comp(d, threadIdx.x, sbx, sby) : 0;
     }
+    if (threadIdx.x < 64) T.nat_of_zig[threadIdx.x] = kNatOfZig[threadIdx.x];
     if (threadIdx.x < 3) {
         T.dc_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].dc_tab;
         T.ac_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].ac_tab;
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                     pred[ci] = wadd(pred[ci], val);
                     D[bi] = pred[ci];
                 } else if (coef > 0) {
-                    mine[nat_of_zig(coef)] = (int16_t)val;
+                    mine[T.nat_of_zig[coef]] = (int16_t)val;
                 }
             } while (z != 0 && !bad);
             __builtin_memcpy(A + bi * 64, mine, 128);  // type-safe copy of the whole block

@@ -64,43 +64,77 @@ ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, i
 
 struct LdsTables {
     Huff huff[4];
+    uint8_t nat_of_zig[64];
     int8_t comp_of[kSpecMaxBpm];
     int8_t dc_of[3], ac_of[3];
 };
 
 // MSB-first reader over U; bytes at or past ulen read as 0xFF (jpeg_dec.h:451-455).
+// Latency hiding: U is fetched in 16-byte chunks with one chunk always in flight -- `A` is
+// being drained 32 bits at a time into the 64-bit window `buf`, `B` (the next chunk) was
+// requested when A was refilled, ~24 codes before it is first needed.
 struct Reader {
     const uint8_t* u;
-    int64_t ulen;
-    uint64_t buf;
+    int64_t ulen, ucap;
+    uint64_t buf;      // left-aligned window, nb valid bits
     int nb;
-    int64_t widx;
-    ICX_HD uint32_t word(int64_t w) const {
-        const int64_t b = w * 4;
-        if (b + 4 <= ulen) return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(u + b));
-        uint32_t v = 0;
-        for (int i = 0; i < 4; ++i) v = (v << 8) | (b + i < ulen ? u[b + i] : 0xFFu);
-        return v;
+    int na;            // 32-bit words left in A
+    uint64_t a0, a1;   // chunk A as a 128-bit left-aligned shift register
+    uint64_t b0, b1;   // chunk B (prefetched)
+    int64_t next;      // index of the chunk B holds + 1
+    ICX_HD void chunk(int64_t c, uint64_t& h, uint64_t& l) const {
+        const int64_t o = c * 16;
+        if (o + 16 <= ulen) {
+            const uint4 v = *reinterpret_cast<const uint4*>(u + o);
+            h = ((uint64_t)__builtin_bswap32(v.x) << 32) | __builtin_bswap32(v.y);
+            l = ((uint64_t)__builtin_bswap32(v.z) << 32) | __builtin_bswap32(v.w);
+            return;
+        }
+        h = l = ~0ull;  // tail chunk: valid bytes then 0xFF padding
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t byte = (o + i < ulen) ? u[o + i] : 0xFFu;
+            if (i < 8) h = (h & ~(0xFFull << (56 - 8 * i))) | (byte << (56 - 8 * i));
+            else l = (l & ~(0xFFull << (56 - 8 * (i - 8)))) | (byte << (56 - 8 * (i - 8)));
+        }
     }
     ICX_HD void refill() {
         if (nb <= 32) {
-            buf |= (uint64_t)word(widx++) << (32 - nb);
+            buf |= (a0 >> 32) << (32 - nb);
             nb += 32;
+            a0 = (a0 << 32) | (a1 >> 32);
+            a1 <<= 32;
+            if (--na == 0) {
+                a0 = b0;
+                a1 = b1;
+                na = 4;
+                chunk(next++, b0, b1);
+            }
         }
     }
     ICX_HD void init(const uint8_t* u_, int64_t ulen_, int64_t bitpos) {
         u = u_;
         ulen = ulen_;
-        widx = bitpos >> 5;
-        nb = 0;
+        const int64_t c = bitpos >> 7;
+        chunk(c, a0, a1);
+        chunk(c + 1, b0, b1);
+        next = c + 2;
+        na = 4;
         buf = 0;
+        nb = 0;
+        int skip = (int)(bitpos & 127);
         refill();
         refill();
-        const int skip = (int)(bitpos & 31);
+        while (skip >= 32) {
+            buf <<= 32;
+            nb -= 32;
+            skip -= 32;
+            refill();
+        }
         buf <<= skip;
         nb -= skip;
+        refill();
     }
-    ICX_HD int64_t pos() const { return widx * 32 - nb; }
+    ICX_HD int64_t pos() const { return next * 128 - 128 - (int64_t)na * 32 - nb; }
     ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
     ICX_HD uint32_t take(int n) {
         const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;

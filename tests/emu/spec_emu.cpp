@@ -85,6 +85,8 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     auto Tp = std::make_unique<LdsTables>();
     LdsTables& T = *Tp;
     std::memcpy(T.huff, d.huff, sizeof(T.huff));
+    for (int t = 0; t < 4; ++t) huff_fill_fast(T.huff[t], 0, 1);
+    for (int k = 0; k < 64; ++k) T.nat_of_zig[k] = (uint8_t)nat_of_zig(k);
     for (int b = 0; b < kSpecMaxBpm; ++b) {
         int sx, sy;
         T.comp_of[b] = b < d.bpm ? (int8_t)mcu_block_comp(d, b, sx, sy) : 0;
@@ -194,6 +196,8 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
     auto Tp = std::make_unique<LdsTables>();
     LdsTables& T = *Tp;
     std::memcpy(T.huff, d.huff, sizeof(T.huff));
+    for (int t = 0; t < 4; ++t) huff_fill_fast(T.huff[t], 0, 1);
+    for (int k = 0; k < 64; ++k) T.nat_of_zig[k] = (uint8_t)nat_of_zig(k);
     for (int b = 0; b < kSpecMaxBpm; ++b) { int sx, sy; T.comp_of[b] = b < d.bpm ? (int8_t)mcu_block_comp(d, b, sx, sy) : 0; }
     for (int c = 0; c < 3; ++c) { T.dc_of[c] = (int8_t)d.c[c].dc_tab; T.ac_of[c] = (int8_t)d.c[c].ac_tab; }
     std::unordered_map<int64_t, int> truth;  // pos -> (b<<8|z)
