@@ -211,12 +211,13 @@ __device__ __forceinline__ Plane pass_plane(const Desc& d, int ci, int p, const 
     return pl;
 }
 
+__device__ __forceinline__ bool fused_ok(const Desc& d);
 // grid: (x: pixel tiles, y: slot*3 + comp). Pass `p` of every component that has one.
 __global__ __launch_bounds__(256) void k_upsample(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
                                                   uint8_t* __restrict__ tmp, int64_t plane_cap, int64_t tmp_cap, int p) {
     const int img = blockIdx.y / 3, ci = blockIdx.y % 3;
     const Desc& d = desc[img];
-    if (d.status != kOk || ci >= d.nc) return;
+    if (d.status != kOk || ci >= d.nc || fused_ok(d)) return;
     uint8_t ops[6];
     const int nops = comp_program(d, ci, ops);
     if (p >= nops) return;
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(256) void k_convert(const Desc* __restrict__ desc, 
                                                  uint8_t* __restrict__ out, uint64_t out_stride) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk) return;
+    if (d.status != kOk || fused_ok(d)) return;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     const uint8_t* tslot = tmp + (int64_t)img * 3 * 2 * tmp_cap;
     Plane pl[3];
@@ -267,6 +268,118 @@ __global__ __launch_bounds__(256) void k_convert(const Desc* __restrict__ desc, 
         } else {
             o[idx] = pl[0].p[(int64_t)y * pl[0].stride + x];
         }
+    }
+}
+
+// ------------------------------------------------------------- fused upsample + convert
+// For the samplings that need at most one doubling per direction per chroma component
+// (4:4:4, 4:2:2, 4:4:0, 4:2:0, ...) and an un-resampled luma plane, njConvert's H/V passes
+// (jpeg_dec.h:736-791) and the YCbCr->RGB step (:834-853) are evaluated per 64x16 output
+// tile straight from the IDCT planes: no intermediate planes, one RGB write per pixel.
+// kind: bit 0 = horizontal doubling, bit 1 = vertical doubling, -1 = not covered.
+__device__ __forceinline__ int fused_kind(const Desc& d, int ci) {
+    uint8_t ops[6];
+    const int n = comp_program(d, ci, ops);
+    if (n == 0) return 0;
+    if (n == 1) return ops[0] == 'H' ? 1 : 2;
+    if (n == 2 && ops[0] == 'H' && ops[1] == 'V') return 3;
+    return -1;
+}
+__device__ __forceinline__ bool fused_ok(const Desc& d) {
+    if (d.nc == 1) return true;
+    if (d.nc != 3 || fused_kind(d, 0) != 0) return false;
+    return fused_kind(d, 1) >= 0 && fused_kind(d, 2) >= 0;
+}
+
+// Horizontal doubling of row r of a plane (w real samples, stride s; right edge from the
+// stride end, jpeg_dec.h:752-756), output column x.
+__device__ __forceinline__ int hval(const uint8_t* P, int w, int s, int r, int x) {
+    const uint8_t* row = P + (int64_t)r * s;
+    return double_tap(x, w, [&](int i) { return (int)row[i]; }, [&](int j) { return (int)row[s - j]; });
+}
+
+constexpr int kTW = 64, kTH = 16, kHR = 12;  // tile width/height, H rows staged per tile
+
+__global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
+                                                       int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (d.status != kOk || !fused_ok(d)) return;
+    __shared__ uint8_t sH[2][kHR][kTW];
+    __shared__ uint8_t sRGB[kTH][kTW * 3];
+    const uint8_t* pslot = planes + (int64_t)img * plane_cap;
+    uint8_t* o = out + (int64_t)img * out_stride;
+    const int W = d.W, H = d.H, t = threadIdx.x;
+    const int ntx = (W + kTW - 1) / kTW, nty = (H + kTH - 1) / kTH;
+    const int64_t ntiles = (int64_t)ntx * nty;
+    const uint8_t* P0 = pslot;
+    const int s0 = d.c[0].stride;
+    if (d.nc == 1) {  // gray: stride removal (jpeg_dec.h:854-865)
+        const int64_t total = (int64_t)W * H;
+        for (int64_t k = (int64_t)blockIdx.x * 256 + t; k < total; k += (int64_t)gridDim.x * 256) {
+            const int y = (int)(k / W), x = (int)(k - (int64_t)y * W);
+            o[k] = P0[(int64_t)y * s0 + x];
+        }
+        return;
+    }
+    const uint8_t* P[3] = {P0, P0 + comp_plane_off(d, 1), P0 + comp_plane_off(d, 2)};
+    const int kind1 = fused_kind(d, 1), kind2 = fused_kind(d, 2);
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int ty = (int)(tile / ntx), tx = (int)(tile - (int64_t)ty * ntx);
+        const int X0 = tx * kTW, Y0 = ty * kTH;
+        // stage the horizontally doubled chroma rows a vertical doubling will read
+        for (int c = 1; c <= 2; ++c) {
+            const int kind = c == 1 ? kind1 : kind2;
+            if (kind != 3) continue;
+            const Comp& cc = d.c[c];
+            const int R0 = max(0, (Y0 >> 1) - 2), R1 = min(cc.h - 1, (Y0 >> 1) + 9);
+            for (int k = t; k < kHR * kTW; k += 256) {
+                const int rr = k / kTW, xx = k - rr * kTW;
+                const int r = R0 + rr, x = X0 + xx;
+                if (r <= R1 && x < W) sH[c - 1][rr][xx] = (uint8_t)hval(P[c], cc.w, cc.stride, r, x);
+            }
+        }
+        __syncthreads();
+        {
+            const int ly = t >> 4, lx0 = (t & 15) * 4;
+            const int y = Y0 + ly;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lx = lx0 + q, x = X0 + lx;
+                if (y < H && x < W) {
+                    int ch[2];
+#pragma unroll
+                    for (int c = 1; c <= 2; ++c) {
+                        const int kind = c == 1 ? kind1 : kind2;
+                        const Comp& cc = d.c[c];
+                        const uint8_t* C = P[c];
+                        int v;
+                        if (kind == 0) {
+                            v = C[(int64_t)y * cc.stride + x];
+                        } else if (kind == 1) {
+                            v = hval(C, cc.w, cc.stride, y, x);
+                        } else if (kind == 2) {  // vertical pass reads the component's own stride (:765)
+                            v = double_tap(y, cc.h, [&](int i) { return (int)C[(int64_t)i * cc.stride + x]; },
+                                           [&](int j) { return (int)C[(int64_t)(cc.h - j) * cc.stride + x]; });
+                        } else {
+                            const int R0 = max(0, (Y0 >> 1) - 2);
+                            v = double_tap(y, cc.h, [&](int i) { return (int)sH[c - 1][i - R0][lx]; },
+                                           [&](int j) { return (int)sH[c - 1][cc.h - j - R0][lx]; });
+                        }
+                        ch[c - 1] = v;
+                    }
+                    ycc_to_rgb(P0[(int64_t)y * s0 + x], ch[0], ch[1], &sRGB[ly][lx * 3]);
+                }
+            }
+        }
+        __syncthreads();
+        const int wpx = min(kTW, W - X0), rowb = wpx * 3;
+        for (int k = t; k < kTH * kTW * 3; k += 256) {
+            const int ly = k / (kTW * 3), bx = k - ly * (kTW * 3);
+            const int y = Y0 + ly;
+            if (y < H && bx < rowb) o[((int64_t)y * W + X0) * 3 + bx] = sRGB[ly][bx];
+        }
+        __syncthreads();
     }
 }
 
@@ -315,6 +428,8 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     E(kStUpsample);
     B(kStConvert);
     const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 16384 / n));
+    hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride);
     hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
                        ws.tmp_cap, d_out, out_stride);
     hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(tb), 0, st, n, ws.desc, d_status, d_dims);

@@ -153,18 +153,20 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
         int32_t pred[3] = {ent[j].p0, ent[j].p1, ent[j].p2};
         const int64_t errbits = errpos == INT64_MAX ? INT64_MAX : errpos * 8;
         bool bad = false;
-        for (int64_t bi = ent[j].G; bi < total && r.pos() < limit && !bad; ++bi) {
-            const int ci = T.comp_of[b];
-            int16_t blk[64];
-            std::memset(blk, 0, sizeof blk);
-            do {
-                if (r.pos() + 16 > errbits) bad = true;
-                const int rc = decode_unit(r, T, bpm, b, z, coefi, val);
-                if (rc != kUnitOk || r.pos() > errbits) bad = true;
-                if (coefi == 0) { pred[ci] = wadd(pred[ci], val); dc[bi] = pred[ci]; }
-                else if (coefi > 0) blk[nat_of_zig(coefi)] = (int16_t)val;
-            } while (z != 0 && !bad);
-            std::memcpy(coef + bi * 64, blk, sizeof blk);
+        int64_t bi = ent[j].G;
+        int ci = 0;
+        while (bi < total) {  // k_spec_write's flat loop
+            if (z == 0) {
+                if (r.pos() >= limit) break;
+                ci = T.comp_of[b];
+            }
+            if (r.pos() + 16 > errbits) bad = true;
+            const int rc = decode_unit(r, T, bpm, b, z, coefi, val);
+            if (rc != kUnitOk || r.pos() > errbits) bad = true;
+            if (bad) break;
+            if (coefi == 0) { pred[ci] = wadd(pred[ci], val); dc[bi] = pred[ci]; }
+            else if (coefi > 0) coef[bi * 64 + T.nat_of_zig[coefi]] = (int16_t)val;
+            if (z == 0) ++bi;
         }
         anybad |= bad;
     }
