@@ -298,20 +298,24 @@ __device__ __forceinline__ int hval(const uint8_t* P, int w, int s, int r, int x
     return double_tap(x, w, [&](int i) { return (int)row[i]; }, [&](int j) { return (int)row[s - j]; });
 }
 
-constexpr int kTW = 64, kTH = 16, kHR = 12;  // tile width/height, H rows staged per tile
+constexpr int kTW = 64, kTH = 16, kHR = 12, kCW = 40;  // tile, staged H rows, staged chroma cols
+
+// Interior 4-tap doubling (jpeg_dec.h:749-750) of samples a..e at output parity odd/even.
+__device__ __forceinline__ int tap_mid(int o, int a, int b, int c, int e) {
+    return (o & 1) ? tap4(a, b, c, e) : tap4(e, c, b, a);
+}
 
 __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
                                                        int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     if (d.status != kOk || !fused_ok(d)) return;
-    __shared__ uint8_t sH[2][kHR][kTW];
-    __shared__ uint8_t sRGB[kTH][kTW * 3];
+    __shared__ uint8_t sC[2][kHR][kCW];      // raw chroma window
+    __shared__ uint8_t sH[2][kHR][kTW];      // horizontally doubled chroma rows
+    __shared__ uint32_t sRGB[kTH][kTW * 3 / 4];
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     uint8_t* o = out + (int64_t)img * out_stride;
     const int W = d.W, H = d.H, t = threadIdx.x;
-    const int ntx = (W + kTW - 1) / kTW, nty = (H + kTH - 1) / kTH;
-    const int64_t ntiles = (int64_t)ntx * nty;
     const uint8_t* P0 = pslot;
     const int s0 = d.c[0].stride;
     if (d.nc == 1) {  // gray: stride removal (jpeg_dec.h:854-865)
@@ -322,62 +326,106 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
         }
         return;
     }
+    const int ntx = (W + kTW - 1) / kTW, nty = (H + kTH - 1) / kTH;
+    const int ntiles = ntx * nty;
     const uint8_t* P[3] = {P0, P0 + comp_plane_off(d, 1), P0 + comp_plane_off(d, 2)};
-    const int kind1 = fused_kind(d, 1), kind2 = fused_kind(d, 2);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int ty = (int)(tile / ntx), tx = (int)(tile - (int64_t)ty * ntx);
+    const int kind[2] = {fused_kind(d, 1), fused_kind(d, 2)};
+    const bool aligned_out = ((W * 3) & 3) == 0;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int ty = tile / ntx, tx = tile - ty * ntx;
         const int X0 = tx * kTW, Y0 = ty * kTH;
-        // stage the horizontally doubled chroma rows a vertical doubling will read
-        for (int c = 1; c <= 2; ++c) {
-            const int kind = c == 1 ? kind1 : kind2;
-            if (kind != 3) continue;
-            const Comp& cc = d.c[c];
-            const int R0 = max(0, (Y0 >> 1) - 2), R1 = min(cc.h - 1, (Y0 >> 1) + 9);
-            for (int k = t; k < kHR * kTW; k += 256) {
-                const int rr = k / kTW, xx = k - rr * kTW;
-                const int r = R0 + rr, x = X0 + xx;
-                if (r <= R1 && x < W) sH[c - 1][rr][xx] = (uint8_t)hval(P[c], cc.w, cc.stride, r, x);
+        const int R0 = max(0, (Y0 >> 1) - 2), CX0 = max(0, (X0 >> 1) - 2);
+        // 1) raw chroma window + 2) horizontally doubled rows, for components doubled both ways
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (kind[c] != 3) continue;
+            const Comp& cc = d.c[c + 1];
+            const uint8_t* C = P[c + 1];
+            const int R1 = min(cc.h - 1, (Y0 >> 1) + 9);
+            for (int k = t; k < kHR * kCW; k += 256) {
+                const int rr = k / kCW, xx = k - rr * kCW;
+                const int r = R0 + rr, x = CX0 + xx;
+                if (r <= R1 && x < cc.stride) sC[c][rr][xx] = C[r * cc.stride + x];
             }
         }
         __syncthreads();
-        {
-            const int ly = t >> 4, lx0 = (t & 15) * 4;
-            const int y = Y0 + ly;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int lx = lx0 + q, x = X0 + lx;
-                if (y < H && x < W) {
+        for (int c = 0; c < 2; ++c) {
+            if (kind[c] != 3) continue;
+            const Comp& cc = d.c[c + 1];
+            const uint8_t* C = P[c + 1];
+            const int R1 = min(cc.h - 1, (Y0 >> 1) + 9), n2 = cc.w << 1;
+            for (int k = t; k < kHR * kTW; k += 256) {
+                const int rr = k / kTW, xx = k - rr * kTW;
+                const int r = R0 + rr, x = X0 + xx;
+                if (r > R1 || x >= W) continue;
+                int v;
+                if (x >= 3 && x < n2 - 3) {
+                    const int q = ((x - 3) >> 1) - CX0;
+                    v = tap_mid(x, sC[c][rr][q], sC[c][rr][q + 1], sC[c][rr][q + 2], sC[c][rr][q + 3]);
+                } else {
+                    v = hval(C, cc.w, cc.stride, r, x);  // image edges (stride-end right taps)
+                }
+                sH[c][rr][xx] = (uint8_t)v;
+            }
+        }
+        __syncthreads();
+        // 3) per pixel: vertical doubling from sH (or the single-direction forms), YCbCr->RGB
+        {
+            const int ly = t >> 4, lx0 = (t & 15) * 4, y = Y0 + ly;
+            uint8_t rgb[12];
+            if (y < H) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int lx = lx0 + q, x = X0 + lx;
+                    if (x >= W) break;
                     int ch[2];
 #pragma unroll
-                    for (int c = 1; c <= 2; ++c) {
-                        const int kind = c == 1 ? kind1 : kind2;
-                        const Comp& cc = d.c[c];
-                        const uint8_t* C = P[c];
+                    for (int c = 0; c < 2; ++c) {
+                        const Comp& cc = d.c[c + 1];
+                        const uint8_t* C = P[c + 1];
                         int v;
-                        if (kind == 0) {
-                            v = C[(int64_t)y * cc.stride + x];
-                        } else if (kind == 1) {
+                        if (kind[c] == 3) {
+                            const int h2 = cc.h << 1;
+                            if (y >= 3 && y < h2 - 3) {
+                                const int rr = ((y - 3) >> 1) - R0;
+                                v = tap_mid(y, sH[c][rr][lx], sH[c][rr + 1][lx], sH[c][rr + 2][lx], sH[c][rr + 3][lx]);
+                            } else {
+                                v = double_tap(y, cc.h, [&](int i) { return (int)sH[c][i - R0][lx]; },
+                                               [&](int j) { return (int)sH[c][cc.h - j - R0][lx]; });
+                            }
+                        } else if (kind[c] == 0) {
+                            v = C[y * cc.stride + x];
+                        } else if (kind[c] == 1) {
                             v = hval(C, cc.w, cc.stride, y, x);
-                        } else if (kind == 2) {  // vertical pass reads the component's own stride (:765)
-                            v = double_tap(y, cc.h, [&](int i) { return (int)C[(int64_t)i * cc.stride + x]; },
-                                           [&](int j) { return (int)C[(int64_t)(cc.h - j) * cc.stride + x]; });
-                        } else {
-                            const int R0 = max(0, (Y0 >> 1) - 2);
-                            v = double_tap(y, cc.h, [&](int i) { return (int)sH[c - 1][i - R0][lx]; },
-                                           [&](int j) { return (int)sH[c - 1][cc.h - j - R0][lx]; });
+                        } else {  // vertical only: the component's own stride (jpeg_dec.h:765)
+                            v = double_tap(y, cc.h, [&](int i) { return (int)C[i * cc.stride + x]; },
+                                           [&](int j) { return (int)C[(cc.h - j) * cc.stride + x]; });
                         }
-                        ch[c - 1] = v;
+                        ch[c] = v;
                     }
-                    ycc_to_rgb(P0[(int64_t)y * s0 + x], ch[0], ch[1], &sRGB[ly][lx * 3]);
+                    ycc_to_rgb(P0[y * s0 + x], ch[0], ch[1], &rgb[3 * q]);
                 }
+                uint8_t* srow = reinterpret_cast<uint8_t*>(&sRGB[ly][0]);
+#pragma unroll
+                for (int k = 0; k < 12; ++k) srow[lx0 * 3 + k] = rgb[k];
             }
         }
         __syncthreads();
         const int wpx = min(kTW, W - X0), rowb = wpx * 3;
-        for (int k = t; k < kTH * kTW * 3; k += 256) {
-            const int ly = k / (kTW * 3), bx = k - ly * (kTW * 3);
-            const int y = Y0 + ly;
-            if (y < H && bx < rowb) o[((int64_t)y * W + X0) * 3 + bx] = sRGB[ly][bx];
+        if (aligned_out && rowb == kTW * 3) {  // full tile row, 4-byte aligned: dword stores
+            for (int k = t; k < kTH * kTW * 3 / 4; k += 256) {
+                const int ly = k / (kTW * 3 / 4), wd = k - ly * (kTW * 3 / 4);
+                const int y = Y0 + ly;
+                if (y < H) reinterpret_cast<uint32_t*>(o + ((int64_t)y * W + X0) * 3)[wd] = sRGB[ly][wd];
+            }
+        } else {
+            for (int k = t; k < kTH * kTW * 3; k += 256) {
+                const int ly = k / (kTW * 3), bx = k - ly * (kTW * 3);
+                const int y = Y0 + ly;
+                if (y < H && bx < rowb)
+                    o[((int64_t)y * W + X0) * 3 + bx] = reinterpret_cast<const uint8_t*>(&sRGB[ly][0])[bx];
+            }
         }
         __syncthreads();
     }

@@ -368,8 +368,11 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
     }
 }
 
-// Coefficients go straight to the (pre-zeroed, k_zero_coef) block buffer: one flat loop over
-// codes per lane, so lanes of a wave never wait for each other at block boundaries.
+// One flat loop over codes per lane (lanes of a wave never wait for each other at block
+// boundaries); each block is assembled in the lane's LDS slot and leaves as eight 16-byte
+// stores when it ends (scattered 2-byte global stores amplified HBM writes ~10x).
+constexpr int kSlotWords = 36;  // 144-byte lane slot: 16-lane b128 groups hit distinct banks
+
 __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     const int32_t* __restrict__ wgpre, const int32_t* __restrict__ totals,
                                                     const uint8_t* __restrict__ U, int64_t ucap,
@@ -377,8 +380,13 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                     int64_t coef_cap) {
     __shared__ LdsTables T;
+    __shared__ int4 slots[kLanes][kSlotWords / 4];
     int cur = -1;
     const int total = totals[1];
+    int4* slot = &slots[threadIdx.x][0];
+    int16_t* sv = reinterpret_cast<int16_t*>(slot);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
         SpecImg& s = spec[i];
@@ -399,7 +407,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         while (z != 0) decode_unit(r, T, bpm, b, z, coef, val);
         int32_t pred[3] = {le.p0, le.p1, le.p2};
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
-        int16_t* A = ac + (int64_t)i * coef_cap * 64;
+        int4* A = reinterpret_cast<int4*>(ac + (int64_t)i * coef_cap * 64);
         int32_t* D = dcv + (int64_t)i * coef_cap;
         const int64_t total_blocks = s.total_blocks;
         int64_t bi = le.G;
@@ -419,25 +427,24 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                 pred[ci] = wadd(pred[ci], val);
                 D[bi] = pred[ci];
             } else if (coef > 0) {
-                A[bi * 64 + T.nat_of_zig[coef]] = (int16_t)val;
+                sv[T.nat_of_zig[coef]] = (int16_t)val;
             }
-            if (z == 0) ++bi;
+            if (z == 0) {  // block complete: flush and clear the slot
+                int4* dst = A + bi * 8;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    dst[q] = slot[q];
+                    slot[q] = make_int4(0, 0, 0, 0);
+                }
+                ++bi;
+            }
         }
-        if (bad) atomicOr(&s.err, kSpecSyntax);
+        if (bad) {
+            atomicOr(&s.err, kSpecSyntax);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
+        }
     }
-}
-
-// Zero the coefficient blocks each parsed image will use (the write pass stores only non-zero
-// AC terms). 16-byte stores, grid-stride over every image's blocks.
-__global__ __launch_bounds__(256) void k_zero_coef(int n, const Desc* __restrict__ desc, int16_t* __restrict__ ac,
-                                                   int64_t coef_cap) {
-    const int i = blockIdx.y;
-    const Desc& d = desc[i];
-    if (d.status != kPending) return;
-    const int64_t words = (int64_t)d.mbw * d.mbh * d.bpm * 8;  // 16-byte words
-    int4* p = reinterpret_cast<int4*>(ac + (int64_t)i * coef_cap * 64);
-    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < words; k += (int64_t)gridDim.x * 256)
-        p[k] = make_int4(0, 0, 0, 0);
 }
 
 __global__ void k_spec_finish(int n, Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
@@ -454,7 +461,6 @@ __global__ void k_spec_finish(int n, Desc* __restrict__ desc, const SpecImg* __r
 
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st) {
     const int g = 2048;  // grid-stride launches: >> 256 CUs
-    hipLaunchKernelGGL(k_zero_coef, dim3(std::max(1, 8192 / n), n), dim3(256), 0, st, n, ws.desc, ws.ac, ws.coef_cap);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.totals,
                        ws.ucap);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
