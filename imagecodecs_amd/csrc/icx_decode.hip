@@ -24,7 +24,7 @@ int64_t ws_tmp_cap(int w, int h) { return ((int64_t)w + 8) * ((int64_t)h + 8); }
 
 // ------------------------------------------------------------------------------ parse
 // One 64-lane workgroup per image: zero the descriptor together, lane 0 walks the markers,
-// then all lanes fill the four 2048-entry fast Huffman tables.
+// then all lanes fill the four 1024-entry fast Huffman tables.
 __global__ __launch_bounds__(64) void k_parse(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                                               const uint64_t* __restrict__ size, Desc* __restrict__ desc, int max_w,
                                               int max_h, uint64_t out_stride) {
@@ -212,6 +212,7 @@ __device__ __forceinline__ Plane pass_plane(const Desc& d, int ci, int p, const 
 }
 
 __device__ __forceinline__ bool fused_ok(const Desc& d);
+__device__ __forceinline__ int stream_kind(const Desc& d);
 // grid: (x: pixel tiles, y: slot*3 + comp). Pass `p` of every component that has one.
 __global__ __launch_bounds__(256) void k_upsample(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
                                                   uint8_t* __restrict__ tmp, int64_t plane_cap, int64_t tmp_cap, int p) {
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
                                                        int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk || !fused_ok(d)) return;
+    if (d.status != kOk || !fused_ok(d) || stream_kind(d) >= 0) return;
     __shared__ uint8_t sC[2][kHR][kCW];      // raw chroma window
     __shared__ uint8_t sH[2][kHR][kTW];      // horizontally doubled chroma rows
     __shared__ uint32_t sRGB[kTH][kTW * 3 / 4];
@@ -318,14 +319,6 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
     const int W = d.W, H = d.H, t = threadIdx.x;
     const uint8_t* P0 = pslot;
     const int s0 = d.c[0].stride;
-    if (d.nc == 1) {  // gray: stride removal (jpeg_dec.h:854-865)
-        const int64_t total = (int64_t)W * H;
-        for (int64_t k = (int64_t)blockIdx.x * 256 + t; k < total; k += (int64_t)gridDim.x * 256) {
-            const int y = (int)(k / W), x = (int)(k - (int64_t)y * W);
-            o[k] = P0[(int64_t)y * s0 + x];
-        }
-        return;
-    }
     const int ntx = (W + kTW - 1) / kTW, nty = (H + kTH - 1) / kTH;
     const int ntiles = ntx * nty;
     const uint8_t* P[3] = {P0, P0 + comp_plane_off(d, 1), P0 + comp_plane_off(d, 2)};
@@ -431,6 +424,184 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
     }
 }
 
+
+// ------------------------------------------------------------ streaming upsample + convert
+// The common layouts -- gray, and 3 components whose luma is full size and whose two chroma
+// components take the same doubling program (4:4:4, 4:2:2, 4:4:0, 4:2:0) -- are converted by
+// register streaming: one wave owns a 256-pixel-wide, kSH-row strip, each lane owns 4 adjacent
+// columns and walks down the strip. Horizontally doubled chroma rows (jpeg_dec.h:736-760) are
+// made from two dword loads per row; the vertical pass (:762-791) slides a 5-row window held in
+// registers; YCbCr->RGB (:834-853) is stored as one 12-byte write per lane. No LDS, no barriers.
+// Vertical edge rows are wave-uniform branches; horizontal edge lanes take the generic taps.
+constexpr int kSH = 64;
+
+// 4 = gray; 0..3 = the shared chroma kind; -1 = left to k_convert_fused / the generic passes.
+__device__ __forceinline__ int stream_kind(const Desc& d) {
+    if (d.nc == 1) return 4;
+    if (d.nc != 3 || fused_kind(d, 0) != 0) return -1;
+    const int k = fused_kind(d, 1);
+    if (k < 0 || fused_kind(d, 2) != k) return -1;
+    if ((k & 1) && min(d.c[1].w, d.c[2].w) < 4) return -1;
+    if ((k & 2) && min(d.c[1].h, d.c[2].h) < 4) return -1;
+    return k;
+}
+
+struct CPl {
+    const uint8_t* p;
+    int w, h, s;
+};
+__device__ __forceinline__ uint32_t ld4(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+__device__ __forceinline__ int bt(uint32_t v, int i) { return (v >> (8 * i)) & 255; }
+// Packs four 0..255 values with v_perm_b32. (A shift/or pack of clamped taps lets the compiler
+// form gfx950's v_ashr_pk_u8_i32, whose result's upper half was observed to leak into the
+// neighbouring bytes; the explicit byte permutes avoid that pattern.)
+__device__ __forceinline__ uint32_t pack4(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3) {
+    const uint32_t lo = __builtin_amdgcn_perm(t1, t0, 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm(t3, t2, 0x0c0c0400u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+template <class F>
+__device__ __forceinline__ uint32_t pmap(F f) {
+    return pack4((uint32_t)f(0), (uint32_t)f(1), (uint32_t)f(2), (uint32_t)f(3));
+}
+
+// Chroma samples for output columns 4M..4M+3 of real row r: the horizontally doubled row when
+// KH, else the raw samples. `fast` = all four outputs use interior taps and stay inside the row.
+template <bool KH>
+__device__ __forceinline__ uint32_t chroma_row(const CPl& c, int r, int M, bool fast) {
+    const uint8_t* row = c.p + (int64_t)r * c.s;
+    if (!KH) return ld4(row + 4 * M);
+    if (fast) {
+        const int base = (2 * M - 2) & ~3;
+        const uint64_t w = (uint64_t)ld4(row + base) | ((uint64_t)ld4(row + base + 4) << 32);
+        const uint64_t b = w >> ((M & 1) ? 0 : 16);  // bytes b0..b5 = samples 2M-2 .. 2M+3
+        const int b0 = (int)(b & 255), b1 = (int)((b >> 8) & 255), b2 = (int)((b >> 16) & 255);
+        const int b3 = (int)((b >> 24) & 255), b4 = (int)((b >> 32) & 255), b5 = (int)((b >> 40) & 255);
+        return pack4(tap4(b3, b2, b1, b0), tap4(b1, b2, b3, b4), tap4(b4, b3, b2, b1), tap4(b2, b3, b4, b5));
+    }
+    const int n2 = c.w << 1, s = c.s;
+    return pmap([&](int i) {
+        const int x = 4 * M + i;
+        if (x >= n2) return 0;
+        return (int)double_tap(x, c.w, [&](int k) { return (int)row[k]; }, [&](int j) { return (int)row[s - j]; });
+    });
+}
+
+// Vertical doubling at output rows 2k (even) / 2k+1 (odd) from the window w0..w4 = doubled
+// rows k-2..k+2 (h >= 4 real rows; the order of the edge cases follows double_tap).
+__device__ __forceinline__ uint32_t vtap_even(int k, int h, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    if (k == 0) return pmap([&](int i) { return tap2(bt(w2, i), bt(w3, i)); });
+    if (k == 1) return pmap([&](int i) { return tap3a(bt(w1, i), bt(w2, i), bt(w3, i)); });
+    if (k == h - 1) return pmap([&](int i) { return tap3x(bt(w2, i), bt(w1, i), bt(w0, i)); });
+    return pmap([&](int i) { return tap4(bt(w3, i), bt(w2, i), bt(w1, i), bt(w0, i)); });
+}
+__device__ __forceinline__ uint32_t vtap_odd(int k, int h, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4) {
+    if (k == 0) return pmap([&](int i) { return tap3x(bt(w2, i), bt(w3, i), bt(w4, i)); });
+    if (k == h - 2) return pmap([&](int i) { return tap3a(bt(w3, i), bt(w2, i), bt(w1, i)); });
+    if (k == h - 1) return pmap([&](int i) { return tap2(bt(w2, i), bt(w1, i)); });
+    return pmap([&](int i) { return tap4(bt(w1, i), bt(w2, i), bt(w3, i), bt(w4, i)); });
+}
+
+struct StreamOut {
+    uint8_t* o;
+    int W;
+    bool vec;  // rows 4-byte aligned
+    __device__ __forceinline__ void put(int y, int x0, const uint8_t (&px)[12], int nb) const {
+        uint8_t* dst = o + ((int64_t)y * W + x0) * 3;
+        if (vec && nb == 12) {
+            uint32_t w[3];
+            __builtin_memcpy(w, px, 12);
+            uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+            __builtin_nontemporal_store(w[0], d32);
+            __builtin_nontemporal_store(w[1], d32 + 1);
+            __builtin_nontemporal_store(w[2], d32 + 2);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 12; ++i)
+                if (i < nb) dst[i] = px[i];
+        }
+    }
+};
+
+template <int K>
+__device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot, const StreamOut& so) {
+    constexpr bool KH = (K & 1) != 0, KV = (K & 2) != 0;
+    const int W = d.W, H = d.H, s0 = d.c[0].stride;
+    const uint8_t* P0 = pslot;
+    CPl c1{}, c2{};
+    if (K != 4) {
+        c1 = CPl{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
+        c2 = CPl{pslot + comp_plane_off(d, 2), d.c[2].w, d.c[2].h, d.c[2].stride};
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int nsx = (W + 255) >> 8, nsy = (H + kSH - 1) / kSH, nstrip = nsx * nsy;
+    for (int strip = blockIdx.x * 4 + wv; strip < nstrip; strip += gridDim.x * 4) {
+        const int sy = strip / nsx, sx = strip - sy * nsx;
+        const int M = sx * 64 + lane, x0 = 4 * M;
+        if (x0 >= W) continue;
+        const int nb = min(4, W - x0) * 3;
+        const int Y0 = sy * kSH, Y1 = min(H, Y0 + kSH);
+        auto emit = [&](int y, uint32_t cb, uint32_t cr) {
+            const uint32_t yv = ld4(P0 + (int64_t)y * s0 + x0);
+            uint8_t px[12];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
+            so.put(y, x0, px, nb);
+        };
+        if (K == 4) {  // gray: stride removal (jpeg_dec.h:854-865)
+            for (int y = Y0; y < Y1; ++y) {
+                const uint32_t v = ld4(P0 + (int64_t)y * s0 + x0);
+                uint8_t* dst = so.o + (int64_t)y * W + x0;
+                if (so.vec && nb == 12) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(dst));
+                else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (3 * i < nb) dst[i] = (uint8_t)bt(v, i);
+                }
+            }
+            continue;
+        }
+        // interior horizontal taps for all 4 outputs, reads inside the row (chroma_row<true>)
+        const bool f1 = M >= 1 && x0 + 3 <= 2 * c1.w - 4 && 2 * M + 5 < c1.s;
+        const bool f2 = M >= 1 && x0 + 3 <= 2 * c2.w - 4 && 2 * M + 5 < c2.s;
+        if (!KV) {
+            for (int y = Y0; y < Y1; ++y) emit(y, chroma_row<KH>(c1, y, M, f1), chroma_row<KH>(c2, y, M, f2));
+            continue;
+        }
+        const int k0 = Y0 >> 1;
+        auto rowc = [&](const CPl& c, int r, bool f) { return chroma_row<KH>(c, min(max(r, 0), c.h - 1), M, f); };
+        uint32_t a0 = rowc(c1, k0 - 2, f1), a1 = rowc(c1, k0 - 1, f1), a2 = rowc(c1, k0, f1), a3 = rowc(c1, k0 + 1, f1);
+        uint32_t e0 = rowc(c2, k0 - 2, f2), e1 = rowc(c2, k0 - 1, f2), e2 = rowc(c2, k0, f2), e3 = rowc(c2, k0 + 1, f2);
+        for (int k = k0; 2 * k < Y1; ++k) {
+            const uint32_t a4 = rowc(c1, k + 2, f1), e4 = rowc(c2, k + 2, f2);
+            emit(2 * k, vtap_even(k, c1.h, a0, a1, a2, a3), vtap_even(k, c2.h, e0, e1, e2, e3));
+            if (2 * k + 1 < Y1)
+                emit(2 * k + 1, vtap_odd(k, c1.h, a1, a2, a3, a4), vtap_odd(k, c2.h, e1, e2, e3, e4));
+            a0 = a1; a1 = a2; a2 = a3; a3 = a4;
+            e0 = e1; e1 = e2; e2 = e3; e3 = e4;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_convert_stream(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
+                                                        int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (d.status != kOk) return;
+    const int k = stream_kind(d);
+    if (k < 0) return;
+    const uint8_t* pslot = planes + (int64_t)img * plane_cap;
+    uint8_t* o = out + (int64_t)img * out_stride;
+    const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
+    switch (k) {
+        case 0: stream_image<0>(d, pslot, so); break;
+        case 1: stream_image<1>(d, pslot, so); break;
+        case 2: stream_image<2>(d, pslot, so); break;
+        case 3: stream_image<3>(d, pslot, so); break;
+        default: stream_image<4>(d, pslot, so); break;
+    }
+}
+
 // --------------------------------------------------------------------------- finalize
 __global__ void k_finalize(int n, const Desc* __restrict__ desc, int32_t* __restrict__ status,
                            int32_t* __restrict__ dims) {
@@ -476,6 +647,10 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     E(kStUpsample);
     B(kStConvert);
     const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 16384 / n));
+    const int sxg = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)(ws.max_w + 255) / 256) *
+                                                                 ((ws.max_h + kSH - 1) / kSH) / 4 + 1, 16384 / n));
+    hipLaunchKernelGGL(k_convert_stream, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride);
     hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride);
     hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,

@@ -54,7 +54,7 @@ ICX_HD uint8_t clip8(int32_t v) { return v < 0 ? 0 : (v > 255 ? 255 : (uint8_t)v
 // a 16-bit window v has code length L = min{L : v < bound[L]}, symbol index
 // first[L] + ((v - bound[L-1]) >> (16-L)); v >= bound[16] is an invalid code (bits == 0).
 // fast[] resolves lengths <= kFastBits with one lookup.
-constexpr int kFastBits = 11;
+constexpr int kFastBits = 10;
 struct Huff {
     uint16_t fast[1 << kFastBits];  // (len << 8) | sym, 0 = not resolvable in kFastBits
     uint32_t bound[17];

@@ -371,7 +371,9 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
 // One flat loop over codes per lane (lanes of a wave never wait for each other at block
 // boundaries); each block is assembled in the lane's LDS slot and leaves as eight 16-byte
 // stores when it ends (scattered 2-byte global stores amplified HBM writes ~10x).
-constexpr int kSlotWords = 36;  // 144-byte lane slot: 16-lane b128 groups hit distinct banks
+// 128-byte lane slot; 16-byte chunk q of lane t lives at chunk q ^ (t & 7), so the b128 reads
+// of a 16-lane group hit distinct banks.
+__device__ __forceinline__ int slot_elem(int t, int n) { return (((n >> 3) ^ (t & 7)) << 3) | (n & 7); }
 
 __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     const int32_t* __restrict__ wgpre, const int32_t* __restrict__ totals,
@@ -380,7 +382,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                     int64_t coef_cap) {
     __shared__ LdsTables T;
-    __shared__ int4 slots[kLanes][kSlotWords / 4];
+    __shared__ int4 slots[kLanes][8];
     int cur = -1;
     const int total = totals[1];
     int4* slot = &slots[threadIdx.x][0];
@@ -427,14 +429,15 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                 pred[ci] = wadd(pred[ci], val);
                 D[bi] = pred[ci];
             } else if (coef > 0) {
-                sv[T.nat_of_zig[coef]] = (int16_t)val;
+                sv[slot_elem(threadIdx.x, T.nat_of_zig[coef])] = (int16_t)val;
             }
             if (z == 0) {  // block complete: flush and clear the slot
                 int4* dst = A + bi * 8;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    dst[q] = slot[q];
-                    slot[q] = make_int4(0, 0, 0, 0);
+                    const int sq = q ^ (threadIdx.x & 7);
+                    dst[q] = slot[sq];
+                    slot[sq] = make_int4(0, 0, 0, 0);
                 }
                 ++bi;
             }
