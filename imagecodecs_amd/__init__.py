@@ -29,7 +29,9 @@ OK, NO_JPEG, UNSUPPORTED, OUT_OF_MEM, INTERNAL_ERR, SYNTAX_ERROR = range(6)  # n
 RESULT_NAMES = ["NJ_OK", "NJ_NO_JPEG", "NJ_UNSUPPORTED", "NJ_OUT_OF_MEM", "NJ_INTERNAL_ERR", "NJ_SYNTAX_ERROR"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libicx.so")
+# ICX_LIB selects another build of the same library (e.g. an instrumented variant); it is
+# still the HIP library, there is no other implementation to select.
+LIB_PATH = os.environ.get("ICX_LIB") or os.path.join(_HERE, "lib", "libicx.so")
 _LIB = None
 
 

@@ -186,7 +186,8 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     ICX_HIP(ctx, hipMalloc(&ws.totals, sizeof(int32_t) * 4), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.tiles, sizeof(TileRec) * ws.tiles_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.tile_obase, sizeof(int32_t) * ws.tiles_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.ucap * group), nullptr);
+    // + slack: the entropy readers load whole 16-byte chunks (icx_spec_core.h Reader)
+    ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.ucap * group + 256), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.X, sizeof(uint64_t) * ws.lanes_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.sub, sizeof(SubRec) * ws.lanes_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.ent, sizeof(LaneEntry) * ws.lanes_cap), nullptr);

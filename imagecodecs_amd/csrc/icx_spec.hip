@@ -185,6 +185,8 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
                                                     const int32_t* __restrict__ tile_obase, uint8_t* __restrict__ U,
                                                     int64_t ucap) {
     __shared__ int sh[256];
+    __shared__ uint32_t sbuf[kTileBytes / 4 + 8];  // the tile's kept bytes, then copied out
+    __shared__ int s_kept;
     const int total = totals[0];
     for (int t = blockIdx.x; t < total; t += gridDim.x) {
         const int i = find_image(tilepre, n, t);
@@ -201,10 +203,29 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
         const int kept = live ? ustf_chunk<false>(R, s.scan_len, a, &end_at, &end_err, nullptr, &giveup) : 0;
         const bool before = live && (end_at >= 0 ? (tend < 0 || end_at <= tend) : (tend < 0 || a < tend));
         const int ex = block_exclusive_scan(before ? kept : 0, sh);
-        if (before && kept) {
-            const int64_t o = obase + ex;
-            if (o + kept <= s.ulen)
-                ustf_chunk<true>(R, s.scan_len, a, &end_at, &end_err, U + (int64_t)i * ucap + o, &giveup);
+        uint8_t* sb = reinterpret_cast<uint8_t*>(sbuf);
+        if (before && kept) ustf_chunk<true>(R, s.scan_len, a, &end_at, &end_err, sb + ex, &giveup);
+        if (threadIdx.x == 255) s_kept = ex + (before ? kept : 0);
+        __syncthreads();
+        // copy out: bytes up to the first 16-byte boundary and after the last one byte-wise
+        // (they may share a 16-byte unit with the neighbouring tiles), the rest as 16-byte units
+        const int64_t nout = live ? min<int64_t>(s_kept, s.ulen - obase) : 0;
+        if (nout > 0) {
+            uint8_t* dst = U + (int64_t)i * ucap + obase;  // U + i*ucap is 4 KiB aligned
+            const int head = (int)min<int64_t>(nout, (16 - (obase & 15)) & 15);
+            const int nunit = (int)((nout - head) >> 4);
+            const int tail0 = head + nunit * 16;
+            const int k = threadIdx.x;
+            if (k < head) dst[k] = sb[k];
+            if (k < nout - tail0) dst[tail0 + k] = sb[tail0 + k];
+            if (k < nunit) {
+                const int b0 = head + 16 * k, shb = (b0 & 3) * 8;
+                const uint32_t* q = sbuf + (b0 >> 2);
+                uint32_t v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (uint32_t)((((uint64_t)q[j + 1] << 32) | q[j]) >> shb);
+                *reinterpret_cast<uint4*>(dst + b0) = make_uint4(v[0], v[1], v[2], v[3]);
+            }
         }
         __syncthreads();
     }
@@ -215,15 +236,7 @@ __device__ __forceinline__ void load_tables(LdsTables& T, const Desc& d) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&d.huff[0]);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&T.huff[0]);
     for (int k = threadIdx.x; k < (int)(sizeof(Huff) * 4 / 4); k += blockDim.x) dst[k] = src[k];
-    if (threadIdx.x < kSpecMaxBpm) {
-        int sbx, sby;
-        T.comp_of[threadIdx.x] = threadIdx.x < d.bpm ? (int8_t)mcu_block_comp(d, threadIdx.x, sbx, sby) : 0;
-    }
     if (threadIdx.x < 64) T.nat_of_zig[threadIdx.x] = kNatOfZig[threadIdx.x];
-    if (threadIdx.x < 3) {
-        T.dc_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].dc_tab;
-        T.ac_of[threadIdx.x] = (int8_t)d.c[threadIdx.x].ac_tab;
-    }
 }
 
 __device__ __forceinline__ int wg_image_setup(const int32_t* wgpre, int n, int wg, int& cur, LdsTables& T,
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(256) void k_spec_guess(int n, const Desc* __restric
         if (j >= s.nsub - 1) continue;  // the last lane's exit is never needed
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
         const int64_t sb = (int64_t)kSubBytes * 8;
-        X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, desc[i].bpm, j * sb, (j + 1) * sb, 0, rec + f * kRec,
+        X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, make_sel(desc[i]), j * sb, (j + 1) * sb, 0, rec + f * kRec,
                           nrec + f, gtot + 4 * f);
     }
 }
@@ -278,7 +291,7 @@ __global__ __launch_bounds__(256) void k_spec_count(int n, const Desc* __restric
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
         SubRec out;
         bool synced;
-        Y[f] = lane_count(U + (int64_t)i * ucap, s.ulen, T, desc[i].bpm, entry, j * sb, (j + 1) * sb, rec + f * kRec,
+        Y[f] = lane_count(U + (int64_t)i * ucap, s.ulen, T, make_sel(desc[i]), entry, j * sb, (j + 1) * sb, rec + f * kRec,
                           nrec[f], gtot + 4 * f, X[f], out, synced);
         sub[f] = out;
         if (out.mism) {  // queue for the serial repair walk
@@ -316,7 +329,7 @@ __global__ __launch_bounds__(64) void k_spec_repair(int n, const Desc* __restric
     for (int a = 0; a < nq; ++a) {
         const int64_t j = q[a];
         if (j <= done) continue;  // re-derived by an earlier walk
-        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, desc[i].bpm, j, s.nsub, (int64_t)kSubBytes * 8, X + base,
+        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, make_sel(desc[i]), j, s.nsub, (int64_t)kSubBytes * 8, X + base,
                            Y + base, rec + base * kRec, nrec + base, gtot + 4 * base, sub + base, 64);
         if (done < 0) { s.mode = 2; return; }  // pathological stream: sequential decode
     }
@@ -373,6 +386,9 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
 // stores when it ends (scattered 2-byte global stores amplified HBM writes ~10x).
 // 128-byte lane slot; 16-byte chunk q of lane t lives at chunk q ^ (t & 7), so the b128 reads
 // of a 16-lane group hit distinct banks.
+#ifndef ICX_EXP_WRITE
+#define ICX_EXP_WRITE 0  // timing experiments only: 1 = no block flush, 2 = no coefficient stores at all
+#endif
 __device__ __forceinline__ int slot_elem(int t, int n) { return (((n >> 3) ^ (t & 7)) << 3) | (n & 7); }
 
 __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
@@ -395,7 +411,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         if (s.mode != 1) continue;
         const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
         if (j >= s.nsub) continue;
-        const int bpm = desc[i].bpm;
+        const Sel S = make_sel(desc[i]);
         const int64_t base = (int64_t)s.wg_base * kLanes;
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[base + j - 1];
         const bool last = j == s.nsub - 1;
@@ -406,7 +422,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         int b = st_b(entry), z = st_z(entry), coef;
         int32_t val;
         // the block in progress at entry belongs to the previous lane
-        while (z != 0) decode_unit(r, T, bpm, b, z, coef, val);
+        while (z != 0) decode_unit(r, T, S, b, z, coef, val);
         int32_t pred[3] = {le.p0, le.p1, le.p2};
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
         int4* A = reinterpret_cast<int4*>(ac + (int64_t)i * coef_cap * 64);
@@ -418,20 +434,23 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         while (bi < total_blocks) {
             if (z == 0) {  // a block starts: stop at the next lane's territory
                 if (r.pos() >= limit) break;
-                ci = T.comp_of[b];
+                ci = S.comp(b);
             }
             // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
             if (r.pos() + 16 > errbits) bad = true;
-            const int rc = decode_unit(r, T, bpm, b, z, coef, val);
+            const int rc = decode_unit(r, T, S, b, z, coef, val);
             if (rc != kUnitOk || r.pos() > errbits) bad = true;
             if (bad) break;
             if (coef == 0) {
                 pred[ci] = wadd(pred[ci], val);
                 D[bi] = pred[ci];
             } else if (coef > 0) {
+#if ICX_EXP_WRITE < 2
                 sv[slot_elem(threadIdx.x, T.nat_of_zig[coef])] = (int16_t)val;
+#endif
             }
             if (z == 0) {  // block complete: flush and clear the slot
+#if ICX_EXP_WRITE == 0
                 int4* dst = A + bi * 8;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -439,6 +458,7 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                     dst[q] = slot[sq];
                     slot[sq] = make_int4(0, 0, 0, 0);
                 }
+#endif
                 ++bi;
             }
         }

@@ -26,12 +26,47 @@ ICX_HD bool carry_after_ff(const uint8_t* R, int64_t a, int32_t* giveup) {
     return k & 1;
 }
 
+// Fast path of the automaton: R[a..a+16) holds no 0xFF and R[a-1] is not 0xFF, so all 16 bytes
+// are kept unchanged. Reads the window with aligned dword loads (the bytes before R are the
+// file's headers, a > 0; the bytes after stay inside the scan, a + 24 <= L) and returns it in w.
+ICX_HD bool ustf_fast(const uint8_t* R, int64_t L, int64_t a, uint32_t (&w)[4]) {
+    if (a < 1 || a + kChunk + 8 > L) return false;
+    const uintptr_t p = reinterpret_cast<uintptr_t>(R + a - 1);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p & ~(uintptr_t)3);
+    const int sh = (int)(p & 3) * 8;
+    uint32_t e[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e[k] = q[k];
+    uint32_t v[5];  // bytes R[a-1 .. a+19)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = (uint32_t)((((uint64_t)e[k + 1] << 32) | e[k]) >> sh);
+    if ((v[0] & 0xFF) == 0xFF) return false;
+    uint32_t ff = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        w[k] = (v[k] >> 8) | (v[k + 1] << 24);
+        const uint32_t x = ~w[k];  // a zero byte of x is an FF byte of w
+        ff |= (x - 0x01010101u) & ~x & 0x80808080u;
+    }
+    return ff == 0;
+}
+
 template <bool WRITE>
 ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, int* end_err,
                                           uint8_t* out, int32_t* giveup) {
     *end_at = -1;
     *end_err = 0;
     if (a >= L) return 0;
+    {
+        uint32_t w[4];
+        if (ustf_fast(R, L, a, w)) {
+            if (WRITE) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) out[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+            }
+            return kChunk;
+        }
+    }
     bool after_ff = carry_after_ff(R, a, giveup);
     int kept = 0;
     const int64_t b = a + kChunk < L ? a + kChunk : L;
@@ -65,14 +100,36 @@ ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, i
 struct LdsTables {
     Huff huff[4];
     uint8_t nat_of_zig[64];
-    int8_t comp_of[kSpecMaxBpm];
-    int8_t dc_of[3], ac_of[3];
 };
+
+// Per-image MCU layout in registers (wave-uniform): component of MCU block b (2 bits per
+// block) and the DC / AC table of block b (4 bits per block: DC in bits 0-1, AC in 2-3), so
+// the code-to-code dependency chain holds a single LDS access (the fast Huffman entry).
+struct Sel {
+    int bpm;
+    uint32_t comps;
+    uint64_t tabs;
+    ICX_HD int comp(int b) const { return (int)((comps >> (2 * b)) & 3u); }
+    ICX_HD int tab(int b, bool dc) const { return (int)((tabs >> (4 * b + (dc ? 0 : 2))) & 3u); }
+};
+ICX_HD Sel make_sel(const Desc& d) {
+    Sel s{d.bpm, 0u, 0ull};
+    for (int b = 0; b < d.bpm && b < kSpecMaxBpm; ++b) {
+        int sbx, sby;
+        const int ci = mcu_block_comp(d, b, sbx, sby);
+        s.comps |= (uint32_t)ci << (2 * b);
+        s.tabs |= (uint64_t)((d.c[ci].dc_tab & 3) | ((d.c[ci].ac_tab & 3) << 2)) << (4 * b);
+    }
+    return s;
+}
 
 // MSB-first reader over U; bytes at or past ulen read as 0xFF (jpeg_dec.h:451-455).
 // Latency hiding: U is fetched in 16-byte chunks with one chunk always in flight -- `A` is
-// being drained 32 bits at a time into the 64-bit window `buf`, `B` (the next chunk) was
-// requested when A was refilled, ~24 codes before it is first needed.
+// being drained 32 bits at a time into the 64-bit window `buf`; `B` (the next chunk) was
+// requested when A was refilled and stays untouched in registers (no byte swap, no tail
+// check) until it becomes A, ~24 codes later, so its load latency is hidden. Loads are
+// 16-byte aligned and unconditional: the buffer behind U has >= 16 bytes of slack, and a
+// chunk at or past ulen is loaded from chunk 0 and replaced by 0xFF when consumed.
 struct Reader {
     const uint8_t* u;
     int64_t ulen, ucap;
@@ -80,21 +137,21 @@ struct Reader {
     int nb;
     int na;            // 32-bit words left in A
     uint64_t a0, a1;   // chunk A as a 128-bit left-aligned shift register
-    uint64_t b0, b1;   // chunk B (prefetched)
+    uint4 braw;        // chunk B as loaded (prefetched)
     int64_t next;      // index of the chunk B holds + 1
-    ICX_HD void chunk(int64_t c, uint64_t& h, uint64_t& l) const {
+    ICX_HD uint4 load(int64_t c) const {
         const int64_t o = c * 16;
-        if (o + 16 <= ulen) {
-            const uint4 v = *reinterpret_cast<const uint4*>(u + o);
-            h = ((uint64_t)__builtin_bswap32(v.x) << 32) | __builtin_bswap32(v.y);
-            l = ((uint64_t)__builtin_bswap32(v.z) << 32) | __builtin_bswap32(v.w);
-            return;
-        }
-        h = l = ~0ull;  // tail chunk: valid bytes then 0xFF padding
-        for (int i = 0; i < 16; ++i) {
-            const uint64_t byte = (o + i < ulen) ? u[o + i] : 0xFFu;
-            if (i < 8) h = (h & ~(0xFFull << (56 - 8 * i))) | (byte << (56 - 8 * i));
-            else l = (l & ~(0xFFull << (56 - 8 * (i - 8)))) | (byte << (56 - 8 * (i - 8)));
+        return *reinterpret_cast<const uint4*>(u + (o < ulen ? o : 0));
+    }
+    // chunk c's raw bytes -> big-endian 128-bit (h, l), bytes at or past ulen forced to 0xFF
+    ICX_HD void expand(int64_t c, const uint4& v, uint64_t& h, uint64_t& l) const {
+        h = ((uint64_t)__builtin_bswap32(v.x) << 32) | __builtin_bswap32(v.y);
+        l = ((uint64_t)__builtin_bswap32(v.z) << 32) | __builtin_bswap32(v.w);
+        const int64_t valid = ulen - c * 16;
+        if (valid < 16) {
+            const int kb = valid <= 0 ? 0 : (int)valid * 8;  // bits kept, 0..120
+            h = kb >= 64 ? h : (kb == 0 ? ~0ull : h | (~0ull >> kb));
+            l = kb <= 64 ? ~0ull : l | (~0ull >> (kb - 64));
         }
     }
     ICX_HD void refill() {
@@ -104,10 +161,9 @@ struct Reader {
             a0 = (a0 << 32) | (a1 >> 32);
             a1 <<= 32;
             if (--na == 0) {
-                a0 = b0;
-                a1 = b1;
+                expand(next - 1, braw, a0, a1);
                 na = 4;
-                chunk(next++, b0, b1);
+                braw = load(next++);
             }
         }
     }
@@ -115,8 +171,8 @@ struct Reader {
         u = u_;
         ulen = ulen_;
         const int64_t c = bitpos >> 7;
-        chunk(c, a0, a1);
-        chunk(c + 1, b0, b1);
+        expand(c, load(c), a0, a1);
+        braw = load(c + 1);
         next = c + 2;
         na = 4;
         buf = 0;
@@ -150,10 +206,10 @@ enum : int { kUnitOk = 0, kUnitErr = 1 };
 // On return: *coef = coefficient index written (0 = DC, 1..63 AC, -1 none), *val = value.
 // Errors (jpeg_dec.h:646, 667, 669) end the block deterministically so speculative lanes
 // keep going; on the true path any error makes the image NJ_SYNTAX_ERROR.
-ICX_HD int decode_unit(Reader& r, const LdsTables& T, int bpm, int& b, int& z, int& coef,
+ICX_HD int decode_unit(Reader& r, const LdsTables& T, const Sel& S, int& b, int& z, int& coef,
                                            int32_t& val) {
-    const int ci = T.comp_of[b];
-    const Huff& H = T.huff[z == 0 ? T.dc_of[ci] : T.ac_of[ci]];
+    const int bpm = S.bpm;
+    const Huff& H = T.huff[S.tab(b, z == 0)];
     r.refill();
     int sym = 0;
     const int len = huff_lookup(H, r.peek16(), sym);
@@ -180,7 +236,7 @@ ICX_HD int decode_unit(Reader& r, const LdsTables& T, int bpm, int& b, int& z, i
 // kRec MCU-start states (b == 0, z == 0) it passes through (rec, *nrec) and its totals tot = {DC codes,
 // DC-diff sums per component} over the whole lane. Returns the exit state: the first code
 // boundary at or after `end`.
-ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, int bpm, int64_t start, int64_t end,
+ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, const Sel& S, int64_t start, int64_t end,
                            int b0, RecState* rec, int32_t* nrec, int32_t* tot) {
     Reader r;
     r.init(U, ulen, start);
@@ -197,9 +253,9 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, i
             e.ds[1] = ds[1];
             e.ds[2] = ds[2];
         }
-        const int ci = T.comp_of[b];
+        const int ci = S.comp(b);
         const bool dc = z == 0;
-        decode_unit(r, T, bpm, b, z, coef, val);
+        decode_unit(r, T, S, b, z, coef, val);
         if (dc) {
             ++cnt;
             ds[ci] = wadd(ds[ci], val);
@@ -217,7 +273,7 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, i
 // one the guess lane recorded, both decodes coincide from there on, so the lane's totals are
 // spliced from the guess lane's and its exit is the guess exit (synced = true). Otherwise the
 // whole lane is decoded and its own exit returned.
-ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, int bpm, uint64_t entry, int64_t start,
+ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, const Sel& S, uint64_t entry, int64_t start,
                            int64_t end, const RecState* rec, int nrec, const int32_t* tot, uint64_t guess_exit,
                            SubRec& out, bool& synced) {
     Reader r;
@@ -240,9 +296,9 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, i
                 return guess_exit;
             }
         }
-        const int ci = T.comp_of[b];
+        const int ci = S.comp(b);
         const bool dc = z == 0;
-        decode_unit(r, T, bpm, b, z, coef, val);
+        decode_unit(r, T, S, b, z, coef, val);
         if (dc) {
             ++cnt;
             ds[ci] = wadd(ds[ci], val);
@@ -260,7 +316,7 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, i
 // Serial repair of one unsynchronised lane j (its count pass derived the true exit Y[j]):
 // adopt it and re-derive the following lanes until one's exit agrees with its guess exit.
 // Returns the last lane touched, or -1 if the walk exceeded `max_walk` lanes.
-ICX_HD int64_t repair_walk(const uint8_t* U, int64_t ulen, const LdsTables& T, int bpm, int64_t j, int64_t nsub,
+ICX_HD int64_t repair_walk(const uint8_t* U, int64_t ulen, const LdsTables& T, const Sel& S, int64_t j, int64_t nsub,
                            int64_t sub_bits, uint64_t* X, const uint64_t* Y, const RecState* rec, const int32_t* nrec,
                            const int32_t* tot, SubRec* sub, int max_walk) {
     X[j] = Y[j];
@@ -269,7 +325,7 @@ ICX_HD int64_t repair_walk(const uint8_t* U, int64_t ulen, const LdsTables& T, i
         if (steps >= max_walk) return -1;
         bool synced;
         SubRec out;
-        const uint64_t ex = lane_count(U, ulen, T, bpm, X[k - 1], k * sub_bits, (k + 1) * sub_bits, rec + k * kRec,
+        const uint64_t ex = lane_count(U, ulen, T, S, X[k - 1], k * sub_bits, (k + 1) * sub_bits, rec + k * kRec,
                                        nrec[k], tot + 4 * k, X[k], out, synced);
         sub[k] = out;
         if (ex == X[k]) break;

@@ -64,7 +64,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
         if (fe < 0 || t <= fe) ulen += tiles[t].kept;
     }
     const int64_t errpos = (fe >= 0 && tiles[fe].end_err) ? ulen : INT64_MAX;
-    std::vector<uint8_t> U(ulen + 8, 0);
+    std::vector<uint8_t> U(ulen + 64, 0);  // Reader slack: whole 16-byte chunks
     for (int64_t t = 0; t < ntiles; ++t) {
         if (obase[t] >= ulen) continue;
         const int64_t tend = tiles[t].end_at;
@@ -87,21 +87,16 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     std::memcpy(T.huff, d.huff, sizeof(T.huff));
     for (int t = 0; t < 4; ++t) huff_fill_fast(T.huff[t], 0, 1);
     for (int k = 0; k < 64; ++k) T.nat_of_zig[k] = (uint8_t)nat_of_zig(k);
-    for (int b = 0; b < kSpecMaxBpm; ++b) {
-        int sx, sy;
-        T.comp_of[b] = b < d.bpm ? (int8_t)mcu_block_comp(d, b, sx, sy) : 0;
-    }
-    for (int c = 0; c < 3; ++c) { T.dc_of[c] = (int8_t)d.c[c].dc_tab; T.ac_of[c] = (int8_t)d.c[c].ac_tab; }
     const int64_t S = sub_bytes;
     const int64_t nsub = ulen > 0 ? (ulen + S - 1) / S : 1;
-    const int bpm = d.bpm;
+    const Sel SL = make_sel(d);
     // ---- guess (k_spec_guess)
     const int64_t sb = S * 8;
     std::vector<uint64_t> X(nsub, 0), Y(nsub, 0);
     std::vector<RecState> rec(nsub * kRec);
     std::vector<int32_t> nrec(nsub, 0), tot(nsub * 4, 0);
     for (int64_t j = 0; j + 1 < nsub; ++j)
-        X[j] = lane_guess(U.data(), ulen, T, bpm, j * sb, (j + 1) * sb, 0, rec.data() + j * kRec, &nrec[j], &tot[4 * j]);
+        X[j] = lane_guess(U.data(), ulen, T, SL, j * sb, (j + 1) * sb, 0, rec.data() + j * kRec, &nrec[j], &tot[4 * j]);
     // ---- count (k_spec_count)
     std::vector<SubRec> sub(nsub, SubRec{0, 0, 0, 0, 0});
     std::vector<int32_t> queue;
@@ -109,7 +104,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     for (int64_t j = 0; j + 1 < nsub; ++j) {
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[j - 1];
         bool synced;
-        Y[j] = lane_count(U.data(), ulen, T, bpm, entry, j * sb, (j + 1) * sb, rec.data() + j * kRec, nrec[j],
+        Y[j] = lane_count(U.data(), ulen, T, SL, entry, j * sb, (j + 1) * sb, rec.data() + j * kRec, nrec[j],
                           &tot[4 * j], X[j], sub[j], synced);
         synced_lanes += synced;
         if (sub[j].mism) queue.push_back((int32_t)j);
@@ -121,7 +116,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     int64_t done = -1;
     for (int32_t j : queue) {
         if (j <= done) continue;
-        done = repair_walk(U.data(), ulen, T, bpm, j, nsub, sb, X.data(), Y.data(), rec.data(), nrec.data(), tot.data(),
+        done = repair_walk(U.data(), ulen, T, SL, j, nsub, sb, X.data(), Y.data(), rec.data(), nrec.data(), tot.data(),
                            sub.data(), 64);
         if (done < 0) { stats[1]++; return 1; }
     }
@@ -149,7 +144,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
         r.init(U.data(), ulen, st_pos(entry));
         int b = st_b(entry), z = st_z(entry), coefi;
         int32_t val;
-        while (z != 0) decode_unit(r, T, bpm, b, z, coefi, val);
+        while (z != 0) decode_unit(r, T, SL, b, z, coefi, val);
         int32_t pred[3] = {ent[j].p0, ent[j].p1, ent[j].p2};
         const int64_t errbits = errpos == INT64_MAX ? INT64_MAX : errpos * 8;
         bool bad = false;
@@ -158,10 +153,10 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
         while (bi < total) {  // k_spec_write's flat loop
             if (z == 0) {
                 if (r.pos() >= limit) break;
-                ci = T.comp_of[b];
+                ci = SL.comp(b);
             }
             if (r.pos() + 16 > errbits) bad = true;
-            const int rc = decode_unit(r, T, bpm, b, z, coefi, val);
+            const int rc = decode_unit(r, T, SL, b, z, coefi, val);
             if (rc != kUnitOk || r.pos() > errbits) bad = true;
             if (bad) break;
             if (coefi == 0) { pred[ci] = wadd(pred[ci], val); dc[bi] = pred[ci]; }
@@ -187,7 +182,7 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
     if (parse_headers(file, size, d) != kPending || d.restart || d.bpm > kSpecMaxBpm) return -1;
     const uint8_t* R = file + d.scan_off;
     const int64_t L = d.size - d.scan_off;
-    std::vector<uint8_t> U(L + 8);
+    std::vector<uint8_t> U(L + 64);
     int64_t e; int er; int32_t gu = 0;
     int64_t ulen = 0;
     for (int64_t a = 0; a < L; a += kChunk) {
@@ -200,8 +195,6 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
     std::memcpy(T.huff, d.huff, sizeof(T.huff));
     for (int t = 0; t < 4; ++t) huff_fill_fast(T.huff[t], 0, 1);
     for (int k = 0; k < 64; ++k) T.nat_of_zig[k] = (uint8_t)nat_of_zig(k);
-    for (int b = 0; b < kSpecMaxBpm; ++b) { int sx, sy; T.comp_of[b] = b < d.bpm ? (int8_t)mcu_block_comp(d, b, sx, sy) : 0; }
-    for (int c = 0; c < 3; ++c) { T.dc_of[c] = (int8_t)d.c[c].dc_tab; T.ac_of[c] = (int8_t)d.c[c].ac_tab; }
     std::unordered_map<int64_t, int> truth;  // pos -> (b<<8|z)
     {
         Reader r; r.init(U.data(), ulen, 0);
@@ -209,7 +202,7 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
         const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
         int64_t blocks = 0;
         truth[0] = 0;
-        while (blocks < total) { bool dc = z == 0; decode_unit(r, T, d.bpm, b, z, c, v); if (dc) ++blocks; truth[r.pos()] = (b << 8) | z; }
+        while (blocks < total) { bool dc = z == 0; decode_unit(r, T, make_sel(d), b, z, c, v); if (dc) ++blocks; truth[r.pos()] = (b << 8) | z; }
     }
     for (int s = 0; s < nstarts; ++s) {
         const int64_t start = (ulen * 8) * s / nstarts;
@@ -217,7 +210,7 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
         int b = guess_b, z = 0, c; int32_t v;
         out[s] = -1;
         while (r.pos() - start < maxbits) {
-            decode_unit(r, T, d.bpm, b, z, c, v);
+            decode_unit(r, T, make_sel(d), b, z, c, v);
             auto it = truth.find(r.pos());
             if (it != truth.end() && it->second == ((b << 8) | z)) { out[s] = r.pos() - start; break; }
         }
