@@ -248,6 +248,8 @@ int icx_batch_path_stats(const icx_batch* b, int32_t* parallel, int32_t* fallbac
     return ICX_OK;
 }
 
+int icx_batch_group(const icx_batch* b) { return b ? b->ws.slots : 0; }
+
 int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int cap) {
     if (!b) return 0;
     float acc[kStCount] = {0};

@@ -13,7 +13,7 @@
 
 namespace icx {
 
-const char* const kStageNames[kStCount] = {"parse", "entropy", "idct", "upsample", "convert"};
+const char* const kStageNames[kStCount] = {"parse", "unstuff", "entropy", "write", "idct", "upsample", "convert"};
 
 int64_t ws_coef_cap(int w, int h) {  // any power-of-two sampling: MCU <= 64 px
     int64_t wp = ((int64_t)w + 63) / 64 * 64, hp = ((int64_t)h + 63) / 64 * 64;
@@ -627,8 +627,8 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
                        out_stride);
     E(kStParse);
+    launch_spec_entropy(ws, n, d_data, d_off, st, hook);
     B(kStEntropy);
-    launch_spec_entropy(ws, n, d_data, d_off, st);
     hipLaunchKernelGGL(k_entropy_seq, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc,
                        ws.coef_cap);
     E(kStEntropy);

@@ -72,14 +72,13 @@ struct GroupWs {
     int32_t* stats = nullptr;   // [4] path counters, accumulated over a batch call
 };
 
-void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st);
 
 int64_t ws_coef_cap(int w, int h);
 int64_t ws_plane_cap(int w, int h);
 int64_t ws_tmp_cap(int w, int h);
 
 // Stage hooks so the host can bracket each stage with HIP events.
-enum Stage { kStParse = 0, kStEntropy, kStIdct, kStUpsample, kStConvert, kStCount };
+enum Stage { kStParse = 0, kStUnstuff, kStEntropy, kStWrite, kStIdct, kStUpsample, kStConvert, kStCount };
 extern const char* const kStageNames[kStCount];
 struct StageHook {
     virtual void begin(Stage s, hipStream_t st) = 0;
@@ -91,6 +90,8 @@ struct StageHook {
 void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
                          const uint64_t* d_size, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
                          int32_t* d_dims, hipStream_t st, StageHook* hook);
+void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
+                         StageHook* hook);
 
 // tiny_jpeg-exact encode on the GPU (icx_encode.hip); `out` receives the whole file.
 bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const uint8_t* src,

@@ -482,8 +482,12 @@ __global__ void k_spec_finish(int n, Desc* __restrict__ desc, const SpecImg* __r
     else if (desc[i].status == kPending) atomicAdd(&stats[2], 1);
 }
 
-void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st) {
+void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
+                         StageHook* hook) {
+    auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
+    auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     const int g = 2048;  // grid-stride launches: >> 256 CUs
+    B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.totals,
                        ws.ucap);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
@@ -491,6 +495,8 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase);
     hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles, ws.tile_obase, ws.U, ws.ucap);
+    E(kStUnstuff);
+    B(kStEntropy);
     hipLaunchKernelGGL(k_spec_guess, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
                        ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt);
     hipLaunchKernelGGL(k_spec_count, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
@@ -498,8 +504,11 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.U, ws.ucap, ws.X, ws.Y, ws.rec,
                        ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
+    E(kStEntropy);
+    B(kStWrite);
     hipLaunchKernelGGL(k_spec_write, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
                        ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);
+    E(kStWrite);
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
 }
 

@@ -98,6 +98,9 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
 int icx_jpeg_batch_decode_host(icx_batch* b, int n, const uint8_t* const* jpegs, const size_t* sizes,
                                uint8_t* const* outs, uint64_t out_stride, int32_t* status, int32_t* dims);
 
+/* Images per workspace group (each kernel of the pipeline launches once per group). */
+int icx_batch_group(const icx_batch* b);
+
 /* Per-stage timings (ms) of the most recent batch call, measured with HIP events on the
  * stream the kernels ran on. Fills up to `cap` entries; returns the number of stages. */
 int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int cap);
