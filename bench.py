@@ -110,8 +110,11 @@ def main():
     n = args.images or wl["n"]
     W, H = wl["w"], wl["h"]
 
-    # inputs first (CPU only, before any GPU init so fork() is safe)
-    seeds = [1234 + rank * 100000 + i for i in range(min(args.pool, n))]
+    # this rank's shard of the job's image range (weak scaling: n images per GPU); its inputs are
+    # generated first (CPU only, before any GPU init so fork() is safe)
+    from imagecodecs_amd import shard
+    first, last = shard.shard_range(n * world, world, rank)
+    seeds = [1234 + first + i for i in range(min(args.pool, n))]
     t = time.perf_counter()
     pool = make_pool(seeds, W, H, wl["sampling"], wl["quality"], procs=min(16, len(seeds)))
     gen_s = time.perf_counter() - t
@@ -144,7 +147,6 @@ def main():
     d_out = torch.empty(n * stride, dtype=torch.uint8, device=dev)
     d_st = torch.empty(n, dtype=torch.int32, device=dev)
     d_dims = torch.empty((n, 3), dtype=torch.int32, device=dev)
-    gathered = [torch.empty_like(d_st) for _ in range(world)] if world > 1 else None
 
     ctx = icx.Context(local)
     batch = icx.Batch(ctx, n, W, H, args.group)
@@ -153,8 +155,9 @@ def main():
     def step():
         batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out.data_ptr(), stride,
                             d_st.data_ptr(), d_dims.data_ptr(), stream.cuda_stream)
-        if world > 1:  # final gather of per-image statuses over RCCL/xGMI
-            dist.all_gather(gathered, d_st)
+        if world > 1:  # final gather of per-image statuses over RCCL/xGMI (the only collective)
+            return shard.gather_results(d_st, dist)
+        return d_st
 
     for _ in range(args.warmup):
         step()
@@ -163,8 +166,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    last = d_st
     for _ in range(args.steps):
-        step()
+        last = step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -178,8 +182,9 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
 
-    # correctness of the measured run: every image OK; pool images bit-exact vs the oracle
-    st = d_st.cpu().numpy()
+    # correctness of the measured run: every image of the job OK (gathered statuses); this rank's
+    # pool images bit-exact vs the oracle
+    st = last.cpu().numpy()
     ok_all = bool((st == 0).all())
     checked = 0
     mismatches = 0

@@ -1,0 +1,150 @@
+/*
+ * imagecodecs/codecs.h -- drop-in ImageCodecs::Image (reference codecs.h:16-103) for the JPEG
+ * path, implemented over the icx C ABI (include/icx.h, libicx.so, MI355X/gfx950).
+ *
+ * Same names, argument meaning and ownership as the reference class:
+ *   read(path)  -- dispatch on the lower-cased extension (codecs.cpp:53-89); ".jpg"/".jpeg"
+ *                  decode on the GPU (readJpg, codecs.cpp:821-849 -> icx_jpeg_decode).
+ *   write(path) -- ".jpg"/".jpeg" encode with tiny_jpeg quality 3 semantics (writeJpg,
+ *                  codecs.cpp:851-854 -> icx_tje_encode_to_file, byte-identical stream).
+ *   pixels_ is new[]-owned and delete[]-d by ~Image (codecs.h:102); load() adopts a buffer.
+ * Every other extension is outside this path: it throws std::invalid_argument exactly like the
+ * reference's unknown-extension branch (codecs.cpp:80-83), so a build that needs those codecs
+ * keeps the reference's codecs.cpp for them.
+ *
+ * Deliberate deviations (DESIGN.md "Boundary"): a grayscale JPEG yields channels() == 1 (the
+ * reference reports 3 and over-reads the 1-channel buffer, codecs.cpp:840-844); errors throw
+ * std::runtime_error (the reference's std::exception(const char*) is MSVC-only, :836). There is
+ * no CPU fallback: without a usable GPU, read()/write() of a JPEG throw.
+ *
+ * Header-only; link with -L<repo>/imagecodecs_amd/lib -licx. One icx context per process
+ * (device ICX_DEVICE, default 0), created on first use and serialised by a mutex -- the
+ * reference's NanoJPEG state is a process global too (jpeg_dec.h:332).
+ */
+#pragma once
+#include <algorithm>
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../icx.h"
+
+namespace ImageCodecs {
+
+enum class Type { UBYTE, USHORT, FLOAT };
+
+namespace detail {
+struct IcxProcess {
+    std::mutex mu;
+    icx_ctx* ctx = nullptr;
+    icx_ctx* get() {  // call with mu held
+        if (!ctx) {
+            const char* dev = std::getenv("ICX_DEVICE");
+            ctx = icx_create(dev ? std::atoi(dev) : 0);
+            if (!ctx) throw std::runtime_error(std::string("icx_create failed: ") + icx_last_error(nullptr));
+        }
+        return ctx;
+    }
+    ~IcxProcess() {
+        if (ctx) icx_destroy(ctx);
+    }
+};
+inline IcxProcess& icx_process() {
+    static IcxProcess p;
+    return p;
+}
+inline std::string lower_ext(const std::string& path) {
+    std::string e = std::filesystem::path(path).extension().string();
+    for (auto& c : e) c = (char)std::tolower((unsigned char)c);
+    return e;
+}
+}  // namespace detail
+
+class Image {
+    int h_ = 0, w_ = 0, d_ = 0;
+    unsigned char* pixels_ = nullptr;
+    Type type_ = Type::UBYTE;
+    bool last_write_ok_ = false;
+
+    int byteSize(Type t) const { return t == Type::FLOAT ? 4 : t == Type::USHORT ? 2 : 1; }
+
+    void readJpg(const std::string& path) {
+        std::FILE* f = std::fopen(path.c_str(), "rb");
+        if (!f) throw std::runtime_error("Could not open " + path);
+        std::vector<uint8_t> buf;
+        uint8_t chunk[1 << 16];
+        size_t k;
+        while ((k = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + k);
+        std::fclose(f);
+        auto& P = detail::icx_process();
+        std::lock_guard<std::mutex> lock(P.mu);
+        uint8_t* out = nullptr;
+        int w = 0, h = 0, d = 0;
+        const int rc = icx_jpeg_decode(P.get(), buf.data(), buf.size(), &out, &w, &h, &d);
+        if (rc != ICX_OK) {
+            icx_free(out);
+            throw std::runtime_error("Error decoding the input file (nj_result_t " + std::to_string(rc) + ").");
+        }
+        const size_t n = (size_t)w * h * d;
+        unsigned char* px = new unsigned char[n ? n : 1];
+        if (n) std::memcpy(px, out, n);
+        icx_free(out);
+        delete[] pixels_;
+        pixels_ = px;
+        w_ = w;
+        h_ = h;
+        d_ = d;
+        type_ = Type::UBYTE;
+    }
+
+    void writeJpg(const std::string& path) {
+        auto& P = detail::icx_process();
+        std::lock_guard<std::mutex> lock(P.mu);
+        // as in the reference, the encoder's 0/1 result is not acted on (codecs.cpp:853; e.g.
+        // d not in {3,4} leaves no image, jpeg_enc.h:954-956); it stays queryable afterwards
+        last_write_ok_ = icx_tje_encode_to_file(P.get(), path.c_str(), w_, h_, d_, pixels_) == 1;
+    }
+
+public:
+    Image() = default;
+    Image(const Image&) = delete;  // the reference's implicit copy double-frees pixels_
+    Image& operator=(const Image&) = delete;
+    ~Image() { delete[] pixels_; }
+
+    int byteSize() const { return byteSize(type_); }
+    int channels() const { return d_; }
+    int cols() const { return w_; }
+    int rows() const { return h_; }
+    unsigned char** data() { return &pixels_; }
+    bool empty() const { return h_ == 0 || w_ == 0 || d_ == 0 || pixels_ == nullptr; }
+    int totalBytes() const { return w_ * h_ * d_ * byteSize(); }
+    Type type() const { return type_; }
+    bool lastWriteOk() const { return last_write_ok_; }  // extension: tje's result of the last write()
+    void load(unsigned char* pixels, int w, int h, int channels) {
+        d_ = channels;
+        w_ = w;
+        h_ = h;
+        pixels_ = pixels;
+    }
+
+    void read(const std::string& filepath) {
+        const std::string ext = detail::lower_ext(filepath);
+        if (ext == ".jpg" || ext == ".jpeg") readJpg(filepath);
+        else throw std::invalid_argument("Cannot parse filetype");
+        if (pixels_ == nullptr) throw std::runtime_error("Could not read image data");
+    }
+
+    void write(const std::string& filepath) {
+        const std::string ext = detail::lower_ext(filepath);
+        if (ext == ".jpg" || ext == ".jpeg") writeJpg(filepath);
+        else throw std::invalid_argument("Cannot parse filetype");
+    }
+};
+
+}  // namespace ImageCodecs
