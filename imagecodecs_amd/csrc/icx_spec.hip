@@ -386,9 +386,6 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
 // stores when it ends (scattered 2-byte global stores amplified HBM writes ~10x).
 // 128-byte lane slot; 16-byte chunk q of lane t lives at chunk q ^ (t & 7), so the b128 reads
 // of a 16-lane group hit distinct banks.
-#ifndef ICX_EXP_WRITE
-#define ICX_EXP_WRITE 0  // timing experiments only: 1 = no block flush, 2 = no coefficient stores at all
-#endif
 __device__ __forceinline__ int slot_elem(int t, int n) { return (((n >> 3) ^ (t & 7)) << 3) | (n & 7); }
 
 __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
@@ -399,8 +396,10 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                                                     int64_t coef_cap) {
     __shared__ LdsTables T;
     __shared__ int4 slots[kLanes][8];
+    __shared__ int2 done_tab[kLanes / 64][64];  // per wave: (slot lane, block index) of completed blocks
     int cur = -1;
     const int total = totals[1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int4* slot = &slots[threadIdx.x][0];
     int16_t* sv = reinterpret_cast<int16_t*>(slot);
 #pragma unroll
@@ -408,58 +407,93 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
         SpecImg& s = spec[i];
-        if (s.mode != 1) continue;
+        if (s.mode != 1) continue;  // uniform per workgroup
         const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
-        if (j >= s.nsub) continue;
         const Sel S = make_sel(desc[i]);
         const int64_t base = (int64_t)s.wg_base * kLanes;
-        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[base + j - 1];
-        const bool last = j == s.nsub - 1;
-        const int64_t limit = last ? INT64_MAX : st_pos(X[base + j]);
-        const LaneEntry le = ent[base + j];
-        Reader r;
-        r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
-        int b = st_b(entry), z = st_z(entry), coef;
-        int32_t val;
-        // the block in progress at entry belongs to the previous lane
-        while (z != 0) decode_unit(r, T, S, b, z, coef, val);
-        int32_t pred[3] = {le.p0, le.p1, le.p2};
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
         int4* A = reinterpret_cast<int4*>(ac + (int64_t)i * coef_cap * 64);
         int32_t* D = dcv + (int64_t)i * coef_cap;
         const int64_t total_blocks = s.total_blocks;
-        int64_t bi = le.G;
-        int ci = 0;
+        bool act = j < s.nsub;
+        Reader r;
+        int b = 0, z = 0, coef, ci = 0;
+        int32_t val, pred[3] = {0, 0, 0};
+        int64_t bi = 0, limit = 0;
         bool bad = false;
-        while (bi < total_blocks) {
-            if (z == 0) {  // a block starts: stop at the next lane's territory
-                if (r.pos() >= limit) break;
-                ci = S.comp(b);
-            }
-            // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
-            if (r.pos() + 16 > errbits) bad = true;
-            const int rc = decode_unit(r, T, S, b, z, coef, val);
-            if (rc != kUnitOk || r.pos() > errbits) bad = true;
-            if (bad) break;
-            if (coef == 0) {
-                pred[ci] = wadd(pred[ci], val);
-                D[bi] = pred[ci];
-            } else if (coef > 0) {
-#if ICX_EXP_WRITE < 2
-                sv[slot_elem(threadIdx.x, T.nat_of_zig[coef])] = (int16_t)val;
-#endif
-            }
-            if (z == 0) {  // block complete: flush and clear the slot
-#if ICX_EXP_WRITE == 0
-                int4* dst = A + bi * 8;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int sq = q ^ (threadIdx.x & 7);
-                    dst[q] = slot[sq];
-                    slot[sq] = make_int4(0, 0, 0, 0);
+        if (act) {
+            const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[base + j - 1];
+            limit = j == s.nsub - 1 ? INT64_MAX : st_pos(X[base + j]);
+            const LaneEntry le = ent[base + j];
+            r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
+            b = st_b(entry);
+            z = st_z(entry);
+            // the block in progress at entry belongs to the previous lane
+            while (z != 0) decode_unit(r, T, S, b, z, coef, val);
+            pred[0] = le.p0;
+            pred[1] = le.p1;
+            pred[2] = le.p2;
+            bi = le.G;
+            act = bi < total_blocks;
+        }
+        // Wave-uniform loop: one code per active lane per iteration, then the wave flushes the
+        // blocks its lanes completed together -- eight 128-byte blocks per round, each lane
+        // moving one 16-byte chunk LDS -> HBM and zeroing it (coalesced full-line stores,
+        // no divergent per-lane flush).
+        while (__any(act)) {
+            bool done = false;
+            int64_t bdone = 0;
+            if (act) {
+                if (z == 0) {  // a block starts: stop at the next lane's territory
+                    if (r.pos() >= limit) act = false;
+                    else ci = S.comp(b);
                 }
+            }
+            if (act) {
+                // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
+                if (r.pos() + 16 > errbits) bad = true;
+                const int rc = decode_unit(r, T, S, b, z, coef, val);
+                if (rc != kUnitOk || r.pos() > errbits) bad = true;
+                if (bad) {
+                    act = false;
+                } else {
+                    if (coef == 0) {
+                        pred[ci] = wadd(pred[ci], val);
+#ifndef ICX_EXP_NODC  // timing experiment only
+                        D[bi] = pred[ci];
 #endif
-                ++bi;
+                    } else if (coef > 0) {
+                        sv[slot_elem(threadIdx.x, T.nat_of_zig[coef])] = (int16_t)val;
+                    }
+                    if (z == 0) {
+                        done = true;
+                        bdone = bi++;
+                        act = bi < total_blocks;
+                    }
+                }
+            }
+            const uint64_t m = __ballot(done);
+            if (m) {
+                if (done) {
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    done_tab[wave][rank] = make_int2(threadIdx.x, (int)bdone);
+                }
+                __builtin_amdgcn_wave_barrier();
+                const int cnt = __popcll(m);
+                for (int k0 = 0; k0 < cnt; k0 += 8) {
+                    const int e = k0 + (lane >> 3), q = lane & 7;
+                    if (e < cnt) {
+                        const int2 t = done_tab[wave][e];
+                        int4* sp = &slots[t.x][0];
+                        const int sq = q ^ (t.x & 7);
+#ifndef ICX_EXP_NOSTORE  // timing experiment only: drop the coefficient stores
+                        A[(int64_t)t.y * 8 + q] = sp[sq];
+#endif
+                        sp[sq] = make_int4(0, 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
             }
         }
         if (bad) {

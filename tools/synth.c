@@ -141,14 +141,13 @@ static void wflush1(wbuf* w) { /* pad with 1-bits to a byte boundary */
 }
 
 static float gCos[8][8];
-static int gCosInit = 0;
-static void init_cos(void) {
-    if (gCosInit) return;
+/* filled once when the library loads, so concurrent synth_jpeg calls (thread pools) only read it */
+__attribute__((constructor)) static void init_cos_table(void) {
     for (int u = 0; u < 8; ++u)
         for (int x = 0; x < 8; ++x)
             gCos[u][x] = (float)((u ? 0.5 : 0.5 / sqrt(2.0)) * cos((2 * x + 1) * u * 3.14159265358979323846 / 16.0));
-    gCosInit = 1;
 }
+static void init_cos(void) {}
 
 static void code_block(wbuf* w, const float* px, const uint16_t* q, const henc* dc, const henc* ac, int* pred) {
     float tmp[64], co[64];
