@@ -104,42 +104,91 @@ __device__ __forceinline__ int find_image(const int32_t* pre, int n, int x) {
 }
 
 // ---------------------------------------------------------------------------- unstuff
+// Unstuff tiles: one wave per 4 KiB raw tile, 64 raw bytes (four 16-byte chunks) per lane; wave
+// shuffles for the prefix / min, no block barriers. Each wave walks a contiguous range of the
+// flat tile list, so the owning image only ever advances (no per-tile search).
+constexpr int kLaneRaw = kTileBytes / 64;
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ long long wave_min_ll(long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+
+// One lane's 64 raw bytes: kept bytes before the lane's first end event (written to `out` when
+// WRITE), that event's raw offset (-1: none) and whether it is an error.
+template <bool WRITE>
+__device__ __forceinline__ int ustf_lane(const uint8_t* R, int64_t L, int64_t a, int64_t& end_at, int& end_err,
+                                         uint8_t* out, int32_t& giveup) {
+    int kept = 0;
+    end_at = -1;
+    end_err = 0;
+#pragma unroll
+    for (int c = 0; c < kLaneRaw / kChunk; ++c) {
+        int64_t e;
+        int er;
+        kept += ustf_chunk<WRITE>(R, L, a + c * kChunk, &e, &er, WRITE ? out + kept : nullptr, &giveup);
+        if (e >= 0) {
+            end_at = e;
+            end_err = er;
+            break;
+        }
+    }
+    return kept;
+}
+
+struct TileRange {
+    int t, t1, i;
+};
+__device__ __forceinline__ TileRange wave_tiles(const int32_t* tilepre, int n, int total) {
+    const int nw = gridDim.x * (blockDim.x >> 6), w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int per = (total + nw - 1) / nw;
+    TileRange r;
+    r.t = min(total, w * per);
+    r.t1 = min(total, r.t + per);
+    r.i = r.t < r.t1 ? find_image(tilepre, n, r.t) : 0;
+    return r;
+}
+
 __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __restrict__ data,
                                                     const uint64_t* __restrict__ off, const Desc* __restrict__ desc,
                                                     SpecImg* __restrict__ spec, const int32_t* __restrict__ tilepre,
                                                     const int32_t* __restrict__ totals, TileRec* __restrict__ tiles) {
-    __shared__ int sh[256];
-    __shared__ int64_t s_end;
-    __shared__ int s_err;
-    const int total = totals[0];
-    for (int t = blockIdx.x; t < total; t += gridDim.x) {
-        const int i = find_image(tilepre, n, t);
-        const Desc& d = desc[i];
-        const uint8_t* R = data + off[i] + d.scan_off;
+    const int lane = threadIdx.x & 63;
+    TileRange tr = wave_tiles(tilepre, n, totals[0]);
+    for (int t = tr.t; t < tr.t1; ++t) {
+        while (t >= tilepre[tr.i + 1]) ++tr.i;
+        const int i = tr.i;
+        const uint8_t* R = data + off[i] + desc[i].scan_off;
         const int64_t L = spec[i].scan_len;
-        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)threadIdx.x * kChunk;
+        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)lane * kLaneRaw;
         int64_t end_at;
         int end_err;
         int32_t giveup = 0;
-        const int kept = ustf_chunk<false>(R, L, a, &end_at, &end_err, nullptr, &giveup);
+        const int kept = ustf_lane<false>(R, L, a, end_at, end_err, nullptr, giveup);
         if (giveup) atomicOr(&spec[i].err, kSpecGiveUp);
-        if (threadIdx.x == 0) { s_end = INT64_MAX; s_err = 0; }
-        __syncthreads();
-        if (end_at >= 0) atomicMin((unsigned long long*)&s_end, (unsigned long long)end_at);
-        __syncthreads();
-        const int64_t tend = s_end;
-        if (end_at >= 0 && end_at == tend) s_err = end_err;  // the unique lane owning that FF
+        const long long tend = wave_min_ll(end_at >= 0 ? (long long)end_at : LLONG_MAX);
         // kept bytes before the tile's first end event
         const bool before = end_at >= 0 ? end_at <= tend : a < tend;
-        const int ex = block_exclusive_scan(before ? kept : 0, sh);
-        if (threadIdx.x == 255) {
+        const int incl = wave_incl_scan(before ? kept : 0);
+        const uint64_t owner = __ballot(end_at >= 0 && end_at == tend);  // the unique lane owning that FF
+        const int err = __shfl(end_err, owner ? __ffsll((long long)owner) - 1 : 0);
+        if (lane == 63) {
             TileRec r;
-            r.kept = ex + (before ? kept : 0);
-            r.end_at = tend == INT64_MAX ? -1 : tend;
-            r.end_err = s_err;
+            r.kept = incl;
+            r.end_at = tend == LLONG_MAX ? -1 : tend;
+            r.end_err = owner ? err : 0;
             tiles[t] = r;
         }
-        __syncthreads();
     }
 }
 
@@ -184,50 +233,48 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
                                                     const int32_t* __restrict__ totals, const TileRec* __restrict__ tiles,
                                                     const int32_t* __restrict__ tile_obase, uint8_t* __restrict__ U,
                                                     int64_t ucap) {
-    __shared__ int sh[256];
-    __shared__ uint32_t sbuf[kTileBytes / 4 + 8];  // the tile's kept bytes, then copied out
-    __shared__ int s_kept;
-    const int total = totals[0];
-    for (int t = blockIdx.x; t < total; t += gridDim.x) {
-        const int i = find_image(tilepre, n, t);
+    __shared__ uint32_t sbuf_all[4][kTileBytes / 4 + 8];  // per wave: the tile's kept bytes
+    const int lane = threadIdx.x & 63;
+    uint32_t* sbuf = sbuf_all[threadIdx.x >> 6];
+    uint8_t* sb = reinterpret_cast<uint8_t*>(sbuf);
+    TileRange tr = wave_tiles(tilepre, n, totals[0]);
+    for (int t = tr.t; t < tr.t1; ++t) {
+        while (t >= tilepre[tr.i + 1]) ++tr.i;
+        const int i = tr.i;
         const SpecImg& s = spec[i];
-        const int64_t tend = tiles[t].end_at;
         const int64_t obase = tile_obase[t];  // == ulen for every tile past the first end event
-        const Desc& d = desc[i];
-        const uint8_t* R = data + off[i] + d.scan_off;
-        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)threadIdx.x * kChunk;
+        if (obase >= s.ulen) continue;        // wave-uniform
+        const int64_t tend = tiles[t].end_at;
+        const uint8_t* R = data + off[i] + desc[i].scan_off;
+        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)lane * kLaneRaw;
         int64_t end_at;
         int end_err;
         int32_t giveup = 0;
-        const bool live = obase < s.ulen;
-        const int kept = live ? ustf_chunk<false>(R, s.scan_len, a, &end_at, &end_err, nullptr, &giveup) : 0;
-        const bool before = live && (end_at >= 0 ? (tend < 0 || end_at <= tend) : (tend < 0 || a < tend));
-        const int ex = block_exclusive_scan(before ? kept : 0, sh);
-        uint8_t* sb = reinterpret_cast<uint8_t*>(sbuf);
-        if (before && kept) ustf_chunk<true>(R, s.scan_len, a, &end_at, &end_err, sb + ex, &giveup);
-        if (threadIdx.x == 255) s_kept = ex + (before ? kept : 0);
-        __syncthreads();
+        const int kept = ustf_lane<false>(R, s.scan_len, a, end_at, end_err, nullptr, giveup);
+        const bool before = end_at >= 0 ? (tend < 0 || end_at <= tend) : (tend < 0 || a < tend);
+        const int k = before ? kept : 0;
+        const int incl = wave_incl_scan(k);
+        if (k) ustf_lane<true>(R, s.scan_len, a, end_at, end_err, sb + (incl - k), giveup);
+        const int tile_kept = __shfl(incl, 63);
+        __builtin_amdgcn_wave_barrier();
         // copy out: bytes up to the first 16-byte boundary and after the last one byte-wise
         // (they may share a 16-byte unit with the neighbouring tiles), the rest as 16-byte units
-        const int64_t nout = live ? min<int64_t>(s_kept, s.ulen - obase) : 0;
-        if (nout > 0) {
-            uint8_t* dst = U + (int64_t)i * ucap + obase;  // U + i*ucap is 4 KiB aligned
-            const int head = (int)min<int64_t>(nout, (16 - (obase & 15)) & 15);
-            const int nunit = (int)((nout - head) >> 4);
-            const int tail0 = head + nunit * 16;
-            const int k = threadIdx.x;
-            if (k < head) dst[k] = sb[k];
-            if (k < nout - tail0) dst[tail0 + k] = sb[tail0 + k];
-            if (k < nunit) {
-                const int b0 = head + 16 * k, shb = (b0 & 3) * 8;
-                const uint32_t* q = sbuf + (b0 >> 2);
-                uint32_t v[4];
+        const int64_t nout = min<int64_t>(tile_kept, s.ulen - obase);
+        uint8_t* dst = U + (int64_t)i * ucap + obase;  // U + i*ucap is 4 KiB aligned
+        const int head = (int)min<int64_t>(nout, (16 - (obase & 15)) & 15);
+        const int nunit = (int)((nout - head) >> 4);
+        const int tail0 = head + nunit * 16;
+        if (lane < head) dst[lane] = sb[lane];
+        if (lane < nout - tail0) dst[tail0 + lane] = sb[tail0 + lane];
+        for (int u = lane; u < nunit; u += 64) {
+            const int b0 = head + 16 * u, shb = (b0 & 3) * 8;
+            const uint32_t* q = sbuf + (b0 >> 2);
+            uint32_t v[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (uint32_t)((((uint64_t)q[j + 1] << 32) | q[j]) >> shb);
-                *reinterpret_cast<uint4*>(dst + b0) = make_uint4(v[0], v[1], v[2], v[3]);
-            }
+            for (int j = 0; j < 4; ++j) v[j] = (uint32_t)((((uint64_t)q[j + 1] << 32) | q[j]) >> shb);
+            *reinterpret_cast<uint4*>(dst + b0) = make_uint4(v[0], v[1], v[2], v[3]);
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
     }
 }
 

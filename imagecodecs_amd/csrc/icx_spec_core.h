@@ -26,29 +26,22 @@ ICX_HD bool carry_after_ff(const uint8_t* R, int64_t a, int32_t* giveup) {
     return k & 1;
 }
 
-// Fast path of the automaton: R[a..a+16) holds no 0xFF and R[a-1] is not 0xFF, so all 16 bytes
-// are kept unchanged. Reads the window with aligned dword loads (the bytes before R are the
-// file's headers, a > 0; the bytes after stay inside the scan, a + 24 <= L) and returns it in w.
-ICX_HD bool ustf_fast(const uint8_t* R, int64_t L, int64_t a, uint32_t (&w)[4]) {
+// Bytes R[a-1 .. a+19) as five little-endian words, read with aligned dword loads (the bytes
+// before R are the file's headers, a > 0; the bytes after stay inside the scan, a + 24 <= L).
+ICX_HD bool ustf_window(const uint8_t* R, int64_t L, int64_t a, uint32_t (&v)[5]) {
     if (a < 1 || a + kChunk + 8 > L) return false;
     const uintptr_t p = reinterpret_cast<uintptr_t>(R + a - 1);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p & ~(uintptr_t)3);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(R + a - 1 - (p & 3));
     const int sh = (int)(p & 3) * 8;
     uint32_t e[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) e[k] = q[k];
-    uint32_t v[5];  // bytes R[a-1 .. a+19)
 #pragma unroll
     for (int k = 0; k < 5; ++k) v[k] = (uint32_t)((((uint64_t)e[k + 1] << 32) | e[k]) >> sh);
-    if ((v[0] & 0xFF) == 0xFF) return false;
-    uint32_t ff = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        w[k] = (v[k] >> 8) | (v[k + 1] << 24);
-        const uint32_t x = ~w[k];  // a zero byte of x is an FF byte of w
-        ff |= (x - 0x01010101u) & ~x & 0x80808080u;
-    }
-    return ff == 0;
+    return true;
+}
+ICX_HD int win_byte(const uint32_t (&v)[5], int i) {  // i = -1 .. 18 -> R[a+i]
+    return (int)((v[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFF);
 }
 
 template <bool WRITE>
@@ -57,15 +50,50 @@ ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, i
     *end_at = -1;
     *end_err = 0;
     if (a >= L) return 0;
-    {
-        uint32_t w[4];
-        if (ustf_fast(R, L, a, w)) {
+    uint32_t v[5];
+    if (ustf_window(R, L, a, v)) {
+        uint32_t ff = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w = (v[k] >> 8) | (v[k + 1] << 24);  // R[a+4k .. a+4k+4)
+            const uint32_t x = ~w;                               // a zero byte of x is an FF byte of w
+            ff |= (x - 0x01010101u) & ~x & 0x80808080u;
+        }
+        bool after_ff = win_byte(v, -1) == 0xFF && carry_after_ff(R, a, giveup);
+        if (!ff && !after_ff) {  // no marker activity: all 16 bytes kept unchanged
             if (WRITE) {
 #pragma unroll
-                for (int k = 0; k < 16; ++k) out[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+                for (int k = 0; k < 16; ++k) out[k] = (uint8_t)win_byte(v, k);
             }
             return kChunk;
         }
+        // the automaton below, on the register window (R[a+16] is byte 16 of the window)
+        int kept = 0;
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) {
+            if (after_ff) { after_ff = false; continue; }
+            const int c = win_byte(v, k);
+            if (c != 0xFF) {
+                if (WRITE) out[kept] = (uint8_t)c;
+                ++kept;
+                continue;
+            }
+            const int m = win_byte(v, k + 1);
+            if (m == 0x00 || m == 0xFF) {
+                if (WRITE) out[kept] = 0xFF;
+                ++kept;
+                after_ff = true;
+            } else if ((m & 0xF8) == 0xD0) {
+                if (WRITE) { out[kept] = 0xFF; out[kept + 1] = (uint8_t)m; }
+                kept += 2;
+                after_ff = true;
+            } else {
+                *end_at = a + k;
+                *end_err = m != 0xD9;
+                break;
+            }
+        }
+        return kept;
     }
     bool after_ff = carry_after_ff(R, a, giveup);
     int kept = 0;
