@@ -467,24 +467,41 @@ __device__ __forceinline__ uint32_t pmap(F f) {
 
 // Chroma samples for output columns 4M..4M+3 of real row r: the horizontally doubled row when
 // KH, else the raw samples. `fast` = all four outputs use interior taps and stay inside the row.
+// Split into the loads (chroma_fetch, issued one row pair ahead) and the taps (chroma_make).
+struct CRaw {
+    uint32_t d0, d1;
+};
 template <bool KH>
-__device__ __forceinline__ uint32_t chroma_row(const CPl& c, int r, int M, bool fast) {
+__device__ __forceinline__ CRaw chroma_fetch(const CPl& c, int r, int M, bool fast) {
     const uint8_t* row = c.p + (int64_t)r * c.s;
-    if (!KH) return ld4(row + 4 * M);
+    if (!KH) return CRaw{ld4(row + 4 * M), 0u};
     if (fast) {
         const int base = (2 * M - 2) & ~3;
-        const uint64_t w = (uint64_t)ld4(row + base) | ((uint64_t)ld4(row + base + 4) << 32);
+        return CRaw{ld4(row + base), ld4(row + base + 4)};
+    }
+    return CRaw{0u, 0u};  // edge lanes load inside chroma_make
+}
+template <bool KH>
+__device__ __forceinline__ uint32_t chroma_make(const CPl& c, int r, int M, bool fast, const CRaw& raw) {
+    if (!KH) return raw.d0;
+    if (fast) {
+        const uint64_t w = (uint64_t)raw.d0 | ((uint64_t)raw.d1 << 32);
         const uint64_t b = w >> ((M & 1) ? 0 : 16);  // bytes b0..b5 = samples 2M-2 .. 2M+3
         const int b0 = (int)(b & 255), b1 = (int)((b >> 8) & 255), b2 = (int)((b >> 16) & 255);
         const int b3 = (int)((b >> 24) & 255), b4 = (int)((b >> 32) & 255), b5 = (int)((b >> 40) & 255);
         return pack4(tap4(b3, b2, b1, b0), tap4(b1, b2, b3, b4), tap4(b4, b3, b2, b1), tap4(b2, b3, b4, b5));
     }
+    const uint8_t* row = c.p + (int64_t)r * c.s;
     const int n2 = c.w << 1, s = c.s;
     return pmap([&](int i) {
         const int x = 4 * M + i;
         if (x >= n2) return 0;
         return (int)double_tap(x, c.w, [&](int k) { return (int)row[k]; }, [&](int j) { return (int)row[s - j]; });
     });
+}
+template <bool KH>
+__device__ __forceinline__ uint32_t chroma_row(const CPl& c, int r, int M, bool fast) {
+    return chroma_make<KH>(c, r, M, fast, chroma_fetch<KH>(c, r, M, fast));
 }
 
 // Vertical doubling at output rows 2k (even) / 2k+1 (odd) from the window w0..w4 = doubled
@@ -541,16 +558,17 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
         if (x0 >= W) continue;
         const int nb = min(4, W - x0) * 3;
         const int Y0 = sy * kSH, Y1 = min(H, Y0 + kSH);
-        auto emit = [&](int y, uint32_t cb, uint32_t cr) {
-            const uint32_t yv = ld4(P0 + (int64_t)y * s0 + x0);
+        auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
             uint8_t px[12];
 #pragma unroll
             for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
             so.put(y, x0, px, nb);
         };
+        auto luma = [&](int y) { return ld4(P0 + (int64_t)y * s0 + x0); };
         if (K == 4) {  // gray: stride removal (jpeg_dec.h:854-865)
+#pragma unroll 4
             for (int y = Y0; y < Y1; ++y) {
-                const uint32_t v = ld4(P0 + (int64_t)y * s0 + x0);
+                const uint32_t v = luma(y);
                 uint8_t* dst = so.o + (int64_t)y * W + x0;
                 if (so.vec && nb == 12) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(dst));
                 else {
@@ -561,24 +579,77 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
             }
             continue;
         }
-        // interior horizontal taps for all 4 outputs, reads inside the row (chroma_row<true>)
+        // interior horizontal taps for all 4 outputs, reads inside the row (chroma_make<true>)
         const bool f1 = M >= 1 && x0 + 3 <= 2 * c1.w - 4 && 2 * M + 5 < c1.s;
         const bool f2 = M >= 1 && x0 + 3 <= 2 * c2.w - 4 && 2 * M + 5 < c2.s;
+        // Software pipelining, unrolled by two with alternating buffers P/Q: the loads of the
+        // next row (pair) are in flight while the current one is computed; the scheduling
+        // barriers keep each buffer's reload after its last use so no in-flight value is copied.
+        struct Pre {
+            CRaw a, e;
+            uint32_t y0, y1;
+        };
         if (!KV) {
-            for (int y = Y0; y < Y1; ++y) emit(y, chroma_row<KH>(c1, y, M, f1), chroma_row<KH>(c2, y, M, f2));
+            auto fetch = [&](int y) {
+                Pre p{};
+                if (y < Y1) {
+                    p.a = chroma_fetch<KH>(c1, y, M, f1);
+                    p.e = chroma_fetch<KH>(c2, y, M, f2);
+                    p.y0 = luma(y);
+                }
+                return p;
+            };
+            auto step = [&](int y, const Pre& p) {
+                emit(y, p.y0, chroma_make<KH>(c1, y, M, f1, p.a), chroma_make<KH>(c2, y, M, f2, p.e));
+            };
+            Pre P = fetch(Y0);
+            for (int y = Y0; y < Y1; y += 2) {
+                const Pre Q = fetch(y + 1);
+                step(y, P);
+                __builtin_amdgcn_sched_barrier(0);
+                if (y + 1 >= Y1) break;
+                P = fetch(y + 2);
+                step(y + 1, Q);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             continue;
         }
         const int k0 = Y0 >> 1;
-        auto rowc = [&](const CPl& c, int r, bool f) { return chroma_row<KH>(c, min(max(r, 0), c.h - 1), M, f); };
-        uint32_t a0 = rowc(c1, k0 - 2, f1), a1 = rowc(c1, k0 - 1, f1), a2 = rowc(c1, k0, f1), a3 = rowc(c1, k0 + 1, f1);
-        uint32_t e0 = rowc(c2, k0 - 2, f2), e1 = rowc(c2, k0 - 1, f2), e2 = rowc(c2, k0, f2), e3 = rowc(c2, k0 + 1, f2);
-        for (int k = k0; 2 * k < Y1; ++k) {
-            const uint32_t a4 = rowc(c1, k + 2, f1), e4 = rowc(c2, k + 2, f2);
-            emit(2 * k, vtap_even(k, c1.h, a0, a1, a2, a3), vtap_even(k, c2.h, e0, e1, e2, e3));
+        auto cr1 = [&](int r) { return min(max(r, 0), c1.h - 1); };
+        auto cr2 = [&](int r) { return min(max(r, 0), c2.h - 1); };
+        uint32_t a0 = chroma_row<KH>(c1, cr1(k0 - 2), M, f1), a1 = chroma_row<KH>(c1, cr1(k0 - 1), M, f1);
+        uint32_t a2 = chroma_row<KH>(c1, cr1(k0), M, f1), a3 = chroma_row<KH>(c1, cr1(k0 + 1), M, f1);
+        uint32_t e0 = chroma_row<KH>(c2, cr2(k0 - 2), M, f2), e1 = chroma_row<KH>(c2, cr2(k0 - 1), M, f2);
+        uint32_t e2 = chroma_row<KH>(c2, cr2(k0), M, f2), e3 = chroma_row<KH>(c2, cr2(k0 + 1), M, f2);
+        // data of row pair k: chroma row k+2, luma rows 2k and 2k+1
+        auto fetch = [&](int k) {
+            Pre p{};
+            if (2 * k < Y1) {
+                p.a = chroma_fetch<KH>(c1, cr1(k + 2), M, f1);
+                p.e = chroma_fetch<KH>(c2, cr2(k + 2), M, f2);
+                p.y0 = luma(2 * k);
+                if (2 * k + 1 < Y1) p.y1 = luma(2 * k + 1);
+            }
+            return p;
+        };
+        auto step = [&](int k, const Pre& p) {
+            const uint32_t a4 = chroma_make<KH>(c1, cr1(k + 2), M, f1, p.a);
+            const uint32_t e4 = chroma_make<KH>(c2, cr2(k + 2), M, f2, p.e);
+            emit(2 * k, p.y0, vtap_even(k, c1.h, a0, a1, a2, a3), vtap_even(k, c2.h, e0, e1, e2, e3));
             if (2 * k + 1 < Y1)
-                emit(2 * k + 1, vtap_odd(k, c1.h, a1, a2, a3, a4), vtap_odd(k, c2.h, e1, e2, e3, e4));
+                emit(2 * k + 1, p.y1, vtap_odd(k, c1.h, a1, a2, a3, a4), vtap_odd(k, c2.h, e1, e2, e3, e4));
             a0 = a1; a1 = a2; a2 = a3; a3 = a4;
             e0 = e1; e1 = e2; e2 = e3; e3 = e4;
+        };
+        Pre P = fetch(k0);
+        for (int k = k0; 2 * k < Y1; k += 2) {
+            const Pre Q = fetch(k + 1);
+            step(k, P);
+            __builtin_amdgcn_sched_barrier(0);
+            if (2 * (k + 1) >= Y1) break;
+            P = fetch(k + 2);
+            step(k + 1, Q);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }

@@ -463,20 +463,19 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         int32_t* D = dcv + (int64_t)i * coef_cap;
         const int64_t total_blocks = s.total_blocks;
         bool act = j < s.nsub;
+        // every lane runs a reader (lanes past the image's last lane idle at position 0)
+        const uint64_t entry = (!act || j == 0) ? pack_state(0, 0, 0) : X[base + j - 1];
         Reader r;
-        int b = 0, z = 0, coef, ci = 0;
+        r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
+        int b = st_b(entry), z = st_z(entry), coef, ci = 0;
         int32_t val, pred[3] = {0, 0, 0};
         int64_t bi = 0, limit = 0;
         bool bad = false;
+        // the block in progress at entry belongs to the previous lane
+        while (z != 0) decode_unit(r, T, S, b, z, coef, val);
         if (act) {
-            const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[base + j - 1];
             limit = j == s.nsub - 1 ? INT64_MAX : st_pos(X[base + j]);
             const LaneEntry le = ent[base + j];
-            r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
-            b = st_b(entry);
-            z = st_z(entry);
-            // the block in progress at entry belongs to the previous lane
-            while (z != 0) decode_unit(r, T, S, b, z, coef, val);
             pred[0] = le.p0;
             pred[1] = le.p1;
             pred[2] = le.p2;
@@ -488,20 +487,22 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         // moving one 16-byte chunk LDS -> HBM and zeroing it (coalesced full-line stores,
         // no divergent per-lane flush).
         while (__any(act)) {
+            // The reader advances on every lane, active or not (an idle lane decodes harmless
+            // garbage; its loads are clamped to U): keeping Reader updates out of divergent
+            // branches stops the compiler from routing the in-flight chunk through loop-header
+            // copies, which made every iteration wait for the newest load and all stores.
+            if (z == 0) {  // a block starts: stop at the next lane's territory
+                if (r.pos() >= limit) act = false;
+                ci = S.comp(b);
+            }
+            // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
+            const bool peek_bad = r.pos() + 16 > errbits;
+            const int rc = decode_unit(r, T, S, b, z, coef, val);
             bool done = false;
             int64_t bdone = 0;
             if (act) {
-                if (z == 0) {  // a block starts: stop at the next lane's territory
-                    if (r.pos() >= limit) act = false;
-                    else ci = S.comp(b);
-                }
-            }
-            if (act) {
-                // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
-                if (r.pos() + 16 > errbits) bad = true;
-                const int rc = decode_unit(r, T, S, b, z, coef, val);
-                if (rc != kUnitOk || r.pos() > errbits) bad = true;
-                if (bad) {
+                if (peek_bad || rc != kUnitOk || r.pos() > errbits) {
+                    bad = true;
                     act = false;
                 } else {
                     if (coef == 0) {

@@ -191,6 +191,12 @@ struct Reader {
             if (--na == 0) {
                 expand(next - 1, braw, a0, a1);
                 na = 4;
+#if defined(__HIP_DEVICE_COMPILE__)
+                // B's old registers must be dead before its next load is issued: if the load
+                // is hoisted above the swap, B lands in other registers and the loop-carried
+                // copy back waits for the load (s_waitcnt vmcnt(0) on every code).
+                __builtin_amdgcn_sched_barrier(0);
+#endif
                 braw = load(next++);
             }
         }
