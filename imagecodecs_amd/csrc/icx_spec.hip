@@ -473,8 +473,14 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
         bool bad = false;
         // the block in progress at entry belongs to the previous lane
         while (z != 0) decode_unit(r, T, S, b, z, coef, val);
+        // lane-relative 32-bit bounds: territory end and the first fetch that is a syntax error
+        const int64_t e0 = st_pos(entry);
+        const uint32_t kFar = 1u << 30;
+        const uint32_t err_rel = errbits == INT64_MAX ? kFar : (uint32_t)min<int64_t>(kFar, max<int64_t>(0, errbits - e0));
+        uint32_t lim_rel = kFar;
         if (act) {
             limit = j == s.nsub - 1 ? INT64_MAX : st_pos(X[base + j]);
+            if (limit != INT64_MAX) lim_rel = (uint32_t)min<int64_t>(kFar, max<int64_t>(0, limit - e0));
             const LaneEntry le = ent[base + j];
             pred[0] = le.p0;
             pred[1] = le.p1;
@@ -492,16 +498,16 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
             // branches stops the compiler from routing the in-flight chunk through loop-header
             // copies, which made every iteration wait for the newest load and all stores.
             if (z == 0) {  // a block starts: stop at the next lane's territory
-                if (r.pos() >= limit) act = false;
+                if (r.used >= lim_rel) act = false;
                 ci = S.comp(b);
             }
             // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
-            const bool peek_bad = r.pos() + 16 > errbits;
+            const bool peek_bad = r.used + 16 > err_rel;
             const int rc = decode_unit(r, T, S, b, z, coef, val);
             bool done = false;
             int64_t bdone = 0;
             if (act) {
-                if (peek_bad || rc != kUnitOk || r.pos() > errbits) {
+                if (peek_bad || rc != kUnitOk || r.used > err_rel) {
                     bad = true;
                     act = false;
                 } else {

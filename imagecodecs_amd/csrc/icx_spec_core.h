@@ -167,6 +167,8 @@ struct Reader {
     uint64_t a0, a1;   // chunk A as a 128-bit left-aligned shift register
     uint4 braw;        // chunk B as loaded (prefetched)
     int64_t next;      // index of the chunk B holds + 1
+    int64_t base;      // bit position at init
+    uint32_t used;     // bits consumed since init (32-bit loop tests in the lane loops)
     ICX_HD uint4 load(int64_t c) const {
         const int64_t o = c * 16;
         return *reinterpret_cast<const uint4*>(u + (o < ulen ? o : 0));
@@ -204,6 +206,8 @@ struct Reader {
     ICX_HD void init(const uint8_t* u_, int64_t ulen_, int64_t bitpos) {
         u = u_;
         ulen = ulen_;
+        base = bitpos;
+        used = 0;
         const int64_t c = bitpos >> 7;
         expand(c, load(c), a0, a1);
         braw = load(c + 1);
@@ -224,12 +228,13 @@ struct Reader {
         nb -= skip;
         refill();
     }
-    ICX_HD int64_t pos() const { return next * 128 - 128 - (int64_t)na * 32 - nb; }
+    ICX_HD int64_t pos() const { return base + used; }
     ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
     ICX_HD uint32_t take(int n) {
         const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
         buf <<= n;
         nb -= n;
+        used += (uint32_t)n;
         return v;
     }
 };
@@ -242,27 +247,41 @@ enum : int { kUnitOk = 0, kUnitErr = 1 };
 // keep going; on the true path any error makes the image NJ_SYNTAX_ERROR.
 ICX_HD int decode_unit(Reader& r, const LdsTables& T, const Sel& S, int& b, int& z, int& coef,
                                            int32_t& val) {
-    const int bpm = S.bpm;
-    const Huff& H = T.huff[S.tab(b, z == 0)];
+    // One table read, one variable shift for code + magnitude bits, one shift to consume them;
+    // the DC / EOB / ZRL / error / end-of-block cases are selects, not branches (the lanes of a
+    // wave take different ones on almost every code). Only codes longer than kFastBits branch.
+    const bool dc = z == 0;
+    const Huff& H = T.huff[S.tab(b, dc)];
     r.refill();
-    int sym = 0;
-    const int len = huff_lookup(H, r.peek16(), sym);
-    coef = -1;
-    val = 0;
-    auto end_block = [&]() { z = 0; b = (b + 1 == bpm) ? 0 : b + 1; };
-    if (!len) { r.take(1); end_block(); return kUnitErr; }
-    r.take(len);
-    const int nbx = sym & 15;
-    const int32_t v = nbx ? extend((int32_t)r.take(nbx), nbx) : 0;
-    if (z == 0) { z = 1; coef = 0; val = v; return kUnitOk; }
-    if (sym == 0) { end_block(); return kUnitOk; }  // EOB
-    if (!nbx && sym != 0xF0) { end_block(); return kUnitErr; }
+    const uint32_t win = r.peek16();
+    const uint32_t e = H.fast[win >> (16 - kFastBits)];
+    int len, sym;
+    if (e) {
+        len = (int)(e >> 8);
+        sym = (int)(e & 0xFF);
+    } else {
+        len = huff_lookup(H, win, sym);
+    }
+    const bool inv = len == 0;               // no such code: consume one bit (jpeg_dec.h:646)
+    const int nbx = inv ? 0 : (sym & 15);
+    const int tot = inv ? 1 : len + nbx;     // <= 31 bits, refill left >= 33
+    const uint32_t m = 1u << nbx;
+    const uint32_t raw = (uint32_t)(r.buf >> (64 - tot)) & (m - 1u);
+    const int32_t v = (int32_t)(raw < (m >> 1) ? raw - m + 1u : raw);  // njGetVLC sign extension (:653-654)
+    r.buf <<= tot;
+    r.nb -= tot;
+    r.used += (uint32_t)tot;
+    const bool eob = !dc && !inv && sym == 0;                              // :667
     const int c = z + (sym >> 4);
-    if (c > 63) { end_block(); return kUnitErr; }
-    coef = c;
-    val = v;
-    if (c == 63) end_block(); else z = c + 1;
-    return kUnitOk;
+    const bool err = inv || (!dc && !eob && ((nbx == 0 && sym != 0xF0) || c > 63));  // :669, :671
+    const bool endb = err || eob || (!dc && c == 63);
+    const bool keep = !err && !eob;
+    coef = dc ? (inv ? -1 : 0) : (keep ? c : -1);
+    val = (keep || (dc && !inv)) ? v : 0;
+    const int bn = b + 1 == S.bpm ? 0 : b + 1;
+    z = endb ? 0 : (dc ? 1 : c + 1);
+    b = endb ? bn : b;
+    return err ? kUnitErr : kUnitOk;
 }
 
 // ------------------------------------------------------------------------ lane logic
@@ -277,10 +296,11 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, c
     int b = b0, z = 0, coef;
     int32_t val, cnt = 0, ds[3] = {0, 0, 0};
     int nr = 0;
-    while (r.pos() < end) {
+    const uint32_t span = (uint32_t)(end - start);
+    while (r.used < span) {
         if (z == 0 && b == 0 && nr < kRec) {  // MCU starts: the true path passes one per MCU
             RecState& e = rec[nr++];
-            e.rel = (uint32_t)(r.pos() - start);
+            e.rel = r.used;
             e.b = b;
             e.cnt = cnt;
             e.ds[0] = ds[0];
@@ -316,9 +336,10 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, c
     int32_t val, cnt = 0, ds[3] = {0, 0, 0};
     int m = 0;
     synced = false;
-    while (r.pos() < end) {
+    const uint32_t off = (uint32_t)(st_pos(entry) - start), span = (uint32_t)(end - start);
+    while (off + r.used < span) {
         if (z == 0 && b == 0 && m < nrec) {
-            const int64_t rel = r.pos() - start;
+            const int64_t rel = off + r.used;
             while (m < nrec && (int64_t)rec[m].rel < rel) ++m;
             if (m < nrec && (int64_t)rec[m].rel == rel) {
                 out.cnt = cnt + tot[0] - rec[m].cnt;
