@@ -183,6 +183,7 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     ICX_HIP(ctx, hipMalloc(&ws.spec, sizeof(SpecImg) * group), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.tilepre, sizeof(int32_t) * (group + 1)), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.wgpre, sizeof(int32_t) * (group + 1)), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.wg2pre, sizeof(int32_t) * (group + 1)), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.totals, sizeof(int32_t) * 4), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.tiles, sizeof(TileRec) * ws.tiles_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.tile_obase, sizeof(int32_t) * ws.tiles_cap), nullptr);
@@ -209,7 +210,7 @@ void icx_batch_destroy(icx_batch* b) {
     (void)hipFree(b->ws.dc);
     (void)hipFree(b->ws.planes);
     (void)hipFree(b->ws.tmp);
-    for (void* p : {(void*)b->ws.spec, (void*)b->ws.tilepre, (void*)b->ws.wgpre, (void*)b->ws.totals,
+    for (void* p : {(void*)b->ws.spec, (void*)b->ws.tilepre, (void*)b->ws.wgpre, (void*)b->ws.wg2pre, (void*)b->ws.totals,
                     (void*)b->ws.tiles, (void*)b->ws.tile_obase, (void*)b->ws.U, (void*)b->ws.X,
                     (void*)b->ws.sub, (void*)b->ws.ent, (void*)b->ws.stats, (void*)b->ws.Y,
                     (void*)b->ws.rec, (void*)b->ws.nrec, (void*)b->ws.guess_cnt, (void*)b->ws.repair})

@@ -15,7 +15,9 @@ constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16
 constexpr int kSubBytes = 2048;    // unstuffed bytes per decode lane (subsequence)
 constexpr int kRec = 16;           // block-start states a guess lane records for resync
 constexpr int kMaxRepair = 1024;   // unsynchronised lanes repaired per image before giving up
-constexpr int kLanes = 256;        // lanes per decode workgroup
+constexpr int kLanes = 256;        // lanes per decode workgroup (lane records are numbered in these)
+constexpr int kWriteLanesBig = 512;  // write-pass workgroup for large images: tables amortised
+                                     // over 512 lanes -> 2 workgroups / CU = 4 waves per SIMD
 constexpr int kSpecMaxBpm = 16;    // blocks per MCU handled by the parallel path
 enum : int32_t { kSpecSyntax = 1, kSpecGiveUp = 2 };
 
@@ -56,8 +58,9 @@ struct GroupWs {
     int64_t lanes_cap = 0;      // flat lane records for the whole group
     SpecImg* spec = nullptr;    // [slots]
     int32_t* tilepre = nullptr; // [slots+1]
-    int32_t* wgpre = nullptr;   // [slots+1]
-    int32_t* totals = nullptr;  // [2]: tiles, lane groups
+    int32_t* wgpre = nullptr;   // [slots+1] 256-lane groups
+    int32_t* wg2pre = nullptr;  // [slots+1] kWriteLanesBig-lane groups (write pass, large images)
+    int32_t* totals = nullptr;  // [4]: tiles, 256-lane groups, big write groups
     TileRec* tiles = nullptr;
     int32_t* tile_obase = nullptr;
     uint8_t* U = nullptr;       // [slots][ucap]

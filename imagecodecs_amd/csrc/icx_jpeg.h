@@ -54,9 +54,16 @@ ICX_HD uint8_t clip8(int32_t v) { return v < 0 ? 0 : (v > 255 ? 255 : (uint8_t)v
 // a 16-bit window v has code length L = min{L : v < bound[L]}, symbol index
 // first[L] + ((v - bound[L-1]) >> (16-L)); v >= bound[16] is an invalid code (bits == 0).
 // fast[] resolves lengths <= kFastBits with one lookup.
+// Codes longer than kFastBits: the 10-bit prefixes holding them are exactly
+// [bound[10] >> 6, ceil(bound[16] / 64)) (bound[10] is a multiple of 64), and prefix p gets the
+// 64-entry subtable p - (bound[10] >> 6), indexed by the next 6 bits: fast[p] = kSubFlag | offset.
+// Tables needing more than kSubTabs subtables keep fast[p] = 0 and take the exact search.
 constexpr int kFastBits = 10;
+constexpr int kSubTabs = 8;
+constexpr uint16_t kSubFlag = 0x8000;
 struct Huff {
-    uint16_t fast[1 << kFastBits];  // (len << 8) | sym, 0 = not resolvable in kFastBits
+    uint16_t fast[1 << kFastBits];  // (len << 8) | sym, kSubFlag | subtable offset, or 0
+    uint16_t sub[kSubTabs << (16 - kFastBits)];  // (len << 8) | sym, 0 = invalid
     uint32_t bound[17];
     int16_t first[17];
     uint8_t sym[256];
@@ -76,30 +83,48 @@ ICX_HD void huff_finalize(Huff& t, const uint8_t* count /*[17], count[0]=0*/) {
     }
 }
 
-// fast[p] for p = lane, lane+step, ... (the GPU fills a table with a whole workgroup).
+ICX_HD int huff_search(const Huff& t, uint32_t win, int from, int& sym) {  // canonical walk
+    int L = from;
+    while (L <= 16 && win >= t.bound[L]) ++L;
+    if (L > 16) return 0;
+    sym = t.sym[t.first[L] + (int)((win - t.bound[L - 1]) >> (16 - L))];
+    return L;
+}
+
+// fast[p] and the subtables for entries lane, lane+step, ... (the GPU fills a table with a
+// whole workgroup).
 ICX_HD void huff_fill_fast(Huff& t, int lane, int step) {
+    constexpr int kSubBits = 16 - kFastBits;
+    const int p0 = (int)(t.bound[kFastBits] >> kSubBits);
+    const int p1 = (int)((t.bound[16] + (1u << kSubBits) - 1) >> kSubBits);
+    const int nsub = p1 - p0 <= kSubTabs ? p1 - p0 : 0;
     for (int p = lane; p < (1 << kFastBits); p += step) {
-        const uint32_t v = (uint32_t)p << (16 - kFastBits);
+        const uint32_t v = (uint32_t)p << kSubBits;
         uint16_t e = 0;
-        for (int L = 1; L <= kFastBits; ++L)
-            if (v < t.bound[L]) {
-                const int s = t.sym[t.first[L] + (int)((v - t.bound[L - 1]) >> (16 - L))];
-                e = (uint16_t)((L << 8) | s);
-                break;
-            }
+        int s = 0;
+        const int L = huff_search(t, v, 1, s);
+        if (L && L <= kFastBits) e = (uint16_t)((L << 8) | s);
+        else if (p >= p0 && p < p0 + nsub) e = (uint16_t)(kSubFlag | ((p - p0) << kSubBits));
         t.fast[p] = e;
+    }
+    for (int q = lane; q < (kSubTabs << kSubBits); q += step) {
+        uint16_t e = 0;
+        if (q < (nsub << kSubBits)) {
+            const uint32_t v = ((uint32_t)(p0 + (q >> kSubBits)) << kSubBits) | (uint32_t)(q & ((1 << kSubBits) - 1));
+            int s = 0;
+            const int L = huff_search(t, v, kFastBits + 1, s);
+            if (L) e = (uint16_t)((L << 8) | s);
+        }
+        t.sub[q] = e;
     }
 }
 
 // Decode one code from a 16-bit window. Returns length (0 = invalid) and symbol.
 ICX_HD int huff_lookup(const Huff& t, uint32_t win, int& sym) {
     uint32_t e = t.fast[win >> (16 - kFastBits)];
+    if (e & kSubFlag) e = t.sub[(e & ~kSubFlag) | (win & ((1u << (16 - kFastBits)) - 1))];
     if (e) { sym = (int)(e & 0xFF); return (int)(e >> 8); }
-    int L = kFastBits + 1;
-    while (L <= 16 && win >= t.bound[L]) ++L;
-    if (L > 16) return 0;
-    sym = t.sym[t.first[L] + (int)((win - t.bound[L - 1]) >> (16 - L))];
-    return L;
+    return huff_search(t, win, kFastBits + 1, sym);
 }
 
 // ---------------------------------------------------------------------------------------

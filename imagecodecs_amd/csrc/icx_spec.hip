@@ -44,12 +44,13 @@ __device__ int block_exclusive_scan(int v, int* sh) {  // blockDim.x <= 1024, re
 
 __global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     int32_t* __restrict__ tilepre, int32_t* __restrict__ wgpre,
-                                                    int32_t* __restrict__ totals, int64_t ucap) {
+                                                    int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
+                                                    int64_t ucap) {
     __shared__ int sh[1024];
-    int carry_t = 0, carry_w = 0;
+    int carry_t = 0, carry_w = 0, carry_w2 = 0;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
         const int i = i0 + threadIdx.x;
-        int nt = 0, nw = 0;
+        int nt = 0, nw = 0, nw2 = 0;
         if (i < n) {
             const Desc& d = desc[i];
             SpecImg& s = spec[i];
@@ -66,30 +67,36 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ de
                 nt = (int)((scan_len + kTileBytes - 1) / kTileBytes);
                 const int64_t nsub = (scan_len + kSubBytes - 1) / kSubBytes;
                 nw = (int)((nsub + kLanes - 1) / kLanes);
+                nw2 = (int)((nsub + kWriteLanesBig - 1) / kWriteLanesBig);
             }
             s.ntiles = nt;
             s.nwg = nw;
         }
         const int et = block_exclusive_scan(nt, sh);
         const int ew = block_exclusive_scan(nw, sh);
+        const int ew2 = block_exclusive_scan(nw2, sh);
         if (i < n) {
             tilepre[i] = carry_t + et;
             wgpre[i] = carry_w + ew;
+            wg2pre[i] = carry_w2 + ew2;
             spec[i].tile_base = carry_t + et;
             spec[i].wg_base = carry_w + ew;
         }
-        __shared__ int last_t, last_w;
-        if (threadIdx.x == blockDim.x - 1) { last_t = et + nt; last_w = ew + nw; }
+        __shared__ int last_t, last_w, last_w2;
+        if (threadIdx.x == blockDim.x - 1) { last_t = et + nt; last_w = ew + nw; last_w2 = ew2 + nw2; }
         __syncthreads();
         carry_t += last_t;
         carry_w += last_w;
+        carry_w2 += last_w2;
         __syncthreads();
     }
     if (threadIdx.x == 0) {
         tilepre[n] = carry_t;
         wgpre[n] = carry_w;
+        wg2pre[n] = carry_w2;
         totals[0] = carry_t;
         totals[1] = carry_w;
+        totals[2] = carry_w2;
     }
 }
 
@@ -435,27 +442,30 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
 // of a 16-lane group hit distinct banks.
 __device__ __forceinline__ int slot_elem(int t, int n) { return (((n >> 3) ^ (t & 7)) << 3) | (n & 7); }
 
-__global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
-                                                    const int32_t* __restrict__ wgpre, const int32_t* __restrict__ totals,
+// NL lanes per workgroup; `wpre` numbers the image's lanes in NL-lane groups (wgpre for 256,
+// wg2pre for kWriteLanesBig), `total` = totals[1] or totals[2].
+template <int NL>
+__global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                    const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                     const uint8_t* __restrict__ U, int64_t ucap,
                                                     const uint64_t* __restrict__ X, const LaneEntry* __restrict__ ent,
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                     int64_t coef_cap) {
     __shared__ LdsTables T;
-    __shared__ int4 slots[kLanes][8];
-    __shared__ int2 done_tab[kLanes / 64][64];  // per wave: (slot lane, block index) of completed blocks
+    __shared__ int4 slots[NL][8];
+    __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
     int cur = -1;
-    const int total = totals[1];
+    const int total = totals[NL == kLanes ? 1 : 2];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int4* slot = &slots[threadIdx.x][0];
     int16_t* sv = reinterpret_cast<int16_t*>(slot);
 #pragma unroll
     for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
-        const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
+        const int i = wg_image_setup(wpre, n, wg, cur, T, desc);
         SpecImg& s = spec[i];
         if (s.mode != 1) continue;  // uniform per workgroup
-        const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
+        const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         const Sel S = make_sel(desc[i]);
         const int64_t base = (int64_t)s.wg_base * kLanes;
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
@@ -527,22 +537,24 @@ __global__ __launch_bounds__(256) void k_spec_write(int n, const Desc* __restric
                 }
             }
             const uint64_t m = __ballot(done);
-            if (m) {
+            if (m) {  // wave-uniform; every lane takes part
                 if (done) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    done_tab[wave][rank] = make_int2(threadIdx.x, (int)bdone);
+                    done_lane[wave][rank] = (uint8_t)lane;
                 }
                 __builtin_amdgcn_wave_barrier();
                 const int cnt = __popcll(m);
                 for (int k0 = 0; k0 < cnt; k0 += 8) {
                     const int e = k0 + (lane >> 3), q = lane & 7;
+                    const int src = done_lane[wave][min(e, cnt - 1)];
+                    const int bsrc = __shfl((int)bdone, src);  // block index of that lane's block
                     if (e < cnt) {
-                        const int2 t = done_tab[wave][e];
-                        int4* sp = &slots[t.x][0];
-                        const int sq = q ^ (t.x & 7);
+                        const int sl = (wave << 6) | src;
+                        int4* sp = &slots[sl][0];
+                        const int sq = q ^ (sl & 7);
 #ifndef ICX_EXP_NOSTORE  // timing experiment only: drop the coefficient stores
-                        A[(int64_t)t.y * 8 + q] = sp[sq];
+                        A[(int64_t)bsrc * 8 + q] = sp[sq];
 #endif
                         sp[sq] = make_int4(0, 0, 0, 0);
                     }
@@ -576,8 +588,8 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     const int g = 2048;  // grid-stride launches: >> 256 CUs
     B(kStUnstuff);
-    hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.totals,
-                       ws.ucap);
+    hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
+                       ws.totals, ws.ucap);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
     hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase);
@@ -594,8 +606,12 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
     E(kStEntropy);
     B(kStWrite);
-    hipLaunchKernelGGL(k_spec_write, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
-                       ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);
+    if ((int64_t)ws.max_w * ws.max_h >= (int64_t)2048 * 2048)  // >= 1 MB of entropy data per image
+        hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec,
+                           ws.wg2pre, ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);
+    else
+        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
+                           ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);
     E(kStWrite);
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
 }

@@ -254,13 +254,14 @@ ICX_HD int decode_unit(Reader& r, const LdsTables& T, const Sel& S, int& b, int&
     const Huff& H = T.huff[S.tab(b, dc)];
     r.refill();
     const uint32_t win = r.peek16();
-    const uint32_t e = H.fast[win >> (16 - kFastBits)];
+    uint32_t e = H.fast[win >> (16 - kFastBits)];
+    if (e & kSubFlag) e = H.sub[(e & ~kSubFlag) | (win & ((1u << (16 - kFastBits)) - 1))];  // > 10-bit codes
     int len, sym;
     if (e) {
         len = (int)(e >> 8);
         sym = (int)(e & 0xFF);
     } else {
-        len = huff_lookup(H, win, sym);
+        len = huff_search(H, win, kFastBits + 1, sym);  // invalid codes, oversized tables
     }
     const bool inv = len == 0;               // no such code: consume one bit (jpeg_dec.h:646)
     const int nbx = inv ? 0 : (sym & 15);

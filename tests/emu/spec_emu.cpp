@@ -218,3 +218,24 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
     return 0;
 }
 }
+
+// ---- two-level Huffman lookup self-check (tests/test_spec_emu.py) ----
+// Builds a table from counts[1..16] and symbols, fills fast + subtables, and returns how many of
+// the 65536 windows huff_lookup decodes differently from the canonical walk; *nsub_out = number
+// of subtables the table needed.
+extern "C" int emu_huff_selftest(const uint8_t* counts17, const uint8_t* syms, int nsyms, int* nsub_out) {
+    auto Tp = std::make_unique<Huff>();
+    Huff& t = *Tp;
+    std::memset(&t, 0, sizeof t);
+    for (int i = 0; i < nsyms && i < 256; ++i) t.sym[i] = syms[i];
+    huff_finalize(t, counts17);
+    huff_fill_fast(t, 0, 1);
+    *nsub_out = (int)(((t.bound[16] + 63) >> 6) - (t.bound[kFastBits] >> 6));
+    int bad = 0;
+    for (uint32_t w = 0; w < 65536; ++w) {
+        int s1 = -1, s2 = -1;
+        const int l1 = huff_lookup(t, w, s1), l2 = huff_search(t, w, 1, s2);
+        if (l1 != l2 || (l1 && s1 != s2)) ++bad;
+    }
+    return bad;
+}

@@ -105,3 +105,48 @@ def test_emulated_resync_statistics_4k():
     assert np.array_equal(coef[: nb.value], ocoef) and np.array_equal(dc[: nb.value], odc)
     lanes = (len(data) + 2047) // 2048
     assert stats[3] >= 0.97 * (lanes - 1), stats  # lanes spliced at a recorded state
+
+
+# Annex K (JPEG spec) luminance/chrominance AC code-length counts; symbols are placeholders.
+_K3 = [0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7D]
+_K5 = [0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77]
+_K1 = [0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0]
+_K2 = [0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0]
+
+
+def _huff_selftest(counts):
+    L = emu_lib()
+    L.emu_huff_selftest.restype = C.c_int
+    L.emu_huff_selftest.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_int)]
+    n = sum(counts)
+    syms = bytes((i * 37 + 11) & 0xFF for i in range(n))
+    nsub = C.c_int()
+    bad = L.emu_huff_selftest(bytes([0] + counts), syms, n, C.byref(nsub))
+    return bad, nsub.value
+
+
+@pytest.mark.parametrize("counts", [_K1, _K2, _K3, _K5], ids=["dc_luma", "dc_chroma", "ac_luma", "ac_chroma"])
+def test_two_level_huffman_annex_k(counts):
+    bad, nsub = _huff_selftest(counts)
+    assert bad == 0
+    assert 0 <= nsub <= 8  # the standard tables fit the subtable budget
+
+
+def test_two_level_huffman_random_tables():
+    rng = np.random.default_rng(7)
+    over_budget = 0
+    for _ in range(300):
+        # random Kraft-valid length counts (possibly incomplete code space), up to 256 symbols
+        counts, space, total = [0] * 16, 1 << 16, 0
+        for L in range(1, 17):
+            cap = min(space >> (16 - L), 256 - total)
+            c = int(rng.integers(0, cap + 1)) if cap > 0 and rng.random() < 0.7 else 0
+            if L == 16 and rng.random() < 0.5:
+                c = cap
+            counts[L - 1] = c
+            space -= c << (16 - L)
+            total += c
+        bad, nsub = _huff_selftest(counts)
+        assert bad == 0, counts
+        over_budget += nsub > 8
+    assert over_budget > 0  # the exact-search fallback was exercised too
