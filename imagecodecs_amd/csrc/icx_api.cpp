@@ -165,10 +165,10 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) +
                              ws.ucap + tiles_per_slot * 20 +
                              lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
-    if (group <= 0) {  // auto: up to 40% of the free HBM (288 GB per MI355X), at least one image
+    if (group <= 0) {  // auto: up to 60% of the free HBM (288 GB per MI355X), at least one image
         size_t free_b = 0, total_b = 0;
         ICX_HIP(ctx, hipMemGetInfo(&free_b, &total_b), nullptr);
-        const int64_t budget = (int64_t)(0.4 * (double)free_b);
+        const int64_t budget = (int64_t)(0.6 * (double)free_b);
         group = (int)std::max<int64_t>(1, std::min<int64_t>(max_images, budget / per_slot));
     }
     group = std::min(group, max_images);
@@ -230,8 +230,12 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     b->hook->reset();
     ICX_HIP(ctx, hipMemsetAsync(b->ws.stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
-    for (int g0 = 0; g0 < n; g0 += b->ws.slots) {
-        const int gn = std::min(b->ws.slots, n - g0);
+    // equal-sized groups (512 images on 361 slots -> 256 + 256, not 361 + 151): every kernel's
+    // grid is sized by the work of its group, so a small tail group leaves the GPU half idle
+    const int ngroups = (n + b->ws.slots - 1) / b->ws.slots;
+    const int per = (n + ngroups - 1) / ngroups;
+    for (int g0 = 0; g0 < n; g0 += per) {
+        const int gn = std::min(per, n - g0);
         launch_decode_group(b->ws, gn, d_data, d_off + g0, d_size + g0, d_out + (uint64_t)g0 * out_stride, out_stride,
                             d_status + g0, d_dims + 3 * g0, st, b->hook.get());
     }

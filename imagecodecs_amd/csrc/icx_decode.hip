@@ -82,7 +82,8 @@ __global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uin
             int32_t v = 0;
             if (nb) { v = extend((int32_t)rb_peek(b, nb), nb); rb_drop(b, nb); }
             pred[ci] = wadd(pred[ci], v);
-            D[blk] = pred[ci];
+            row[0] = dc_cell(pred[ci]);
+            if (row[0] == kDcEscape) D[blk] = pred[ci];
             // AC (jpeg_dec.h:664-671)
             int k = 0;
             do {
@@ -124,6 +125,17 @@ __device__ __forceinline__ int64_t comp_plane_off(const Desc& d, int ci) {
 // --------------------------------------------------------------------------------- IDCT
 // 256 lanes = 32 blocks x 8 rows. Lane (b, r) dequantizes and row-transforms row r of block
 // b, then column-transforms column r, then stores row r of the 8x8 pixel tile (8 bytes).
+// The kernel is VALU-bound: the MCU layout comes from an LDS table, lane positions advance by
+// the grid stride without divisions, and the multiplies are 24-bit whenever every multiplied
+// operand fits (always for dequantisation; per row / column for the transforms, with the exact
+// 32-bit wrap path otherwise).
+struct IdctGeo {
+    int64_t off;     // plane offset of the block's component
+    int32_t stride;  // plane stride
+    int32_t dx, dy;  // pixel offset of the block inside the MCU
+    int32_t mx, my;  // MCU pitch in pixels in this plane (8*hs, 8*vs)
+    int32_t ci;
+};
 __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                               const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
                                               int64_t coef_cap, int64_t plane_cap) {
@@ -131,6 +143,7 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
     const Desc& d = desc[img];
     if (d.status != kOk) return;
     __shared__ int32_t qn[3][64];        // natural-order dequant table per component
+    __shared__ IdctGeo geo[kSpecMaxBpm];  // per block-in-MCU
     __shared__ int32_t rows[32][8][9];   // row-pass output, padded
     __shared__ uint8_t pix[32][8][8];
     const int t = threadIdx.x;
@@ -138,27 +151,52 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
         const int ci = t >> 6, n = t & 63;
         qn[ci][n] = ci < d.nc ? d.q[d.c[ci].tq][kZigOfNat[n]] : 0;
     }
+    const int bpm = d.bpm, mbw = d.mbw;
+    if (t < kSpecMaxBpm && t < bpm) {
+        int sbx, sby;
+        const int ci = mcu_block_comp(d, t, sbx, sby);
+        const Comp& c = d.c[ci];
+        geo[t] = IdctGeo{comp_plane_off(d, ci), c.stride, sbx * 8, sby * 8, c.hs * 8, c.vs * 8, ci};
+    }
     __syncthreads();
-    const int64_t nblocks = (int64_t)d.mbw * d.mbh * d.bpm;
+    const int64_t nblocks = (int64_t)d.mbw * d.mbh * bpm;
     const int lb = t >> 3, r = t & 7;
     const int16_t* A = ac + (int64_t)img * coef_cap * 64;
     const int32_t* D = dcv + (int64_t)img * coef_cap;
     uint8_t* P = planes + (int64_t)img * plane_cap;
-    for (int64_t base = (int64_t)blockIdx.x * 32; base < nblocks; base += (int64_t)gridDim.x * 32) {
-        const int64_t n = base + lb;
+    const bool small_mcu = bpm <= kSpecMaxBpm;
+    // lane position (block-in-MCU k, MCU column / row) advanced by the grid stride without
+    // divisions: step = q MCUs + rr blocks, q = qy MCU rows + qx MCU columns
+    const int64_t step = (int64_t)gridDim.x * 32;
+    const int64_t q = step / bpm;
+    const int rr = (int)(step - q * bpm);
+    const int64_t qy = q / mbw;
+    const int qx = (int)(q - qy * mbw);
+    int64_t n = (int64_t)blockIdx.x * 32 + lb;
+    const int64_t mcu0 = n / bpm;
+    int k = (int)(n - mcu0 * bpm);
+    int64_t mby = mcu0 / mbw;
+    int mbx = (int)(mcu0 - mby * mbw);
+    for (int64_t base = (int64_t)blockIdx.x * 32; base < nblocks; base += step) {
         const bool live = n < nblocks;
-        int ci = 0, sbx = 0, sby = 0;
-        int64_t mcu = 0;
+        IdctGeo g;
+        if (small_mcu) {
+            g = geo[k];
+        } else {  // > 16 blocks per MCU: walk the component list
+            int sbx = 0, sby = 0;
+            const int ci = mcu_block_comp(d, k, sbx, sby);
+            const Comp& c = d.c[ci];
+            g = IdctGeo{comp_plane_off(d, ci), c.stride, sbx * 8, sby * 8, c.hs * 8, c.vs * 8, ci};
+        }
         if (live) {
-            mcu = n / d.bpm;
-            ci = mcu_block_comp(d, (int)(n - mcu * d.bpm), sbx, sby);
             int16_t s[8];
             __builtin_memcpy(s, A + n * 64 + r * 8, sizeof s);
             int32_t v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = wmul(s[j], qn[ci][r * 8 + j]);
-            if (r == 0) v[0] = wmul(D[n], qn[ci][0]);
-            idct_row(v);
+            for (int j = 0; j < 8; ++j) v[j] = m24(s[j], qn[g.ci][r * 8 + j]);  // int16 x 8-bit: exact
+            if (r == 0 && s[0] == kDcEscape) v[0] = wmul(D[n], qn[g.ci][0]);  // DC outside int16
+            if (idct_fast_ok(v)) idct_row<true>(v);
+            else idct_row<false>(v);
 #pragma unroll
             for (int j = 0; j < 8; ++j) rows[lb][r][j] = v[j];
         }
@@ -168,19 +206,23 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
             uint8_t o[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) col[j] = rows[lb][j][r];
-            idct_col(col, o);
+            if (idct_fast_ok(col)) idct_col<true>(col, o);
+            else idct_col<false>(col, o);
 #pragma unroll
             for (int j = 0; j < 8; ++j) pix[lb][j][r] = o[j];
         }
         __syncthreads();
         if (live) {
-            const Comp& c = d.c[ci];
-            const int64_t mby = mcu / d.mbw, mbx = mcu - mby * d.mbw;
-            const int64_t y = (mby * c.vs + sby) * 8 + r, x = (mbx * c.hs + sbx) * 8;
-            uint8_t* dst = P + comp_plane_off(d, ci) + y * c.stride + x;
-            __builtin_memcpy(dst, &pix[lb][r][0], 8);
+            const int64_t y = mby * g.my + g.dy + r, x = (int64_t)mbx * g.mx + g.dx;
+            __builtin_memcpy(P + g.off + y * g.stride + x, &pix[lb][r][0], 8);
         }
         __syncthreads();
+        n += step;
+        k += rr;
+        mbx += qx;
+        mby += qy;
+        if (k >= bpm) { k -= bpm; ++mbx; }
+        if (mbx >= mbw) { mbx -= mbw; ++mby; }
     }
 }
 

@@ -41,6 +41,14 @@ struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
 
 // Device workspace for one group of images processed together (slot i = image i of the
 // group). Capacities are per slot and cover any sampling NanoJPEG accepts at max_w x max_h.
+// Absolute quantized DC per block: stored in the block itself (natural index 0, never an AC
+// position) as int16; values outside int16 (only corrupt streams) store kDcEscape there and the
+// exact int32 in GroupWs::dc. Keeps the DC inside the block's 128-byte line (no scattered stores).
+constexpr int16_t kDcEscape = INT16_MIN;
+__host__ __device__ inline int16_t dc_cell(int32_t dc) {
+    return (dc > -32768 && dc <= 32767) ? (int16_t)dc : kDcEscape;
+}
+
 struct GroupWs {
     int slots = 0;
     int max_w = 0, max_h = 0;
@@ -49,7 +57,7 @@ struct GroupWs {
     int64_t tmp_cap = 0;     // bytes per ping-pong buffer per component per slot
     Desc* desc = nullptr;    // [slots]
     int16_t* ac = nullptr;   // [slots][coef_cap][64] quantized coefficients, natural order
-    int32_t* dc = nullptr;   // [slots][coef_cap] absolute quantized DC per block
+    int32_t* dc = nullptr;   // [slots][coef_cap] int32 DC of blocks whose cell holds kDcEscape
     uint8_t* planes = nullptr;  // [slots][plane_cap]
     uint8_t* tmp = nullptr;     // [slots][3 comps][2 buffers][tmp_cap]
     // parallel entropy decode

@@ -376,6 +376,27 @@ ICX_HD int32_t extend(int32_t v, int nb) {
 // shortcuts exactly as the reference tests them (on the shifted values).
 enum { kW1 = 2841, kW2 = 2676, kW3 = 2408, kW5 = 1609, kW6 = 1108, kW7 = 565 };
 
+// 24-bit multiply: the low 32 bits of the product of two operands that fit in signed 24 bits,
+// i.e. exactly wmul for such operands (v_mul_i32_i24, full rate; v_mul_lo_u32 is quarter rate).
+ICX_HD int32_t m24(int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __mul24(a, b);
+#else
+    return (int32_t)(uint32_t)((int64_t)a * (int64_t)b);
+#endif
+}
+template <bool F>
+ICX_HD int32_t imul(int32_t a, int32_t b) { return F ? m24(a, b) : wmul(a, b); }
+// The IDCT passes multiply constants by inputs and by pairwise sums of inputs (the 181 products
+// of the last butterfly stay 32-bit): with every multiplied input below 2^22 in magnitude all
+// those operands fit in 24 bits, so the F = true instantiation is exact.
+ICX_HD bool idct_fast_ok(const int32_t (&v)[8]) {
+    const uint32_t lim = 1u << 22;
+    auto ok = [&](int32_t x) { return (uint32_t)(x + (int32_t)lim) < 2 * lim; };
+    return ok(v[1]) && ok(v[2]) && ok(v[3]) && ok(v[5]) && ok(v[6]) && ok(v[7]);
+}
+
+template <bool F = false>
 ICX_HD void idct_row(int32_t (&r)[8]) {
     int32_t a4 = wshl(r[4], 11);
     if (!(a4 | r[6] | r[2] | r[1] | r[7] | r[5] | r[3])) {
@@ -385,17 +406,17 @@ ICX_HD void idct_row(int32_t (&r)[8]) {
     }
     int32_t x0 = wadd(wshl(r[0], 11), 128), x1 = a4, x2 = r[6], x3 = r[2];
     int32_t x4 = r[1], x5 = r[7], x6 = r[5], x7 = r[3], x8;
-    x8 = wmul(kW7, wadd(x4, x5));
-    x4 = wadd(x8, wmul(kW1 - kW7, x4));
-    x5 = wsub(x8, wmul(kW1 + kW7, x5));
-    x8 = wmul(kW3, wadd(x6, x7));
-    x6 = wsub(x8, wmul(kW3 - kW5, x6));
-    x7 = wsub(x8, wmul(kW3 + kW5, x7));
+    x8 = imul<F>(kW7, wadd(x4, x5));
+    x4 = wadd(x8, imul<F>(kW1 - kW7, x4));
+    x5 = wsub(x8, imul<F>(kW1 + kW7, x5));
+    x8 = imul<F>(kW3, wadd(x6, x7));
+    x6 = wsub(x8, imul<F>(kW3 - kW5, x6));
+    x7 = wsub(x8, imul<F>(kW3 + kW5, x7));
     x8 = wadd(x0, x1);
     x0 = wsub(x0, x1);
-    x1 = wmul(kW6, wadd(x3, x2));
-    x2 = wsub(x1, wmul(kW2 + kW6, x2));
-    x3 = wadd(x1, wmul(kW2 - kW6, x3));
+    x1 = imul<F>(kW6, wadd(x3, x2));
+    x2 = wsub(x1, imul<F>(kW2 + kW6, x2));
+    x3 = wadd(x1, imul<F>(kW2 - kW6, x3));
     x1 = wadd(x4, x6);
     x4 = wsub(x4, x6);
     x6 = wadd(x5, x7);
@@ -417,6 +438,7 @@ ICX_HD void idct_row(int32_t (&r)[8]) {
 }
 
 // Column pass: v[i] = coefficient row i of one column; writes 8 clipped samples.
+template <bool F = false>
 ICX_HD void idct_col(const int32_t (&v)[8], uint8_t (&out)[8]) {
     int32_t a4 = wshl(v[4], 8);
     if (!(a4 | v[6] | v[2] | v[1] | v[7] | v[5] | v[3])) {
@@ -426,17 +448,17 @@ ICX_HD void idct_col(const int32_t (&v)[8], uint8_t (&out)[8]) {
     }
     int32_t x0 = wadd(wshl(v[0], 8), 8192), x1 = a4, x2 = v[6], x3 = v[2];
     int32_t x4 = v[1], x5 = v[7], x6 = v[5], x7 = v[3], x8;
-    x8 = wadd(wmul(kW7, wadd(x4, x5)), 4);
-    x4 = wadd(x8, wmul(kW1 - kW7, x4)) >> 3;
-    x5 = wsub(x8, wmul(kW1 + kW7, x5)) >> 3;
-    x8 = wadd(wmul(kW3, wadd(x6, x7)), 4);
-    x6 = wsub(x8, wmul(kW3 - kW5, x6)) >> 3;
-    x7 = wsub(x8, wmul(kW3 + kW5, x7)) >> 3;
+    x8 = wadd(imul<F>(kW7, wadd(x4, x5)), 4);
+    x4 = wadd(x8, imul<F>(kW1 - kW7, x4)) >> 3;
+    x5 = wsub(x8, imul<F>(kW1 + kW7, x5)) >> 3;
+    x8 = wadd(imul<F>(kW3, wadd(x6, x7)), 4);
+    x6 = wsub(x8, imul<F>(kW3 - kW5, x6)) >> 3;
+    x7 = wsub(x8, imul<F>(kW3 + kW5, x7)) >> 3;
     x8 = wadd(x0, x1);
     x0 = wsub(x0, x1);
-    x1 = wadd(wmul(kW6, wadd(x3, x2)), 4);
-    x2 = wsub(x1, wmul(kW2 + kW6, x2)) >> 3;
-    x3 = wadd(x1, wmul(kW2 - kW6, x3)) >> 3;
+    x1 = wadd(imul<F>(kW6, wadd(x3, x2)), 4);
+    x2 = wsub(x1, imul<F>(kW2 + kW6, x2)) >> 3;
+    x3 = wadd(x1, imul<F>(kW2 - kW6, x3)) >> 3;
     x1 = wadd(x4, x6);
     x4 = wsub(x4, x6);
     x6 = wadd(x5, x7);

@@ -523,9 +523,9 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
                 } else {
                     if (coef == 0) {
                         pred[ci] = wadd(pred[ci], val);
-#ifndef ICX_EXP_NODC  // timing experiment only
-                        D[bi] = pred[ci];
-#endif
+                        const int16_t cell = dc_cell(pred[ci]);
+                        sv[slot_elem(threadIdx.x, 0)] = cell;
+                        if (cell == kDcEscape) D[bi] = pred[ci];
                     } else if (coef > 0) {
                         sv[slot_elem(threadIdx.x, T.nat_of_zig[coef])] = (int16_t)val;
                     }
