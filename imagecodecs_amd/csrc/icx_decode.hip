@@ -523,15 +523,26 @@ __device__ __forceinline__ CRaw chroma_fetch(const CPl& c, int r, int M, bool fa
     }
     return CRaw{0u, 0u};  // edge lanes load inside chroma_make
 }
+// The 4-tap kernel as one v_dot4 on four packed samples: samples are biased to int8 (x ^ 0x80
+// = x - 128) and, since the taps sum to 128, sum(k*x) + 64 = dot(k, x - 128) + 128*128 + 64.
+// kTapFwd weighs bytes (s0..s3) as tap4(s0, s1, s2, s3); kTapRev as tap4(s3, s2, s1, s0).
+constexpr uint32_t kBias8 = 0x80808080u;
+constexpr int32_t kTapFwd = (int32_t)((uint32_t)(uint8_t)-9 | (111u << 8) | (29u << 16) | ((uint32_t)(uint8_t)-3 << 24));
+constexpr int32_t kTapRev = (int32_t)((uint32_t)(uint8_t)-3 | (29u << 8) | (111u << 16) | ((uint32_t)(uint8_t)-9 << 24));
+__device__ __forceinline__ uint32_t dtap(uint32_t biased, int32_t k) {
+    const int32_t v = __builtin_amdgcn_sdot4((int)biased, k, 128 * 128 + 64, false) >> 7;
+    return (uint32_t)min(max(v, 0), 255);
+}
+
 template <bool KH>
 __device__ __forceinline__ uint32_t chroma_make(const CPl& c, int r, int M, bool fast, const CRaw& raw) {
     if (!KH) return raw.d0;
     if (fast) {
-        const uint64_t w = (uint64_t)raw.d0 | ((uint64_t)raw.d1 << 32);
-        const uint64_t b = w >> ((M & 1) ? 0 : 16);  // bytes b0..b5 = samples 2M-2 .. 2M+3
-        const int b0 = (int)(b & 255), b1 = (int)((b >> 8) & 255), b2 = (int)((b >> 16) & 255);
-        const int b3 = (int)((b >> 24) & 255), b4 = (int)((b >> 32) & 255), b5 = (int)((b >> 40) & 255);
-        return pack4(tap4(b3, b2, b1, b0), tap4(b1, b2, b3, b4), tap4(b4, b3, b2, b1), tap4(b2, b3, b4, b5));
+        const uint64_t w = ((uint64_t)raw.d0 | ((uint64_t)raw.d1 << 32)) ^ 0x8080808080808080ull;
+        const uint64_t b = w >> ((M & 1) ? 0 : 16);  // bytes b0..b5 = samples 2M-2 .. 2M+3 (biased)
+        const uint32_t w0 = (uint32_t)b, w1 = (uint32_t)(b >> 8), w2 = (uint32_t)(b >> 16);
+        // tap4(b3,b2,b1,b0), tap4(b1,b2,b3,b4), tap4(b4,b3,b2,b1), tap4(b2,b3,b4,b5)
+        return pack4(dtap(w0, kTapRev), dtap(w1, kTapFwd), dtap(w1, kTapRev), dtap(w2, kTapFwd));
     }
     const uint8_t* row = c.p + (int64_t)r * c.s;
     const int n2 = c.w << 1, s = c.s;
@@ -674,12 +685,44 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
             }
             return p;
         };
+        // Interior rows: per output column i, a dword of the 4 window rows' samples (biased),
+        // E = rows k-2..k+1 (even output 2k: kTapRev), O = rows k-1..k+2 (odd 2k+1: kTapFwd);
+        // each row pair shifts one new row into the columns with one v_perm per column.
+        auto column = [](uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, int i) {
+            const uint32_t sel = 0x0c0c0400u | (uint32_t)(i * 0x0101);  // byte i of the low operand, byte i of the high
+            return __builtin_amdgcn_perm(r1, r0, sel) | (__builtin_amdgcn_perm(r3, r2, sel) << 16);
+        };
+        uint32_t ca[4], ce[4];  // E columns of components 1 and 2
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ca[i] = column(a0, a1, a2, a3, i) ^ kBias8;
+            ce[i] = column(e0, e1, e2, e3, i) ^ kBias8;
+        }
+        auto vsteps = [&](int k, uint32_t (&cc)[4], uint32_t nrow, int h, uint32_t w0, uint32_t w1, uint32_t w2,
+                          uint32_t w3, uint32_t& ev, uint32_t& od) {
+            const uint32_t nb = nrow ^ kBias8;
+            uint32_t oc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)  // O = (E >> 8) | new row's byte i << 24
+                oc[i] = __builtin_amdgcn_perm(nb, cc[i], 0x00030201u | ((uint32_t)(4 + i) << 24));
+            if (k >= 2 && k <= h - 3) {  // both outputs interior (wave-uniform)
+                ev = pack4(dtap(cc[0], kTapRev), dtap(cc[1], kTapRev), dtap(cc[2], kTapRev), dtap(cc[3], kTapRev));
+                od = pack4(dtap(oc[0], kTapFwd), dtap(oc[1], kTapFwd), dtap(oc[2], kTapFwd), dtap(oc[3], kTapFwd));
+            } else {
+                ev = vtap_even(k, h, w0, w1, w2, w3);
+                od = vtap_odd(k, h, w1, w2, w3, nrow);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cc[i] = oc[i];
+        };
         auto step = [&](int k, const Pre& p) {
             const uint32_t a4 = chroma_make<KH>(c1, cr1(k + 2), M, f1, p.a);
             const uint32_t e4 = chroma_make<KH>(c2, cr2(k + 2), M, f2, p.e);
-            emit(2 * k, p.y0, vtap_even(k, c1.h, a0, a1, a2, a3), vtap_even(k, c2.h, e0, e1, e2, e3));
-            if (2 * k + 1 < Y1)
-                emit(2 * k + 1, p.y1, vtap_odd(k, c1.h, a1, a2, a3, a4), vtap_odd(k, c2.h, e1, e2, e3, e4));
+            uint32_t ae, ao, ee, eo;
+            vsteps(k, ca, a4, c1.h, a0, a1, a2, a3, ae, ao);
+            vsteps(k, ce, e4, c2.h, e0, e1, e2, e3, ee, eo);
+            emit(2 * k, p.y0, ae, ee);
+            if (2 * k + 1 < Y1) emit(2 * k + 1, p.y1, ao, eo);
             a0 = a1; a1 = a2; a2 = a3; a3 = a4;
             e0 = e1; e1 = e2; e2 = e3; e3 = e4;
         };
