@@ -216,7 +216,7 @@ def main():
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             if tj.get("workload") == args.workload and tj.get("kernel") == kname and \
-                    tj.get("images_per_bench_step") in (None, n):
+                    tj.get("images_per_launch") == -(-n // launches):
                 traffic = tj.get("bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

@@ -46,7 +46,9 @@ def parse(fetch_dir, write_dir, kernel, workload, images):
     w_kib = sum(wv) / len(wv)
     fetch_b = 2.0 * f_kib * 1024.0  # gfx950: FETCH_SIZE = half the bytes of 16 B/lane reads
     write_b = w_kib * 1024.0
-    return {"workload": workload, "kernel": kernel, "images_per_bench_step": images,
+    n_images = images or {"c3": 512, "c2": 1024}.get(workload)
+    return {"workload": workload, "kernel": kernel, "images_per_bench_step": n_images,
+            "images_per_launch": n_images // len(fv) if n_images else None,
             "launches": len(fv), "fetch_size_kib_raw": round(f_kib, 1), "write_size_kib_raw": round(w_kib, 1),
             "fetch_bytes": round(fetch_b), "write_bytes": round(write_b),
             "bytes_per_launch": round(fetch_b + write_b),
