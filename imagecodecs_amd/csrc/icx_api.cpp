@@ -161,9 +161,10 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     ws.tmp_cap = ws_tmp_cap(max_w, max_h);
     ws.ucap = ((int64_t)max_w * max_h + 4095) / 4096 * 4096;  // 1 B/px of entropy data (q90 ~0.4)
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
+    ws.rst_cap = ((int64_t)max_w / 8 + 1) * ((int64_t)max_h / 8 + 1);  // >= MCUs per image
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
     const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) +
-                             ws.ucap + tiles_per_slot * 20 +
+                             ws.ucap + tiles_per_slot * 28 + ws.rst_cap * 8 +
                              lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
     if (group <= 0) {  // auto: up to 60% of the free HBM (288 GB per MI355X), at least one image
         size_t free_b = 0, total_b = 0;
@@ -191,6 +192,8 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.ucap * group + 256), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.X, sizeof(uint64_t) * ws.lanes_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.sub, sizeof(SubRec) * ws.lanes_cap), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.rst, sizeof(int64_t) * ws.rst_cap * group), nullptr);
+    ICX_HIP(ctx, hipMalloc(&ws.tile_rbase, sizeof(int32_t) * ws.tiles_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.ent, sizeof(LaneEntry) * ws.lanes_cap), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.stats, sizeof(int32_t) * 4), nullptr);
     ICX_HIP(ctx, hipMalloc(&ws.Y, sizeof(uint64_t) * ws.lanes_cap), nullptr);
@@ -212,7 +215,7 @@ void icx_batch_destroy(icx_batch* b) {
     (void)hipFree(b->ws.tmp);
     for (void* p : {(void*)b->ws.spec, (void*)b->ws.tilepre, (void*)b->ws.wgpre, (void*)b->ws.wg2pre, (void*)b->ws.totals,
                     (void*)b->ws.tiles, (void*)b->ws.tile_obase, (void*)b->ws.U, (void*)b->ws.X,
-                    (void*)b->ws.sub, (void*)b->ws.ent, (void*)b->ws.stats, (void*)b->ws.Y,
+                    (void*)b->ws.sub, (void*)b->ws.rst, (void*)b->ws.tile_rbase, (void*)b->ws.ent, (void*)b->ws.stats, (void*)b->ws.Y,
                     (void*)b->ws.rec, (void*)b->ws.nrec, (void*)b->ws.guess_cnt, (void*)b->ws.repair})
         if (p) (void)hipFree(p);
     if (b->d_hin) (void)hipFree(b->d_hin);

@@ -22,17 +22,19 @@ constexpr int kSpecMaxBpm = 16;    // blocks per MCU handled by the parallel pat
 enum : int32_t { kSpecSyntax = 1, kSpecGiveUp = 2 };
 
 struct SpecImg {
-    int32_t mode;          // 0 not on this path, 1 active, 2 fall back to the sequential kernel
+    int32_t mode;          // 0 not on this path, 1 active, 2 fall back to the sequential kernel,
+                           // 3 restart intervals (DRI): one write lane per interval
     int32_t err;           // kSpecSyntax | kSpecGiveUp (atomicOr)
     int32_t ntiles, tile_base;
     int32_t nwg, wg_base;  // 256-lane decode groups, flat numbering over the batch group
     int32_t nsub, nrepair;   // lanes; unsynchronised lanes queued for repair
+    int32_t nint, nrst;      // DRI (mode 3): restart intervals; restart markers found in U
     int64_t scan_len;      // raw entropy-coded bytes (file end - scan start)
     int64_t ulen;          // unstuffed data bytes before FF D9 / end of file / bad marker
     int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)
     int64_t total_blocks;
 };
-struct TileRec { int32_t kept, end_err; int64_t end_at; };
+struct TileRec { int32_t kept, end_err; int64_t end_at; int32_t nrst, pad_; };
 struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };
 // A block-start state seen by a guess lane: bit offset from the lane start, block-in-MCU,
 // DC codes decoded before it, and the per-component DC-diff sums before it.
@@ -79,6 +81,9 @@ struct GroupWs {
     int32_t* guess_cnt = nullptr;  // [lanes_cap][4]: DC codes and DC sums over the whole guess lane
     int32_t* repair = nullptr;  // [slots][kMaxRepair] lanes whose chain needs a serial repair
     SubRec* sub = nullptr;      // [lanes_cap]
+    int64_t rst_cap = 0;        // restart markers recorded per slot (>= MCUs per image)
+    int64_t* rst = nullptr;     // [slots][rst_cap] (U byte index << 3) | marker number
+    int32_t* tile_rbase = nullptr;  // [tiles_cap] restart markers before the tile (per image)
     LaneEntry* ent = nullptr;   // [lanes_cap]
     int32_t* stats = nullptr;   // [4] path counters, accumulated over a batch call
 };

@@ -57,15 +57,20 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ de
             s.mode = 0;
             s.err = 0;
             s.nrepair = 0;
+            s.nrst = 0;
             const int64_t scan_len = d.size - d.scan_off;
-            const bool ok = d.status == kPending && d.restart == 0 && d.nc >= 1 && d.bpm <= kSpecMaxBpm &&
-                            scan_len > 0 && scan_len <= ucap;
+            const bool ok = d.status == kPending && d.nc >= 1 && d.bpm <= kSpecMaxBpm && scan_len > 0 &&
+                            scan_len <= ucap;
             if (ok) {
-                s.mode = 1;
+                s.mode = d.restart == 0 ? 1 : 3;
                 s.scan_len = scan_len;
                 s.total_blocks = (int64_t)d.mbw * d.mbh * d.bpm;
                 nt = (int)((scan_len + kTileBytes - 1) / kTileBytes);
-                const int64_t nsub = (scan_len + kSubBytes - 1) / kSubBytes;
+                // lanes: 2 KiB subsequences, or (DRI) one per restart interval
+                const int64_t nmcu = (int64_t)d.mbw * d.mbh;
+                const int64_t nsub = s.mode == 1 ? (scan_len + kSubBytes - 1) / kSubBytes
+                                                 : (nmcu + d.restart - 1) / d.restart;
+                s.nint = s.mode == 3 ? (int32_t)nsub : 0;
                 nw = (int)((nsub + kLanes - 1) / kLanes);
                 nw2 = (int)((nsub + kWriteLanesBig - 1) / kWriteLanesBig);
             }
@@ -135,15 +140,17 @@ __device__ __forceinline__ long long wave_min_ll(long long v) {
 // WRITE), that event's raw offset (-1: none) and whether it is an error.
 template <bool WRITE>
 __device__ __forceinline__ int ustf_lane(const uint8_t* R, int64_t L, int64_t a, int64_t& end_at, int& end_err,
-                                         uint8_t* out, int32_t& giveup) {
+                                         uint8_t* out, int32_t& giveup, RstSink& rs) {
     int kept = 0;
     end_at = -1;
     end_err = 0;
+    const int64_t ub = rs.ubase;
 #pragma unroll
     for (int c = 0; c < kLaneRaw / kChunk; ++c) {
         int64_t e;
         int er;
-        kept += ustf_chunk<WRITE>(R, L, a + c * kChunk, &e, &er, WRITE ? out + kept : nullptr, &giveup);
+        rs.ubase = ub + kept;
+        kept += ustf_chunk<WRITE>(R, L, a + c * kChunk, &e, &er, WRITE ? out + kept : nullptr, &giveup, &rs);
         if (e >= 0) {
             end_at = e;
             end_err = er;
@@ -181,12 +188,14 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
         int64_t end_at;
         int end_err;
         int32_t giveup = 0;
-        const int kept = ustf_lane<false>(R, L, a, end_at, end_err, nullptr, giveup);
+        RstSink rs{0, 0, nullptr, 0, 0};
+        const int kept = ustf_lane<false>(R, L, a, end_at, end_err, nullptr, giveup, rs);
         if (giveup) atomicOr(&spec[i].err, kSpecGiveUp);
         const long long tend = wave_min_ll(end_at >= 0 ? (long long)end_at : LLONG_MAX);
-        // kept bytes before the tile's first end event
+        // kept bytes (and restart markers) before the tile's first end event
         const bool before = end_at >= 0 ? end_at <= tend : a < tend;
         const int incl = wave_incl_scan(before ? kept : 0);
+        const int rincl = wave_incl_scan(before ? rs.n : 0);
         const uint64_t owner = __ballot(end_at >= 0 && end_at == tend);  // the unique lane owning that FF
         const int err = __shfl(end_err, owner ? __ffsll((long long)owner) - 1 : 0);
         if (lane == 63) {
@@ -194,6 +203,8 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
             r.kept = incl;
             r.end_at = tend == LLONG_MAX ? -1 : tend;
             r.end_err = owner ? err : 0;
+            r.nrst = rincl;
+            r.pad_ = 0;
             tiles[t] = r;
         }
     }
@@ -201,13 +212,13 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
 
 // Per image: exclusive prefix of kept bytes over tiles, data length, error position.
 __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ spec, TileRec* __restrict__ tiles,
-                                                   int32_t* __restrict__ tile_obase) {
+                                                   int32_t* __restrict__ tile_obase, int32_t* __restrict__ tile_rbase) {
     __shared__ int sh[256];
     __shared__ int s_first_end;
     const int i = blockIdx.x;
     if (i >= n) return;
     SpecImg& s = spec[i];
-    if (s.mode != 1) return;
+    if (s.mode != 1 && s.mode != 3) return;
     if (threadIdx.x == 0) s_first_end = INT32_MAX;
     __syncthreads();
     for (int t = threadIdx.x; t < s.ntiles; t += blockDim.x)
@@ -215,22 +226,31 @@ __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ 
     __syncthreads();
     const int fe = s_first_end;
     int64_t carry = 0;
+    int32_t rcarry = 0;
     for (int t0 = 0; t0 < s.ntiles; t0 += blockDim.x) {
         const int t = t0 + threadIdx.x;
-        const int k = (t < s.ntiles && t <= fe) ? tiles[s.tile_base + t].kept : 0;
+        const bool in = t < s.ntiles && t <= fe;
+        const int k = in ? tiles[s.tile_base + t].kept : 0;
+        const int nr = in ? tiles[s.tile_base + t].nrst : 0;
         const int ex = block_exclusive_scan(k, sh);
-        if (t < s.ntiles) tile_obase[s.tile_base + t] = (int32_t)(carry + ex);
-        __shared__ int s_sum;
-        if (threadIdx.x == blockDim.x - 1) s_sum = ex + k;
+        const int rex = block_exclusive_scan(nr, sh);
+        if (t < s.ntiles) {
+            tile_obase[s.tile_base + t] = (int32_t)(carry + ex);
+            tile_rbase[s.tile_base + t] = rcarry + rex;
+        }
+        __shared__ int s_sum, s_rsum;
+        if (threadIdx.x == blockDim.x - 1) { s_sum = ex + k; s_rsum = rex + nr; }
         __syncthreads();
         carry += s_sum;
+        rcarry += s_rsum;
         __syncthreads();
     }
     if (threadIdx.x == 0) {
         s.ulen = carry;
+        s.nrst = rcarry;
         s.errpos = (fe != INT32_MAX && tiles[s.tile_base + fe].end_err) ? carry : INT64_MAX;
         const int64_t nsub = carry > 0 ? (carry + kSubBytes - 1) / kSubBytes : 1;
-        s.nsub = (int32_t)nsub;
+        s.nsub = s.mode == 3 ? s.nint : (int32_t)nsub;
     }
 }
 
@@ -238,8 +258,9 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
                                                     const uint64_t* __restrict__ off, const Desc* __restrict__ desc,
                                                     const SpecImg* __restrict__ spec, const int32_t* __restrict__ tilepre,
                                                     const int32_t* __restrict__ totals, const TileRec* __restrict__ tiles,
-                                                    const int32_t* __restrict__ tile_obase, uint8_t* __restrict__ U,
-                                                    int64_t ucap) {
+                                                    const int32_t* __restrict__ tile_obase,
+                                                    const int32_t* __restrict__ tile_rbase, uint8_t* __restrict__ U,
+                                                    int64_t ucap, int64_t* __restrict__ rst, int64_t rst_cap) {
     __shared__ uint32_t sbuf_all[4][kTileBytes / 4 + 8];  // per wave: the tile's kept bytes
     const int lane = threadIdx.x & 63;
     uint32_t* sbuf = sbuf_all[threadIdx.x >> 6];
@@ -257,11 +278,19 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
         int64_t end_at;
         int end_err;
         int32_t giveup = 0;
-        const int kept = ustf_lane<false>(R, s.scan_len, a, end_at, end_err, nullptr, giveup);
+        RstSink rs0{0, 0, nullptr, 0, 0};
+        const int kept = ustf_lane<false>(R, s.scan_len, a, end_at, end_err, nullptr, giveup, rs0);
         const bool before = end_at >= 0 ? (tend < 0 || end_at <= tend) : (tend < 0 || a < tend);
         const int k = before ? kept : 0;
         const int incl = wave_incl_scan(k);
-        if (k) ustf_lane<true>(R, s.scan_len, a, end_at, end_err, sb + (incl - k), giveup);
+        const int nr = before ? rs0.n : 0;
+        const int rincl = wave_incl_scan(nr);
+        if (k) {
+            // restart markers go to the image's list in stream order (ordinal = markers before)
+            RstSink rs{0, obase + (incl - k), nr ? rst + (int64_t)i * rst_cap : nullptr,
+                       tile_rbase[t] + rincl - nr, (int32_t)min<int64_t>(rst_cap, INT32_MAX)};
+            ustf_lane<true>(R, s.scan_len, a, end_at, end_err, sb + (incl - k), giveup, rs);
+        }
         const int tile_kept = __shfl(incl, 63);
         __builtin_amdgcn_wave_barrier();
         // copy out: bytes up to the first 16-byte boundary and after the last one byte-wise
@@ -316,6 +345,7 @@ __global__ __launch_bounds__(256) void k_spec_guess(int n, const Desc* __restric
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
         const SpecImg& s = spec[i];
+        if (s.mode != 1) continue;  // uniform per workgroup
         const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
         if (j >= s.nsub - 1) continue;  // the last lane's exit is never needed
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
@@ -338,6 +368,7 @@ __global__ __launch_bounds__(256) void k_spec_count(int n, const Desc* __restric
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
         SpecImg& s = spec[i];
+        if (s.mode != 1) continue;  // uniform per workgroup
         const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
         if (j >= s.nsub - 1) continue;
         const int64_t base = (int64_t)s.wg_base * kLanes, f = base + j;
@@ -450,7 +481,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
                                                     const uint8_t* __restrict__ U, int64_t ucap,
                                                     const uint64_t* __restrict__ X, const LaneEntry* __restrict__ ent,
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
-                                                    int64_t coef_cap) {
+                                                    int64_t coef_cap, const int64_t* __restrict__ rst, int64_t rst_cap) {
     __shared__ LdsTables T;
     __shared__ int4 slots[NL][8];
     __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
@@ -464,17 +495,28 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wpre, n, wg, cur, T, desc);
         SpecImg& s = spec[i];
-        if (s.mode != 1) continue;  // uniform per workgroup
+        if (s.mode != 1 && s.mode != 3) continue;  // uniform per workgroup
+        const bool dri = s.mode == 3;
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         const Sel S = make_sel(desc[i]);
+        // DRI: lane j = restart interval j, from the byte after marker j-1, exactly R MCUs, DC 0
+        const int64_t* RS = rst + (int64_t)i * rst_cap;
+        const int64_t iblocks = (int64_t)desc[i].restart * desc[i].bpm;
+        bool lane_ok = true;
+        int64_t start_byte = 0;
+        if (dri && j < s.nsub && j > 0) {
+            if (j - 1 < s.nrst && j - 1 < rst_cap) start_byte = (RS[j - 1] >> 3) + 2;
+            else lane_ok = false;  // marker missing: the sequential decoder decides
+        }
         const int64_t base = (int64_t)s.wg_base * kLanes;
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
         int4* A = reinterpret_cast<int4*>(ac + (int64_t)i * coef_cap * 64);
         int32_t* D = dcv + (int64_t)i * coef_cap;
         const int64_t total_blocks = s.total_blocks;
-        bool act = j < s.nsub;
+        bool act = j < s.nsub && lane_ok;
         // every lane runs a reader (lanes past the image's last lane idle at position 0)
-        const uint64_t entry = (!act || j == 0) ? pack_state(0, 0, 0) : X[base + j - 1];
+        const uint64_t entry = dri ? pack_state(start_byte * 8, 0, 0)
+                                   : ((!act || j == 0) ? pack_state(0, 0, 0) : X[base + j - 1]);
         Reader r;
         r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
         int b = st_b(entry), z = st_z(entry), coef, ci = 0;
@@ -488,7 +530,13 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
         const uint32_t kFar = 1u << 30;
         const uint32_t err_rel = errbits == INT64_MAX ? kFar : (uint32_t)min<int64_t>(kFar, max<int64_t>(0, errbits - e0));
         uint32_t lim_rel = kFar;
-        if (act) {
+        int64_t bend = total_blocks;  // block index the lane stops at
+        uint32_t used_end = 0;        // bits consumed when the lane's last block completed
+        if (act && dri) {
+            bi = j * iblocks;
+            bend = min(total_blocks, bi + iblocks);
+            act = bi < bend;
+        } else if (act) {
             limit = j == s.nsub - 1 ? INT64_MAX : st_pos(X[base + j]);
             if (limit != INT64_MAX) lim_rel = (uint32_t)min<int64_t>(kFar, max<int64_t>(0, limit - e0));
             const LaneEntry le = ent[base + j];
@@ -532,7 +580,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
                     if (z == 0) {
                         done = true;
                         bdone = bi++;
-                        act = bi < total_blocks;
+                        act = bi < bend;
+                        used_end = r.used;  // (the reader keeps moving once the lane is idle)
                     }
                 }
             }
@@ -567,17 +616,30 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
 #pragma unroll
             for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
         }
+        if (dri && j < s.nsub) {
+            // NanoJPEG after R MCUs: byte-align, read 16 bits = FF D0+(j&7) (jpeg_dec.h:707-715).
+            // The parallel result stands only if that is exactly marker j at the aligned end of
+            // the interval and no error byte was in the data; else the sequential decoder runs.
+            bool exact = lane_ok && s.errpos == INT64_MAX;
+            if (exact && !bad && j + 1 < s.nsub) {
+                const int64_t endbyte = (start_byte * 8 + used_end + 7) >> 3;
+                exact = j < s.nrst && j < rst_cap && (RS[j] >> 3) == endbyte && (int)(RS[j] & 7) == (int)(j & 7);
+            }
+            if (!exact) atomicOr(&s.err, kSpecGiveUp);
+        }
     }
 }
 
-__global__ void k_spec_finish(int n, Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
+__global__ void k_spec_finish(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                               int32_t* __restrict__ stats) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const SpecImg& s = spec[i];
-    if (s.mode == 1) desc[i].status = (s.err & kSpecSyntax) ? kSyntaxError : kOk;
-    // path statistics: [0] parallel path, [1] parallel -> sequential fallback, [2] sequential only
-    if (s.mode == 1) atomicAdd(&stats[0], 1);
+    SpecImg& s = spec[i];
+    if (s.mode == 3 && (s.err & kSpecGiveUp)) s.mode = 2;  // DRI markers not where NanoJPEG reads them
+    if (s.mode == 1 || s.mode == 3) desc[i].status = (s.err & kSpecSyntax) ? kSyntaxError : kOk;
+    // path statistics: [0] parallel path (incl. DRI intervals), [1] parallel -> sequential
+    // fallback, [2] sequential only
+    if (s.mode == 1 || s.mode == 3) atomicAdd(&stats[0], 1);
     else if (s.mode == 2) atomicAdd(&stats[1], 1);
     else if (desc[i].status == kPending) atomicAdd(&stats[2], 1);
 }
@@ -592,9 +654,9 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
                        ws.totals, ws.ucap);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
-    hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase);
+    hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase);
     hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
-                       ws.totals, ws.tiles, ws.tile_obase, ws.U, ws.ucap);
+                       ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.ucap, ws.rst, ws.rst_cap);
     E(kStUnstuff);
     B(kStEntropy);
     hipLaunchKernelGGL(k_spec_guess, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
@@ -608,10 +670,10 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     B(kStWrite);
     if ((int64_t)ws.max_w * ws.max_h >= (int64_t)2048 * 2048)  // >= 1 MB of entropy data per image
         hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec,
-                           ws.wg2pre, ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);
+                           ws.wg2pre, ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
     else
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap);
+                           ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
     E(kStWrite);
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
 }

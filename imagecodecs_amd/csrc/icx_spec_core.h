@@ -26,6 +26,20 @@ ICX_HD bool carry_after_ff(const uint8_t* R, int64_t a, int32_t* giveup) {
     return k & 1;
 }
 
+// Restart markers met by the unstuff automaton (DRI images): counted, and when `pos` is set,
+// recorded in stream order as (byte index in U << 3) | marker number.
+struct RstSink {
+    int32_t n;      // markers seen
+    int64_t ubase;  // U index of out[0] (WRITE)
+    int64_t* pos;   // destination array (WRITE), indexed by ord
+    int32_t ord, cap;
+    ICX_HD void hit(int kept, int m) {
+        if (pos && ord < cap) pos[ord] = ((ubase + kept) << 3) | (m & 7);
+        ++ord;
+        ++n;
+    }
+};
+
 // Bytes R[a-1 .. a+19) as five little-endian words, read with aligned dword loads (the bytes
 // before R are the file's headers, a > 0; the bytes after stay inside the scan, a + 24 <= L).
 ICX_HD bool ustf_window(const uint8_t* R, int64_t L, int64_t a, uint32_t (&v)[5]) {
@@ -46,7 +60,7 @@ ICX_HD int win_byte(const uint32_t (&v)[5], int i) {  // i = -1 .. 18 -> R[a+i]
 
 template <bool WRITE>
 ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, int* end_err,
-                                          uint8_t* out, int32_t* giveup) {
+                                          uint8_t* out, int32_t* giveup, RstSink* rs = nullptr) {
     *end_at = -1;
     *end_err = 0;
     if (a >= L) return 0;
@@ -85,6 +99,7 @@ ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, i
                 after_ff = true;
             } else if ((m & 0xF8) == 0xD0) {
                 if (WRITE) { out[kept] = 0xFF; out[kept + 1] = (uint8_t)m; }
+                if (rs) rs->hit(kept, m);
                 kept += 2;
                 after_ff = true;
             } else {
@@ -114,6 +129,7 @@ ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, i
             after_ff = true;
         } else if ((m & 0xF8) == 0xD0) {  // RSTn: both bytes enter the bit buffer (:472-475)
             if (WRITE) { out[kept] = 0xFF; out[kept + 1] = m; }
+            if (rs) rs->hit(kept, m);
             kept += 2;
             after_ff = true;
         } else {  // D9 ends the data (:468); anything else is a syntax error (:470-471)
