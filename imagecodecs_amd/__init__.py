@@ -72,6 +72,11 @@ _SIGS = {
     "icx_tje_encode_with_func": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "icx_tje_encode_to_file_at_quality": (_i32, [_vp, C.c_char_p, _i32, _i32, _i32, _i32, _vp]),
     "icx_tje_encode_to_file": (_i32, [_vp, C.c_char_p, _i32, _i32, _i32, _vp]),
+    "icx_jpeg_encode_with_func": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "icx_encoder_create": (_vp, [_vp]),
+    "icx_encoder_destroy": (None, [_vp]),
+    "icx_encoder_stage_times": (_i32, [_vp, _vp, _vp, _i32]),
+    "icx_jpeg_encode_device": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
 }
 
 WRITE_FUNC = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
@@ -195,6 +200,53 @@ class Context:
         buf = C.create_string_buffer(bytes(src), max(1, len(src)))
         ok = lib().icx_tje_encode_with_func(self._p, sink, None, quality, width, height, comps, buf)
         return b"".join(chunks) if ok == 1 else None
+
+    def jpeg_encode(self, quality: int, subsampling: int, width: int, height: int, comps: int, src: bytes):
+        """C4 extension encode (IJG quality 1..100, subsampling 444|420) -> bytes, or None."""
+        chunks = []
+
+        @WRITE_FUNC
+        def sink(_ctx, data, size):
+            chunks.append(C.string_at(data, size))
+
+        buf = C.create_string_buffer(bytes(src), max(1, len(src)))
+        ok = lib().icx_jpeg_encode_with_func(self._p, sink, None, quality, subsampling, width, height, comps, buf)
+        return b"".join(chunks) if ok == 1 else None
+
+
+class Encoder:
+    """Device-resident encode (icx_encoder_* / icx_jpeg_encode_device); pointers are device
+    addresses (ints) on the context's device."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._p = lib().icx_encoder_create(ctx.ptr)
+        if not self._p:
+            raise ICXError("icx_encoder_create failed: " + _err(ctx.ptr))
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().icx_encoder_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+    def encode_device(self, quality, subsampling, width, height, comps, d_src, d_out, out_cap, stream=0):
+        """-> (icx_result, file size in bytes)."""
+        n = C.c_uint64()
+        rc = lib().icx_jpeg_encode_device(self._p, quality, subsampling, width, height, comps, d_src, d_out,
+                                          out_cap, C.byref(n), stream or None)
+        if rc not in (OK, OUT_OF_MEM):
+            raise ICXError(f"icx_jpeg_encode_device -> {rc}: {_err(self.ctx.ptr)}")
+        return rc, int(n.value)
+
+    def stage_times(self) -> dict:
+        """Summed per-stage ms since the previous call (icx_encoder_stage_times)."""
+        names = (C.c_char_p * 8)()
+        ms = (C.c_float * 8)()
+        k = lib().icx_encoder_stage_times(self._p, names, ms, 8)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
 
 
 def probe(jpeg: bytes):

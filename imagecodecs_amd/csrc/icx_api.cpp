@@ -430,4 +430,72 @@ int icx_tje_encode_to_file(icx_ctx* ctx, const char* dest_path, int width, int h
     return icx_tje_encode_to_file_at_quality(ctx, dest_path, 3, width, height, num_components, src);  // :1177-1185
 }
 
+// ------------------------------------------------------------------ encode extension (C4)
+static const char* enc_args_bad(int quality, int subsampling, int width, int height, int comps) {
+    if (quality < 1 || quality > 100) return "quality must be 1..100";
+    if (subsampling != 444 && subsampling != 420) return "subsampling must be 444 or 420";
+    if (comps != 3 && comps != 4) return "num_components must be 3 or 4";
+    if (width > 0xFFFF || height > 0xFFFF || width < 0 || height < 0) return "image too large";
+    return nullptr;
+}
+
+int icx_jpeg_encode_with_func(icx_ctx* ctx, icx_write_func* func, void* context, int quality, int subsampling,
+                              int width, int height, int num_components, const unsigned char* src) {
+    if (!ctx || !func) return 0;
+    if (const char* e = enc_args_bad(quality, subsampling, width, height, num_components)) { ctx->err = e; return 0; }
+    if ((int64_t)width * height > 0 && !src) { ctx->err = "null source"; return 0; }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), 0);
+    std::vector<uint8_t> file;
+    if (!jpeg_encode_gpu(ctx->stream, quality, subsampling, width, height, num_components, src, file)) {
+        ctx->err = "HIP failure in jpeg_encode_gpu";
+        return 0;
+    }
+    for (size_t o = 0; o < file.size(); o += 1023)
+        func(context, file.data() + o, (int)std::min<size_t>(1023, file.size() - o));
+    return 1;
+}
+
+struct icx_encoder {
+    icx_ctx* ctx = nullptr;
+    EncWs* ws = nullptr;
+};
+
+icx_encoder* icx_encoder_create(icx_ctx* ctx) {
+    if (!ctx) return nullptr;
+    icx_encoder* e = new icx_encoder();
+    e->ctx = ctx;
+    e->ws = enc_ws_create();
+    return e;
+}
+
+void icx_encoder_destroy(icx_encoder* enc) {
+    if (!enc) return;
+    (void)hipSetDevice(enc->ctx->device);
+    enc_ws_destroy(enc->ws);
+    delete enc;
+}
+
+int icx_encoder_stage_times(icx_encoder* enc, const char** names, float* ms, int cap) {
+    if (!enc || cap <= 0) return 0;
+    return enc_ws_stage_times(enc->ws, names, ms, cap);
+}
+
+int icx_jpeg_encode_device(icx_encoder* enc, int quality, int subsampling, int width, int height,
+                           int num_components, const uint8_t* d_src, uint8_t* d_out, uint64_t out_cap,
+                           uint64_t* out_size, void* hip_stream) {
+    if (!enc || !out_size) return ICX_UNSUPPORTED;
+    icx_ctx* ctx = enc->ctx;
+    if (const char* e = enc_args_bad(quality, subsampling, width, height, num_components)) {
+        ctx->err = e;
+        return ICX_UNSUPPORTED;
+    }
+    if (((int64_t)width * height > 0 && !d_src) || (out_cap && !d_out)) { ctx->err = "null buffer"; return ICX_UNSUPPORTED; }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    const int rc = jpeg_encode_device(st, enc->ws, quality, subsampling, width, height, num_components, d_src, d_out,
+                                      out_cap, out_size);
+    if (rc < 0) { ctx->err = "HIP failure in jpeg_encode_device"; return ICX_INTERNAL_ERR; }
+    return rc == 0 ? ICX_OK : ICX_OUT_OF_MEM;
+}
+
 }  // extern "C"

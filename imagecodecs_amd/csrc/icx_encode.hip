@@ -1,7 +1,8 @@
-// icx_encode.hip -- gfx950 tiny_jpeg-exact encoder (jpeg_enc.h:786-1175).
+// icx_encode.hip -- gfx950 JPEG encoder: tiny_jpeg-exact (jpeg_enc.h:786-1175) and the C4
+// extension (4:2:0 / 4:4:4, IJG quality; defined by oracle/tje_oracle.c or_jpeg_encode).
 //
-//   k_enc_units   gather + float RGB->YCbCr + AAN float FDCT + quantize, one lane per
-//                 (8x8 block, component) unit                 (jpeg_enc.h:1094-1126, 656-817)
+//   k_enc_units   gather + float RGB->YCbCr (+ 2x2 chroma mean for 4:2:0) + AAN float FDCT +
+//                 quantize, one lane per data unit in MCU order (jpeg_enc.h:1094-1126, 656-817)
 //   k_enc_count   Huffman bit length of every unit            (jpeg_enc.h:831-887)
 //   (scan)        exclusive prefix sum of unit bit lengths -> bit offsets (hipCUB)
 //   k_enc_emit    pack each unit's codes at its bit offset    (jpeg_enc.h:613-643)
@@ -22,6 +23,24 @@ struct EncTables {
     uint16_t code[4][256];    // 0 luma DC, 1 luma AC, 2 chroma DC, 3 chroma AC
     uint8_t len[4][256];
 };
+
+// Data units in stream order: MCU m (raster), unit k of upm in the MCU. tiny_jpeg: 8x8 MCUs of
+// (Y, Cb, Cr); 4:2:0 extension: 16x16 MCUs of (Y0 Y1 Y2 Y3 Cb Cr), chroma = 2x2 pixel means.
+struct EncLayout {
+    int upm;                 // units per MCU
+    int ms;                  // MCU size in pixels (8 or 16)
+    int mbw;                 // MCUs per row
+    int sub;                 // chroma units average 2x2 pixels
+    int8_t comp[6], bx[6], by[6];
+    int8_t prevk[6];         // previous unit of the same component in the MCU, or -1
+    int8_t lastk[3];         // last unit of each component in an MCU
+};
+__device__ __forceinline__ int64_t pred_unit(const EncLayout& L, int64_t u) {  // DC predictor source
+    const int64_t m = u / L.upm;
+    const int k = (int)(u - m * L.upm);
+    if (L.prevk[k] >= 0) return m * L.upm + L.prevk[k];
+    return m > 0 ? (m - 1) * L.upm + L.lastk[L.comp[k]] : -1;
+}
 
 __constant__ static const uint8_t kZigOfNatE[64] = {
     0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43,
@@ -54,33 +73,46 @@ __device__ __forceinline__ void fdct8(float* p) {
 }
 
 __global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ src, int w, int h, int comps,
-                                                   int bw, int64_t nunits, const EncTables* __restrict__ T,
+                                                   EncLayout L, int64_t nunits, const EncTables* __restrict__ T,
                                                    int16_t* __restrict__ zz) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nunits) return;
-    const int64_t blk = u / 3;
-    const int c = (int)(u - blk * 3);
-    const int bx = (int)(blk % bw), by = (int)(blk / bw);
+    const int64_t m = u / L.upm;
+    const int k = (int)(u - m * L.upm);
+    const int c = L.comp[k];
+    const int mx = (int)(m % L.mbw), my = (int)(m / L.mbw);
+    auto pix = [&](int x, int y) {  // edge clamp (jpeg_enc.h:1106-1111)
+        return src + ((int64_t)min(y, h - 1) * w + min(x, w - 1)) * comps;
+    };
+    auto ycc = [&](const uint8_t* p) {  // jpeg_enc.h:1118-1120, evaluated left to right
+        const uint8_t r = p[0], g = p[1], b = p[2];
+        if (c == 0) return 0.299f * r + 0.587f * g + 0.114f * b - 128;
+        if (c == 1) return -0.1687f * r - 0.3313f * g + 0.5f * b;
+        return 0.5f * r - 0.4187f * g - 0.0813f * b;
+    };
     float f[64];
+    if (c != 0 && L.sub) {  // 4:2:0 chroma: ((a + b) + (c + d)) * 0.25f of the per-pixel values
+        const int x0 = mx * L.ms, y0 = my * L.ms;
 #pragma unroll
-    for (int oy = 0; oy < 8; ++oy) {
-        const int row = min(by * 8 + oy, h - 1);  // edge clamp (jpeg_enc.h:1106-1111)
+        for (int oy = 0; oy < 8; ++oy)
 #pragma unroll
-        for (int ox = 0; ox < 8; ++ox) {
-            const int col = min(bx * 8 + ox, w - 1);
-            const uint8_t* p = src + ((int64_t)row * w + col) * comps;
-            const uint8_t r = p[0], g = p[1], b = p[2];
-            float v;  // jpeg_enc.h:1118-1120, evaluated left to right
-            if (c == 0) v = 0.299f * r + 0.587f * g + 0.114f * b - 128;
-            else if (c == 1) v = -0.1687f * r - 0.3313f * g + 0.5f * b;
-            else v = 0.5f * r - 0.4187f * g - 0.0813f * b;
-            f[oy * 8 + ox] = v;
-        }
+            for (int ox = 0; ox < 8; ++ox) {
+                const int x = x0 + 2 * ox, y = y0 + 2 * oy;
+                const float a = ycc(pix(x, y)), b = ycc(pix(x + 1, y));
+                const float cc = ycc(pix(x, y + 1)), d = ycc(pix(x + 1, y + 1));
+                f[oy * 8 + ox] = ((a + b) + (cc + d)) * 0.25f;
+            }
+    } else {
+        const int x0 = mx * L.ms + L.bx[k] * 8, y0 = my * L.ms + L.by[k] * 8;
+#pragma unroll
+        for (int oy = 0; oy < 8; ++oy)
+#pragma unroll
+            for (int ox = 0; ox < 8; ++ox) f[oy * 8 + ox] = ycc(pix(x0 + ox, y0 + oy));
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) fdct8<1>(f + 8 * r);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) fdct8<8>(f + k);
+    for (int q = 0; q < 8; ++q) fdct8<8>(f + q);
     const float* pq = T->pq[c ? 1 : 0];
     int16_t* o = zz + u * 64;
 #pragma unroll
@@ -132,25 +164,27 @@ __device__ __forceinline__ void unit_codes(const int16_t* zz, int pred, const En
     if (last != 63) put(T->len[ta][0], T->code[ta][0]);
 }
 
-__global__ __launch_bounds__(256) void k_enc_count(const int16_t* __restrict__ zz, int64_t nunits,
+__global__ __launch_bounds__(256) void k_enc_count(const int16_t* __restrict__ zz, int64_t nunits, EncLayout L,
                                                    const EncTables* __restrict__ T, uint64_t* __restrict__ nbits) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nunits) return;
-    const int c = (int)(u % 3);
-    const int pred = u >= 3 ? zz[(u - 3) * 64] : 0;  // DC predictor never resets (:834-835)
+    const int c = L.comp[u % L.upm];
+    const int64_t pu = pred_unit(L, u);
+    const int pred = pu >= 0 ? zz[pu * 64] : 0;  // DC predictor never resets (:834-835)
     uint64_t total = 0;
     unit_codes(zz + u * 64, pred, T, c, [&](int n, uint32_t) { total += (uint64_t)n; });
     nbits[u] = total;
 }
 
 // Stream words hold bits MSB-first: word k covers stream bits [32k, 32k+32).
-__global__ __launch_bounds__(256) void k_enc_emit(const int16_t* __restrict__ zz, int64_t nunits,
+__global__ __launch_bounds__(256) void k_enc_emit(const int16_t* __restrict__ zz, int64_t nunits, EncLayout L,
                                                   const EncTables* __restrict__ T, const uint64_t* __restrict__ off,
                                                   uint32_t* __restrict__ words) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nunits) return;
-    const int c = (int)(u % 3);
-    const int pred = u >= 3 ? zz[(u - 3) * 64] : 0;
+    const int c = L.comp[u % L.upm];
+    const int64_t pu = pred_unit(L, u);
+    const int pred = pu >= 0 ? zz[pu * 64] : 0;
     uint64_t pos = off[u];
     uint64_t wi = pos >> 5;
     uint32_t acc = 0;
@@ -282,12 +316,225 @@ static void tje_header(std::vector<uint8_t>& o, int w, int h, const uint8_t* ql,
     u8(0); u8(63); u8(0);
 }
 
-#define ENC_HIP(call)                               \
-    do {                                            \
-        if ((call) != hipSuccess) { ok = false; goto done; } \
+static const uint8_t kK2Chroma[64] = {  // JPEG spec table K.2, natural order (C4 extension)
+    17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99, 24, 26, 56, 99, 99, 99, 99, 99,
+    47, 66, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+    99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+
+// Quantizer reciprocals for per-natural-position tables qnl/qnc (jpeg_enc.h:980-986) + Huffman.
+static void build_tables(EncTables& T, const uint8_t* qnl, const uint8_t* qnc) {
+    std::memset(&T, 0, sizeof T);
+    static const float aan[8] = {1.0f, 1.387039845f, 1.306562965f, 1.175875602f,
+                                 1.0f, 0.785694958f, 0.541196100f, 0.275899379f};
+    for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) {
+            const int i = y * 8 + x;
+            T.pq[0][i] = 1.0f / (8 * aan[x] * aan[y] * qnl[i]);
+            T.pq[1][i] = 1.0f / (8 * aan[x] * aan[y] * qnc[i]);
+        }
+    huff_codes(T.code[0], T.len[0], kDcLB, kDcV);
+    huff_codes(T.code[1], T.len[1], kAcLB, kAcLV);
+    huff_codes(T.code[2], T.len[2], kDcCB, kDcV);
+    huff_codes(T.code[3], T.len[3], kAcCB, kAcCV);
+}
+
+static EncLayout make_layout(int subsampling, int w) {
+    EncLayout L;
+    std::memset(&L, 0, sizeof L);
+    if (subsampling == 420) {
+        L.upm = 6;
+        L.ms = 16;
+        L.sub = 1;
+        const int8_t comp[6] = {0, 0, 0, 0, 1, 2}, bx[6] = {0, 1, 0, 1, 0, 0}, by[6] = {0, 0, 1, 1, 0, 0};
+        const int8_t prevk[6] = {-1, 0, 1, 2, -1, -1};
+        for (int k = 0; k < 6; ++k) { L.comp[k] = comp[k]; L.bx[k] = bx[k]; L.by[k] = by[k]; L.prevk[k] = prevk[k]; }
+        L.lastk[0] = 3; L.lastk[1] = 4; L.lastk[2] = 5;
+    } else {  // 4:4:4 (tiny_jpeg's only layout)
+        L.upm = 3;
+        L.ms = 8;
+        for (int k = 0; k < 3; ++k) { L.comp[k] = (int8_t)k; L.prevk[k] = -1; L.lastk[k] = (int8_t)k; }
+    }
+    L.mbw = (w + L.ms - 1) / L.ms;
+    return L;
+}
+
+// C4 extension header: tiny_jpeg's layout with zig-zag DQT and the sampling in SOF0.
+static void ext_header(std::vector<uint8_t>& o, int w, int h, const uint8_t* qnl, const uint8_t* qnc, int subsampling) {
+    auto u8 = [&](int v) { o.push_back((uint8_t)v); };
+    auto be = [&](int v) { u8(v >> 8); u8(v & 255); };
+    static const uint8_t jfif[] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0,
+                                   0x01, 0x02, 0x01, 0x00, 0x60, 0x00, 0x60, 0x00, 0x00};
+    o.insert(o.end(), jfif, jfif + sizeof jfif);
+    static const char com[] = "icx JPEG encoder";
+    be(0xFFFE);
+    be(2 + (int)sizeof(com) - 1);
+    o.insert(o.end(), com, com + sizeof(com) - 1);
+    uint8_t zq[64];
+    for (int k = 0; k < 64; ++k) zq[kZigOfNatH[k]] = qnl[k];
+    be(0xFFDB); be(0x43); u8(0); o.insert(o.end(), zq, zq + 64);
+    for (int k = 0; k < 64; ++k) zq[kZigOfNatH[k]] = qnc[k];
+    be(0xFFDB); be(0x43); u8(1); o.insert(o.end(), zq, zq + 64);
+    be(0xFFC0); be(17); u8(8); be(h); be(w); u8(3);
+    for (int i = 0; i < 3; ++i) { u8(i + 1); u8(i == 0 && subsampling == 420 ? 0x22 : 0x11); u8(i ? 1 : 0); }
+    const uint8_t* hb[4] = {kDcLB, kAcLB, kDcCB, kAcCB};
+    const uint8_t* hv[4] = {kDcV, kAcLV, kDcV, kAcCV};
+    const int id[4] = {0x00, 0x10, 0x01, 0x11};
+    for (int t = 0; t < 4; ++t) {
+        int n = 0;
+        for (int i = 0; i < 16; ++i) n += hb[t][i];
+        be(0xFFC4); be(2 + 1 + 16 + n); u8(id[t]);
+        o.insert(o.end(), hb[t], hb[t] + 16);
+        o.insert(o.end(), hv[t], hv[t] + n);
+    }
+    be(0xFFDA); be(12); u8(3);
+    u8(1); u8(0x00); u8(2); u8(0x11); u8(3); u8(0x11);
+    u8(0); u8(63); u8(0);
+}
+
+static void ijg_table(const uint8_t* base, int q, uint8_t* out) {  // IJG jpeg_quality_scaling
+    const int scale = q < 50 ? 5000 / q : 200 - 2 * q;
+    for (int i = 0; i < 64; ++i) {
+        const int v = (base[i] * scale + 50) / 100;
+        out[i] = (uint8_t)(v < 1 ? 1 : v > 255 ? 255 : v);
+    }
+}
+
+// ----------------------------------------------------------------------- device pipeline
+struct EncWs {
+    EncTables* T = nullptr;
+    int16_t* zz = nullptr;
+    uint64_t *nb = nullptr, *off = nullptr;
+    int64_t units_cap = 0;
+    uint32_t* words = nullptr;
+    uint64_t words_cap = 0;  // bytes
+    uint32_t *cnt = nullptr, *base = nullptr;
+    int64_t chunks_cap = 0;
+    void* tmp = nullptr;
+    size_t tmp_cap = 0;
+    // per-stage HIP events of the last entropy pass (icx_encoder_stage_times): units, count,
+    // scan, emit, stuff; ms[] accumulates over calls until read
+    hipEvent_t ev[10] = {};  // stage i spans ev[2i] .. ev[2i+1]
+    bool timed = false;
+    float ms[5] = {};
+    ~EncWs() {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        for (void* p : {(void*)T, (void*)zz, (void*)nb, (void*)off, (void*)words, (void*)cnt, (void*)base, tmp})
+            if (p) (void)hipFree(p);
+    }
+};
+EncWs* enc_ws_create() {
+    EncWs* ws = new EncWs();
+    for (hipEvent_t& e : ws->ev)
+        if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+    return ws;
+}
+const char* const kEncStageNames[5] = {"units", "count", "scan", "emit", "stuff"};
+int enc_ws_stage_times(EncWs* ws, const char** names, float* ms, int cap) {
+    const int k = cap < 5 ? cap : 5;
+    for (int i = 0; i < k; ++i) {
+        if (names) names[i] = kEncStageNames[i];
+        if (ms) ms[i] = ws->ms[i];
+    }
+    for (float& m : ws->ms) m = 0.f;
+    return k;
+}
+void enc_ws_destroy(EncWs* ws) { delete ws; }
+
+#define ENC_HIP(call)                                  \
+    do {                                               \
+        if ((call) != hipSuccess) return false;        \
     } while (0)
 
-// Encode on the GPU; returns false on a HIP failure. `out` receives the whole file.
+template <class Ptr>
+static bool grow(Ptr*& p, size_t need, size_t& cap_bytes) {
+    if (need <= cap_bytes && p) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap_bytes = 0;
+    if (hipMalloc(&p, need) != hipSuccess) return false;
+    cap_bytes = need;
+    return true;
+}
+
+// Entropy-coded data of the image at d_src (device) -> d_out[0 .. *n) (stuffed bytes), using the
+// workspace. Returns false on a HIP failure; *n > cap means the output did not fit (not written).
+static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables& T, const uint8_t* d_src,
+                           int w, int h, int comps, uint8_t* d_out, uint64_t cap, uint64_t* n) {
+    const int64_t mbh = (h + L.ms - 1) / L.ms;
+    const int64_t nunits = (int64_t)L.mbw * mbh * L.upm;
+    *n = 0;
+    if (nunits == 0 || w == 0 || h == 0) return true;
+    size_t c0 = ws.units_cap * 128, c1 = ws.units_cap * 8, c2 = c1;
+    if (nunits > ws.units_cap) {
+        size_t tcap = ws.T ? sizeof(EncTables) : 0;
+        if (!grow(ws.T, sizeof(EncTables), tcap)) return false;
+        if (!grow(ws.zz, (size_t)nunits * 128, c0) || !grow(ws.nb, (size_t)nunits * 8, c1) ||
+            !grow(ws.off, (size_t)nunits * 8, c2))
+            return false;
+        ws.units_cap = nunits;
+    }
+    ENC_HIP(hipMemcpyAsync(ws.T, &T, sizeof T, hipMemcpyHostToDevice, st));
+    const int TB = 256;
+    const int gu = (int)((nunits + TB - 1) / TB);
+    const bool ev = ws.ev[9] != nullptr;
+    auto mark = [&](int i) {
+        if (ev) (void)hipEventRecord(ws.ev[i], st);
+    };
+    mark(0);
+    hipLaunchKernelGGL(k_enc_units, dim3(gu), dim3(TB), 0, st, d_src, w, h, comps, L, nunits, ws.T, ws.zz);
+    mark(1);
+    mark(2);
+    hipLaunchKernelGGL(k_enc_count, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.nb);
+    mark(3);
+    mark(4);
+    size_t tmp_b = 0;
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, ws.nb, ws.off, (int)nunits, st));
+    if (!grow(ws.tmp, tmp_b, ws.tmp_cap)) return false;
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b, ws.nb, ws.off, (int)nunits, st));
+    mark(5);
+    uint64_t last_off = 0, last_nb = 0;
+    ENC_HIP(hipMemcpyAsync(&last_off, ws.off + nunits - 1, 8, hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipMemcpyAsync(&last_nb, ws.nb + nunits - 1, 8, hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipStreamSynchronize(st));
+    const uint64_t nbytes = (last_off + last_nb + 7) / 8;  // final partial byte zero-padded (:1161-1165)
+    const uint64_t wbytes = ((nbytes + 3) / 4 + 1) * 4;
+    if (!grow(ws.words, wbytes, ws.words_cap)) return false;
+    ENC_HIP(hipMemsetAsync(ws.words, 0, wbytes, st));
+    mark(6);
+    hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.off, ws.words);
+    mark(7);
+    mark(8);
+    const int64_t nchunks = (int64_t)((nbytes + kStuffChunk - 1) / kStuffChunk);
+    if (nchunks == 0) return true;
+    size_t cc = ws.chunks_cap * 4, cb = cc;
+    if (nchunks > ws.chunks_cap) {
+        if (!grow(ws.cnt, (size_t)nchunks * 4, cc) || !grow(ws.base, (size_t)nchunks * 4, cb)) return false;
+        ws.chunks_cap = nchunks;
+    }
+    const int gc = (int)((nchunks + TB - 1) / TB);
+    hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, ws.words, nbytes, ws.cnt, nchunks);
+    size_t tmp_b2 = 0;
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
+    if (!grow(ws.tmp, tmp_b2, ws.tmp_cap)) return false;
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
+    uint32_t last_cnt = 0, last_base = 0;
+    ENC_HIP(hipMemcpyAsync(&last_cnt, ws.cnt + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipMemcpyAsync(&last_base, ws.base + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipStreamSynchronize(st));
+    *n = nbytes + (uint64_t)last_cnt + last_base;
+    if (*n > cap) return true;
+    hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, ws.words, nbytes, ws.base, nchunks, d_out);
+    ENC_HIP(hipGetLastError());
+    mark(9);
+    ws.timed = ev;
+    return true;
+}
+
+bool encode_host_image(hipStream_t st, const EncLayout& L, const EncTables& T, int w, int h, int comps,
+                       const uint8_t* src, std::vector<uint8_t>& out);
+
+// tiny_jpeg-exact encode (quality 1..3, 4:4:4) of a host image; `out` receives the whole file.
 bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const uint8_t* src,
                     std::vector<uint8_t>& out) {
     uint8_t ql[64], qc[64];
@@ -299,99 +546,93 @@ bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const 
         qc[i] = (uint8_t)(kChromaQ[i] / div);
         if (!qc[i]) qc[i] = 1;
     }
+    uint8_t qnl[64], qnc[64];  // tiny_jpeg indexes its tables through the zig-zag map (:983-984)
+    for (int i = 0; i < 64; ++i) { qnl[i] = ql[kZigOfNatH[i]]; qnc[i] = qc[kZigOfNatH[i]]; }
     EncTables T;
-    std::memset(&T, 0, sizeof T);
-    static const float aan[8] = {1.0f, 1.387039845f, 1.306562965f, 1.175875602f,
-                                 1.0f, 0.785694958f, 0.541196100f, 0.275899379f};
-    for (int y = 0; y < 8; ++y)
-        for (int x = 0; x < 8; ++x) {
-            const int i = y * 8 + x;
-            T.pq[0][i] = 1.0f / (8 * aan[x] * aan[y] * ql[kZigOfNatH[i]]);
-            T.pq[1][i] = 1.0f / (8 * aan[x] * aan[y] * qc[kZigOfNatH[i]]);
-        }
-    huff_codes(T.code[0], T.len[0], kDcLB, kDcV);
-    huff_codes(T.code[1], T.len[1], kAcLB, kAcLV);
-    huff_codes(T.code[2], T.len[2], kDcCB, kDcV);
-    huff_codes(T.code[3], T.len[3], kAcCB, kAcCV);
+    build_tables(T, qnl, qnc);
     out.clear();
     tje_header(out, w, h, ql, qc);
+    return encode_host_image(st, make_layout(444, w), T, w, h, comps, src, out);
+}
 
-    const int bw = (w + 7) / 8, bh = (h + 7) / 8;
-    const int64_t nunits = (int64_t)bw * bh * 3;
+// Shared tail of the host entry points: upload, encode, download, EOI.
+bool encode_host_image(hipStream_t st, const EncLayout& L, const EncTables& T, int w, int h, int comps,
+                       const uint8_t* src, std::vector<uint8_t>& out) {
+    EncWs ws;
     const size_t srcb = (size_t)w * h * comps;
-    bool ok = true;
     uint8_t *d_src = nullptr, *d_out = nullptr;
-    EncTables* d_T = nullptr;
-    int16_t* d_zz = nullptr;
-    uint64_t *d_nb = nullptr, *d_off = nullptr;
-    uint32_t *d_words = nullptr, *d_cnt = nullptr, *d_base = nullptr;
-    void* d_tmp = nullptr;
-    size_t tmp_b = 0, tmp_b2 = 0;
-    uint64_t last_off = 0, last_nb = 0, total_bits = 0, nbytes = 0, nff = 0;
-    uint32_t last_cnt = 0, last_base = 0;
-    int64_t nchunks = 0;
-    const int TB = 256;
-    const int gu = (int)((nunits + TB - 1) / TB);
-    if (nunits == 0) {  // empty image: headers + EOI only
-        out.push_back(0xFF);
-        out.push_back(0xD9);
-        return true;
-    }
-    ENC_HIP(hipMalloc(&d_src, srcb));
-    ENC_HIP(hipMalloc(&d_T, sizeof T));
-    ENC_HIP(hipMalloc(&d_zz, (size_t)nunits * 64 * 2));
-    ENC_HIP(hipMalloc(&d_nb, (size_t)nunits * 8));
-    ENC_HIP(hipMalloc(&d_off, (size_t)nunits * 8));
-    ENC_HIP(hipMemcpyAsync(d_src, src, srcb, hipMemcpyHostToDevice, st));
-    ENC_HIP(hipMemcpyAsync(d_T, &T, sizeof T, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_enc_units, dim3(gu), dim3(TB), 0, st, d_src, w, h, comps, bw, nunits, d_T, d_zz);
-    hipLaunchKernelGGL(k_enc_count, dim3(gu), dim3(TB), 0, st, d_zz, nunits, d_T, d_nb);
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, d_nb, d_off, (int)nunits, st));
-    ENC_HIP(hipMalloc(&d_tmp, tmp_b));
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_b, d_nb, d_off, (int)nunits, st));
-    ENC_HIP(hipMemcpyAsync(&last_off, d_off + nunits - 1, 8, hipMemcpyDeviceToHost, st));
-    ENC_HIP(hipMemcpyAsync(&last_nb, d_nb + nunits - 1, 8, hipMemcpyDeviceToHost, st));
-    ENC_HIP(hipStreamSynchronize(st));
-    total_bits = last_off + last_nb;
-    nbytes = (total_bits + 7) / 8;  // final partial byte zero-padded (jpeg_enc.h:1161-1165)
-    ENC_HIP(hipMalloc(&d_words, ((nbytes + 3) / 4 + 1) * 4));
-    ENC_HIP(hipMemsetAsync(d_words, 0, ((nbytes + 3) / 4 + 1) * 4, st));
-    hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, d_zz, nunits, d_T, d_off, d_words);
-    nchunks = (int64_t)((nbytes + kStuffChunk - 1) / kStuffChunk);
-    if (nchunks > 0) {
-        ENC_HIP(hipMalloc(&d_cnt, (size_t)nchunks * 4));
-        ENC_HIP(hipMalloc(&d_base, (size_t)nchunks * 4));
-        const int gc = (int)((nchunks + TB - 1) / TB);
-        hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, d_words, nbytes, d_cnt, nchunks);
-        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, d_cnt, d_base, (int)nchunks, st));
-        if (tmp_b2 > tmp_b) {
-            ENC_HIP(hipFree(d_tmp));
-            d_tmp = nullptr;
-            ENC_HIP(hipMalloc(&d_tmp, tmp_b2));
-            tmp_b = tmp_b2;
+    bool ok = true;
+    uint64_t n = 0;
+    if (srcb) {
+        ok = hipMalloc(&d_src, srcb) == hipSuccess &&
+             hipMemcpyAsync(d_src, src, srcb, hipMemcpyHostToDevice, st) == hipSuccess;
+        // first pass sizes the output, the second (only when it did not fit) writes it
+        uint64_t cap = srcb + 65536;
+        ok = ok && hipMalloc(&d_out, cap) == hipSuccess && encode_entropy(st, ws, L, T, d_src, w, h, comps, d_out, cap, &n);
+        if (ok && n > cap) {
+            (void)hipFree(d_out);
+            d_out = nullptr;
+            cap = n;
+            ok = hipMalloc(&d_out, cap) == hipSuccess && encode_entropy(st, ws, L, T, d_src, w, h, comps, d_out, cap, &n);
         }
-        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_b, d_cnt, d_base, (int)nchunks, st));
-        ENC_HIP(hipMemcpyAsync(&last_cnt, d_cnt + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
-        ENC_HIP(hipMemcpyAsync(&last_base, d_base + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
-        ENC_HIP(hipStreamSynchronize(st));
-        nff = (uint64_t)last_cnt + last_base;
-        ENC_HIP(hipMalloc(&d_out, nbytes + nff));
-        hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, d_words, nbytes, d_base, nchunks, d_out);
-        {
+        if (ok && n) {
             const size_t h0 = out.size();
-            out.resize(h0 + nbytes + nff);
-            ENC_HIP(hipMemcpyAsync(out.data() + h0, d_out, nbytes + nff, hipMemcpyDeviceToHost, st));
+            out.resize(h0 + n);
+            ok = hipMemcpyAsync(out.data() + h0, d_out, n, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                 hipStreamSynchronize(st) == hipSuccess;
         }
     }
-    ENC_HIP(hipStreamSynchronize(st));
-    ENC_HIP(hipGetLastError());
+    if (d_src) (void)hipFree(d_src);
+    if (d_out) (void)hipFree(d_out);
     out.push_back(0xFF);
     out.push_back(0xD9);
-done:
-    for (void* p : {(void*)d_src, (void*)d_T, (void*)d_zz, (void*)d_nb, (void*)d_off, (void*)d_words, (void*)d_cnt,
-                    (void*)d_base, d_tmp, (void*)d_out})
-        if (p) (void)hipFree(p);
     return ok;
+}
+
+// C4 extension, host image -> whole file.
+bool jpeg_encode_gpu(hipStream_t st, int quality, int subsampling, int w, int h, int comps, const uint8_t* src,
+                     std::vector<uint8_t>& out) {
+    uint8_t qnl[64], qnc[64];
+    ijg_table(kLumaQ, quality, qnl);
+    ijg_table(kK2Chroma, quality, qnc);
+    EncTables T;
+    build_tables(T, qnl, qnc);
+    out.clear();
+    ext_header(out, w, h, qnl, qnc, subsampling);
+    return encode_host_image(st, make_layout(subsampling, w), T, w, h, comps, src, out);
+}
+
+// C4 extension, device image -> whole file in d_out (device). Returns 0 ok, 1 d_out too small
+// (*size = bytes needed), -1 HIP failure.
+int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, int w, int h, int comps,
+                       const uint8_t* d_src, uint8_t* d_out, uint64_t cap, uint64_t* size) {
+    uint8_t qnl[64], qnc[64];
+    ijg_table(kLumaQ, quality, qnl);
+    ijg_table(kK2Chroma, quality, qnc);
+    EncTables T;
+    build_tables(T, qnl, qnc);
+    std::vector<uint8_t> head;
+    ext_header(head, w, h, qnl, qnc, subsampling);
+    const uint64_t hn = head.size();
+    uint64_t n = 0;
+    if (!encode_entropy(st, *ws, make_layout(subsampling, w), T, d_src, w, h, comps,
+                        cap > hn ? d_out + hn : d_out, cap > hn ? cap - hn : 0, &n))
+        return -1;
+    *size = hn + n + 2;
+    if (*size > cap) return 1;
+    static const uint8_t eoi[2] = {0xFF, 0xD9};
+    if (hipMemcpyAsync(d_out, head.data(), hn, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_out + hn + n, eoi, 2, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return -1;
+    if (ws->timed) {
+        for (int i = 0; i < 5; ++i) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, ws->ev[2 * i], ws->ev[2 * i + 1]) == hipSuccess) ws->ms[i] += t;
+        }
+        ws->timed = false;
+    }
+    return 0;
 }
 
 }  // namespace icx

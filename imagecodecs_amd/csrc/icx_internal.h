@@ -112,5 +112,14 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
 // tiny_jpeg-exact encode on the GPU (icx_encode.hip); `out` receives the whole file.
 bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const uint8_t* src,
                     std::vector<uint8_t>& out);
+// C4 extension encoder (4:4:4 / 4:2:0, IJG quality 1..100; oracle/tje_oracle.c or_jpeg_encode).
+struct EncWs;
+EncWs* enc_ws_create();
+void enc_ws_destroy(EncWs* ws);
+int enc_ws_stage_times(EncWs* ws, const char** names, float* ms, int cap);
+bool jpeg_encode_gpu(hipStream_t st, int quality, int subsampling, int w, int h, int comps, const uint8_t* src,
+                     std::vector<uint8_t>& out);
+int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, int w, int h, int comps,
+                       const uint8_t* d_src, uint8_t* d_out, uint64_t cap, uint64_t* size);
 
 }  // namespace icx

@@ -124,6 +124,31 @@ int icx_tje_encode_to_file_at_quality(icx_ctx* ctx, const char* dest_path, int q
 int icx_tje_encode_to_file(icx_ctx* ctx, const char* dest_path, int width, int height,
                            int num_components, const unsigned char* src);
 
+/* ---- encode extension (IJG quality 1..100, 4:4:4 or 4:2:0) ----------
+ * tiny_jpeg only offers quality 1..3 at 4:4:4 (jpeg_enc.h:1223-1256). The extension keeps its
+ * entropy coder and float AAN DCT (jpeg_enc.h:980-1100) and adds IJG-scaled tables (luma =
+ * tiny_jpeg's, chroma = JPEG spec K.2) and 2x2-mean 4:2:0 chroma. The byte stream is defined by
+ * oracle/tje_oracle.c or_jpeg_encode and decodes with NanoJPEG. */
+/* Host image -> file bytes through `func`; returns 1 on success, 0 on error. */
+int icx_jpeg_encode_with_func(icx_ctx* ctx, icx_write_func* func, void* context, int quality,
+                              int subsampling, int width, int height, int num_components,
+                              const unsigned char* src);
+
+typedef struct icx_encoder icx_encoder;
+/* Reusable device workspace for device-resident encodes on ctx's device. */
+icx_encoder* icx_encoder_create(icx_ctx* ctx);
+void icx_encoder_destroy(icx_encoder* enc);
+/* Device image d_src (width*height*num_components bytes) -> whole JPEG file at d_out.
+ * Synchronous on `hip_stream` (NULL = the context's stream). *out_size receives the file size.
+ * Returns ICX_OK, ICX_OUT_OF_MEM when out_cap < *out_size (nothing written),
+ * ICX_UNSUPPORTED for bad arguments, ICX_INTERNAL_ERR on a HIP failure. */
+int icx_jpeg_encode_device(icx_encoder* enc, int quality, int subsampling, int width, int height,
+                           int num_components, const uint8_t* d_src, uint8_t* d_out, uint64_t out_cap,
+                           uint64_t* out_size, void* hip_stream);
+/* Per-stage GPU time (HIP events) of the encodes since the previous call, summed: units
+ * (DCT+quantise), count, scan, emit, stuff. Returns the number of stages filled (<= cap). */
+int icx_encoder_stage_times(icx_encoder* enc, const char** names, float* ms, int cap);
+
 #ifdef __cplusplus
 }
 #endif

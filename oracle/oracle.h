@@ -42,6 +42,11 @@ int or_nj_decode(const uint8_t* jpeg, int64_t size, uint8_t** out, int* w, int* 
 int or_tje_encode(int quality, int w, int h, int comps, const uint8_t* src,
                   uint8_t** out, int64_t* outlen);
 
+/* C4 extension (defined in tje_oracle.c, no reference exists): IJG quality 1..100,
+ * subsampling 444 or 420, comps 3 or 4. Same return contract as or_tje_encode. */
+int or_jpeg_encode(int quality, int subsampling, int w, int h, int comps, const uint8_t* src,
+                   uint8_t** out, int64_t* outlen);
+
 void or_free(void* p);
 
 #ifdef __cplusplus

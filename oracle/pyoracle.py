@@ -39,6 +39,9 @@ def lib():
         L.or_tje_encode.restype = C.c_int
         L.or_tje_encode.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                     C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.or_jpeg_encode.restype = C.c_int
+        L.or_jpeg_encode.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                     C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
         L.or_free.argtypes = [C.c_void_p]
         _LIB = L
     return _LIB
@@ -76,9 +79,24 @@ def decode_trace(data: bytes, cap_blocks: int = 1 << 20):
     return code, coef[:n].copy(), dc[:n].copy()
 
 
+def jpeg_encode(quality: int, subsampling: int, w: int, h: int, comps: int, rgb: bytes):
+    """C4 extension encoder definition (IJG quality 1..100, 4:4:4 / 4:2:0); None on error."""
+    L = lib()
+    data = bytes(rgb)
+    src = C.create_string_buffer(data, max(1, len(data)))
+    out = C.c_void_p()
+    n = C.c_int64()
+    if not L.or_jpeg_encode(quality, subsampling, w, h, comps, src, C.byref(out), C.byref(n)):
+        return None
+    res = C.string_at(out.value, n.value)
+    L.or_free(out)
+    return res
+
+
 def tje_encode(quality: int, w: int, h: int, comps: int, rgb: bytes):
     L = lib()
-    src = C.create_string_buffer(bytes(rgb), max(1, len(rgb)))
+    data = bytes(rgb)
+    src = C.create_string_buffer(data, max(1, len(data)))
     out = C.c_void_p()
     n = C.c_int64()
     ok = L.or_tje_encode(quality, w, h, comps, src, C.byref(out), C.byref(n))
@@ -121,7 +139,8 @@ def ref_decode(data: bytes, cap: int = 1 << 28):
 
 def ref_tje_encode(quality: int, w: int, h: int, comps: int, rgb: bytes, cap: int = 1 << 28):
     L = ref()
-    src = C.create_string_buffer(bytes(rgb), max(1, len(rgb)))
+    data = bytes(rgb)
+    src = C.create_string_buffer(data, max(1, len(data)))
     out = C.create_string_buffer(cap)
     n = C.c_longlong()
     ok = L.ref_tje_encode(quality, w, h, comps, src, out, cap, C.byref(n))

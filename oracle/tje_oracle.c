@@ -283,3 +283,136 @@ int or_tje_encode(int quality, int w, int h, int comps, const uint8_t* src, uint
     *outlen = s.len;
     return 1;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * C4 extension: baseline JPEG with 4:2:0 (or 4:4:4) sampling and IJG
+ * quality scaling. tiny_jpeg has neither, so there is no reference to restate: THIS FUNCTION
+ * IS THE DEFINITION of the extension, and the GPU encoder (icx_jpeg_encode*) must reproduce its
+ * bytes exactly. It keeps tiny_jpeg's arithmetic everywhere it overlaps:
+ *   - per-pixel float RGB->YCbCr with the same expressions (jpeg_enc.h:1118-1120), edge clamp
+ *     of rows/cols to the image (:1106-1111);
+ *   - 4:2:0: each chroma sample is ((c(x,y) + c(x+1,y)) + (c(x,y+1) + c(x+1,y+1))) * 0.25f of the
+ *     per-pixel values, with the same edge clamp;
+ *   - AAN float FDCT, pq = 1/(8*aan[x]*aan[y]*q), floorf(v*pq + 1024 + 0.5f) - 1024;
+ *   - Annex K Huffman tables, MSB-first emit with FF00 stuffing, zero-bit final pad, DC
+ *     predictors never reset.
+ * Quantization: the JPEG spec K.1 / K.2 tables (natural order) scaled as IJG libjpeg does
+ * (q < 50 ? 5000/q : 200 - 2q; (t*scale + 50)/100 clamped to 1..255), written to DQT in
+ * zig-zag order. MCU 16x16 for 4:2:0 (Y0 Y1 Y2 Y3 Cb Cr), 8x8 for 4:4:4.
+ * ---------------------------------------------------------------------------------------- */
+static const uint8_t kK2Chroma[64] = {  /* JPEG spec table K.2, natural order */
+    17, 18, 24, 47, 99, 99, 99, 99,   18, 21, 26, 66, 99, 99, 99, 99,
+    24, 26, 56, 99, 99, 99, 99, 99,   47, 66, 99, 99, 99, 99, 99, 99,
+    99, 99, 99, 99, 99, 99, 99, 99,   99, 99, 99, 99, 99, 99, 99, 99,
+    99, 99, 99, 99, 99, 99, 99, 99,   99, 99, 99, 99, 99, 99, 99, 99 };
+
+static void ijg_table(const uint8_t* base, int q, uint8_t* out) {
+    const int scale = q < 50 ? 5000 / q : 200 - 2 * q;
+    for (int i = 0; i < 64; ++i) {
+        int v = (base[i] * scale + 50) / 100;
+        out[i] = (uint8_t)(v < 1 ? 1 : v > 255 ? 255 : v);
+    }
+}
+
+int or_jpeg_encode(int quality, int subsampling, int w, int h, int comps, const uint8_t* src,
+                   uint8_t** out, int64_t* outlen) {
+    *out = NULL;
+    *outlen = 0;
+    if (quality < 1 || quality > 100) return 0;
+    if (subsampling != 444 && subsampling != 420) return 0;
+    if (comps != 3 && comps != 4) return 0;
+    if (w > 0xFFFF || h > 0xFFFF) return 0;
+    uint8_t ql[64], qc[64];   /* natural order */
+    ijg_table(kLumaQ, quality, ql);      /* kLumaQ is table K.1 in natural order */
+    ijg_table(kK2Chroma, quality, qc);
+    static const float aan[8] = { 1.0f, 1.387039845f, 1.306562965f, 1.175875602f,
+                                  1.0f, 0.785694958f, 0.541196100f, 0.275899379f };
+    float pl[64], pc[64];
+    for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) {
+            int i = y * 8 + x;
+            pl[i] = 1.0f / (8 * aan[x] * aan[y] * ql[i]);
+            pc[i] = 1.0f / (8 * aan[x] * aan[y] * qc[i]);
+        }
+    huff_enc hdl, hal, hdc, hac;
+    build_huff(&hdl, kDcLumaBits, kDcVals);
+    build_huff(&hal, kAcLumaBits, kAcLumaVals);
+    build_huff(&hdc, kDcChromaBits, kDcVals);
+    build_huff(&hac, kAcChromaBits, kAcChromaVals);
+
+    sink s;
+    memset(&s, 0, sizeof(s));
+    static const uint8_t jfif[] = { 0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0,
+                                    0x01, 0x02, 0x01, 0x00, 0x60, 0x00, 0x60, 0x00, 0x00 };
+    put(&s, jfif, sizeof(jfif));
+    static const char com[] = "icx JPEG encoder";
+    put_be16(&s, 0xFFFE);
+    put_be16(&s, 2 + (int)sizeof(com) - 1);
+    put(&s, com, (int64_t)sizeof(com) - 1);
+    uint8_t zq[64];
+    for (int k = 0; k < 64; ++k) zq[kZigOf[k]] = ql[k];   /* DQT holds zig-zag order */
+    put_be16(&s, 0xFFDB); put_be16(&s, 0x43); put_u8(&s, 0); put(&s, zq, 64);
+    for (int k = 0; k < 64; ++k) zq[kZigOf[k]] = qc[k];
+    put_be16(&s, 0xFFDB); put_be16(&s, 0x43); put_u8(&s, 1); put(&s, zq, 64);
+    put_be16(&s, 0xFFC0); put_be16(&s, 17); put_u8(&s, 8);
+    put_be16(&s, h); put_be16(&s, w); put_u8(&s, 3);
+    for (int i = 0; i < 3; ++i) {
+        put_u8(&s, i + 1);
+        put_u8(&s, i == 0 && subsampling == 420 ? 0x22 : 0x11);
+        put_u8(&s, i ? 1 : 0);
+    }
+    put_dht(&s, 0x00, kDcLumaBits, kDcVals);
+    put_dht(&s, 0x10, kAcLumaBits, kAcLumaVals);
+    put_dht(&s, 0x01, kDcChromaBits, kDcVals);
+    put_dht(&s, 0x11, kAcChromaBits, kAcChromaVals);
+    put_be16(&s, 0xFFDA); put_be16(&s, 12); put_u8(&s, 3);
+    put_u8(&s, 1); put_u8(&s, 0x00); put_u8(&s, 2); put_u8(&s, 0x11); put_u8(&s, 3); put_u8(&s, 0x11);
+    put_u8(&s, 0); put_u8(&s, 63); put_u8(&s, 0);
+
+    const int ms = subsampling == 420 ? 16 : 8;
+    float blk[64];
+    int py = 0, pu = 0, pv = 0;
+#define PIX(X, Y) (src + ((int64_t)((Y) < h ? (Y) : h - 1) * w + ((X) < w ? (X) : w - 1)) * comps)
+    for (int my = 0; my < h; my += ms)
+        for (int mx = 0; mx < w; mx += ms) {
+            for (int sb = 0; sb < (ms == 16 ? 4 : 1); ++sb) {       /* luma blocks, raster order */
+                const int bx = mx + (sb & 1) * 8, by = my + (sb >> 1) * 8;
+                for (int oy = 0; oy < 8; ++oy)
+                    for (int ox = 0; ox < 8; ++ox) {
+                        const uint8_t* p = PIX(bx + ox, by + oy);
+                        const uint8_t r = p[0], g = p[1], b = p[2];
+                        blk[oy * 8 + ox] = 0.299f * r + 0.587f * g + 0.114f * b - 128;
+                    }
+                encode_unit(&s, blk, pl, &hdl, &hal, &py);
+            }
+            for (int c = 1; c <= 2; ++c) {
+                for (int oy = 0; oy < 8; ++oy)
+                    for (int ox = 0; ox < 8; ++ox) {
+                        float v;
+                        if (ms == 8) {
+                            const uint8_t* p = PIX(mx + ox, my + oy);
+                            const uint8_t r = p[0], g = p[1], b = p[2];
+                            v = c == 1 ? -0.1687f * r - 0.3313f * g + 0.5f * b : 0.5f * r - 0.4187f * g - 0.0813f * b;
+                        } else {
+                            float q4[4];
+                            for (int d = 0; d < 4; ++d) {
+                                const uint8_t* p = PIX(mx + 2 * ox + (d & 1), my + 2 * oy + (d >> 1));
+                                const uint8_t r = p[0], g = p[1], b = p[2];
+                                q4[d] = c == 1 ? -0.1687f * r - 0.3313f * g + 0.5f * b
+                                               : 0.5f * r - 0.4187f * g - 0.0813f * b;
+                            }
+                            v = ((q4[0] + q4[1]) + (q4[2] + q4[3])) * 0.25f;
+                        }
+                        blk[oy * 8 + ox] = v;
+                    }
+                encode_unit(&s, blk, pc, &hdc, &hac, c == 1 ? &pu : &pv);
+            }
+        }
+#undef PIX
+    if (s.fill > 0 && s.fill < 8) put_bits(&s, (int)(8 - s.fill), 0);
+    put_be16(&s, 0xFFD9);
+    if (s.oom) { free(s.buf); return 0; }
+    *out = s.buf;
+    *outlen = s.len;
+    return 1;
+}

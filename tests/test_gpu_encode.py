@@ -51,3 +51,51 @@ def test_tje_large_matches_oracle_and_roundtrips(ctx, q):
 def test_tje_rejects_like_reference(ctx):
     assert ctx.tje_encode(0, 8, 8, 3, bytes(192)) is None
     assert ctx.tje_encode(3, 8, 8, 2, bytes(128)) is None
+
+
+# ---- C4 encode extension: byte-exact to oracle/tje_oracle.c or_jpeg_encode -----------------
+EXT = json.load(open(os.path.join(GOLDEN, "ext_manifest.json")))
+
+
+@pytest.mark.parametrize("key", sorted(EXT))
+def test_ext_manifest(ctx, key):
+    e = EXT[key]
+    px = S.rgb(e["seed"], e["w"], e["h"], e["comps"]).tobytes()
+    out = ctx.jpeg_encode(e["quality"], e["subsampling"], e["w"], e["h"], e["comps"], px)
+    assert out is not None and len(out) == e["len"] and hashlib.sha256(out).hexdigest() == e["sha256"]
+
+
+@pytest.mark.parametrize("w,h,c", [(1, 1, 3), (16, 16, 3), (15, 17, 4), (640, 480, 3), (1023, 769, 4)])
+@pytest.mark.parametrize("q,sub", [(1, 420), (10, 444), (50, 420), (90, 420), (90, 444), (100, 420)])
+def test_ext_matches_oracle(ctx, w, h, c, q, sub):
+    px = S.rgb(w * 31 + h + q, w, h, c).tobytes()
+    out = ctx.jpeg_encode(q, sub, w, h, c, px)
+    assert out == O.jpeg_encode(q, sub, w, h, c, px)
+
+
+def test_ext_device_4096_roundtrip(ctx):
+    """BASELINE's C4 workload shape (4096^2, 4:2:0, q90) through the device-resident entry."""
+    import torch
+    w = h = 4096
+    px = S.rgb(2024, w, h, 3)
+    enc = icx.Encoder(ctx)
+    d_src = torch.from_numpy(px).cuda()
+    d_out = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
+    rc, n = enc.encode_device(90, 420, w, h, 3, d_src.data_ptr(), d_out.data_ptr(), 64)
+    assert rc == icx.OUT_OF_MEM and n > 64  # size query without writing
+    rc, n2 = enc.encode_device(90, 420, w, h, 3, d_src.data_ptr(), d_out.data_ptr(), d_out.numel())
+    assert rc == icx.OK and n2 == n
+    jpg = d_out[:n].cpu().numpy().tobytes()
+    assert jpg == O.jpeg_encode(90, 420, w, h, 3, px.tobytes())
+    code, dw, dh, nc, dec = ctx.decode(jpg)
+    assert code == 0 and (dw, dh, nc) == (w, h, 3) and dec == O.decode(jpg)[4]
+    enc.close()
+
+
+def test_ext_rejects(ctx):
+    px = bytes(8 * 8 * 4)
+    assert ctx.jpeg_encode(0, 444, 8, 8, 3, px) is None
+    assert ctx.jpeg_encode(101, 444, 8, 8, 3, px) is None
+    assert ctx.jpeg_encode(90, 422, 8, 8, 3, px) is None
+    assert ctx.jpeg_encode(90, 420, 8, 8, 2, px) is None
+    assert ctx.jpeg_encode(90, 420, 0, 0, 3, b"") == O.jpeg_encode(90, 420, 0, 0, 3, b"")  # header + EOI
