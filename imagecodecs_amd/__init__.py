@@ -76,6 +76,11 @@ _SIGS = {
     "icx_encoder_create": (_vp, [_vp]),
     "icx_encoder_destroy": (None, [_vp]),
     "icx_encoder_stage_times": (_i32, [_vp, _vp, _vp, _i32]),
+    "icx_png_encode_with_func": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32]),
+    "icx_png_save_to_file": (_i32, [_vp, C.c_char_p, _vp, _i32, _i32, _i32]),
+    "icx_png_encoder_create": (_vp, [_vp]),
+    "icx_png_encoder_destroy": (None, [_vp]),
+    "icx_png_encode_device": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
     "icx_jpeg_encode_device": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
 }
 
@@ -201,6 +206,18 @@ class Context:
         ok = lib().icx_tje_encode_with_func(self._p, sink, None, quality, width, height, comps, buf)
         return b"".join(chunks) if ok == 1 else None
 
+    def png_encode(self, width: int, height: int, d: int, src: bytes):
+        """PNG bytes of an RGB8 (d=3) / RGBA8 (d=4) image (png_encoder::saveToFile), or None."""
+        chunks = []
+
+        @WRITE_FUNC
+        def sink(_ctx, data, size):
+            chunks.append(C.string_at(data, size))
+
+        buf = C.create_string_buffer(bytes(src), max(1, len(src)))
+        ok = lib().icx_png_encode_with_func(self._p, sink, None, buf, width, height, d)
+        return b"".join(chunks) if ok == 1 else None
+
     def jpeg_encode(self, quality: int, subsampling: int, width: int, height: int, comps: int, src: bytes):
         """C4 extension encode (IJG quality 1..100, subsampling 444|420) -> bytes, or None."""
         chunks = []
@@ -214,8 +231,34 @@ class Context:
         return b"".join(chunks) if ok == 1 else None
 
 
+class PngEncoder:
+    """Device-resident PNG encode (icx_png_encoder_* / icx_png_encode_device)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._p = lib().icx_png_encoder_create(ctx.ptr)
+        if not self._p:
+            raise ICXError("icx_png_encoder_create failed: " + _err(ctx.ptr))
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().icx_png_encoder_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+    def encode_device(self, width, height, d, d_src, d_out, out_cap, stream=0):
+        """-> (icx_result, file size in bytes)."""
+        n = C.c_uint64()
+        rc = lib().icx_png_encode_device(self._p, width, height, d, d_src, d_out, out_cap, C.byref(n), stream or None)
+        if rc not in (OK, OUT_OF_MEM):
+            raise ICXError(f"icx_png_encode_device -> {rc}: {_err(self.ctx.ptr)}")
+        return rc, int(n.value)
+
+
 class Encoder:
-    """Device-resident encode (icx_encoder_* / icx_jpeg_encode_device); pointers are device
+    """Device-resident JPEG encode (icx_encoder_* / icx_jpeg_encode_device); pointers are device
     addresses (ints) on the context's device."""
 
     def __init__(self, ctx: Context):
@@ -357,9 +400,12 @@ class Image:
 
     def write(self, filepath: str):
         ext = os.path.splitext(filepath)[1].lower()
-        if ext not in (".jpg", ".jpeg"):
+        if ext == ".png":  # writePng -> png_encoder::saveToFile (codecs.cpp:1022-1025)
+            out = self.context().png_encode(self.w_, self.h_, self.d_, self.pixels_.tobytes())
+        elif ext in (".jpg", ".jpeg"):
+            out = self.context().tje_encode(3, self.w_, self.h_, self.d_, self.pixels_.tobytes())  # codecs.cpp:853
+        else:
             raise ValueError("Cannot parse filetype")
-        out = self.context().tje_encode(3, self.w_, self.h_, self.d_, self.pixels_.tobytes())  # codecs.cpp:853
         with open(filepath, "wb") as f:
             if out is not None:
                 f.write(out)

@@ -498,4 +498,71 @@ int icx_jpeg_encode_device(icx_encoder* enc, int quality, int subsampling, int w
     return rc == 0 ? ICX_OK : ICX_OUT_OF_MEM;
 }
 
+// ------------------------------------------------------------------ PNG (png_encoder::saveToFile)
+static const char* png_args_bad(int w, int h, int d) {
+    if (d != 3 && d != 4) return "d must be 3 or 4";
+    if (w <= 0 || h <= 0) return "empty image";
+    if ((int64_t)w * h > (int64_t)1 << 31) return "image too large";
+    return nullptr;
+}
+
+int icx_png_encode_with_func(icx_ctx* ctx, icx_write_func* func, void* context, const unsigned char* pixels, int width,
+                             int height, int d) {
+    if (!ctx || !func) return 0;
+    if (const char* e = png_args_bad(width, height, d)) { ctx->err = e; return 0; }
+    if (!pixels) { ctx->err = "null source"; return 0; }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), 0);
+    std::vector<uint8_t> file;
+    if (!png_encode_gpu(ctx->stream, width, height, d, pixels, file)) {
+        ctx->err = "HIP failure in png_encode_gpu";
+        return 0;
+    }
+    for (size_t o = 0; o < file.size(); o += 1023)
+        func(context, file.data() + o, (int)std::min<size_t>(1023, file.size() - o));
+    return 1;
+}
+
+int icx_png_save_to_file(icx_ctx* ctx, const char* path, const unsigned char* pixels, int width, int height, int d) {
+    if (!ctx || !path) return ICX_UNSUPPORTED;
+    FILE* fd = std::fopen(path, "wb");
+    if (!fd) { ctx->err = "could not open file for writing"; return ICX_INTERNAL_ERR; }
+    const int ok = icx_png_encode_with_func(ctx, file_sink, fd, pixels, width, height, d);
+    const bool closed = std::fclose(fd) == 0;
+    if (!ok) return png_args_bad(width, height, d) || !pixels ? ICX_UNSUPPORTED : ICX_INTERNAL_ERR;
+    return closed ? ICX_OK : ICX_INTERNAL_ERR;
+}
+
+struct icx_png_encoder {
+    icx_ctx* ctx = nullptr;
+    PngWs* ws = nullptr;
+};
+
+icx_png_encoder* icx_png_encoder_create(icx_ctx* ctx) {
+    if (!ctx) return nullptr;
+    icx_png_encoder* e = new icx_png_encoder();
+    e->ctx = ctx;
+    e->ws = png_ws_create();
+    return e;
+}
+
+void icx_png_encoder_destroy(icx_png_encoder* enc) {
+    if (!enc) return;
+    (void)hipSetDevice(enc->ctx->device);
+    png_ws_destroy(enc->ws);
+    delete enc;
+}
+
+int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, const uint8_t* d_src, uint8_t* d_out,
+                          uint64_t out_cap, uint64_t* out_size, void* hip_stream) {
+    if (!enc || !out_size) return ICX_UNSUPPORTED;
+    icx_ctx* ctx = enc->ctx;
+    if (const char* e = png_args_bad(width, height, d)) { ctx->err = e; return ICX_UNSUPPORTED; }
+    if (!d_src || (out_cap && !d_out)) { ctx->err = "null buffer"; return ICX_UNSUPPORTED; }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    const int rc = png_encode_device(st, enc->ws, width, height, d, d_src, d_out, out_cap, out_size);
+    if (rc < 0) { ctx->err = "HIP failure in png_encode_device"; return ICX_INTERNAL_ERR; }
+    return rc == 0 ? ICX_OK : ICX_OUT_OF_MEM;
+}
+
 }  // extern "C"

@@ -172,12 +172,16 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
     const int rr = (int)(step - q * bpm);
     const int64_t qy = q / mbw;
     const int qx = (int)(q - qy * mbw);
-    int64_t n = (int64_t)blockIdx.x * 32 + lb;
+    // XCD-aware chunks: workgroups dispatched to one XCD (linear id % 8, gridDim.x a multiple
+    // of 8) take adjacent 32-block chunks, so the partial plane lines they write merge in that
+    // XCD's L2 (measured: k_idct -17%)
+    const int64_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    int64_t n = chunk0 * 32 + lb;
     const int64_t mcu0 = n / bpm;
     int k = (int)(n - mcu0 * bpm);
     int64_t mby = mcu0 / mbw;
     int mbx = (int)(mcu0 - mby * mbw);
-    for (int64_t base = (int64_t)blockIdx.x * 32; base < nblocks; base += step) {
+    for (int64_t base = chunk0 * 32; base < nblocks; base += step) {
         const bool live = n < nblocks;
         IdctGeo g;
         if (small_mcu) {
@@ -791,7 +795,8 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     B(kStIdct);
     const int64_t maxblk = ws.coef_cap;
     // ~16K workgroups per launch in total; every kernel grid-strides over its image's work
-    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 31) / 32, 16384 / n));
+    int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 31) / 32, 16384 / n));
+    if (gx >= 8) gx &= ~7;  // XCD-aware chunk order in k_idct needs a multiple of 8
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap);
     E(kStIdct);

@@ -122,4 +122,12 @@ bool jpeg_encode_gpu(hipStream_t st, int quality, int subsampling, int w, int h,
 int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, int w, int h, int comps,
                        const uint8_t* d_src, uint8_t* d_out, uint64_t cap, uint64_t* size);
 
+// PNG encoder (icx_png.hip): png_encoder::saveToFile's colour choice and filters, GPU deflate.
+struct PngWs;
+PngWs* png_ws_create();
+void png_ws_destroy(PngWs* ws);
+int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
+                      uint64_t cap, uint64_t* size);
+bool png_encode_gpu(hipStream_t st, int w, int h, int d, const uint8_t* src, std::vector<uint8_t>& out);
+
 }  // namespace icx

@@ -1,0 +1,1161 @@
+// icx_png.hip -- gfx950 PNG encoder behind png_encoder::saveToFile (png_encoder.cpp:4474-4486).
+//
+// Parity contract: lodepng's colour-mode choice and filter bytes are
+// reproduced exactly (lodepng_compute_color_stats :3357-3543, auto_choose_color :3552-3616,
+// filter :3935-3983 with LFS_MINSUM and filter_palette_zero); the IDAT is a valid zlib stream
+// that inflates to that identical filtered stream. The deflate is our own segment-parallel
+// coder (lodepng's single shared hash chain, png_encoder.cpp:1840, is inherently serial).
+//
+//   k_png_stats      colour statistics: colored, alpha cases, grey bit needs, first transparent
+//                    pixel, distinct colours (LDS set per workgroup -> global set, capped at 257)
+//   k_png_keycheck   the colour-key cases (:3518-3528) once the key colour is known
+//   k_png_convert    lodepng_convert to the chosen mode (palette index / grey bits / drop alpha),
+//                    rows padded to whole bytes (preProcessScanlines)
+//   k_png_filter     one workgroup per row: the five filters, MINSUM scores, strict-< choice,
+//                    filtered row with its type byte
+//   k_png_lz77       one lane per 4 KiB segment: greedy LZ77 over fixed candidate distances
+//                    (1, pixel, 2 pixels, row above +-pixel), tokens + per-block histograms +
+//                    Adler-32 partials; 64 segments = one 256 KiB deflate block
+//   k_png_huff       one workgroup per block: length-limited Huffman codes (15/7 bits), the
+//                    dynamic block header bits
+//   k_png_segbits    bits per segment -> (scan) bit offsets
+//   k_png_emit       one lane per segment: LSB-first bit packing of its tokens at its offset
+//   k_png_crc*       CRC-32 of the IDAT chunk: per-segment table CRCs combined by x^(8n) shifts
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "icx_internal.h"
+
+namespace icx {
+
+namespace png {
+
+constexpr int kSeg = 4096;            // LZ77 / emit segment (bytes of the filtered stream)
+constexpr int kSegPerBlock = 64;      // 256 KiB deflate blocks (lodepng's size at this scale, :1830)
+constexpr int kNLL = 286, kND = 30;   // literal/length and distance alphabets
+constexpr int kHdrWords = 96;         // per-block header bit buffer (<= 3072 bits)
+constexpr int kCrcSeg = 65536;
+constexpr uint32_t kAdlerMod = 65521;
+enum { kGrey = 0, kRGB = 2, kPalette = 3, kGreyAlpha = 4, kRGBA = 6 };
+
+struct Stats {
+    uint32_t colored;    // some pixel with r != g or r != b
+    uint32_t alpha_mid;  // some alpha not in {0, 255}
+    uint32_t bits;       // max getValueRequiredBits(r)
+    uint32_t any_a0;     // some alpha == 0
+    unsigned long long first_a0;  // smallest pixel index with alpha == 0
+    uint32_t ncolors;    // distinct RGBA colours inserted (saturates past 256)
+    uint32_t overflow;   // > 256 distinct colours
+    uint32_t a2, a3;     // key cases: transparent pixel of another colour / opaque key colour
+};
+
+constexpr int kSetSlots = 4096;  // global colour set: (colour | 1<<32) keys, min pixel index values
+
+struct Mode {
+    int colortype, bitdepth, bpp, bw;  // bpp in bits, bw = filter byte width
+    int64_t lb;                        // bytes per (padded) row
+    int npal;
+    uint32_t pal[256];                 // RGBA packed r | g<<8 | b<<16 | a<<24
+};
+
+// ---- deflate tables (RFC 1951 3.2.5)
+__constant__ uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                      35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769,
+                                       1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+
+__device__ __forceinline__ int len_code(int len) {  // 3..258 -> 0..28
+    int c = 0;
+    while (c < 28 && kLenBase[c + 1] <= len) ++c;
+    return c;
+}
+__device__ __forceinline__ int dist_code(int d) {  // 1..32768 -> 0..29
+    int c = 0;
+    while (c < 29 && kDistBase[c + 1] <= d) ++c;
+    return c;
+}
+
+struct BlockCodes {
+    uint16_t ll_code[kNLL];  // bit-reversed (LSB-first emission)
+    uint8_t ll_len[kNLL];
+    uint16_t d_code[kND];
+    uint8_t d_len[kND];
+    uint32_t hdr[kHdrWords];  // header bits, LSB-first
+    uint32_t hdr_bits;
+    uint32_t pad_;
+};
+
+__device__ __forceinline__ uint32_t required_bits(uint32_t v) {  // :3349-3355
+    if (v == 0 || v == 255) return 1;
+    if (v % 17 == 0) return v % 85 == 0 ? 2 : 4;
+    return 8;
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t c) { return (c * 2654435761u) >> 20; }
+
+// ------------------------------------------------------------------------------- stats
+// Grid-stride over pixels. Colours go through a per-workgroup LDS set first (one global insert
+// per distinct colour per workgroup); > 256 distinct colours anywhere ends the counting.
+__global__ __launch_bounds__(256) void k_png_stats(const uint8_t* __restrict__ px, int64_t np, int d,
+                                                   Stats* __restrict__ st, unsigned long long* __restrict__ gset_key,
+                                                   unsigned long long* __restrict__ gset_idx) {
+    __shared__ uint32_t s_key[1024];
+    __shared__ unsigned long long s_idx[1024];
+    __shared__ uint32_t s_n, s_over;
+    const int t = threadIdx.x;
+    for (int i = t; i < 1024; i += 256) {
+        s_key[i] = 0xFFFFFFFFu;
+        s_idx[i] = ~0ull;
+    }
+    if (t == 0) {
+        s_n = 0;
+        s_over = 0;
+    }
+    __syncthreads();
+    uint32_t colored = 0, amid = 0, bits = 1, any0 = 0;
+    unsigned long long first0 = ~0ull;
+    const bool count_colors = st->overflow == 0;
+    // the LDS set reserves key 0xFFFFFFFF as empty: that colour (opaque white) uses slot s_white
+    __shared__ unsigned long long s_white;
+    if (t == 0) s_white = ~0ull;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < np; i += (int64_t)gridDim.x * 256) {
+        const uint8_t* p = px + i * d;
+        const uint32_t r = p[0], g = p[1], b = p[2], a = d == 4 ? p[3] : 255;
+        colored |= (r != g) | (r != b);
+        bits = max(bits, required_bits(r));
+        if (d == 4) {
+            amid |= a != 0 && a != 255;
+            if (a == 0) {
+                any0 = 1;
+                first0 = min(first0, (unsigned long long)i);
+            }
+        }
+        if (count_colors && !s_over) {
+            const uint32_t c = r | g << 8 | b << 16 | a << 24;
+            if (c == 0xFFFFFFFFu) {
+                atomicMin(&s_white, (unsigned long long)i);
+            } else {
+                uint32_t h = hash32(c) & 1023;
+                for (int probe = 0; probe < 1024; ++probe, h = (h + 1) & 1023) {
+                    const uint32_t old = atomicCAS(&s_key[h], 0xFFFFFFFFu, c);
+                    if (old == 0xFFFFFFFFu) {
+                        if (atomicAdd(&s_n, 1u) >= 256) s_over = 1;
+                    }
+                    if (old == 0xFFFFFFFFu || old == c) {
+                        atomicMin(&s_idx[h], (unsigned long long)i);
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    // workgroup reductions
+    colored = __syncthreads_or(colored);
+    amid = __syncthreads_or(amid);
+    any0 = __syncthreads_or(any0);
+    for (int o = 32; o > 0; o >>= 1) {
+        bits = max(bits, (uint32_t)__shfl_xor((int)bits, o));
+        first0 = min(first0, (unsigned long long)__shfl_xor((long long)first0, o));
+    }
+    __shared__ uint32_t s_bits;
+    __shared__ unsigned long long s_first;
+    if (t == 0) {
+        s_bits = 1;
+        s_first = ~0ull;
+    }
+    __syncthreads();
+    if ((t & 63) == 0) {
+        atomicMax(&s_bits, bits);
+        atomicMin(&s_first, first0);
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (colored) atomicOr(&st->colored, 1u);
+        if (amid) atomicOr(&st->alpha_mid, 1u);
+        if (any0) {
+            atomicOr(&st->any_a0, 1u);
+            atomicMin(&st->first_a0, s_first);
+        }
+        atomicMax(&st->bits, s_bits);
+        if (s_over) atomicOr(&st->overflow, 1u);
+    }
+    if (!count_colors || s_over) return;
+    // merge this workgroup's colours into the global set
+    auto ginsert = [&](uint32_t c, unsigned long long idx) {
+        const unsigned long long k = (unsigned long long)c | (1ull << 32);
+        uint32_t h = hash32(c) & (kSetSlots - 1);
+        for (int probe = 0; probe < kSetSlots; ++probe, h = (h + 1) & (kSetSlots - 1)) {
+            const unsigned long long old = atomicCAS(&gset_key[h], 0ull, k);
+            if (old == 0ull) {
+                if (atomicAdd(&st->ncolors, 1u) >= 256) atomicOr(&st->overflow, 1u);
+            }
+            if (old == 0ull || old == k) {
+                atomicMin(&gset_idx[h], idx);
+                return;
+            }
+        }
+        atomicOr(&st->overflow, 1u);
+    };
+    for (int i = t; i < 1024; i += 256)
+        if (s_key[i] != 0xFFFFFFFFu) ginsert(s_key[i], s_idx[i]);
+    if (t == 0 && s_white != ~0ull) ginsert(0xFFFFFFFFu, s_white);
+}
+
+// The colour-key cases once the first transparent pixel's colour K is known (d == 4, no alpha
+// yet): a transparent pixel of another colour, or a non-transparent pixel of colour K.
+__global__ __launch_bounds__(256) void k_png_keycheck(const uint8_t* __restrict__ px, int64_t np, uint32_t key,
+                                                      Stats* __restrict__ st) {
+    uint32_t a2 = 0, a3 = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < np; i += (int64_t)gridDim.x * 256) {
+        const uint8_t* p = px + i * 4;
+        const uint32_t rgb = p[0] | p[1] << 8 | p[2] << 16;
+        a2 |= p[3] == 0 && rgb != key;
+        a3 |= p[3] != 0 && rgb == key;
+    }
+    a2 = __syncthreads_or(a2);
+    a3 = __syncthreads_or(a3);
+    if (threadIdx.x == 0) {
+        if (a2) atomicOr(&st->a2, 1u);
+        if (a3) atomicOr(&st->a3, 1u);
+    }
+}
+
+// ----------------------------------------------------------------------------- convert
+// One output byte per thread: lodepng_convert (rgba8ToPixel :2781-2835) + row padding.
+__global__ __launch_bounds__(256) void k_png_convert(const uint8_t* __restrict__ px, int w, int h, int d,
+                                                     const Mode* __restrict__ mode, uint8_t* __restrict__ out) {
+    __shared__ uint32_t s_used[512], s_col[512];
+    __shared__ uint8_t s_val[512];
+    const Mode& M = *mode;
+    if (M.colortype == kPalette) {  // colour -> palette index (color_tree_get)
+        for (int i = threadIdx.x; i < 512; i += 256) s_used[i] = 0;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int k = 0; k < M.npal; ++k) {
+                const uint32_t c = M.pal[k];
+                uint32_t hh = hash32(c) & 511;
+                while (s_used[hh]) hh = (hh + 1) & 511;
+                s_used[hh] = 1;
+                s_col[hh] = c;
+                s_val[hh] = (uint8_t)k;
+            }
+        __syncthreads();
+    }
+    auto pixel = [&](int64_t y, int64_t x, uint32_t& r, uint32_t& g, uint32_t& b, uint32_t& a) {
+        const uint8_t* p = px + (y * w + x) * d;
+        r = p[0];
+        g = p[1];
+        b = p[2];
+        a = d == 4 ? p[3] : 255;
+    };
+    auto index_of = [&](int64_t y, int64_t x) -> uint32_t {
+        uint32_t r, g, b, a;
+        pixel(y, x, r, g, b, a);
+        const uint32_t c = r | g << 8 | b << 16 | a << 24;
+        uint32_t hh = hash32(c) & 511;
+        for (int probe = 0; probe < 512; ++probe, hh = (hh + 1) & 511) {
+            if (!s_used[hh]) return 0;
+            if (s_col[hh] == c) return s_val[hh];
+        }
+        return 0;
+    };
+    const int64_t total = M.lb * h;
+    for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (int64_t)gridDim.x * 256) {
+        const int64_t y = o / M.lb, xb = o - y * M.lb;
+        uint32_t v = 0;
+        if (M.bitdepth == 8) {
+            const int ch = M.bpp / 8;
+            const int64_t x = xb / ch;
+            const int c = (int)(xb - x * ch);
+            uint32_t r, g, b, a;
+            pixel(y, x, r, g, b, a);
+            switch (M.colortype) {
+                case kRGBA: v = c == 0 ? r : c == 1 ? g : c == 2 ? b : a; break;
+                case kRGB: v = c == 0 ? r : c == 1 ? g : b; break;
+                case kGreyAlpha: v = c == 0 ? r : a; break;
+                case kGrey: v = r; break;
+                default: v = index_of(y, x); break;
+            }
+        } else {  // 1/2/4-bit grey or palette, MSB-first (addColorBits :2706-2714), zero pad
+            const int per = 8 / M.bitdepth;
+            for (int k = 0; k < per; ++k) {
+                const int64_t x = xb * per + k;
+                uint32_t s = 0;
+                if (x < w) {
+                    if (M.colortype == kGrey) {
+                        uint32_t r, g, b, a;
+                        pixel(y, x, r, g, b, a);
+                        s = (r >> (8 - M.bitdepth)) & ((1u << M.bitdepth) - 1u);
+                    } else {
+                        s = index_of(y, x) & ((1u << M.bitdepth) - 1u);
+                    }
+                }
+                v |= s << (M.bitdepth * (per - 1 - k));
+            }
+        }
+        out[o] = (uint8_t)v;
+    }
+}
+
+// ------------------------------------------------------------------------------ filter
+__device__ __forceinline__ uint32_t paeth(uint32_t a, uint32_t b, uint32_t c) {  // :3621-3631
+    int pa = abs((int)b - (int)c), pb = abs((int)a - (int)c), pc = abs((int)a + (int)b - 2 * (int)c);
+    if (pb < pa) {
+        a = b;
+        pa = pb;
+    }
+    return pc < pa ? c : a;
+}
+__device__ __forceinline__ uint32_t filt(int type, uint32_t s, uint32_t left, uint32_t up, uint32_t ul) {
+    switch (type) {
+        case 1: return (s - left) & 255;
+        case 2: return (s - up) & 255;
+        case 3: return (s - ((left + up) >> 1)) & 255;
+        case 4: return (s - paeth(left, up, ul)) & 255;
+        default: return s;
+    }
+}
+
+// One workgroup per row (grid-stride): MINSUM over the five filters, ties to the lower type
+// (`sum < smallest`, :3968), type 0 scored unsigned; palette / < 8 bits: type 0 (:3950).
+__global__ __launch_bounds__(256) void k_png_filter(const uint8_t* __restrict__ img, int h, const Mode* __restrict__ mode,
+                                                    uint8_t* __restrict__ out) {
+    const Mode& M = *mode;
+    const int64_t lb = M.lb;
+    const int bw = M.bw;
+    const bool zero = M.colortype == kPalette || M.bitdepth < 8;
+    __shared__ uint32_t s_sum[5][4];
+    for (int y = blockIdx.x; y < h; y += gridDim.x) {
+        const uint8_t* cur = img + (int64_t)y * lb;
+        const uint8_t* prv = y ? cur - lb : nullptr;
+        int best = 0;
+        if (!zero) {
+            uint32_t sum[5] = {0, 0, 0, 0, 0};
+            for (int64_t i = threadIdx.x; i < lb; i += 256) {
+                const uint32_t s = cur[i], left = i >= bw ? cur[i - bw] : 0, up = prv ? prv[i] : 0,
+                               ul = (prv && i >= bw) ? prv[i - bw] : 0;
+                sum[0] += s;
+#pragma unroll
+                for (int tt = 1; tt < 5; ++tt) {
+                    const uint32_t f = filt(tt, s, left, up, ul);
+                    sum[tt] += f < 128 ? f : 255u - f;
+                }
+            }
+#pragma unroll
+            for (int tt = 0; tt < 5; ++tt)
+                for (int o = 32; o > 0; o >>= 1) sum[tt] += (uint32_t)__shfl_xor((int)sum[tt], o);
+            if ((threadIdx.x & 63) == 0)
+                for (int tt = 0; tt < 5; ++tt) s_sum[tt][threadIdx.x >> 6] = sum[tt];
+            __syncthreads();
+            uint32_t smallest = 0;
+            for (int tt = 0; tt < 5; ++tt) {
+                const uint32_t v = s_sum[tt][0] + s_sum[tt][1] + s_sum[tt][2] + s_sum[tt][3];
+                if (tt == 0 || v < smallest) {
+                    best = tt;
+                    smallest = v;
+                }
+            }
+            __syncthreads();
+        }
+        uint8_t* o = out + (int64_t)y * (lb + 1);
+        if (threadIdx.x == 0) o[0] = (uint8_t)best;
+        for (int64_t i = threadIdx.x; i < lb; i += 256) {
+            const uint32_t s = cur[i], left = i >= bw ? cur[i - bw] : 0, up = prv ? prv[i] : 0,
+                           ul = (prv && i >= bw) ? prv[i - bw] : 0;
+            o[1 + i] = (uint8_t)filt(best, s, left, up, ul);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------- LZ77
+// Token: literal = byte value (< 256); match = 1<<31 | (len-3) << 15 | (dist-1).
+__device__ __forceinline__ int match_len(const uint8_t* F, int64_t p, int64_t dist, int64_t maxlen) {
+    int l = 0;
+    while (l < maxlen && F[p + l] == F[p - dist + l]) ++l;
+    return l;
+}
+
+// One workgroup (one wave) per 256 KiB block, one lane per 4 KiB segment.
+__global__ __launch_bounds__(64) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
+                                                 int bw, uint32_t* __restrict__ tok, uint32_t* __restrict__ ntok,
+                                                 uint32_t* __restrict__ hist, uint32_t* __restrict__ adl) {
+    __shared__ uint32_t h_ll[kNLL], h_d[kND];
+    const int64_t blk = blockIdx.x;
+    for (int i = threadIdx.x; i < kNLL; i += 64) h_ll[i] = 0;
+    if (threadIdx.x < kND) h_d[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t seg = blk * kSegPerBlock + threadIdx.x;
+    if (seg < nseg) {
+        const int64_t s0 = seg * kSeg, s1 = min(N, s0 + kSeg);
+        uint32_t* T = tok + s0;
+        uint32_t nt = 0;
+        int64_t cand[6] = {1, bw, 2 * bw, rowlen, rowlen - bw, rowlen + bw};
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (cand[k] <= 0 || cand[k] > 32768) cand[k] = 0;
+        uint64_t a1 = 0, a2 = 0;  // Adler-32 partials: sum b, sum (N - g) b (reduced at the end)
+        uint32_t wgt = (uint32_t)((N - s0) % kAdlerMod);  // (N - g) mod 65521 for g = p
+        int64_t p = s0;
+        while (p < s1) {
+            const int64_t maxlen = min((int64_t)258, s1 - p);
+            int best = 0;
+            int64_t bd = 0;
+            if (maxlen >= 3) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const int64_t dd = cand[k];
+                    if (dd == 0 || dd > p) continue;
+                    if (F[p] != F[p - dd] || F[p + 1] != F[p - dd + 1] || F[p + 2] != F[p - dd + 2]) continue;
+                    const int l = 3 + match_len(F, p + 3, dd, maxlen - 3);
+                    if (l > best) {
+                        best = l;
+                        bd = dd;
+                    }
+                }
+            }
+            const int adv = best >= 3 ? best : 1;
+            for (int k = 0; k < adv; ++k) {
+                const uint32_t b = F[p + k];
+                a1 += b;
+                a2 += (uint64_t)wgt * b;
+                wgt = wgt ? wgt - 1 : kAdlerMod - 1;
+            }
+            if (best >= 3) {
+                T[nt++] = 0x80000000u | (uint32_t)(best - 3) << 15 | (uint32_t)(bd - 1);
+                atomicAdd(&h_ll[257 + len_code(best)], 1u);
+                atomicAdd(&h_d[dist_code((int)bd)], 1u);
+            } else {
+                const uint32_t b = F[p];
+                T[nt++] = b;
+                atomicAdd(&h_ll[b], 1u);
+            }
+            p += adv;
+        }
+        ntok[seg] = nt;
+        adl[2 * seg] = (uint32_t)(a1 % kAdlerMod);
+        adl[2 * seg + 1] = (uint32_t)(a2 % kAdlerMod);
+    }
+    __syncthreads();
+    uint32_t* H = hist + blk * (kNLL + kND);
+    for (int i = threadIdx.x; i < kNLL; i += 64) H[i] = h_ll[i] + (i == 256 ? 1u : 0u);  // + EOB
+    if (threadIdx.x < kND) H[kNLL + threadIdx.x] = h_d[threadIdx.x];
+}
+
+// ------------------------------------------------------------------------------ Huffman
+// Code lengths for freq[0..n) limited to maxbits (Huffman by sorting + JPEG Annex K.3
+// "adjust bits" length limiting, which keeps the code complete). Single thread; scratch in LDS.
+__device__ void huff_lengths(const uint32_t* freq, int n, int maxbits, uint8_t* len, uint16_t* order, uint32_t* wt,
+                             int16_t* parent, int* nused_out) {
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        len[i] = 0;
+        if (freq[i]) order[m++] = (uint16_t)i;
+    }
+    *nused_out = m;
+    if (m == 0) return;
+    if (m == 1) {
+        len[order[0]] = 1;
+        return;
+    }
+    // insertion sort by (freq, symbol) ascending
+    for (int a = 1; a < m; ++a) {
+        const uint16_t v = order[a];
+        int b = a - 1;
+        while (b >= 0 && (freq[order[b]] > freq[v] || (freq[order[b]] == freq[v] && order[b] > v))) {
+            order[b + 1] = order[b];
+            --b;
+        }
+        order[b + 1] = v;
+    }
+    // two-queue Huffman: leaves 0..m-1 (sorted), internal nodes m..2m-2
+    for (int i = 0; i < m; ++i) wt[i] = freq[order[i]];
+    int li = 0, ii = m, in_end = m;
+    for (int k = 0; k < m - 1; ++k) {
+        int pick[2];
+        for (int q = 0; q < 2; ++q) {
+            if (li < m && (ii >= in_end || wt[li] <= wt[ii])) pick[q] = li++;
+            else pick[q] = ii++;
+        }
+        wt[in_end] = wt[pick[0]] + wt[pick[1]];
+        parent[pick[0]] = (int16_t)in_end;
+        parent[pick[1]] = (int16_t)in_end;
+        ++in_end;
+    }
+    // depths top-down (a parent always has a larger index than its children); wt is reused
+    uint32_t* dep = wt;
+    dep[in_end - 1] = 0;
+    for (int k = in_end - 2; k >= 0; --k) dep[k] = dep[parent[k]] + 1;
+    int bl[40];
+    for (int i = 0; i < 40; ++i) bl[i] = 0;
+    int maxd = 0;
+    for (int i = 0; i < m; ++i) {
+        const int dd = dep[i] > 39 ? 39 : (int)dep[i];
+        ++bl[dd];
+        maxd = dd > maxd ? dd : maxd;
+    }
+    for (int i = maxd; i > maxbits; --i) {  // Annex K.3 Adjust_BITS
+        while (bl[i] > 0) {
+            int j = i - 2;
+            while (j > 1 && bl[j] == 0) --j;
+            bl[i] -= 2;
+            bl[i - 1] += 1;
+            bl[j + 1] += 2;
+            bl[j] -= 1;
+        }
+    }
+    // most frequent symbols get the shortest codes: walk sorted order from the top
+    int k = m - 1;
+    for (int l = 1; l <= maxbits; ++l)
+        for (int c = 0; c < bl[l]; ++c) len[order[k--]] = (uint8_t)l;
+}
+
+__device__ void canon_codes(const uint8_t* len, int n, uint16_t* code) {  // RFC 1951 3.2.2, bit-reversed
+    int bl[16] = {0};
+    for (int i = 0; i < n; ++i) ++bl[len[i]];
+    bl[0] = 0;
+    int next[16];
+    int c = 0;
+    for (int b = 1; b < 16; ++b) {
+        c = (c + bl[b - 1]) << 1;
+        next[b] = c;
+    }
+    for (int i = 0; i < n; ++i) {
+        const int l = len[i];
+        code[i] = 0;
+        if (!l) continue;
+        const uint32_t v = (uint32_t)next[l]++;
+        code[i] = (uint16_t)(__brev(v) >> (32 - l));
+    }
+}
+
+struct BitW {
+    uint32_t* w;
+    uint32_t n = 0;  // bits written
+    __device__ void put(uint32_t v, int nb) {
+        if (!nb) return;
+        const uint32_t s = n & 31;
+        w[n >> 5] |= v << s;
+        if (s + nb > 32) w[(n >> 5) + 1] |= v >> (32 - s);
+        n += nb;
+    }
+};
+
+// One workgroup per block, thread 0 builds everything (deterministic, tiny).
+__global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hist, int64_t nblk, BlockCodes* __restrict__ bc) {
+    __shared__ uint32_t f_ll[kNLL], f_d[kND];
+    __shared__ uint16_t order[kNLL];
+    __shared__ uint32_t wt[2 * kNLL];
+    __shared__ int16_t parent[2 * kNLL];
+    __shared__ uint8_t l_ll[kNLL], l_d[kND];
+    __shared__ uint8_t rle_sym[kNLL + kND];
+    __shared__ uint8_t rle_ext[kNLL + kND];
+    const int64_t blk = blockIdx.x;
+    const uint32_t* H = hist + blk * (kNLL + kND);
+    for (int i = threadIdx.x; i < kNLL; i += 64) f_ll[i] = H[i];
+    if (threadIdx.x < kND) f_d[threadIdx.x] = H[kNLL + threadIdx.x];
+    BlockCodes& B = bc[blk];
+    for (int i = threadIdx.x; i < kHdrWords; i += 64) B.hdr[i] = 0;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    // at least two codes per tree keeps every code complete
+    {
+        int u = 0;
+        for (int i = 0; i < kNLL; ++i) u += f_ll[i] != 0;
+        if (u < 2) f_ll[f_ll[0] ? 1 : 0] = 1;
+        u = 0;
+        for (int i = 0; i < kND; ++i) u += f_d[i] != 0;
+        if (u < 2) {
+            if (!f_d[0]) f_d[0] = 1;
+            if (!f_d[1]) f_d[1] = 1;
+        }
+    }
+    int used;
+    huff_lengths(f_ll, kNLL, 15, l_ll, order, wt, parent, &used);
+    huff_lengths(f_d, kND, 15, l_d, order, wt, parent, &used);
+    canon_codes(l_ll, kNLL, B.ll_code);
+    canon_codes(l_d, kND, B.d_code);
+    for (int i = 0; i < kNLL; ++i) B.ll_len[i] = l_ll[i];
+    for (int i = 0; i < kND; ++i) B.d_len[i] = l_d[i];
+    int hlit = kNLL;
+    while (hlit > 257 && l_ll[hlit - 1] == 0) --hlit;
+    int hdist = kND;
+    while (hdist > 1 && l_d[hdist - 1] == 0) --hdist;
+    // run-length code the concatenated lengths (16: repeat 3-6, 17: zeros 3-10, 18: zeros 11-138)
+    int ns = 0;
+    const int tot = hlit + hdist;
+    auto L = [&](int i) { return i < hlit ? l_ll[i] : l_d[i - hlit]; };
+    for (int i = 0; i < tot;) {
+        const int cur = L(i);
+        int run = 1;
+        while (i + run < tot && L(i + run) == cur) ++run;
+        int left = run;
+        if (cur == 0) {
+            while (left >= 11) {
+                const int r = min(left, 138);
+                rle_sym[ns] = 18;
+                rle_ext[ns++] = (uint8_t)(r - 11);
+                left -= r;
+            }
+            if (left >= 3) {
+                rle_sym[ns] = 17;
+                rle_ext[ns++] = (uint8_t)(left - 3);
+                left = 0;
+            }
+            while (left > 0) {
+                rle_sym[ns] = 0;
+                rle_ext[ns++] = 0;
+                --left;
+            }
+        } else {
+            rle_sym[ns] = (uint8_t)cur;
+            rle_ext[ns++] = 0;
+            --left;
+            while (left >= 3) {
+                const int r = min(left, 6);
+                rle_sym[ns] = 16;
+                rle_ext[ns++] = (uint8_t)(r - 3);
+                left -= r;
+            }
+            while (left > 0) {
+                rle_sym[ns] = (uint8_t)cur;
+                rle_ext[ns++] = 0;
+                --left;
+            }
+        }
+        i += run;
+    }
+    uint32_t f_cl[19];
+    for (int i = 0; i < 19; ++i) f_cl[i] = 0;
+    for (int i = 0; i < ns; ++i) ++f_cl[rle_sym[i]];
+    {
+        int u = 0;
+        for (int i = 0; i < 19; ++i) u += f_cl[i] != 0;
+        if (u < 2) {
+            if (!f_cl[0]) f_cl[0] = 1;
+            else f_cl[1] = 1;
+        }
+    }
+    uint8_t l_cl[19];
+    uint16_t c_cl[19];
+    huff_lengths(f_cl, 19, 7, l_cl, order, wt, parent, &used);
+    canon_codes(l_cl, 19, c_cl);
+    int hclen = 19;
+    while (hclen > 4 && l_cl[kClOrder[hclen - 1]] == 0) --hclen;
+    BitW bw{B.hdr};
+    bw.put(blk == nblk - 1 ? 1u : 0u, 1);  // BFINAL
+    bw.put(2u, 2);                          // BTYPE = dynamic
+    bw.put((uint32_t)(hlit - 257), 5);
+    bw.put((uint32_t)(hdist - 1), 5);
+    bw.put((uint32_t)(hclen - 4), 4);
+    for (int i = 0; i < hclen; ++i) bw.put(l_cl[kClOrder[i]], 3);
+    for (int i = 0; i < ns; ++i) {
+        const int s = rle_sym[i];
+        bw.put(c_cl[s], l_cl[s]);
+        if (s == 16) bw.put(rle_ext[i], 2);
+        else if (s == 17) bw.put(rle_ext[i], 3);
+        else if (s == 18) bw.put(rle_ext[i], 7);
+    }
+    B.hdr_bits = bw.n;
+}
+
+__device__ __forceinline__ uint32_t token_bits(const BlockCodes& B, uint32_t t) {
+    if (!(t & 0x80000000u)) return B.ll_len[t];
+    const int len = (int)((t >> 15) & 255) + 3, dist = (int)(t & 0x7FFF) + 1;
+    const int lc = len_code(len), dc = dist_code(dist);
+    return B.ll_len[257 + lc] + kLenExtra[lc] + B.d_len[dc] + kDistExtra[dc];
+}
+
+__global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint32_t* __restrict__ tok,
+                                                     const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
+                                                     unsigned long long* __restrict__ bits) {
+    const int64_t seg = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (seg >= nseg) return;
+    const int64_t blk = seg / kSegPerBlock;
+    const BlockCodes& B = bc[blk];
+    const uint32_t* T = tok + seg * kSeg;
+    const uint32_t nt = ntok[seg];
+    unsigned long long b = 0;
+    if (seg % kSegPerBlock == 0) b += B.hdr_bits;
+    for (uint32_t i = 0; i < nt; ++i) b += token_bits(B, T[i]);
+    if (seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1) b += B.ll_len[256];  // EOB
+    bits[seg] = b;
+}
+
+// Bit writer for one segment: words strictly inside the segment's range are stored, the two
+// boundary words are OR-ed in (shared with the neighbouring segments); `out` was zeroed.
+struct SegWriter {
+    uint32_t* out;
+    unsigned long long pos;  // bit position of acc's bit 0
+    uint64_t acc = 0;
+    int nacc = 0;
+    unsigned long long first_word, last_word;
+    __device__ void flush_word(uint32_t v) {
+        const unsigned long long wi = pos >> 5;
+        if (wi == first_word || wi == last_word) atomicOr(out + wi, v);
+        else out[wi] = v;
+        pos += 32;
+    }
+    __device__ void put(uint32_t v, int nb) {
+        if (!nb) return;
+        acc |= (uint64_t)v << nacc;
+        nacc += nb;
+        if (nacc >= 32) {
+            flush_word((uint32_t)acc);
+            acc >>= 32;
+            nacc -= 32;
+        }
+    }
+    __device__ void finish() {
+        if (nacc > 0) flush_word((uint32_t)acc);
+    }
+};
+
+__global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint32_t* __restrict__ tok,
+                                                  const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
+                                                  const unsigned long long* __restrict__ off,
+                                                  const unsigned long long* __restrict__ bits, uint32_t* __restrict__ out,
+                                                  unsigned long long base_bits) {
+    const int64_t seg = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (seg >= nseg) return;
+    const int64_t blk = seg / kSegPerBlock;
+    const BlockCodes& B = bc[blk];
+    const uint32_t* T = tok + seg * kSeg;
+    const uint32_t nt = ntok[seg];
+    const unsigned long long o0 = base_bits + off[seg], o1 = o0 + bits[seg];
+    if (o1 == o0) return;
+    SegWriter w;
+    w.out = out;
+    w.pos = o0 & ~31ull;
+    w.nacc = (int)(o0 & 31);
+    w.first_word = o0 >> 5;
+    w.last_word = (o1 - 1) >> 5;
+    if (seg % kSegPerBlock == 0)
+        for (uint32_t b = 0; b < B.hdr_bits; b += 16) {
+            const uint32_t n = min(16u, B.hdr_bits - b);
+            const uint32_t v = (B.hdr[b >> 5] >> (b & 31)) & ((1u << n) - 1u);  // 16-bit pieces stay in one word
+            w.put(v, (int)n);
+        }
+    for (uint32_t i = 0; i < nt; ++i) {
+        const uint32_t t = T[i];
+        if (!(t & 0x80000000u)) {
+            w.put(B.ll_code[t], B.ll_len[t]);
+        } else {
+            const int len = (int)((t >> 15) & 255) + 3, dist = (int)(t & 0x7FFF) + 1;
+            const int lc = len_code(len), dc = dist_code(dist);
+            w.put(B.ll_code[257 + lc], B.ll_len[257 + lc]);
+            w.put((uint32_t)(len - kLenBase[lc]), kLenExtra[lc]);
+            w.put(B.d_code[dc], B.d_len[dc]);
+            w.put((uint32_t)(dist - kDistBase[dc]), kDistExtra[dc]);
+        }
+    }
+    if (seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1) w.put(B.ll_code[256], B.ll_len[256]);
+    w.finish();
+}
+
+// ------------------------------------------------------------------------------- CRC-32
+__device__ __forceinline__ uint32_t crc_table(uint32_t i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    return c;
+}
+// Raw CRC (register starts at 0, no final xor) of each kCrcSeg-byte segment.
+__global__ __launch_bounds__(256) void k_png_crc_seg(const uint8_t* __restrict__ p, int64_t n, int64_t nseg,
+                                                     uint32_t* __restrict__ part) {
+    __shared__ uint32_t tab[256];
+    tab[threadIdx.x] = crc_table(threadIdx.x);
+    __syncthreads();
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= nseg) return;
+    const int64_t a = s * kCrcSeg, b = min(n, a + kCrcSeg);
+    uint32_t c = 0;
+    for (int64_t i = a; i < b; ++i) c = tab[(c ^ p[i]) & 255] ^ (c >> 8);
+    part[s] = c;
+}
+// a(x) * b(x) mod P(x), reflected (bit 31 = x^0)
+__device__ __host__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+__device__ __host__ inline uint32_t x8n(uint64_t n) {  // x^(8n) mod P
+    uint32_t r = 1u << 31, sq = 1u << 23;            // x^0 ; x^8
+    while (n) {
+        if (n & 1) r = multmodp(sq, r);
+        sq = multmodp(sq, sq);
+        n >>= 1;
+    }
+    return r;
+}
+// crc32 (standard) of the whole range from the raw segment CRCs: raw(A|B) = raw(A)*x^(8|B|) ^ raw(B)
+__global__ void k_png_crc_combine(const uint32_t* __restrict__ part, int64_t n, int64_t nseg, uint32_t init_raw,
+                                  uint32_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const uint32_t xs = x8n(kCrcSeg);
+    uint32_t c = init_raw;  // raw CRC of the bytes before the range ("IDAT")
+    for (int64_t s = 0; s < nseg; ++s) {
+        const int64_t len = min((int64_t)kCrcSeg, n - s * kCrcSeg);
+        c = multmodp(len == kCrcSeg ? xs : x8n((uint64_t)len), c) ^ part[s];
+    }
+    *out = c;
+}
+
+__global__ void k_png_adler(const uint32_t* __restrict__ adl, int64_t nseg, uint32_t* __restrict__ out) {
+    // two sums over segment partials, one lane each (nseg is small: N / 4 KiB)
+    __shared__ unsigned long long s[2][256];
+    unsigned long long a = 0, b = 0;
+    for (int64_t i = threadIdx.x; i < nseg; i += 256) {
+        a += adl[2 * i];
+        b += adl[2 * i + 1];
+    }
+    s[0][threadIdx.x] = a;
+    s[1][threadIdx.x] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long A = 0, B = 0;
+        for (int i = 0; i < 256; ++i) {
+            A += s[0][i];
+            B += s[1][i];
+        }
+        out[0] = (uint32_t)(A % kAdlerMod);
+        out[1] = (uint32_t)(B % kAdlerMod);
+    }
+}
+
+}  // namespace png
+
+// =============================================================================== host side
+using namespace png;
+
+struct PngWs {
+    Stats* st = nullptr;
+    unsigned long long *set_key = nullptr, *set_idx = nullptr;
+    Mode* mode = nullptr;
+    uint8_t *conv = nullptr, *filt = nullptr;
+    size_t conv_cap = 0, filt_cap = 0;
+    uint32_t *tok = nullptr, *ntok = nullptr, *hist = nullptr, *adl = nullptr, *crc = nullptr, *small = nullptr;
+    size_t tok_cap = 0, seg_cap = 0, blk_cap = 0, hist_cap = 0, crc_cap = 0;
+    BlockCodes* bc = nullptr;
+    unsigned long long *bits = nullptr, *off = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_cap = 0;
+    ~PngWs() {
+        for (void* p : {(void*)st, (void*)set_key, (void*)set_idx, (void*)mode, (void*)conv, (void*)filt, (void*)tok,
+                        (void*)ntok, (void*)hist, (void*)adl, (void*)crc, (void*)small, (void*)bc, (void*)bits,
+                        (void*)off, tmp})
+            if (p) (void)hipFree(p);
+    }
+};
+PngWs* png_ws_create() { return new PngWs(); }
+void png_ws_destroy(PngWs* ws) { delete ws; }
+
+#define PNG_HIP(call)                               \
+    do {                                            \
+        if ((call) != hipSuccess) return -1;        \
+    } while (0)
+
+template <class T>
+static bool pgrow(T*& p, size_t bytes, size_t& cap) {
+    if (p && bytes <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 64)) != hipSuccess) return false;
+    cap = bytes;
+    return true;
+}
+
+static void be32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24);
+    p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);
+    p[3] = (uint8_t)v;
+}
+static uint32_t crc32_host(uint32_t c, const uint8_t* p, size_t n) {  // standard CRC-32, running
+    c = ~c;
+    for (size_t i = 0; i < n; ++i) {
+        c ^= p[i];
+        for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    }
+    return ~c;
+}
+static void chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data, uint32_t n) {
+    uint8_t h[8];
+    be32(h, n);
+    std::memcpy(h + 4, type, 4);
+    o.insert(o.end(), h, h + 8);
+    if (n) o.insert(o.end(), data, data + n);
+    uint8_t c[4];
+    be32(c, crc32_host(0, o.data() + o.size() - n - 4, n + 4));
+    o.insert(o.end(), c, c + 4);
+}
+
+// Encode the device image d_src (w*h*d bytes, d = 3 RGB8 / 4 RGBA8) into a whole PNG file at
+// d_out. Returns 0 ok, 1 d_out too small (*size = bytes needed), -1 HIP failure.
+int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
+                      uint64_t cap, uint64_t* size) {
+    const int64_t np = (int64_t)w * h;
+    size_t c1 = ws->st ? sizeof(Stats) : 0, c2 = ws->set_key ? kSetSlots * 8 : 0, c3 = c2, c4 = ws->mode ? sizeof(Mode) : 0;
+    if (!pgrow(ws->st, sizeof(Stats), c1) || !pgrow(ws->set_key, kSetSlots * 8, c2) ||
+        !pgrow(ws->set_idx, kSetSlots * 8, c3) || !pgrow(ws->mode, sizeof(Mode), c4))
+        return -1;
+    // ---- P1: colour statistics (lodepng_compute_color_stats) and auto_choose_color
+    Stats zero{};
+    zero.bits = 1;
+    zero.first_a0 = ~0ull;
+    PNG_HIP(hipMemcpyAsync(ws->st, &zero, sizeof zero, hipMemcpyHostToDevice, st));
+    PNG_HIP(hipMemsetAsync(ws->set_key, 0, kSetSlots * 8, st));
+    PNG_HIP(hipMemsetAsync(ws->set_idx, 0xFF, kSetSlots * 8, st));
+    const int gs = (int)std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 4096));
+    if (np) hipLaunchKernelGGL(k_png_stats, dim3(gs), dim3(256), 0, st, d_src, np, d, ws->st, ws->set_key, ws->set_idx);
+    Stats S;
+    PNG_HIP(hipMemcpyAsync(&S, ws->st, sizeof S, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipStreamSynchronize(st));
+    uint32_t kr = 0, kg = 0, kb = 0;
+    bool alpha = S.alpha_mid != 0, key = false;
+    if (d == 4 && !alpha && S.any_a0) {
+        uint8_t kp[4];
+        PNG_HIP(hipMemcpy(kp, d_src + S.first_a0 * 4, 4, hipMemcpyDeviceToHost));
+        kr = kp[0];
+        kg = kp[1];
+        kb = kp[2];
+        hipLaunchKernelGGL(k_png_keycheck, dim3(gs), dim3(256), 0, st, d_src, np, kr | kg << 8 | kb << 16, ws->st);
+        PNG_HIP(hipMemcpyAsync(&S, ws->st, sizeof S, hipMemcpyDeviceToHost, st));
+        PNG_HIP(hipStreamSynchronize(st));
+        alpha = S.a2 || S.a3;
+        key = !alpha;
+    }
+    uint32_t bits = S.bits;
+    const bool colored = S.colored != 0;
+    if (colored || alpha) bits = std::max(bits, 8u);  // :3480, :3491, :3503
+    const uint32_t ncol = S.overflow ? 257u : std::min(S.ncolors, 257u);
+    // auto_choose_color (:3552-3616)
+    if (key && np <= 16) {
+        alpha = true;
+        key = false;
+        bits = std::max(bits, 8u);
+    }
+    const bool gray_ok = !colored;
+    if (!gray_ok && bits < 8) bits = 8;
+    const uint32_t palettebits = ncol <= 2 ? 1 : (ncol <= 4 ? 2 : (ncol <= 16 ? 4 : 8));
+    bool palette_ok = ncol <= 256 && bits <= 8 && ncol != 0;
+    if ((uint64_t)np < (uint64_t)ncol * 2) palette_ok = false;
+    if (gray_ok && !alpha && bits <= palettebits) palette_ok = false;
+    Mode M;
+    std::memset(&M, 0, sizeof M);
+    bool key_defined = false;
+    uint32_t key16[3] = {kr + (kr << 8), kg + (kg << 8), kb + (kb << 8)};
+    if (palette_ok) {
+        M.colortype = kPalette;
+        M.bitdepth = (int)palettebits;
+        std::vector<unsigned long long> keys(kSetSlots), idx(kSetSlots);
+        PNG_HIP(hipMemcpy(keys.data(), ws->set_key, kSetSlots * 8, hipMemcpyDeviceToHost));
+        PNG_HIP(hipMemcpy(idx.data(), ws->set_idx, kSetSlots * 8, hipMemcpyDeviceToHost));
+        std::vector<std::pair<unsigned long long, uint32_t>> cols;
+        for (int i = 0; i < kSetSlots; ++i)
+            if (keys[i]) cols.push_back({idx[i], (uint32_t)keys[i]});
+        std::sort(cols.begin(), cols.end());  // first-seen order (lodepng's palette order, :3500-3509)
+        M.npal = (int)cols.size();
+        for (int i = 0; i < M.npal; ++i) M.pal[i] = cols[i].second;
+    } else {
+        M.bitdepth = (int)bits;
+        M.colortype = alpha ? (gray_ok ? kGreyAlpha : kRGBA) : (gray_ok ? kGrey : kRGB);
+        if (key) {
+            const uint32_t mask = (1u << M.bitdepth) - 1u;
+            key_defined = true;
+            for (uint32_t& k : key16) k &= mask;
+        }
+    }
+    const int ch = M.colortype == kRGB ? 3 : M.colortype == kRGBA ? 4 : M.colortype == kGreyAlpha ? 2 : 1;
+    M.bpp = ch * M.bitdepth;
+    M.bw = (M.bpp + 7) / 8;
+    M.lb = ((int64_t)w * M.bpp + 7) / 8;
+    PNG_HIP(hipMemcpyAsync(ws->mode, &M, sizeof M, hipMemcpyHostToDevice, st));
+
+    // ---- header bytes (host; tiny)
+    std::vector<uint8_t> head = {137, 80, 78, 71, 13, 10, 26, 10};
+    uint8_t ihdr[13];
+    be32(ihdr, (uint32_t)w);
+    be32(ihdr + 4, (uint32_t)h);
+    ihdr[8] = (uint8_t)M.bitdepth;
+    ihdr[9] = (uint8_t)M.colortype;
+    ihdr[10] = ihdr[11] = ihdr[12] = 0;
+    chunk(head, "IHDR", ihdr, 13);
+    if (M.colortype == kPalette) {
+        uint8_t pl[768];
+        for (int i = 0; i < M.npal; ++i) {
+            pl[3 * i] = (uint8_t)M.pal[i];
+            pl[3 * i + 1] = (uint8_t)(M.pal[i] >> 8);
+            pl[3 * i + 2] = (uint8_t)(M.pal[i] >> 16);
+        }
+        chunk(head, "PLTE", pl, (uint32_t)M.npal * 3);
+        uint32_t ntr = (uint32_t)M.npal;
+        while (ntr && (M.pal[ntr - 1] >> 24) == 255) --ntr;
+        uint8_t tr[256];
+        for (uint32_t i = 0; i < ntr; ++i) tr[i] = (uint8_t)(M.pal[i] >> 24);
+        if (ntr) chunk(head, "tRNS", tr, ntr);
+    } else if (key_defined && M.colortype == kGrey) {
+        uint8_t tr[2] = {(uint8_t)(key16[0] >> 8), (uint8_t)key16[0]};
+        chunk(head, "tRNS", tr, 2);
+    } else if (key_defined && M.colortype == kRGB) {
+        uint8_t tr[6];
+        for (int i = 0; i < 3; ++i) {
+            tr[2 * i] = (uint8_t)(key16[i] >> 8);
+            tr[2 * i + 1] = (uint8_t)key16[i];
+        }
+        chunk(head, "tRNS", tr, 6);
+    }
+
+    // ---- P2: convert (unless the input already is the chosen mode) and filter
+    const int64_t N = (int64_t)h * (1 + M.lb);
+    const bool identity = (M.colortype == kRGBA && d == 4) || (M.colortype == kRGB && d == 3);
+    const uint8_t* img = d_src;
+    if (!identity) {
+        if (!pgrow(ws->conv, (size_t)(M.lb * h), ws->conv_cap)) return -1;
+        const int gc = (int)std::max<int64_t>(1, std::min<int64_t>((M.lb * h + 255) / 256, 16384));
+        hipLaunchKernelGGL(k_png_convert, dim3(gc), dim3(256), 0, st, d_src, w, h, d, ws->mode, ws->conv);
+        img = ws->conv;
+    }
+    if (!pgrow(ws->filt, (size_t)N, ws->filt_cap)) return -1;
+    hipLaunchKernelGGL(k_png_filter, dim3(std::max(1, std::min(h, 16384))), dim3(256), 0, st, img, h, ws->mode, ws->filt);
+
+    // ---- P3/P4: deflate
+    const int64_t nseg = (N + kSeg - 1) / kSeg, nblk = (nseg + kSegPerBlock - 1) / kSegPerBlock;
+    size_t c5 = ws->seg_cap, c6 = ws->seg_cap, c7 = ws->seg_cap, c8 = ws->seg_cap, c9 = ws->blk_cap, c10 = ws->blk_cap;
+    if (!pgrow(ws->tok, (size_t)nseg * kSeg * 4, ws->tok_cap)) return -1;
+    if ((size_t)nseg * 8 > ws->seg_cap || !ws->ntok) {
+        if (!pgrow(ws->ntok, (size_t)nseg * 8, c5) || !pgrow(ws->adl, (size_t)nseg * 8, c6) ||
+            !pgrow(ws->bits, (size_t)nseg * 8, c7) || !pgrow(ws->off, (size_t)nseg * 8, c8))
+            return -1;
+        ws->seg_cap = (size_t)nseg * 8;
+    }
+    (void)c9;
+    (void)c10;
+    if (!pgrow(ws->hist, (size_t)nblk * (kNLL + kND) * 4, ws->hist_cap) ||
+        !pgrow(ws->bc, (size_t)nblk * sizeof(BlockCodes), ws->blk_cap))
+        return -1;
+    size_t c11 = ws->small ? 64 : 0;
+    if (!pgrow(ws->small, 64, c11)) return -1;
+    hipLaunchKernelGGL(k_png_lz77, dim3((unsigned)nblk), dim3(64), 0, st, ws->filt, N, nseg, 1 + M.lb, M.bw, ws->tok,
+                       ws->ntok, ws->hist, ws->adl);
+    hipLaunchKernelGGL(k_png_huff, dim3((unsigned)nblk), dim3(64), 0, st, ws->hist, nblk, ws->bc);
+    const unsigned gseg = (unsigned)((nseg + 255) / 256);
+    hipLaunchKernelGGL(k_png_segbits, dim3(gseg), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->bits);
+    size_t tb = 0;
+    PNG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ws->bits, ws->off, (int)nseg, st));
+    if (!pgrow(ws->tmp, tb, ws->tmp_cap)) return -1;
+    PNG_HIP(hipcub::DeviceScan::ExclusiveSum(ws->tmp, tb, ws->bits, ws->off, (int)nseg, st));
+    hipLaunchKernelGGL(k_png_adler, dim3(1), dim3(256), 0, st, ws->adl, nseg, ws->small);
+    unsigned long long last_off = 0, last_bits = 0;
+    uint32_t ad[2];
+    PNG_HIP(hipMemcpyAsync(&last_off, ws->off + nseg - 1, 8, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipMemcpyAsync(&last_bits, ws->bits + nseg - 1, 8, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipMemcpyAsync(ad, ws->small, 8, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipStreamSynchronize(st));
+    const uint64_t dbytes = (last_off + last_bits + 7) / 8;  // deflate stream, zero-padded
+    const uint64_t zlen = 2 + dbytes + 4;
+    const uint64_t idat_at = head.size();  // IDAT chunk header position
+    const uint64_t data_at = idat_at + 8;   // zlib stream position
+    const uint64_t total = data_at + zlen + 4 + 12;
+    *size = total;
+    if (total > cap) return 1;
+    // The deflate bits go to a 4-byte aligned word view of d_out starting at data_at + 2
+    // rounded down; the few bytes before it (zlib header) are rewritten afterwards.
+    const uint64_t dstart = data_at + 2;
+    const uint64_t wbase = dstart & ~3ull;
+    const unsigned long long base_bits = (dstart - wbase) * 8;
+    PNG_HIP(hipMemsetAsync(d_out + wbase, 0, ((dbytes + (dstart - wbase) + 3) & ~3ull) + 4, st));
+    hipLaunchKernelGGL(k_png_emit, dim3(gseg), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->off, ws->bits,
+                       reinterpret_cast<uint32_t*>(d_out + wbase), base_bits);
+    // signature + IHDR/PLTE/tRNS + IDAT length/type + zlib header (78 01, :1932-1941)
+    std::vector<uint8_t> pre = head;
+    uint8_t ih[8];
+    be32(ih, (uint32_t)zlen);
+    std::memcpy(ih + 4, "IDAT", 4);
+    pre.insert(pre.end(), ih, ih + 8);
+    pre.push_back(0x78);
+    pre.push_back(0x01);
+    PNG_HIP(hipMemcpyAsync(d_out, pre.data(), pre.size(), hipMemcpyHostToDevice, st));
+    uint8_t adl[4];
+    const uint32_t s1 = (1 + ad[0]) % kAdlerMod, s2 = (uint32_t)(((uint64_t)N + ad[1]) % kAdlerMod);
+    be32(adl, s2 << 16 | s1);
+    PNG_HIP(hipMemcpyAsync(d_out + dstart + dbytes, adl, 4, hipMemcpyHostToDevice, st));
+    // CRC-32 over "IDAT" + zlib stream
+    const int64_t ncs = (int64_t)((zlen + kCrcSeg - 1) / kCrcSeg);
+    size_t c12 = ws->crc_cap;
+    if ((size_t)(ncs + 1) * 4 > ws->crc_cap || !ws->crc) {
+        if (!pgrow(ws->crc, (size_t)(ncs + 1) * 4, c12)) return -1;
+        ws->crc_cap = (size_t)(ncs + 1) * 4;
+    }
+    uint32_t init_raw = 0;  // raw CRC of 0xFFFFFFFF-initialised register over "IDAT", as raw state
+    {
+        // standard crc = raw(init=~0) ^ ~0; raw over "IDAT" from register ~0:
+        uint32_t c = 0xFFFFFFFFu;
+        const uint8_t t4[4] = {'I', 'D', 'A', 'T'};
+        for (int i = 0; i < 4; ++i) {
+            c ^= t4[i];
+            for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        }
+        init_raw = c;
+    }
+    hipLaunchKernelGGL(k_png_crc_seg, dim3((unsigned)((ncs + 255) / 256)), dim3(256), 0, st, d_out + data_at,
+                       (int64_t)zlen, ncs, ws->crc);
+    hipLaunchKernelGGL(k_png_crc_combine, dim3(1), dim3(64), 0, st, ws->crc, (int64_t)zlen, ncs, init_raw,
+                       ws->crc + ncs);
+    uint32_t craw = 0;
+    PNG_HIP(hipMemcpyAsync(&craw, ws->crc + ncs, 4, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipStreamSynchronize(st));
+    uint8_t tail[16];
+    be32(tail, ~craw);
+    const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+    std::memcpy(tail + 4, iend, 12);
+    PNG_HIP(hipMemcpyAsync(d_out + data_at + zlen, tail, 16, hipMemcpyHostToDevice, st));
+    PNG_HIP(hipGetLastError());
+    PNG_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+bool png_encode_gpu(hipStream_t st, int w, int h, int d, const uint8_t* src, std::vector<uint8_t>& out) {
+    PngWs ws;
+    const size_t srcb = (size_t)w * h * d;
+    uint8_t *d_src = nullptr, *d_out = nullptr;
+    bool ok = hipMalloc(&d_src, std::max<size_t>(srcb, 1)) == hipSuccess &&
+              hipMemcpyAsync(d_src, src, srcb, hipMemcpyHostToDevice, st) == hipSuccess;
+    uint64_t cap = srcb + srcb / 64 + (1 << 20), n = 0;
+    int rc = -1;
+    if (ok) {
+        ok = hipMalloc(&d_out, cap) == hipSuccess;
+        if (ok) rc = png_encode_device(st, &ws, w, h, d, d_src, d_out, cap, &n);
+        if (rc == 1) {
+            (void)hipFree(d_out);
+            d_out = nullptr;
+            cap = n;
+            ok = hipMalloc(&d_out, cap) == hipSuccess;
+            if (ok) rc = png_encode_device(st, &ws, w, h, d, d_src, d_out, cap, &n);
+        }
+        ok = ok && rc == 0;
+        if (ok) {
+            out.resize(n);
+            ok = hipMemcpy(out.data(), d_out, n, hipMemcpyDeviceToHost) == hipSuccess;
+        }
+    }
+    if (d_src) (void)hipFree(d_src);
+    if (d_out) (void)hipFree(d_out);
+    return ok;
+}
+
+}  // namespace icx

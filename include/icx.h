@@ -149,6 +149,27 @@ int icx_jpeg_encode_device(icx_encoder* enc, int quality, int subsampling, int w
  * (DCT+quantise), count, scan, emit, stuff. Returns the number of stages filled (<= cap). */
 int icx_encoder_stage_times(icx_encoder* enc, const char** names, float* ms, int cap);
 
+/* ---- PNG encode (png_encoder::saveToFile, png_encoder.h:7 / png_encoder.cpp:4474-4486) ------
+ * d = 3 (RGB8) or 4 (RGBA8) like saveToFile. lodepng's automatic colour type (palette / grey /
+ * grey+alpha / RGB / RGBA, tRNS key) and its MINSUM filter bytes are reproduced exactly; the IDAT
+ * is our GPU deflate (valid zlib, inflates to lodepng's filtered stream; bytes differ). */
+/* Host image -> PNG bytes through `func` (<= 1023-byte chunks); returns 1 on success, 0 on error. */
+int icx_png_encode_with_func(icx_ctx* ctx, icx_write_func* func, void* context, const unsigned char* pixels,
+                             int width, int height, int d);
+/* png_encoder::saveToFile: returns ICX_OK or an error code (the reference returns nothing). */
+int icx_png_save_to_file(icx_ctx* ctx, const char* path, const unsigned char* pixels, int width, int height,
+                         int d);
+
+typedef struct icx_png_encoder icx_png_encoder;
+icx_png_encoder* icx_png_encoder_create(icx_ctx* ctx);
+void icx_png_encoder_destroy(icx_png_encoder* enc);
+/* Device image d_src (width*height*d bytes) -> whole PNG file at d_out; synchronous on
+ * hip_stream (NULL = the context's stream). Returns ICX_OK, ICX_OUT_OF_MEM when out_cap <
+ * *out_size (nothing written), ICX_UNSUPPORTED for bad arguments, ICX_INTERNAL_ERR on a HIP
+ * failure. */
+int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, const uint8_t* d_src,
+                          uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

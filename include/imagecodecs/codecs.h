@@ -7,6 +7,9 @@
  *                  decode on the GPU (readJpg, codecs.cpp:821-849 -> icx_jpeg_decode).
  *   write(path) -- ".jpg"/".jpeg" encode with tiny_jpeg quality 3 semantics (writeJpg,
  *                  codecs.cpp:851-854 -> icx_tje_encode_to_file, byte-identical stream).
+ *               ".png" encodes with png_encoder::saveToFile semantics (writePng,
+ *               codecs.cpp:1022-1025 -> icx_png_save_to_file: lodepng's colour type and
+ *               filter bytes, GPU deflate).
  *   pixels_ is new[]-owned and delete[]-d by ~Image (codecs.h:102); load() adopts a buffer.
  * Every other extension is outside this path: it throws std::invalid_argument exactly like the
  * reference's unknown-extension branch (codecs.cpp:80-83), so a build that needs those codecs
@@ -111,6 +114,13 @@ class Image {
         last_write_ok_ = icx_tje_encode_to_file(P.get(), path.c_str(), w_, h_, d_, pixels_) == 1;
     }
 
+    void writePng(const std::string& path) {
+        auto& P = detail::icx_process();
+        std::lock_guard<std::mutex> lock(P.mu);
+        // saveToFile returns nothing (png_encoder.h:7); the result stays queryable
+        last_write_ok_ = icx_png_save_to_file(P.get(), path.c_str(), pixels_, w_, h_, d_) == ICX_OK;
+    }
+
 public:
     Image() = default;
     Image(const Image&) = delete;  // the reference's implicit copy double-frees pixels_
@@ -143,6 +153,7 @@ public:
     void write(const std::string& filepath) {
         const std::string ext = detail::lower_ext(filepath);
         if (ext == ".jpg" || ext == ".jpeg") writeJpg(filepath);
+        else if (ext == ".png") writePng(filepath);
         else throw std::invalid_argument("Cannot parse filetype");
     }
 };

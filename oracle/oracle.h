@@ -47,6 +47,22 @@ int or_tje_encode(int quality, int w, int h, int comps, const uint8_t* src,
 int or_jpeg_encode(int quality, int subsampling, int w, int h, int comps, const uint8_t* src,
                    uint8_t** out, int64_t* outlen);
 
+/* PNG path (png_oracle.c): lodepng's colour-mode choice and filtered IDAT stream for
+ * png_encoder::saveToFile input (d = 3 RGB8, d = 4 RGBA8). colortype/bitdepth as in IHDR. */
+typedef struct {
+    int colortype, bitdepth;
+    int npal;
+    uint8_t pal[256 * 4];
+    int key_defined, key_r, key_g, key_b;
+} or_png_mode;
+int or_png_choose(const uint8_t* px, int w, int h, int d, or_png_mode* m);
+int64_t or_png_linebytes(int w, const or_png_mode* m);
+int64_t or_png_filtered_size(int w, int h, const or_png_mode* m);
+/* Filtered stream h*(1+linebytes) into out; 1 on success. */
+int or_png_filter(const uint8_t* px, int w, int h, int d, const or_png_mode* m, uint8_t* out);
+/* Whole PNG with the IDAT deflated by the system zlib at `zlevel` (size proxy, CPU baseline). */
+int or_png_encode(const uint8_t* px, int w, int h, int d, int zlevel, uint8_t** out, int64_t* size);
+
 void or_free(void* p);
 
 #ifdef __cplusplus

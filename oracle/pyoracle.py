@@ -42,6 +42,15 @@ def lib():
         L.or_jpeg_encode.restype = C.c_int
         L.or_jpeg_encode.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.or_png_choose.restype = C.c_int
+        L.or_png_choose.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.or_png_filtered_size.restype = C.c_int64
+        L.or_png_filtered_size.argtypes = [C.c_int, C.c_int, C.c_void_p]
+        L.or_png_filter.restype = C.c_int
+        L.or_png_filter.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.or_png_encode.restype = C.c_int
+        L.or_png_encode.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p),
+                                    C.POINTER(C.c_int64)]
         L.or_free.argtypes = [C.c_void_p]
         _LIB = L
     return _LIB
@@ -90,6 +99,48 @@ def jpeg_encode(quality: int, subsampling: int, w: int, h: int, comps: int, rgb:
         return None
     res = C.string_at(out.value, n.value)
     L.or_free(out)
+    return res
+
+
+class PngMode(C.Structure):
+    _fields_ = [("colortype", C.c_int), ("bitdepth", C.c_int), ("npal", C.c_int), ("pal", C.c_uint8 * 1024),
+                ("key_defined", C.c_int), ("key_r", C.c_int), ("key_g", C.c_int), ("key_b", C.c_int)]
+
+    def as_dict(self):
+        return {"colortype": self.colortype, "bitdepth": self.bitdepth, "npal": self.npal,
+                "palette": bytes(self.pal[: 4 * self.npal]), "key": (self.key_r, self.key_g, self.key_b)
+                if self.key_defined else None}
+
+
+def png_choose(px: bytes, w: int, h: int, d: int) -> PngMode:
+    """lodepng auto_convert decision for saveToFile input (d=3 RGB8, d=4 RGBA8)."""
+    m = PngMode()
+    src = C.create_string_buffer(bytes(px), max(1, len(px)))
+    if not lib().or_png_choose(src, w, h, d, C.byref(m)):
+        raise ValueError("or_png_choose failed")
+    return m
+
+
+def png_filtered(px: bytes, w: int, h: int, d: int, mode: PngMode = None) -> bytes:
+    """The filtered (pre-deflate) IDAT stream lodepng produces for this image."""
+    m = mode or png_choose(px, w, h, d)
+    n = lib().or_png_filtered_size(w, h, C.byref(m))
+    out = C.create_string_buffer(max(1, n))
+    src = C.create_string_buffer(bytes(px), max(1, len(px)))
+    if not lib().or_png_filter(src, w, h, d, C.byref(m), out):
+        raise ValueError("or_png_filter failed")
+    return out.raw[:n]
+
+
+def png_encode_zlib(px: bytes, w: int, h: int, d: int, level: int = 6):
+    """Whole PNG: restated colour choice + filters, IDAT by the system zlib (size proxy)."""
+    src = C.create_string_buffer(bytes(px), max(1, len(px)))
+    out = C.c_void_p()
+    n = C.c_int64()
+    if not lib().or_png_encode(src, w, h, d, level, C.byref(out), C.byref(n)):
+        return None
+    res = C.string_at(out.value, n.value)
+    lib().or_free(out)
     return res
 
 

@@ -1,0 +1,123 @@
+"""GPU PNG encoder parity: through the C ABI, lodepng's colour
+type / palette / tRNS and its filter bytes must equal the oracle exactly, and the IDAT must
+inflate (Python zlib) to the oracle's filtered stream; the whole file must decode back to the
+input pixels. Compressed size is reported against the system zlib (level 6) on the identical
+filtered stream -- lodepng's own deflate is unbuildable here (png.h absent), see DESIGN.md."""
+import zlib
+
+import numpy as np
+import pytest
+
+import imagecodecs_amd as icx
+from oracle import pyoracle as O
+import pngutil as P
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = icx.Context(0)
+    yield c
+    c.close()
+
+
+def check(ctx, px, decode=True):
+    h, w, d = px.shape
+    png = ctx.png_encode(w, h, d, px.tobytes())
+    assert png is not None
+    I = P.info(png)  # also verifies every chunk CRC
+    m = O.png_choose(px.tobytes(), w, h, d)
+    assert (I["colortype"], I["bitdepth"]) == (m.colortype, m.bitdepth)
+    if m.colortype == 3:
+        pal = np.frombuffer(bytes(m.pal[: 4 * m.npal]), np.uint8).reshape(-1, 4)
+        assert I["plte"] == pal[:, :3].tobytes()
+        a = pal[:, 3]
+        nz = np.nonzero(a != 255)[0]
+        assert I["trns"] == (a[: nz[-1] + 1].tobytes() if len(nz) else None)
+    elif m.key_defined:
+        k = [m.key_r, m.key_g, m.key_b] if m.colortype == 2 else [m.key_r]
+        assert I["trns"] == b"".join(int(v).to_bytes(2, "big") for v in k)
+    else:
+        assert I["trns"] is None
+    assert zlib.decompress(I["idat"]) == O.png_filtered(px.tobytes(), w, h, d, m)
+    if decode:
+        np.testing.assert_array_equal(P.decode_rgba(png), P.to_rgba(px))
+    return png
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (3, 2), (37, 23), (257, 5), (64, 64)])
+@pytest.mark.parametrize("kind", ["rgba", "opaque", "rgb3"])
+def test_png_synthetic(ctx, w, h, kind):
+    px = P.synth_rgba(w * 7 + h, w, h, opaque=kind != "rgba")
+    if kind == "rgb3":
+        px = np.ascontiguousarray(px[..., :3])
+    check(ctx, px)
+
+
+def _palette_img(rng, n, w, h, alpha=False):
+    pal = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    if not alpha:
+        pal[:, 3] = 255
+    return pal[rng.integers(0, n, (h, w))]
+
+
+@pytest.mark.parametrize("case", ["grey8", "grey1", "grey2", "grey4", "pal2", "pal4", "pal16", "pal60", "pal256",
+                                  "pal_alpha", "key_rgb", "key_grey", "grey_alpha", "white_only"])
+def test_png_colour_modes(ctx, case):
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    w, h = 45, 31
+    if case.startswith("grey") and case != "grey_alpha":
+        levels = {"grey8": 256, "grey1": 2, "grey2": 4, "grey4": 16}[case]
+        g = (rng.integers(0, levels, (h, w, 1)) * (255 // (levels - 1))).astype(np.uint8)
+        px = np.repeat(g, 3, axis=2)
+    elif case.startswith("pal") and case != "pal_alpha":
+        px = _palette_img(rng, int(case[3:]), w, h)
+    elif case == "pal_alpha":
+        px = _palette_img(rng, 40, w, h, alpha=True)
+    elif case == "key_rgb":
+        px = P.synth_rgba(5, w, h, opaque=True)
+        px[..., :3][(px[..., :3] == (9, 9, 9)).all(axis=2)] = 10
+        px[3:6, 4:9] = (9, 9, 9, 0)
+    elif case == "key_grey":
+        g = rng.integers(0, 256, (h, w, 1)).astype(np.uint8)
+        g[g == 77] = 78
+        px = np.concatenate([np.repeat(g, 3, axis=2), np.full((h, w, 1), 255, np.uint8)], axis=2)
+        px[2:4, 2:4] = (77, 77, 77, 0)
+    elif case == "grey_alpha":
+        g = rng.integers(0, 256, (h, w, 1)).astype(np.uint8)
+        px = np.concatenate([np.repeat(g, 3, axis=2), rng.integers(0, 256, (h, w, 1)).astype(np.uint8)], axis=2)
+    else:
+        px = np.full((h, w, 4), 255, np.uint8)
+    check(ctx, px)
+
+
+def test_png_large_rgba_and_size(ctx):
+    """A 2048^2 alpha-gradient image: exact filtered stream, size within 5% of zlib -6."""
+    w = h = 2048
+    px = P.synth_rgba(99, w, h)
+    png = check(ctx, px, decode=False)
+    ref = O.png_encode_zlib(px.tobytes(), w, h, 4, 6)
+    assert len(png) <= 1.05 * len(ref), (len(png), len(ref))
+
+
+def test_png_device_api(ctx):
+    import torch
+    w, h = 640, 480
+    px = P.synth_rgba(1, w, h)
+    enc = icx.PngEncoder(ctx)
+    d_src = torch.from_numpy(px).cuda()
+    d_out = torch.empty(w * h * 4 * 2, dtype=torch.uint8, device="cuda")
+    rc, n = enc.encode_device(w, h, 4, d_src.data_ptr(), d_out.data_ptr(), 100)
+    assert rc == icx.OUT_OF_MEM and n > 100
+    rc, n2 = enc.encode_device(w, h, 4, d_src.data_ptr(), d_out.data_ptr(), d_out.numel())
+    assert rc == icx.OK and n2 == n
+    png = d_out[:n].cpu().numpy().tobytes()
+    assert png == ctx.png_encode(w, h, 4, px.tobytes())  # deterministic
+    np.testing.assert_array_equal(P.decode_rgba(png), px)
+    enc.close()
+
+
+def test_png_rejects(ctx):
+    assert ctx.png_encode(4, 4, 2, bytes(32)) is None
+    assert ctx.png_encode(0, 4, 4, b"") is None
