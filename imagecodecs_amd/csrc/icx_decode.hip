@@ -97,7 +97,7 @@ __global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uin
                 if (nb) { v = extend((int32_t)rb_peek(b, nb), nb); rb_drop(b, nb); }
                 k += (sym >> 4) + 1;
                 if (k > 63) { err = kSyntaxError; break; }
-                row[nat_of_zig(k)] = (int16_t)v;
+                row[k] = (int16_t)v;  // blocks are kept in zig-zag order (k_idct reorders)
             } while (k < 63);
             if (b.err) err = b.err;
         }
@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
     __shared__ IdctGeo geo[kSpecMaxBpm];  // per block-in-MCU
     __shared__ int32_t rows[32][8][9];   // row-pass output, padded
     __shared__ uint8_t pix[32][8][8];
+    __shared__ int4 zzb[32][8];          // the blocks as stored: zig-zag order
     const int t = threadIdx.x;
     if (t < 3 * 64) {
         const int ci = t >> 6, n = t & 63;
@@ -161,6 +162,11 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
     __syncthreads();
     const int64_t nblocks = (int64_t)d.mbw * d.mbh * bpm;
     const int lb = t >> 3, r = t & 7;
+    // natural row r = zig-zag positions kZigOfNat[8r .. 8r+7] of the staged block (byte offsets)
+    uint32_t zo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zo[j] = 2u * kZigOfNat[r * 8 + j];
+    const uint8_t* zrow = reinterpret_cast<const uint8_t*>(&zzb[lb][0]);
     const int16_t* A = ac + (int64_t)img * coef_cap * 64;
     const int32_t* D = dcv + (int64_t)img * coef_cap;
     uint8_t* P = planes + (int64_t)img * plane_cap;
@@ -192,9 +198,12 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
             const Comp& c = d.c[ci];
             g = IdctGeo{comp_plane_off(d, ci), c.stride, sbx * 8, sby * 8, c.hs * 8, c.vs * 8, ci};
         }
+        if (live) zzb[lb][r] = *reinterpret_cast<const int4*>(A + n * 64 + r * 8);  // a block's 8 lanes share a wave
+        __builtin_amdgcn_wave_barrier();
         if (live) {
             int16_t s[8];
-            __builtin_memcpy(s, A + n * 64 + r * 8, sizeof s);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] = *reinterpret_cast<const int16_t*>(zrow + zo[j]);
             int32_t v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = m24(s[j], qn[g.ci][r * 8 + j]);  // int16 x 8-bit: exact

@@ -58,7 +58,7 @@ struct GroupWs {
     int64_t plane_cap = 0;   // bytes per slot (all components' IDCT planes)
     int64_t tmp_cap = 0;     // bytes per ping-pong buffer per component per slot
     Desc* desc = nullptr;    // [slots]
-    int16_t* ac = nullptr;   // [slots][coef_cap][64] quantized coefficients, natural order
+    int16_t* ac = nullptr;   // [slots][coef_cap][64] quantized coefficients, zig-zag order
     int32_t* dc = nullptr;   // [slots][coef_cap] int32 DC of blocks whose cell holds kDcEscape
     uint8_t* planes = nullptr;  // [slots][plane_cap]
     uint8_t* tmp = nullptr;     // [slots][3 comps][2 buffers][tmp_cap]

@@ -59,8 +59,9 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ de
             s.nrepair = 0;
             s.nrst = 0;
             const int64_t scan_len = d.size - d.scan_off;
+            // (U also holds the reader padding: u_pad_end(ulen) <= ulen + 32, ulen <= scan_len)
             const bool ok = d.status == kPending && d.nc >= 1 && d.bpm <= kSpecMaxBpm && scan_len > 0 &&
-                            scan_len <= ucap;
+                            scan_len + 64 <= ucap;
             if (ok) {
                 s.mode = d.restart == 0 ? 1 : 3;
                 s.scan_len = scan_len;
@@ -212,7 +213,8 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
 
 // Per image: exclusive prefix of kept bytes over tiles, data length, error position.
 __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ spec, TileRec* __restrict__ tiles,
-                                                   int32_t* __restrict__ tile_obase, int32_t* __restrict__ tile_rbase) {
+                                                   int32_t* __restrict__ tile_obase, int32_t* __restrict__ tile_rbase,
+                                                   uint8_t* __restrict__ U, int64_t ucap) {
     __shared__ int sh[256];
     __shared__ int s_first_end;
     const int i = blockIdx.x;
@@ -244,6 +246,10 @@ __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ 
         carry += s_sum;
         rcarry += s_rsum;
         __syncthreads();
+    }
+    {  // 0xFF padding behind the data for the lane readers (icx_spec_core.h, u_pad_end)
+        uint8_t* u = U + (int64_t)i * ucap;
+        for (int64_t p = carry + threadIdx.x; p < u_pad_end(carry); p += blockDim.x) u[p] = 0xFF;
     }
     if (threadIdx.x == 0) {
         s.ulen = carry;
@@ -546,6 +552,11 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
             bi = le.G;
             act = bi < total_blocks;
         }
+        // The predictors come from a load issued before the loop: without this the compiler
+        // waits for them at their first use inside the loop with vmcnt(0) -- i.e. for every
+        // coefficient store and prefetch in flight -- on every DC code.
+        asm volatile("" : "+v"(pred[0]), "+v"(pred[1]), "+v"(pred[2]));
+        r.phase();  // the prelude above ran a lane-dependent number of codes
         // Wave-uniform loop: one code per active lane per iteration, then the wave flushes the
         // blocks its lanes completed together -- eight 128-byte blocks per round, each lane
         // moving one 16-byte chunk LDS -> HBM and zeroing it (coalesced full-line stores,
@@ -575,7 +586,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
                         sv[slot_elem(threadIdx.x, 0)] = cell;
                         if (cell == kDcEscape) D[bi] = pred[ci];
                     } else if (coef > 0) {
-                        sv[slot_elem(threadIdx.x, T.nat_of_zig[coef])] = (int16_t)val;
+                        sv[slot_elem(threadIdx.x, coef)] = (int16_t)val;  // zig-zag order (k_idct reorders)
                     }
                     if (z == 0) {
                         done = true;
@@ -654,7 +665,8 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
                        ws.totals, ws.ucap);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
-    hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase);
+    hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,
+                       ws.U, ws.ucap);
     hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.ucap, ws.rst, ws.rst_cap);
     E(kStUnstuff);

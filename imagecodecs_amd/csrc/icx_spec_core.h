@@ -153,84 +153,111 @@ struct Sel {
     int bpm;
     uint32_t comps;
     uint64_t tabs;
+    uint32_t b10[4];  // per table: bound[kFastBits], the first 16-bit window of a > 10-bit code
     ICX_HD int comp(int b) const { return (int)((comps >> (2 * b)) & 3u); }
     ICX_HD int tab(int b, bool dc) const { return (int)((tabs >> (4 * b + (dc ? 0 : 2))) & 3u); }
+    ICX_HD uint32_t bound10(int t) const { return (t & 2) ? ((t & 1) ? b10[3] : b10[2]) : ((t & 1) ? b10[1] : b10[0]); }
 };
 ICX_HD Sel make_sel(const Desc& d) {
-    Sel s{d.bpm, 0u, 0ull};
+    Sel s{d.bpm, 0u, 0ull, {0u, 0u, 0u, 0u}};
     for (int b = 0; b < d.bpm && b < kSpecMaxBpm; ++b) {
         int sbx, sby;
         const int ci = mcu_block_comp(d, b, sbx, sby);
         s.comps |= (uint32_t)ci << (2 * b);
         s.tabs |= (uint64_t)((d.c[ci].dc_tab & 3) | ((d.c[ci].ac_tab & 3) << 2)) << (4 * b);
     }
+    for (int t = 0; t < 4; ++t) s.b10[t] = d.huff[t].bound[kFastBits];
     return s;
 }
 
-// MSB-first reader over U; bytes at or past ulen read as 0xFF (jpeg_dec.h:451-455).
-// Latency hiding: U is fetched in 16-byte chunks with one chunk always in flight -- `A` is
-// being drained 32 bits at a time into the 64-bit window `buf`; `B` (the next chunk) was
-// requested when A was refilled and stays untouched in registers (no byte swap, no tail
-// check) until it becomes A, ~24 codes later, so its load latency is hidden. Loads are
-// 16-byte aligned and unconditional: the buffer behind U has >= 16 bytes of slack, and a
-// chunk at or past ulen is loaded from chunk 0 and replaced by 0xFF when consumed.
+// U as the lane readers see it: the unstuffed data, then 0xFF from ulen up to (ulen/16 + 2)*16
+// (written by k_ustf_scan), so chunk u_pad_chunk(ulen) and every chunk before it are readable
+// and every byte at or past ulen reads 0xFF (jpeg_dec.h:451-455). Chunks past that index are
+// read as that all-0xFF chunk.
+ICX_HD uint32_t u_pad_chunk(int64_t ulen) { return (uint32_t)(ulen >> 4) + 1u; }
+ICX_HD int64_t u_pad_end(int64_t ulen) { return ((ulen >> 4) + 2) << 4; }
+
+// Wave-wide helpers that are the identity on the host (the CPU emulator runs one lane).
+ICX_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __any(p);
+#else
+    return p;
+#endif
+}
+
+// MSB-first reader over U (padded as above).
+// Latency hiding at the WAVE level: a wave's vmcnt counts every lane's loads in issue order, so a
+// lane cannot wait for "its own" older load while a neighbour's newer one is in flight. Loads
+// are therefore issued only at slots -- every 4th refill, a point all lanes of a wave reach
+// together when they call decode_unit in lockstep -- and their data is first used at the NEXT
+// slot, 4 codes later. Between slots a lane draws on registers only: the 64-bit window `buf`,
+// chunk A (128 bits, drained 32 bits per refill) and chunk B (expanded at the slot, taken when A
+// runs out). A refill takes at most one word and a code at most 31 bits, so 4 refills use at
+// most 4 words: with B full after every slot, A never runs dry before the next slot.
 struct Reader {
     const uint8_t* u;
-    int64_t ulen, ucap;
+    uint32_t cmax;     // chunks past cmax read as chunk cmax (all 0xFF)
+    uint32_t next;     // chunk to load at the next slot that finds B taken
     uint64_t buf;      // left-aligned window, nb valid bits
     int nb;
     int na;            // 32-bit words left in A
     uint64_t a0, a1;   // chunk A as a 128-bit left-aligned shift register
-    uint4 braw;        // chunk B as loaded (prefetched)
-    int64_t next;      // index of the chunk B holds + 1
+    uint64_t b0, b1;   // chunk B, byte-swapped (valid when hb)
+    uint4 lraw;        // chunk L, the load in flight (chunk next - 1)
+    bool hb;
+    uint32_t tick;     // refills since the last slot phase reset
     int64_t base;      // bit position at init
     uint32_t used;     // bits consumed since init (32-bit loop tests in the lane loops)
-    ICX_HD uint4 load(int64_t c) const {
-        const int64_t o = c * 16;
-        return *reinterpret_cast<const uint4*>(u + (o < ulen ? o : 0));
+    ICX_HD uint4 load(uint32_t c) const {
+        return *reinterpret_cast<const uint4*>(u + (size_t)(c < cmax ? c : cmax) * 16);
     }
-    // chunk c's raw bytes -> big-endian 128-bit (h, l), bytes at or past ulen forced to 0xFF
-    ICX_HD void expand(int64_t c, const uint4& v, uint64_t& h, uint64_t& l) const {
+    ICX_HD static void expand(const uint4& v, uint64_t& h, uint64_t& l) {
         h = ((uint64_t)__builtin_bswap32(v.x) << 32) | __builtin_bswap32(v.y);
         l = ((uint64_t)__builtin_bswap32(v.z) << 32) | __builtin_bswap32(v.w);
-        const int64_t valid = ulen - c * 16;
-        if (valid < 16) {
-            const int kb = valid <= 0 ? 0 : (int)valid * 8;  // bits kept, 0..120
-            h = kb >= 64 ? h : (kb == 0 ? ~0ull : h | (~0ull >> kb));
-            l = kb <= 64 ? ~0ull : l | (~0ull >> (kb - 64));
+    }
+    ICX_HD void slot() {
+        if (!hb) {  // B was taken since the last slot: L (issued >= 4 refills ago) becomes B
+            expand(lraw, b0, b1);
+            hb = true;
+            lraw = load(next);
+            next = next < cmax ? next + 1 : cmax;
         }
     }
+    // Branch-free except for the slot: one word from A into buf when buf runs low, B into A when
+    // A runs out.
     ICX_HD void refill() {
-        if (nb <= 32) {
-            buf |= (a0 >> 32) << (32 - nb);
-            nb += 32;
-            a0 = (a0 << 32) | (a1 >> 32);
-            a1 <<= 32;
-            if (--na == 0) {
-                expand(next - 1, braw, a0, a1);
-                na = 4;
-#if defined(__HIP_DEVICE_COMPILE__)
-                // B's old registers must be dead before its next load is issued: if the load
-                // is hoisted above the swap, B lands in other registers and the loop-carried
-                // copy back waits for the load (s_waitcnt vmcnt(0) on every code).
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                braw = load(next++);
-            }
-        }
+        if ((tick++ & 3u) == 0) slot();
+        const bool need = nb <= 32;
+        const uint64_t w = (a0 >> 32) << ((32 - nb) & 63);
+        buf |= need ? w : 0ull;
+        nb += need ? 32 : 0;
+        na -= need ? 1 : 0;
+        const bool take = na == 0;
+        const uint64_t s0 = (a0 << 32) | (a1 >> 32), s1 = a1 << 32;
+        a0 = take ? b0 : (need ? s0 : a0);
+        a1 = take ? b1 : (need ? s1 : a1);
+        na = take ? 4 : na;
+        hb = hb && !take;
     }
-    ICX_HD void init(const uint8_t* u_, int64_t ulen_, int64_t bitpos) {
+    // Call where every lane of the wave is about to decode in lockstep: the next refill is a slot.
+    ICX_HD void phase() { tick = 0; }
+    ICX_HD void init(const uint8_t* u_, int64_t ulen, int64_t bitpos) {
         u = u_;
-        ulen = ulen_;
+        cmax = u_pad_chunk(ulen);
         base = bitpos;
         used = 0;
-        const int64_t c = bitpos >> 7;
-        expand(c, load(c), a0, a1);
-        braw = load(c + 1);
-        next = c + 2;
+        const int64_t c64 = bitpos >> 7;
+        const uint32_t c = c64 < (int64_t)cmax ? (uint32_t)c64 : cmax;
+        expand(load(c), a0, a1);
+        expand(load(c + 1), b0, b1);
+        hb = true;
+        lraw = load(c + 2);
+        next = c + 3 < cmax ? c + 3 : cmax;
         na = 4;
         buf = 0;
         nb = 0;
+        tick = 1;  // no slot during init
         int skip = (int)(bitpos & 127);
         refill();
         refill();
@@ -243,6 +270,7 @@ struct Reader {
         buf <<= skip;
         nb -= skip;
         refill();
+        tick = 0;
     }
     ICX_HD int64_t pos() const { return base + used; }
     ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
@@ -267,17 +295,22 @@ ICX_HD int decode_unit(Reader& r, const LdsTables& T, const Sel& S, int& b, int&
     // the DC / EOB / ZRL / error / end-of-block cases are selects, not branches (the lanes of a
     // wave take different ones on almost every code). Only codes longer than kFastBits branch.
     const bool dc = z == 0;
-    const Huff& H = T.huff[S.tab(b, dc)];
+    const int tb = S.tab(b, dc);
+    const Huff& H = T.huff[tb];
     r.refill();
     const uint32_t win = r.peek16();
     uint32_t e = H.fast[win >> (16 - kFastBits)];
-    if (e & kSubFlag) e = H.sub[(e & ~kSubFlag) | (win & ((1u << (16 - kFastBits)) - 1))];  // > 10-bit codes
-    int len, sym;
-    if (e) {
-        len = (int)(e >> 8);
-        sym = (int)(e & 0xFF);
-    } else {
-        len = huff_search(H, win, kFastBits + 1, sym);  // invalid codes, oversized tables
+    // > 10-bit codes: the subtable entry sits at win - bound[10] (huff_fill_fast). Behind a
+    // wave-uniform branch whose body is a select, so a wave where no lane needs it skips it.
+    if (wave_any(e & kSubFlag)) {
+        const uint32_t q = win - S.bound10(tb);
+        constexpr uint32_t kSubN = kSubTabs << (16 - kFastBits);
+        const uint32_t es = H.sub[q < kSubN ? q : kSubN - 1];
+        e = (e & kSubFlag) ? es : e;
+    }
+    int len = (int)(e >> 8), sym = (int)(e & 0xFF);
+    if (wave_any(e == 0)) {  // invalid codes, oversized tables (a wave-uniform branch: rare)
+        if (e == 0) len = huff_search(H, win, kFastBits + 1, sym);
     }
     const bool inv = len == 0;               // no such code: consume one bit (jpeg_dec.h:646)
     const int nbx = inv ? 0 : (sym & 15);

@@ -64,7 +64,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
         if (fe < 0 || t <= fe) ulen += tiles[t].kept;
     }
     const int64_t errpos = (fe >= 0 && tiles[fe].end_err) ? ulen : INT64_MAX;
-    std::vector<uint8_t> U(ulen + 64, 0);  // Reader slack: whole 16-byte chunks
+    std::vector<uint8_t> U(ulen + 64, 0xFF);  // reader padding (icx_spec_core.h u_pad_end)
     for (int64_t t = 0; t < ntiles; ++t) {
         if (obase[t] >= ulen) continue;
         const int64_t tend = tiles[t].end_at;
@@ -182,7 +182,7 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
     if (parse_headers(file, size, d) != kPending || d.restart || d.bpm > kSpecMaxBpm) return -1;
     const uint8_t* R = file + d.scan_off;
     const int64_t L = d.size - d.scan_off;
-    std::vector<uint8_t> U(L + 64);
+    std::vector<uint8_t> U(L + 64, 0xFF);  // reader padding (icx_spec_core.h u_pad_end)
     int64_t e; int er; int32_t gu = 0;
     int64_t ulen = 0;
     for (int64_t a = 0; a < L; a += kChunk) {
