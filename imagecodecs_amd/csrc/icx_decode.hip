@@ -592,12 +592,12 @@ struct StreamOut {
     __device__ __forceinline__ void put(int y, int x0, const uint8_t (&px)[12], int nb) const {
         uint8_t* dst = o + ((int64_t)y * W + x0) * 3;
         if (vec && nb == 12) {
-            uint32_t w[3];
-            __builtin_memcpy(w, px, 12);
-            uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-            __builtin_nontemporal_store(w[0], d32);
-            __builtin_nontemporal_store(w[1], d32 + 1);
-            __builtin_nontemporal_store(w[2], d32 + 2);
+            // one 12-byte store per lane (global_store_dwordx3): a wave writes 768 contiguous bytes
+            // per instruction instead of three strided dword passes over them
+            typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+            u32x3 w;
+            __builtin_memcpy(&w, px, 12);
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x3*>(dst));
         } else {
 #pragma unroll
             for (int i = 0; i < 12; ++i)
@@ -752,23 +752,18 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
     }
 }
 
+// One instantiation per layout (K as in stream_kind), so each gets its own register allocation;
+// every instantiation is launched and skips the images of other layouts.
+template <int K>
 __global__ __launch_bounds__(256) void k_convert_stream(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
                                                         int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk) return;
-    const int k = stream_kind(d);
-    if (k < 0) return;
+    if (d.status != kOk || stream_kind(d) != K) return;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     uint8_t* o = out + (int64_t)img * out_stride;
     const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
-    switch (k) {
-        case 0: stream_image<0>(d, pslot, so); break;
-        case 1: stream_image<1>(d, pslot, so); break;
-        case 2: stream_image<2>(d, pslot, so); break;
-        case 3: stream_image<3>(d, pslot, so); break;
-        default: stream_image<4>(d, pslot, so); break;
-    }
+    stream_image<K>(d, pslot, so);
 }
 
 // --------------------------------------------------------------------------- finalize
@@ -819,7 +814,15 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 16384 / n));
     const int sxg = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)(ws.max_w + 255) / 256) *
                                                                  ((ws.max_h + kSH - 1) / kSH) / 4 + 1, 16384 / n));
-    hipLaunchKernelGGL(k_convert_stream, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+    hipLaunchKernelGGL(k_convert_stream<3>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride);
+    hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride);
+    hipLaunchKernelGGL(k_convert_stream<1>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride);
+    hipLaunchKernelGGL(k_convert_stream<2>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride);
+    hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride);
     hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride);
