@@ -46,6 +46,10 @@ WORKLOADS = {
                   desc="C3 shard with restart markers every MCU row (DRI 256): camera-style streams"),
     "c4": dict(n=64, w=4096, h=4096, sampling="420", quality=90,
                desc="C4 encode: 64 x 4096x4096 RGB -> baseline JPEG 4:2:0 q90 per GPU (encode extension)"),
+    "hdr": dict(n=32, w=4096, h=4096, mode=0,
+                desc="HDR read: 32 x 4096x4096 Radiance RGBE, new-style RLE scanlines -> 4 floats/px (readHdr)"),
+    "hdrflat": dict(n=32, w=4096, h=4096, mode=1,
+                    desc="HDR read: 32 x 4096x4096 Radiance RGBE, flat pixel data -> 4 floats/px (readHdr)"),
 }
 
 # encode stage (icx_encoder_stage_times) -> kernels it times
@@ -231,6 +235,138 @@ def main_encode(args, wl, world, rank, local):
         dist.destroy_process_group()
 
 
+HDR_STAGE_KERNEL = {"parse": "k_hdr_parse", "locate": "k_hdr_scan+k_hdr_flatcheck+k_hdr_link+k_hdr_walk",
+                    "unpack": "k_hdr_unpack", "convert": "k_hdr_convert+k_hdr_finish"}
+
+
+def _oracle_hdr(data):
+    from oracle import pyoracle
+    t = time.perf_counter()
+    code, w, h, rows, arr = pyoracle.hdr_decode(data)
+    return time.perf_counter() - t, code, hashlib.sha256(arr.tobytes()).hexdigest(), w * h
+
+
+def main_hdr(args, wl, world, rank, local):
+    """Radiance .hdr read: one icx_hdr_batch_decode of the rank's images
+    per step, files resident in HBM, floats written to HBM."""
+    from imagecodecs_amd import shard
+    from tools import synthpy
+    n = args.images or wl["n"]
+    W, H = wl["w"], wl["h"]
+    first, _ = shard.shard_range(n * world, world, rank)
+    npool = min(args.pool, n, 4)
+    with ThreadPool(npool) as p:
+        files = p.map(lambda i: synthpy.hdr(synthpy.rgbe(1234 + first + i, W, H), wl["mode"]), range(npool))
+    cpu, cpu_hashes = None, {}
+    if rank == 0 and not args.no_cpu:
+        probe_t = _oracle_hdr(files[0])[0]
+        cores = args.cpu_cores
+        per_core = max(1, int(args.cpu_seconds / max(probe_t, 1e-3)))
+        sample = [files[i % npool] for i in range(per_core * cores)]
+        t0 = time.perf_counter()
+        with ThreadPool(cores) as p:
+            res = p.map(_oracle_hdr, sample)
+        wall = time.perf_counter() - t0
+        cpu = {"value": round(sum(r[3] for r in res) / 1e6 / wall, 2), "unit": "megapixels/s", "cores": cores,
+               "kind": "port", "sample": f"{len(sample)} decodes of the same files ({per_core} per core), oracle/ "
+                                         f"readHdr restatement, {wall:.1f} s wall"}
+        cpu_hashes = {i % npool: r[2] for i, r in enumerate(res)}
+
+    import torch
+    import imagecodecs_amd as icx
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    fl = [files[i % npool] for i in range(n)]
+    sizes = np.array([len(f) for f in fl], np.int64)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum((sizes[:-1] + 15) // 16 * 16)
+    blob = np.zeros(int(offs[-1] + sizes[-1]), np.uint8)
+    for i, f in enumerate(fl):
+        blob[offs[i]: offs[i] + sizes[i]] = np.frombuffer(f, np.uint8)
+    d_data = torch.from_numpy(blob).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_sz = torch.from_numpy(sizes).to(dev)
+    stride = W * H * 4
+    d_out = torch.empty(n * stride, dtype=torch.float32, device=dev)
+    d_st = torch.empty(n, dtype=torch.int32, device=dev)
+    d_dims = torch.empty((n, 3), dtype=torch.int32, device=dev)
+    ctx = icx.Context(local)
+    batch = icx.HdrBatch(ctx, n, W, H)
+    stream = torch.cuda.current_stream(dev)
+    stage_acc = {}
+
+    def step():
+        batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out.data_ptr(), stride,
+                            d_st.data_ptr(), d_dims.data_ptr(), stream.cuda_stream)
+        return d_st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        for k, v in batch.stage_times().items():  # synchronises on the step's stage events
+            stage_acc[k] = stage_acc.get(k, 0.0) + v
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    last = shard.gather_results(d_st, dist) if world > 1 else d_st
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    stages = {k: v / args.steps for k, v in stage_acc.items()}
+    ok_all = bool((last.cpu().numpy() == 0).all())
+    checked = mismatches = 0
+    for i, hx in cpu_hashes.items():
+        got = hashlib.sha256(d_out[i * stride: (i + 1) * stride].cpu().numpy().tobytes()).hexdigest()
+        checked += 1
+        mismatches += got != hx
+    ms_step = elapsed / args.steps * 1e3
+    value = world * n * W * H / 1e6 / (elapsed / args.steps)
+    file_b = float(sizes.sum())
+    alg_bytes = file_b + n * W * H * 16.0  # read the files, write 4 floats per pixel
+    dom = max((k for k in stages if stages[k] > 0), key=lambda k: stages[k], default=None)
+    roof = None
+    if dom:
+        # per-launch algorithmic bytes of the dominant stage over the whole batch (one launch per
+        # step): convert reads RGBE (planes or file) 4 B/px and writes 16 B/px; locate and unpack
+        # read the pixel data once (unpack also writes the 4 B/px RGBE planes)
+        per = {"convert": n * W * H * 20.0, "unpack": file_b + n * W * H * 4.0, "locate": file_b,
+               "parse": 0.0}.get(dom, alg_bytes)
+        achieved = per / (stages[dom] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": HDR_STAGE_KERNEL.get(dom, dom),
+                "launches_per_step": 1, "alg_bytes_per_launch": round(per), "avg_launch_ms": round(stages[dom], 4),
+                "stage_ms": {k: round(v, 3) for k, v in stages.items()},
+                "pipeline_frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    out = {
+        "metric": "megapixels/s Radiance HDR read, 4096x4096 RGBE -> float", "value": round(value, 2),
+        "unit": "megapixels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8->f32", "data": "synthetic (tools/synth.c synth_rgbe + hdr_encode, seeded)",
+        "config": {"workload": wl["desc"], "images_per_gpu": n, "pool": npool, "width": W, "height": H,
+                   "file_bytes_per_pixel": round(file_b / (n * W * H), 4),
+                   "parallelism": f"dp{world} (images sharded; RCCL gather of statuses)"},
+        "roofline": roof, "cpu_baseline": cpu,
+        "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,6 +388,8 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     if args.workload == "c4":
         return main_encode(args, wl, world, rank, local)
+    if args.workload.startswith("hdr"):
+        return main_hdr(args, wl, world, rank, local)
     n = args.images or wl["n"]
     W, H = wl["w"], wl["h"]
 

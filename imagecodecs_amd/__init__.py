@@ -9,7 +9,9 @@ callers (tests, bench): it binds the C ABI with ctypes and offers
   * ``Context.nj_decode`` & co.   -- njInit/njDecode/njGet* semantics (jpeg_dec.h:117-171)
   * ``Context.decode``            -- Image::readJpg's one-shot decode (codecs.cpp:821-849)
   * ``Batch``                     -- device-resident batched decode (the throughput path)
-  * ``Image``                     -- ImageCodecs::Image (codecs.h:16-103) for .jpg/.jpeg
+  * ``Context.hdr_decode``        -- Image::readHdr's Radiance RGBE -> float decode (codecs.cpp:706-777)
+  * ``HdrBatch``                  -- device-resident batched .hdr decode
+  * ``Image``                     -- ImageCodecs::Image (codecs.h:16-103) for .jpg/.jpeg/.png/.hdr
 
 There is deliberately no CPU fallback: if libicx.so is missing or no GPU is visible every
 entry point raises ``ICXError``.
@@ -22,8 +24,10 @@ import subprocess
 
 import numpy as np
 
-__all__ = ["ICXError", "Context", "Batch", "Image", "lib", "build", "LIB_PATH",
-           "OK", "NO_JPEG", "UNSUPPORTED", "OUT_OF_MEM", "INTERNAL_ERR", "SYNTAX_ERROR"]
+__all__ = ["ICXError", "Context", "Batch", "HdrBatch", "Image", "lib", "build", "LIB_PATH",
+           "OK", "NO_JPEG", "UNSUPPORTED", "OUT_OF_MEM", "INTERNAL_ERR", "SYNTAX_ERROR",
+           "HDR_OK", "HDR_NOT_RADIANCE", "HDR_BAD_HEADER", "HDR_MALFORMED", "HDR_TRUNCATED",
+           "HDR_TOO_LARGE", "HDR_INTERNAL_ERR", "hdr_probe"]
 
 OK, NO_JPEG, UNSUPPORTED, OUT_OF_MEM, INTERNAL_ERR, SYNTAX_ERROR = range(6)  # nj_result_t
 RESULT_NAMES = ["NJ_OK", "NJ_NO_JPEG", "NJ_UNSUPPORTED", "NJ_OUT_OF_MEM", "NJ_INTERNAL_ERR", "NJ_SYNTAX_ERROR"]
@@ -82,7 +86,17 @@ _SIGS = {
     "icx_png_encoder_destroy": (None, [_vp]),
     "icx_png_encode_device": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
     "icx_jpeg_encode_device": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
+    "icx_hdr_probe": (_i32, [_vp, _sz, C.POINTER(_i32), C.POINTER(_i32)]),
+    "icx_hdr_decode": (_i32, [_vp, _vp, _sz, C.POINTER(_vp), C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
+    "icx_hdr_batch_create": (_vp, [_vp, _i32, _i32, _i32]),
+    "icx_hdr_batch_destroy": (None, [_vp]),
+    "icx_hdr_batch_decode": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "icx_hdr_batch_stage_times": (_i32, [_vp, _vp, _vp, _i32]),
 }
+
+# icx_hdr_result (include/icx.h): Image::readHdr outcomes
+HDR_OK, HDR_NOT_RADIANCE, HDR_BAD_HEADER, HDR_MALFORMED, HDR_TRUNCATED, HDR_TOO_LARGE = range(6)
+HDR_INTERNAL_ERR = -1
 
 WRITE_FUNC = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
 
@@ -205,6 +219,22 @@ class Context:
         buf = C.create_string_buffer(bytes(src), max(1, len(src)))
         ok = lib().icx_tje_encode_with_func(self._p, sink, None, quality, width, height, comps, buf)
         return b"".join(chunks) if ok == 1 else None
+
+    def hdr_decode(self, data: bytes):
+        """Image::readHdr (codecs.cpp:706-777) on the GPU -> (code, w, h, rows, float32 (h, w, 4) or
+        None). Rows past `rows` (a truncated file) are zero; code is an icx_hdr_result."""
+        buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+        out = C.c_void_p()
+        w, h, rows = C.c_int(), C.c_int(), C.c_int()
+        code = lib().icx_hdr_decode(self._p, buf, len(data), C.byref(out), C.byref(w), C.byref(h), C.byref(rows))
+        if code == HDR_INTERNAL_ERR:
+            raise ICXError("icx_hdr_decode: " + _err(self._p))
+        arr = None
+        if out.value:
+            n = w.value * h.value * 4
+            arr = np.frombuffer(C.string_at(out.value, n * 4), np.float32).reshape(h.value, w.value, 4).copy()
+            lib().icx_free(out)
+        return code, w.value, h.value, rows.value, arr
 
     def png_encode(self, width: int, height: int, d: int, src: bytes):
         """PNG bytes of an RGB8 (d=3) / RGBA8 (d=4) image (png_encoder::saveToFile), or None."""
@@ -368,18 +398,61 @@ class Batch:
         return {names[i].decode(): float(ms[i]) for i in range(k)}
 
 
+def hdr_probe(data: bytes):
+    """Host header walk of readHdr (codecs.cpp:713-750) -> (code, width, height)."""
+    w, h = C.c_int(), C.c_int()
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    code = lib().icx_hdr_probe(buf, len(data), C.byref(w), C.byref(h))
+    return code, w.value, h.value
+
+
+class HdrBatch:
+    """Device-resident batched Radiance .hdr decode (icx_hdr_batch_*): image i is
+    d_data[d_offsets[i] .. + d_sizes[i]); 4 floats per pixel at d_out + i*out_stride floats."""
+
+    def __init__(self, ctx: Context, max_images: int, max_width: int, max_height: int):
+        self.ctx = ctx
+        self._p = lib().icx_hdr_batch_create(ctx.ptr, max_images, max_width, max_height)
+        if not self._p:
+            raise ICXError("icx_hdr_batch_create failed: " + _err(ctx.ptr))
+        self.max_images, self.max_width, self.max_height = max_images, max_width, max_height
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().icx_hdr_batch_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+    def decode_device(self, n, d_data, d_offsets, d_sizes, d_out, out_stride, d_status, d_dims, stream=0):
+        rc = lib().icx_hdr_batch_decode(self._p, n, d_data, d_offsets, d_sizes, d_out, out_stride,
+                                        d_status, d_dims, stream or None)
+        if rc != HDR_OK:
+            raise ICXError(f"icx_hdr_batch_decode -> {rc}: {_err(self.ctx.ptr)}")
+
+    def stage_times(self) -> dict:
+        names = (C.c_char_p * 8)()
+        ms = (C.c_float * 8)()
+        k = lib().icx_hdr_batch_stage_times(self._p, names, ms, 8)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+
 class Image:
     """ImageCodecs::Image (codecs.h:16-103) for the JPEG hot path.
 
     read()/write() dispatch on the lower-cased extension like Image::read/write
-    (codecs.cpp:53-122); only .jpg/.jpeg are on this path -- other extensions raise
-    ValueError (the reference's std::invalid_argument for unknown types)."""
+    (codecs.cpp:53-122): read .jpg/.jpeg (readJpg) and .hdr (readHdr: d = 4, type FLOAT, the
+    floats' bytes in pixels_), write .jpg/.jpeg and .png. Other extensions raise ValueError (the
+    reference's std::invalid_argument for unknown types)."""
 
+    UBYTE, USHORT, FLOAT = range(3)  # ImageCodecs::Type (codecs.h:14)
     _ctx = None
 
     def __init__(self):
         self.h_ = self.w_ = self.d_ = 0
         self.pixels_ = None
+        self.type_ = Image.UBYTE
 
     @classmethod
     def context(cls):
@@ -389,6 +462,9 @@ class Image:
 
     def read(self, filepath: str):
         ext = os.path.splitext(filepath)[1].lower()
+        if ext == ".hdr":
+            self._read_hdr(filepath)
+            return
         if ext not in (".jpg", ".jpeg"):
             raise ValueError("Cannot parse filetype")
         data = open(filepath, "rb").read()
@@ -397,6 +473,19 @@ class Image:
             raise RuntimeError("Error decoding the input file.\n")  # codecs.cpp:836
         self.w_, self.h_, self.d_ = w, h, n
         self.pixels_ = np.frombuffer(pix, np.uint8).copy()
+        self.type_ = Image.UBYTE
+
+    def _read_hdr(self, filepath: str):
+        """readHdr (codecs.cpp:706-777). A truncated file keeps its decoded rows (the rest are
+        zero; the reference leaves them uninitialised); header errors and run-length data the
+        reference cannot decode raise RuntimeError("Invalid file format") (:732, :748)."""
+        data = open(filepath, "rb").read()
+        code, w, h, rows, px = self.context().hdr_decode(data)
+        if code not in (HDR_OK, HDR_TRUNCATED):
+            raise RuntimeError("Invalid file format")
+        self.w_, self.h_, self.d_ = w, h, 4
+        self.pixels_ = px.reshape(-1).view(np.uint8).copy()
+        self.type_ = Image.FLOAT
 
     def write(self, filepath: str):
         ext = os.path.splitext(filepath)[1].lower()
@@ -413,6 +502,7 @@ class Image:
     def load(self, pixels, w: int, h: int, channels: int):
         self.pixels_ = np.ascontiguousarray(pixels, np.uint8).reshape(-1)
         self.w_, self.h_, self.d_ = w, h, channels
+        self.type_ = Image.UBYTE
 
     def rows(self):
         return self.h_
@@ -426,8 +516,14 @@ class Image:
     def empty(self):
         return self.h_ == 0 or self.w_ == 0 or self.d_ == 0 or self.pixels_ is None
 
+    def byteSize(self):
+        return 4 if self.type_ == Image.FLOAT else 2 if self.type_ == Image.USHORT else 1
+
+    def type(self):
+        return self.type_
+
     def totalBytes(self):
-        return self.w_ * self.h_ * self.d_
+        return self.w_ * self.h_ * self.d_ * self.byteSize()
 
     def data(self):
         return self.pixels_

@@ -565,4 +565,126 @@ int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, co
     return rc == 0 ? ICX_OK : ICX_OUT_OF_MEM;
 }
 
+// --------------------------------------------------------- Radiance .hdr (Image::readHdr)
+struct icx_hdr_batch {
+    icx_ctx* ctx = nullptr;
+    HdrWs ws;
+    std::unique_ptr<EventHook> hook;
+};
+
+int icx_hdr_probe(const uint8_t* data, size_t size, int* w, int* h) {
+    int ww = 0, hh = 0;
+    const int rc = data ? hdr_probe(data, (int64_t)size, &ww, &hh) : ICX_HDR_NOT_RADIANCE;
+    if (w) *w = rc == ICX_HDR_OK ? ww : 0;
+    if (h) *h = rc == ICX_HDR_OK ? hh : 0;
+    return rc;
+}
+
+icx_hdr_batch* icx_hdr_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h) {
+    if (!ctx || max_images <= 0 || max_w <= 0 || max_h <= 0) {
+        if (ctx) ctx->err = "icx_hdr_batch_create: bad arguments";
+        return nullptr;
+    }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), nullptr);
+    auto* b = new icx_hdr_batch();
+    b->ctx = ctx;
+    b->hook = std::make_unique<EventHook>();
+    if (!hdr_ws_alloc(b->ws, max_images, max_w, max_h)) {
+        hdr_ws_free(b->ws);
+        delete b;
+        ctx->err = "icx_hdr_batch_create: out of device memory";
+        return nullptr;
+    }
+    return b;
+}
+
+void icx_hdr_batch_destroy(icx_hdr_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->ctx->device);
+    hdr_ws_free(b->ws);
+    delete b;
+}
+
+int icx_hdr_batch_decode(icx_hdr_batch* b, int n, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_size,
+                         float* d_out, uint64_t out_stride, int32_t* d_status, int32_t* d_dims, void* stream) {
+    if (!b) return ICX_HDR_INTERNAL_ERR;
+    icx_ctx* ctx = b->ctx;
+    if (n < 0 || n > b->ws.max_images) { ctx->err = "icx_hdr_batch_decode: n exceeds batch capacity"; return ICX_HDR_INTERNAL_ERR; }
+    if (n == 0) return ICX_HDR_OK;
+    if (!d_data || !d_off || !d_size || !d_out || !d_status || !d_dims) { ctx->err = "null pointer"; return ICX_HDR_INTERNAL_ERR; }
+    if (out_stride < 4ull * b->ws.max_w * b->ws.max_h) { ctx->err = "icx_hdr_batch_decode: out_stride too small"; return ICX_HDR_INTERNAL_ERR; }
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_HDR_INTERNAL_ERR);
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    b->hook->reset();
+    launch_hdr_decode(b->ws, n, d_data, d_off, d_size, d_out, out_stride, d_status, d_dims, st, b->hook.get());
+    ICX_HIP(ctx, hipGetLastError(), ICX_HDR_INTERNAL_ERR);
+    return ICX_HDR_OK;
+}
+
+int icx_hdr_batch_stage_times(const icx_hdr_batch* b, const char** names, float* ms, int cap) {
+    if (!b) return 0;
+    static const Stage order[4] = {kStParse, kStUnstuff, kStEntropy, kStConvert};
+    static const char* const label[4] = {"parse", "locate", "unpack", "convert"};
+    float acc[kStCount] = {0};
+    for (auto& r : b->hook->recs) {
+        float t = 0;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) acc[r.s] += t;
+    }
+    for (int k = 0; k < 4 && k < cap; ++k) {
+        if (names) names[k] = label[k];
+        if (ms) ms[k] = acc[order[k]];
+    }
+    return 4;
+}
+
+int icx_hdr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out, int* w, int* h, int* rows) {
+    if (out) *out = nullptr;
+    if (w) *w = 0;
+    if (h) *h = 0;
+    if (rows) *rows = 0;
+    if (!ctx || !out) return ICX_HDR_INTERNAL_ERR;
+    int ww = 0, hh = 0;
+    const int prc = icx_hdr_probe(data, size, &ww, &hh);
+    if (prc != ICX_HDR_OK) return prc;  // header errors need no device work
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_HDR_INTERNAL_ERR);
+    icx_hdr_batch* b = icx_hdr_batch_create(ctx, 1, ww, hh);
+    if (!b) return ICX_HDR_INTERNAL_ERR;
+    const uint64_t nout = 4ull * ww * hh;
+    uint8_t* d_in = nullptr;
+    float* d_out = nullptr;
+    uint64_t* d_meta = nullptr;
+    int32_t* d_res = nullptr;
+    int rc = ICX_HDR_INTERNAL_ERR;
+    const uint64_t meta[2] = {0, (uint64_t)size};
+    int32_t res[4] = {0, 0, 0, 0};
+    hipStream_t st = ctx->stream;
+    if (hipMalloc(&d_in, size + 16) == hipSuccess && hipMalloc(&d_out, nout * 4) == hipSuccess &&
+        hipMalloc(&d_meta, 16) == hipSuccess && hipMalloc(&d_res, 16) == hipSuccess &&
+        hipMemcpyAsync(d_in, data, size, hipMemcpyHostToDevice, st) == hipSuccess &&
+        hipMemcpyAsync(d_meta, meta, 16, hipMemcpyHostToDevice, st) == hipSuccess &&
+        icx_hdr_batch_decode(b, 1, d_in, d_meta, d_meta + 1, d_out, nout, d_res, d_res + 1, st) == ICX_HDR_OK &&
+        hipMemcpyAsync(res, d_res, 16, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess) {
+        rc = res[0];
+        float* hostp = (float*)std::malloc(nout * 4);
+        if (hostp && hipMemcpy(hostp, d_out, nout * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+            *out = hostp;
+            if (w) *w = res[1];
+            if (h) *h = res[2];
+            if (rows) *rows = res[3];
+        } else {
+            std::free(hostp);
+            ctx->err = "icx_hdr_decode: host allocation or copy failed";
+            rc = ICX_HDR_INTERNAL_ERR;
+        }
+    } else if (ctx->err.empty()) {
+        ctx->err = "icx_hdr_decode: HIP failure";
+    }
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    (void)hipFree(d_meta);
+    (void)hipFree(d_res);
+    icx_hdr_batch_destroy(b);
+    return rc;
+}
+
 }  // extern "C"

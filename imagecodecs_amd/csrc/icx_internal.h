@@ -130,4 +130,36 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
                       uint64_t cap, uint64_t* size);
 bool png_encode_gpu(hipStream_t st, int w, int h, int d, const uint8_t* src, std::vector<uint8_t>& out);
 
+// Radiance .hdr decode (icx_hdr.hip; Image::readHdr, codecs.cpp:706-777). Status codes match
+// include/icx.h ICX_HDR_*; kHdrPending is internal.
+enum : int32_t {
+    kHdrOk = 0, kHdrNotRadiance = 1, kHdrBadHeader = 2, kHdrMalformed = 3, kHdrTruncated = 4, kHdrTooLarge = 5,
+    kHdrPending = 6
+};
+struct HdrDesc {
+    int32_t status, w, h, rows;
+    int64_t ds, size;      // pixel data start, file size
+    int32_t has_marker;    // an aligned old-style run marker exists (k_hdr_scan)
+    int32_t not_flat;      // some row is not a plain RGBE row at ds + 4*w*y (k_hdr_flatcheck)
+    int32_t ncand, new_ok; // new-style scanline starts found; they chain over all rows (k_hdr_link)
+    int32_t mode;          // 0 failed, 1 all rows plain, 2 all rows new-style, 3 per-row table (k_hdr_walk)
+    int32_t pad_;
+};
+struct HdrWs {
+    int max_images = 0, max_w = 0, max_h = 0;
+    HdrDesc* desc = nullptr;   // [max_images]
+    int32_t* cq = nullptr;     // [max_images][kHdrCandCap] new-style scanline starts (relative to ds)
+    int32_t* ce = nullptr;     // [max_images][kHdrCandCap] their ends (relative), or -1/-2/-3
+    int64_t* start = nullptr;  // [max_images][max_h] row start (byte offset in the file)
+    uint8_t* kind = nullptr;   // [max_images][max_h] row kind (mode 3)
+    uint8_t* planes = nullptr; // [max_images][max_h][4][max_w] RGBE planes of run-length coded rows
+};
+int hdr_probe(const uint8_t* data, int64_t size, int* w, int* h);
+int64_t hdr_ws_bytes(int max_images, int max_w, int max_h);
+bool hdr_ws_alloc(HdrWs& ws, int max_images, int max_w, int max_h);
+void hdr_ws_free(HdrWs& ws);
+void launch_hdr_decode(const HdrWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_size,
+                       float* d_out, uint64_t out_stride, int32_t* d_status, int32_t* d_dims, hipStream_t st,
+                       StageHook* hook);
+
 }  // namespace icx

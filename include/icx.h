@@ -170,6 +170,43 @@ void icx_png_encoder_destroy(icx_png_encoder* enc);
 int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, const uint8_t* d_src,
                           uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* hip_stream);
 
+/* ---- Radiance .hdr read (Image::readHdr, codecs.cpp:706-777) -----------------------------------
+ * Output as readHdr returns it (d = 4, Type::FLOAT): 4 floats per pixel, rows in file order,
+ * R, G, B = convertComponent(E - 128, v) = v * 2^(E - 136) (codecs.cpp:610-615; exact, so the
+ * GPU result equals the reference's bit for bit) and the fourth float = E (:624).
+ * Where the reference's behaviour is undefined (runs past the scanline, a run on a scanline's first
+ * pixel, a header without an empty line, a partial resolution line) the result is MALFORMED or
+ * BAD_HEADER; rows after a scanline the reference stops at (it leaves them uninitialised,
+ * :765-769) are zero and counted out of *rows. */
+enum icx_hdr_result {
+    ICX_HDR_OK = 0,            /* all rows decoded                                   */
+    ICX_HDR_NOT_RADIANCE = 1,  /* "Invalid file format": no "#?RADIANCE" (:717-720)  */
+    ICX_HDR_BAD_HEADER = 2,    /* header / resolution line not as readHdr parses it   */
+    ICX_HDR_MALFORMED = 3,     /* run-length data the reference cannot decode (UB)     */
+    ICX_HDR_TRUNCATED = 4,     /* the file ends first: rows < height                   */
+    ICX_HDR_TOO_LARGE = 5,     /* larger than the batch workspace                      */
+    ICX_HDR_INTERNAL_ERR = -1  /* HIP failure (see icx_last_error)                     */
+};
+/* Header only (host): width/height of a well-formed header, else the error code. */
+int icx_hdr_probe(const uint8_t* data, size_t size, int* width, int* height);
+/* One image, host in / host out: *out receives a malloc()'d width*height*4 float buffer (free
+ * with icx_free); *rows = decoded rows. */
+int icx_hdr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out, int* width, int* height,
+                   int* rows);
+/* Device-resident batch: image i = d_data[d_offsets[i] .. + d_sizes[i]), output floats at
+ * d_out + i*out_stride (out_stride >= 4*width*height of every image), per-image status in
+ * d_status[i] and {width, height, rows} in d_dims[3i..]. Asynchronous on hip_stream (NULL = the
+ * context's stream). Returns ICX_HDR_OK or ICX_HDR_INTERNAL_ERR. */
+typedef struct icx_hdr_batch icx_hdr_batch;
+icx_hdr_batch* icx_hdr_batch_create(icx_ctx* ctx, int max_images, int max_width, int max_height);
+void icx_hdr_batch_destroy(icx_hdr_batch* b);
+int icx_hdr_batch_decode(icx_hdr_batch* b, int n, const uint8_t* d_data, const uint64_t* d_offsets,
+                         const uint64_t* d_sizes, float* d_out, uint64_t out_stride, int32_t* d_status,
+                         int32_t* d_dims, void* hip_stream);
+/* Milliseconds per stage of the last icx_hdr_batch_decode ("parse", "locate", "unpack",
+ * "convert"; synchronises). Returns the number of stages. */
+int icx_hdr_batch_stage_times(const icx_hdr_batch* b, const char** names, float* ms, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,6 +5,8 @@
  * Same names, argument meaning and ownership as the reference class:
  *   read(path)  -- dispatch on the lower-cased extension (codecs.cpp:53-89); ".jpg"/".jpeg"
  *                  decode on the GPU (readJpg, codecs.cpp:821-849 -> icx_jpeg_decode).
+ *               ".hdr" decodes Radiance RGBE to 4 floats per pixel on the GPU (readHdr,
+ *               codecs.cpp:706-777 -> icx_hdr_decode; bit-identical floats).
  *   write(path) -- ".jpg"/".jpeg" encode with tiny_jpeg quality 3 semantics (writeJpg,
  *                  codecs.cpp:851-854 -> icx_tje_encode_to_file, byte-identical stream).
  *               ".png" encodes with png_encoder::saveToFile semantics (writePng,
@@ -106,6 +108,40 @@ class Image {
         type_ = Type::UBYTE;
     }
 
+    // readHdr (codecs.cpp:706-777): d = 4, Type::FLOAT, R, G, B = v * 2^(E-136) and E per pixel,
+    // decoded on the GPU (icx_hdr_decode). A truncated file keeps its decoded rows and zeroes the
+    // rest (the reference leaves them uninitialised); header errors and run-length data the
+    // reference cannot decode throw "Invalid file format" (:719, :748).
+    void readHdr(const std::string& path) {
+        std::FILE* f = std::fopen(path.c_str(), "rb");
+        if (!f) throw std::runtime_error("Cannot open file");  // codecs.cpp:713-714
+        std::vector<uint8_t> buf;
+        uint8_t chunk[1 << 16];
+        size_t k;
+        while ((k = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + k);
+        std::fclose(f);
+        auto& P = detail::icx_process();
+        std::lock_guard<std::mutex> lock(P.mu);
+        float* out = nullptr;
+        int w = 0, h = 0, rows = 0;
+        const int rc = icx_hdr_decode(P.get(), buf.data(), buf.size(), &out, &w, &h, &rows);
+        if (rc != ICX_HDR_OK && rc != ICX_HDR_TRUNCATED) {
+            icx_free(out);
+            if (rc == ICX_HDR_INTERNAL_ERR) throw std::runtime_error(std::string("icx_hdr_decode: ") + icx_last_error(P.get()));
+            throw std::runtime_error("Invalid file format");
+        }
+        const size_t n = (size_t)w * h * 4 * sizeof(float);
+        unsigned char* px = new unsigned char[n ? n : 1];
+        if (n) std::memcpy(px, out, n);
+        icx_free(out);
+        delete[] pixels_;
+        pixels_ = px;
+        w_ = w;
+        h_ = h;
+        d_ = 4;
+        type_ = Type::FLOAT;
+    }
+
     void writeJpg(const std::string& path) {
         auto& P = detail::icx_process();
         std::lock_guard<std::mutex> lock(P.mu);
@@ -146,6 +182,7 @@ public:
     void read(const std::string& filepath) {
         const std::string ext = detail::lower_ext(filepath);
         if (ext == ".jpg" || ext == ".jpeg") readJpg(filepath);
+        else if (ext == ".hdr") readHdr(filepath);
         else throw std::invalid_argument("Cannot parse filetype");
         if (pixels_ == nullptr) throw std::runtime_error("Could not read image data");
     }

@@ -63,6 +63,12 @@ int or_png_filter(const uint8_t* px, int w, int h, int d, const or_png_mode* m, 
 /* Whole PNG with the IDAT deflated by the system zlib at `zlevel` (size proxy, CPU baseline). */
 int or_png_encode(const uint8_t* px, int w, int h, int d, int zlevel, uint8_t** out, int64_t* size);
 
+/* Radiance .hdr reader (hdr_oracle.c; Image::readHdr, codecs.cpp:706-777). Result codes: */
+enum { OR_HDR_OK = 0, OR_HDR_NOT_RADIANCE = 1, OR_HDR_BAD_HEADER = 2, OR_HDR_MALFORMED = 3, OR_HDR_TRUNCATED = 4 };
+int or_hdr_header(const uint8_t* data, int64_t size, int* w, int* h, int64_t* data_start);
+/* *out: malloc'd w*h*4 floats (R, G, B, E per pixel; rows past *rows are 0). */
+int or_hdr_decode(const uint8_t* data, int64_t size, float** out, int* w, int* h, int* rows);
+
 void or_free(void* p);
 
 #ifdef __cplusplus

@@ -51,6 +51,9 @@ def lib():
         L.or_png_encode.restype = C.c_int
         L.or_png_encode.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p),
                                     C.POINTER(C.c_int64)]
+        L.or_hdr_decode.restype = C.c_int
+        L.or_hdr_decode.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.or_free.argtypes = [C.c_void_p]
         _LIB = L
     return _LIB
@@ -198,3 +201,21 @@ def ref_tje_encode(quality: int, w: int, h: int, comps: int, rgb: bytes, cap: in
     if ok != 1:
         return None
     return out.raw[: n.value]
+
+
+HDR_OK, HDR_NOT_RADIANCE, HDR_BAD_HEADER, HDR_MALFORMED, HDR_TRUNCATED = 0, 1, 2, 3, 4
+
+
+def hdr_decode(data: bytes):
+    """Image::readHdr restatement -> (code, w, h, rows, float32 array (h, w, 4) or None)."""
+    L = lib()
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    out = C.c_void_p()
+    w, h, rows = C.c_int(), C.c_int(), C.c_int()
+    code = L.or_hdr_decode(buf, len(data), C.byref(out), C.byref(w), C.byref(h), C.byref(rows))
+    arr = None
+    if out.value:
+        n = w.value * h.value * 4
+        arr = np.frombuffer(C.string_at(out.value, n * 4), dtype=np.float32).reshape(h.value, w.value, 4).copy()
+        L.or_free(out)
+    return code, w.value, h.value, rows.value, arr

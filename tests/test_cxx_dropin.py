@@ -62,3 +62,20 @@ def test_dropin_write_matches_tiny_jpeg(demo, tmp_path):
     code, w, h, n, pix = pyoracle.decode(open(os.path.join(GOLDEN, "test.jpg"), "rb").read())
     assert code == 0
     assert open(dst, "rb").read() == pyoracle.tje_encode(3, w, h, 3, pix)
+
+
+@pytest.mark.gpu
+def test_dropin_read_hdr(demo, tmp_path):
+    """Image::read(".hdr") (readHdr, codecs.cpp:706-777): d = 4 floats per pixel, bit-identical
+    to the oracle on the reference's data/test.hdr."""
+    from oracle import pyoracle
+    src = os.path.join(GOLDEN, "test.hdr")
+    out = str(tmp_path / "t.f32")
+    r = run(demo, "read", src, out)
+    assert r.returncode == 0, r.stderr
+    raw = open(out, "rb").read()
+    w, h, d = np.frombuffer(raw[:12], np.int32)
+    assert (w, h, d) == (499, 289, 4)
+    code, _, _, rows, arr = pyoracle.hdr_decode(open(src, "rb").read())
+    assert code == 0 and rows == 289
+    assert raw[12:] == arr.tobytes()

@@ -12,6 +12,7 @@
  *    decode parity is always judged against the NanoJPEG oracle on its output.
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -285,4 +286,107 @@ int64_t synth_jpeg(const uint8_t* px, int w, int h, int comps_in, int sampling, 
     wflush1(&W);
     wb16(&W, 0xFFD9);
     return W.full ? -1 : W.n;
+}
+
+/* ---------------------------------------------------------------- Radiance .hdr (RGBE) inputs
+ * synth_rgbe: smooth RGBE pixels with noise (mantissas 128..255, exponents around 128) and a band of
+ * constant rows so that run-length coding has runs to find. Never emits R=G=B=1 (an old-style run
+ * marker). hdr_encode writes the header the reference reader expects (codecs.cpp:713-750) and the
+ * pixel data as mode 0: new-style per-component RLE (Radiance RGBE_WriteBytes_RLE scheme),
+ * mode 1: flat RGBE (what Image::writeHdr writes, codecs.cpp:779-817), mode 2: old-style RLE
+ * (repeated pixels as (1,1,1,count) markers, count < 256). */
+int synth_rgbe(uint64_t seed, int w, int h, uint8_t* out) {
+    if (w <= 0 || h <= 0) return 0;
+    uint64_t s = seed * 0x9E3779B97F4A7C15ull + 12345;
+    const double fx = 0.002 + 0.01 * unif(&s), fy = 0.002 + 0.01 * unif(&s), ph = 6.283 * unif(&s);
+    const int band0 = h / 3, band1 = band0 + h / 10;
+    for (int y = 0; y < h; ++y) {
+        for (int x = 0; x < w; ++x) {
+            uint8_t* p = out + ((size_t)y * w + x) * 4;
+            if (y >= band0 && y < band1) { p[0] = 200; p[1] = 150; p[2] = 180; p[3] = 129; continue; }
+            const double v = sin(x * fx + ph) * cos(y * fy);
+            const int e = 128 + (int)floor(2.5 * v);
+            for (int c = 0; c < 3; ++c) {
+                int m = 128 + (int)(60 + 55 * sin(x * fx * (c + 1) + y * fy + c) + 10 * (unif(&s) - 0.5));
+                p[c] = (uint8_t)(m < 128 ? 128 : (m > 255 ? 255 : m));
+            }
+            p[3] = (uint8_t)e;
+        }
+    }
+    return 1;
+}
+
+static int64_t hdr_put(uint8_t* out, int64_t n, int64_t cap, int v) {
+    if (n < cap) out[n] = (uint8_t)v;
+    return n + 1;
+}
+
+/* one component of one scanline, Radiance's RLE scheme (runs >= 4, literals <= 128) */
+static int64_t hdr_rle_comp(const uint8_t* px, int w, int c, uint8_t* out, int64_t n, int64_t cap) {
+    int cur = 0;
+#define D(i) px[4 * (i) + c]
+    while (cur < w) {
+        int beg = cur, run = 0, old_run = 0;
+        while (run < 4 && beg < w) {
+            beg += run;
+            old_run = run;
+            run = 1;
+            while (beg + run < w && run < 127 && D(beg) == D(beg + run)) run++;
+        }
+        if (old_run > 1 && old_run == beg - cur) {
+            n = hdr_put(out, n, cap, 128 + old_run);
+            n = hdr_put(out, n, cap, D(cur));
+            cur = beg;
+        }
+        while (cur < beg) {
+            int k = beg - cur;
+            if (k > 128) k = 128;
+            n = hdr_put(out, n, cap, k);
+            for (int i = 0; i < k; ++i) n = hdr_put(out, n, cap, D(cur + i));
+            cur += k;
+        }
+        if (run >= 4) {
+            n = hdr_put(out, n, cap, 128 + run);
+            n = hdr_put(out, n, cap, D(beg));
+            cur += run;
+        }
+    }
+#undef D
+    return n;
+}
+
+int64_t hdr_encode(const uint8_t* rgbe, int w, int h, int mode, uint8_t* out, int64_t cap) {
+    char hdr[128];
+    const int hl = snprintf(hdr, sizeof hdr, "#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y %d +X %d\n", h, w);
+    int64_t n = 0;
+    for (int i = 0; i < hl; ++i) n = hdr_put(out, n, cap, hdr[i]);
+    for (int y = 0; y < h; ++y) {
+        const uint8_t* px = rgbe + (size_t)y * w * 4;
+        if (mode == 0 && w >= 8 && w <= 0x7fff) {
+            n = hdr_put(out, n, cap, 2);
+            n = hdr_put(out, n, cap, 2);
+            n = hdr_put(out, n, cap, w >> 8);
+            n = hdr_put(out, n, cap, w & 255);
+            for (int c = 0; c < 4; ++c) n = hdr_rle_comp(px, w, c, out, n, cap);
+        } else if (mode == 2) {
+            int x = 0;
+            while (x < w) {
+                for (int k = 0; k < 4; ++k) n = hdr_put(out, n, cap, px[4 * x + k]);
+                int r = 0;
+                while (x + 1 + r < w && r < 255 && !memcmp(px + 4 * x, px + 4 * (x + 1 + r), 4)) r++;
+                if (r >= 2) {
+                    n = hdr_put(out, n, cap, 1);
+                    n = hdr_put(out, n, cap, 1);
+                    n = hdr_put(out, n, cap, 1);
+                    n = hdr_put(out, n, cap, r);
+                    x += 1 + r;
+                } else {
+                    x += 1;
+                }
+            }
+        } else {
+            for (int i = 0; i < w * 4; ++i) n = hdr_put(out, n, cap, px[i]);
+        }
+    }
+    return n <= cap ? n : -n;
 }

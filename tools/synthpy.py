@@ -28,6 +28,10 @@ def lib():
         L.synth_jpeg.restype = C.c_int64
         L.synth_jpeg.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_void_p, C.c_int64]
+        L.synth_rgbe.restype = C.c_int
+        L.synth_rgbe.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_void_p]
+        L.hdr_encode.restype = C.c_int64
+        L.hdr_encode.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64]
         _LIB = L
     return _LIB
 
@@ -55,3 +59,25 @@ def jpeg(pixels: np.ndarray, sampling: str = "420", quality: int = 90, restart: 
 
 def synth_jpeg(seed: int, w: int, h: int, sampling: str = "420", quality: int = 90, restart: int = 0) -> bytes:
     return jpeg(rgb(seed, w, h, 1 if sampling == "gray" else 3), sampling, quality, restart)
+
+
+HDR_RLE, HDR_FLAT, HDR_OLD_RLE = 0, 1, 2
+
+
+def rgbe(seed: int, w: int, h: int) -> np.ndarray:
+    out = np.empty((h, w, 4), np.uint8)
+    if not lib().synth_rgbe(seed, w, h, out.ctypes.data):
+        raise ValueError("synth_rgbe failed")
+    return out
+
+
+def hdr(pixels: np.ndarray, mode: int = HDR_RLE) -> bytes:
+    """Radiance .hdr file of RGBE pixels (h, w, 4): new RLE, flat, or old-style RLE."""
+    pixels = np.ascontiguousarray(pixels, dtype=np.uint8)
+    h, w, _ = pixels.shape
+    cap = w * h * 5 + 4 * h + 256
+    out = np.empty(cap, np.uint8)
+    n = lib().hdr_encode(pixels.ctypes.data, w, h, mode, out.ctypes.data, cap)
+    if n < 0:
+        raise ValueError("hdr_encode overflow")
+    return out[:n].tobytes()
