@@ -85,6 +85,7 @@ _SIGS = {
     "icx_png_encoder_create": (_vp, [_vp]),
     "icx_png_encoder_destroy": (None, [_vp]),
     "icx_png_encode_device": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
+    "icx_png_encoder_stage_times": (_i32, [_vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), _i32]),
     "icx_jpeg_encode_device": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
     "icx_hdr_probe": (_i32, [_vp, _sz, C.POINTER(_i32), C.POINTER(_i32)]),
     "icx_hdr_decode": (_i32, [_vp, _vp, _sz, C.POINTER(_vp), C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
@@ -285,6 +286,13 @@ class PngEncoder:
         if rc not in (OK, OUT_OF_MEM):
             raise ICXError(f"icx_png_encode_device -> {rc}: {_err(self.ctx.ptr)}")
         return rc, int(n.value)
+
+    def stage_times(self) -> dict:
+        """Summed per-stage ms since the previous call (icx_png_encoder_stage_times)."""
+        names = (C.c_char_p * 8)()
+        ms = (C.c_float * 8)()
+        k = lib().icx_png_encoder_stage_times(self._p, names, ms, 8)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
 
 
 class Encoder:

@@ -33,10 +33,17 @@ struct icx_ctx {
 
 struct EventHook;
 
+// Up to kMaxPipes decode pipelines per batch, each a workspace + a stream: consecutive groups of
+// a call alternate between them, so one group's entropy kernels (latency/LDS-bound) run beside
+// another group's IDCT/convert (memory-bound) instead of after them.
+constexpr int kMaxPipes = 2;
 struct icx_batch {
     icx_ctx* ctx = nullptr;
     int max_images = 0;
-    GroupWs ws;
+    int pipes = 1;
+    GroupWs ws[kMaxPipes];
+    hipStream_t pst[kMaxPipes] = {};  // pst[0] unused: pipe 0 runs on the caller's stream
+    hipEvent_t fork = nullptr, join[kMaxPipes] = {};
     uint8_t* d_hin = nullptr;  // staging for icx_jpeg_batch_decode_host
     size_t d_hin_cap = 0;
     std::unique_ptr<EventHook> hook;
@@ -144,6 +151,67 @@ int icx_jpeg_probe(const uint8_t* jpeg, size_t size, int* w, int* h, int* ncomp)
 }
 
 // ----------------------------------------------------------------------------- batches
+// Bytes of one workspace slot (one image in flight) for max_w x max_h images; fills the caps.
+static int64_t ws_per_slot(GroupWs& ws, int max_w, int max_h) {
+    ws.max_w = max_w;
+    ws.max_h = max_h;
+    ws.coef_cap = ws_coef_cap(max_w, max_h);
+    ws.plane_cap = ws_plane_cap(max_w, max_h);
+    ws.tmp_cap = ws_tmp_cap(max_w, max_h);
+    ws.ucap = ((int64_t)max_w * max_h + 4095) / 4096 * 4096;  // 1 B/px of entropy data (q90 ~0.4)
+    ws.rst_cap = ((int64_t)max_w / 8 + 1) * ((int64_t)max_h / 8 + 1);  // >= MCUs per image
+    const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
+    const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
+    return ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
+           tiles_per_slot * 28 + ws.rst_cap * 8 +
+           lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
+}
+
+static void ws_free(GroupWs& ws) {
+    for (void* p : {(void*)ws.desc, (void*)ws.ac, (void*)ws.dc, (void*)ws.planes, (void*)ws.tmp, (void*)ws.spec,
+                    (void*)ws.tilepre, (void*)ws.wgpre, (void*)ws.wg2pre, (void*)ws.totals, (void*)ws.tiles,
+                    (void*)ws.tile_obase, (void*)ws.U, (void*)ws.X, (void*)ws.sub, (void*)ws.rst, (void*)ws.tile_rbase,
+                    (void*)ws.ent, (void*)ws.stats, (void*)ws.Y, (void*)ws.rec, (void*)ws.nrec, (void*)ws.guess_cnt,
+                    (void*)ws.repair})
+        if (p) (void)hipFree(p);
+    ws = GroupWs{};
+}
+
+static bool ws_alloc(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int max_h) {
+    (void)ws_per_slot(ws, max_w, max_h);
+    const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
+    const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
+    ws.slots = group;
+    ICX_HIP(ctx, hipMalloc(&ws.desc, sizeof(Desc) * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)ws.coef_cap * 64 * 2 * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)ws.coef_cap * 4 * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.planes, (size_t)ws.plane_cap * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), false);
+    ws.tiles_cap = tiles_per_slot * group;
+    ws.lanes_cap = lanes_per_slot * group;
+    ICX_HIP(ctx, hipMalloc(&ws.spec, sizeof(SpecImg) * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.tilepre, sizeof(int32_t) * (group + 1)), false);
+    ICX_HIP(ctx, hipMalloc(&ws.wgpre, sizeof(int32_t) * (group + 1)), false);
+    ICX_HIP(ctx, hipMalloc(&ws.wg2pre, sizeof(int32_t) * (group + 1)), false);
+    ICX_HIP(ctx, hipMalloc(&ws.totals, sizeof(int32_t) * 4), false);
+    ICX_HIP(ctx, hipMalloc(&ws.tiles, sizeof(TileRec) * ws.tiles_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.tile_obase, sizeof(int32_t) * ws.tiles_cap), false);
+    // + slack: the entropy readers load whole 16-byte chunks (icx_spec_core.h Reader)
+    ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.ucap * group + 256), false);
+    ICX_HIP(ctx, hipMalloc(&ws.X, sizeof(uint64_t) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.sub, sizeof(SubRec) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.rst, sizeof(int64_t) * ws.rst_cap * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.tile_rbase, sizeof(int32_t) * ws.tiles_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.ent, sizeof(LaneEntry) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.stats, sizeof(int32_t) * 4), false);
+    ICX_HIP(ctx, hipMalloc(&ws.Y, sizeof(uint64_t) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.rec, sizeof(RecState) * kRec * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.nrec, sizeof(int32_t) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.guess_cnt, sizeof(int32_t) * 4 * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.repair, sizeof(int32_t) * kMaxRepair * group), false);
+    return true;
+}
+
 icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, int group) {
     if (!ctx || max_images <= 0 || max_w <= 0 || max_h <= 0 || max_w > 65535 || max_h > 65535) {
         if (ctx) ctx->err = "icx_batch_create: bad arguments";
@@ -153,19 +221,12 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     auto b = std::make_unique<icx_batch>();
     b->ctx = ctx;
     b->max_images = max_images;
-    GroupWs& ws = b->ws;
-    ws.max_w = max_w;
-    ws.max_h = max_h;
-    ws.coef_cap = ws_coef_cap(max_w, max_h);
-    ws.plane_cap = ws_plane_cap(max_w, max_h);
-    ws.tmp_cap = ws_tmp_cap(max_w, max_h);
-    ws.ucap = ((int64_t)max_w * max_h + 4095) / 4096 * 4096;  // 1 B/px of entropy data (q90 ~0.4)
-    const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
-    ws.rst_cap = ((int64_t)max_w / 8 + 1) * ((int64_t)max_h / 8 + 1);  // >= MCUs per image
-    const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
-    const int64_t per_slot = ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) +
-                             ws.ucap + tiles_per_slot * 28 + ws.rst_cap * 8 +
-                             lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
+    // pipelines: ICX_PIPES (1..2, default 2) when the batch holds at least two images
+    int pipes = kMaxPipes;
+    if (const char* e = std::getenv("ICX_PIPES")) pipes = std::max(1, std::min(kMaxPipes, std::atoi(e)));
+    if (max_images < 2) pipes = 1;
+    GroupWs probe;
+    const int64_t per_slot = ws_per_slot(probe, max_w, max_h);
     if (group <= 0) {  // auto: up to 60% of the free HBM (288 GB per MI355X), at least one image
         size_t free_b = 0, total_b = 0;
         ICX_HIP(ctx, hipMemGetInfo(&free_b, &total_b), nullptr);
@@ -173,34 +234,16 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
         group = (int)std::max<int64_t>(1, std::min<int64_t>(max_images, budget / per_slot));
     }
     group = std::min(group, max_images);
-    ws.slots = group;
-    ICX_HIP(ctx, hipMalloc(&ws.desc, sizeof(Desc) * group), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)ws.coef_cap * 64 * 2 * group), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)ws.coef_cap * 4 * group), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.planes, (size_t)ws.plane_cap * group), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), nullptr);
-    ws.tiles_cap = tiles_per_slot * group;
-    ws.lanes_cap = lanes_per_slot * group;
-    ICX_HIP(ctx, hipMalloc(&ws.spec, sizeof(SpecImg) * group), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.tilepre, sizeof(int32_t) * (group + 1)), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.wgpre, sizeof(int32_t) * (group + 1)), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.wg2pre, sizeof(int32_t) * (group + 1)), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.totals, sizeof(int32_t) * 4), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.tiles, sizeof(TileRec) * ws.tiles_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.tile_obase, sizeof(int32_t) * ws.tiles_cap), nullptr);
-    // + slack: the entropy readers load whole 16-byte chunks (icx_spec_core.h Reader)
-    ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.ucap * group + 256), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.X, sizeof(uint64_t) * ws.lanes_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.sub, sizeof(SubRec) * ws.lanes_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.rst, sizeof(int64_t) * ws.rst_cap * group), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.tile_rbase, sizeof(int32_t) * ws.tiles_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.ent, sizeof(LaneEntry) * ws.lanes_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.stats, sizeof(int32_t) * 4), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.Y, sizeof(uint64_t) * ws.lanes_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.rec, sizeof(RecState) * kRec * ws.lanes_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.nrec, sizeof(int32_t) * ws.lanes_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.guess_cnt, sizeof(int32_t) * 4 * ws.lanes_cap), nullptr);
-    ICX_HIP(ctx, hipMalloc(&ws.repair, sizeof(int32_t) * kMaxRepair * group), nullptr);
+    if (group < 2) pipes = 1;
+    b->pipes = pipes;
+    for (int p = 0; p < pipes; ++p) {
+        // `group` images in flight over all pipes: each workspace holds its share
+        const int slots = (group + pipes - 1) / pipes;
+        if (!ws_alloc(ctx, b->ws[p], slots, max_w, max_h)) return nullptr;
+        if (p > 0) ICX_HIP(ctx, hipStreamCreateWithFlags(&b->pst[p], hipStreamNonBlocking), nullptr);
+        ICX_HIP(ctx, hipEventCreateWithFlags(&b->join[p], hipEventDisableTiming), nullptr);
+    }
+    ICX_HIP(ctx, hipEventCreateWithFlags(&b->fork, hipEventDisableTiming), nullptr);
     b->hook = std::make_unique<EventHook>();
     return b.release();
 }
@@ -208,16 +251,12 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
 void icx_batch_destroy(icx_batch* b) {
     if (!b) return;
     (void)hipSetDevice(b->ctx->device);
-    (void)hipFree(b->ws.desc);
-    (void)hipFree(b->ws.ac);
-    (void)hipFree(b->ws.dc);
-    (void)hipFree(b->ws.planes);
-    (void)hipFree(b->ws.tmp);
-    for (void* p : {(void*)b->ws.spec, (void*)b->ws.tilepre, (void*)b->ws.wgpre, (void*)b->ws.wg2pre, (void*)b->ws.totals,
-                    (void*)b->ws.tiles, (void*)b->ws.tile_obase, (void*)b->ws.U, (void*)b->ws.X,
-                    (void*)b->ws.sub, (void*)b->ws.rst, (void*)b->ws.tile_rbase, (void*)b->ws.ent, (void*)b->ws.stats, (void*)b->ws.Y,
-                    (void*)b->ws.rec, (void*)b->ws.nrec, (void*)b->ws.guess_cnt, (void*)b->ws.repair})
-        if (p) (void)hipFree(p);
+    for (int p = 0; p < kMaxPipes; ++p) {
+        ws_free(b->ws[p]);
+        if (b->pst[p]) (void)hipStreamDestroy(b->pst[p]);
+        if (b->join[p]) (void)hipEventDestroy(b->join[p]);
+    }
+    if (b->fork) (void)hipEventDestroy(b->fork);
     if (b->d_hin) (void)hipFree(b->d_hin);
     delete b;
 }
@@ -232,15 +271,28 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     b->hook->reset();
-    ICX_HIP(ctx, hipMemsetAsync(b->ws.stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
+    for (int p = 0; p < b->pipes; ++p)
+        ICX_HIP(ctx, hipMemsetAsync(b->ws[p].stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
     // equal-sized groups (512 images on 361 slots -> 256 + 256, not 361 + 151): every kernel's
     // grid is sized by the work of its group, so a small tail group leaves the GPU half idle
-    const int ngroups = (n + b->ws.slots - 1) / b->ws.slots;
+    const int slots = b->ws[0].slots;
+    const int ngroups = (n + slots - 1) / slots;
     const int per = (n + ngroups - 1) / ngroups;
-    for (int g0 = 0; g0 < n; g0 += per) {
+    const int used = std::min(b->pipes, ngroups);
+    if (used > 1) {  // the other pipes start after the caller's prior work on `st`
+        ICX_HIP(ctx, hipEventRecord(b->fork, st), ICX_INTERNAL_ERR);
+        for (int p = 1; p < used; ++p) ICX_HIP(ctx, hipStreamWaitEvent(b->pst[p], b->fork, 0), ICX_INTERNAL_ERR);
+    }
+    int gi = 0;
+    for (int g0 = 0; g0 < n; g0 += per, ++gi) {
         const int gn = std::min(per, n - g0);
-        launch_decode_group(b->ws, gn, d_data, d_off + g0, d_size + g0, d_out + (uint64_t)g0 * out_stride, out_stride,
-                            d_status + g0, d_dims + 3 * g0, st, b->hook.get());
+        const int p = gi % used;
+        launch_decode_group(b->ws[p], gn, d_data, d_off + g0, d_size + g0, d_out + (uint64_t)g0 * out_stride, out_stride,
+                            d_status + g0, d_dims + 3 * g0, p == 0 ? st : b->pst[p], b->hook.get());
+    }
+    for (int p = 1; p < used; ++p) {  // the caller's stream waits for every pipe
+        ICX_HIP(ctx, hipEventRecord(b->join[p], b->pst[p]), ICX_INTERNAL_ERR);
+        ICX_HIP(ctx, hipStreamWaitEvent(st, b->join[p], 0), ICX_INTERNAL_ERR);
     }
     ICX_HIP(ctx, hipGetLastError(), ICX_INTERNAL_ERR);
     return ICX_OK;
@@ -249,14 +301,18 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
 int icx_batch_path_stats(const icx_batch* b, int32_t* parallel, int32_t* fallback, int32_t* sequential) {
     if (!b) return ICX_INTERNAL_ERR;
     int32_t h[4] = {0, 0, 0, 0};
-    ICX_HIP(b->ctx, hipMemcpy(h, b->ws.stats, sizeof h, hipMemcpyDeviceToHost), ICX_INTERNAL_ERR);
+    for (int p = 0; p < b->pipes; ++p) {
+        int32_t q[4];
+        ICX_HIP(b->ctx, hipMemcpy(q, b->ws[p].stats, sizeof q, hipMemcpyDeviceToHost), ICX_INTERNAL_ERR);
+        for (int k = 0; k < 4; ++k) h[k] += q[k];
+    }
     if (parallel) *parallel = h[0];
     if (fallback) *fallback = h[1];
     if (sequential) *sequential = h[2];
     return ICX_OK;
 }
 
-int icx_batch_group(const icx_batch* b) { return b ? b->ws.slots : 0; }
+int icx_batch_group(const icx_batch* b) { return b ? b->ws[0].slots : 0; }
 
 int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int cap) {
     if (!b) return 0;
@@ -329,7 +385,7 @@ static int decode_one(icx_ctx* ctx, const uint8_t* jpeg, size_t size, std::vecto
     int pw = 0, ph = 0, pc = 0;
     const int probe = icx_jpeg_probe(jpeg, size, &pw, &ph, &pc);
     if (probe != ICX_OK) return probe;  // header-level result is final (no entropy data reached)
-    if (!ctx->single || ctx->single->ws.max_w < pw || ctx->single->ws.max_h < ph) {
+    if (!ctx->single || ctx->single->ws[0].max_w < pw || ctx->single->ws[0].max_h < ph) {
         if (ctx->single) icx_batch_destroy(ctx->single);
         ctx->single = icx_batch_create(ctx, 1, std::max(pw, 1), std::max(ph, 1), 1);
         if (!ctx->single) return ICX_OUT_OF_MEM;
@@ -563,6 +619,11 @@ int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, co
     const int rc = png_encode_device(st, enc->ws, width, height, d, d_src, d_out, out_cap, out_size);
     if (rc < 0) { ctx->err = "HIP failure in png_encode_device"; return ICX_INTERNAL_ERR; }
     return rc == 0 ? ICX_OK : ICX_OUT_OF_MEM;
+}
+
+int icx_png_encoder_stage_times(icx_png_encoder* enc, const char** names, float* ms, int cap) {
+    if (!enc || cap <= 0) return 0;
+    return png_ws_stage_times(enc->ws, names, ms, cap);
 }
 
 // --------------------------------------------------------- Radiance .hdr (Image::readHdr)

@@ -126,6 +126,7 @@ int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, 
 struct PngWs;
 PngWs* png_ws_create();
 void png_ws_destroy(PngWs* ws);
+int png_ws_stage_times(PngWs* ws, const char** names, float* ms, int cap);
 int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
                       uint64_t cap, uint64_t* size);
 bool png_encode_gpu(hipStream_t st, int w, int h, int d, const uint8_t* src, std::vector<uint8_t>& out);

@@ -76,8 +76,10 @@ void icx_free(void* p);
 typedef struct icx_batch icx_batch;
 
 /* Workspace for up to `max_images` images per call, each at most max_width x max_height
- * (any sampling NanoJPEG accepts). Images are processed in groups of `group` (0 = auto)
- * that reuse one workspace. Returns NULL on allocation failure. */
+ * (any sampling NanoJPEG accepts). At most `group` images (0 = auto: 60% of free HBM) are in
+ * flight at once, split over up to two decode pipelines (a workspace and a HIP stream each;
+ * env ICX_PIPES=1 keeps one): consecutive groups alternate between the pipelines so their
+ * kernels overlap, and the call's stream waits for both. Returns NULL on allocation failure. */
 icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_width, int max_height, int group);
 void icx_batch_destroy(icx_batch* b);
 
@@ -99,7 +101,7 @@ int icx_jpeg_batch_decode_host(icx_batch* b, int n, const uint8_t* const* jpegs,
                                uint8_t* const* outs, uint64_t out_stride, int32_t* status, int32_t* dims);
 
 /* Images per workspace group (each kernel of the pipeline launches once per group). */
-int icx_batch_group(const icx_batch* b);
+int icx_batch_group(const icx_batch* b); /* images per group (one pipeline's workspace) */
 
 /* Per-stage timings (ms) of the most recent batch call, measured with HIP events on the
  * stream the kernels ran on. Fills up to `cap` entries; returns the number of stages. */
@@ -169,6 +171,10 @@ void icx_png_encoder_destroy(icx_png_encoder* enc);
  * failure. */
 int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, const uint8_t* d_src,
                           uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* hip_stream);
+/* Milliseconds per stage summed over the icx_png_encode_device calls since the previous read
+ * ("stats", "filter", "lz77", "huff", "emit", "crc"; HIP events on the launch stream). Returns
+ * the number of stages. */
+int icx_png_encoder_stage_times(icx_png_encoder* enc, const char** names, float* ms, int cap);
 
 /* ---- Radiance .hdr read (Image::readHdr, codecs.cpp:706-777) -----------------------------------
  * Output as readHdr returns it (d = 4, Type::FLOAT): 4 floats per pixel, rows in file order,
