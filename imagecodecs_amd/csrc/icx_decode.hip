@@ -123,12 +123,15 @@ __device__ __forceinline__ int64_t comp_plane_off(const Desc& d, int ci) {
 }
 
 // --------------------------------------------------------------------------------- IDCT
-// 256 lanes = 32 blocks x 8 rows. Lane (b, r) dequantizes and row-transforms row r of block
-// b, then column-transforms column r, then stores row r of the 8x8 pixel tile (8 bytes).
-// The kernel is VALU-bound: the MCU layout comes from an LDS table, lane positions advance by
-// the grid stride without divisions, and the multiplies are 24-bit whenever every multiplied
-// operand fits (always for dequantisation; per row / column for the transforms, with the exact
-// 32-bit wrap path otherwise).
+// Every wave works alone on octets of 8 consecutive blocks: lane (b, r) dequantizes and
+// row-transforms natural row r of block b, then column-transforms column r, then stores row r
+// of the 8x8 pixel tile (8 bytes). The row->column and column->row exchanges go through the
+// wave's own LDS area, ordered by wave barriers only (a wave's LDS operations execute in issue
+// order), so the four waves of a workgroup never wait for each other. Each wave loads kIdctU
+// octets (kIdctU 16-byte chunks per lane) before transforming the first: more bytes in flight
+// per wave is what the HBM needs (the old 32-block, 3-__syncthreads loop sat at ~2.4 TB/s).
+// Multiplies are 24-bit whenever every multiplied operand fits (always for dequantisation;
+// per row / column for the transforms, with the exact 32-bit wrap path otherwise).
 struct IdctGeo {
     int64_t off;     // plane offset of the block's component
     int32_t stride;  // plane stride
@@ -136,17 +139,19 @@ struct IdctGeo {
     int32_t mx, my;  // MCU pitch in pixels in this plane (8*hs, 8*vs)
     int32_t ci;
 };
-__global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+constexpr int kIdctU = 4;
+constexpr int kIdctUnitBlocks = 64;
+__global__ __launch_bounds__(256) void k_idct_any(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                               const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
                                               int64_t coef_cap, int64_t plane_cap) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk) return;
-    __shared__ int32_t qn[3][64];        // natural-order dequant table per component
-    __shared__ IdctGeo geo[kSpecMaxBpm];  // per block-in-MCU
-    __shared__ int32_t rows[32][8][9];   // row-pass output, padded
-    __shared__ uint8_t pix[32][8][8];
-    __shared__ int4 zzb[32][8];          // the blocks as stored: zig-zag order
+    if (d.status != kOk || d.bpm <= kIdctUnitBlocks) return;  // k_idct takes those
+    __shared__ int32_t qn[3][64];          // natural-order dequant table per component
+    __shared__ IdctGeo geo[kSpecMaxBpm];   // per block-in-MCU
+    __shared__ int4 zzb[4][8][8];          // per wave: the octet's blocks as stored (zig-zag order)
+    __shared__ int32_t rows[4][8][8][9];   // per wave: row-pass output, padded
+    __shared__ uint2 pix[4][8][8];         // per wave: 8x8 pixel tiles, one 8-byte row per entry
     const int t = threadIdx.x;
     if (t < 3 * 64) {
         const int ci = t >> 6, n = t & 63;
@@ -160,82 +165,206 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
         geo[t] = IdctGeo{comp_plane_off(d, ci), c.stride, sbx * 8, sby * 8, c.hs * 8, c.vs * 8, ci};
     }
     __syncthreads();
-    const int64_t nblocks = (int64_t)d.mbw * d.mbh * bpm;
-    const int lb = t >> 3, r = t & 7;
+    const uint32_t nblocks = (uint32_t)((int64_t)d.mbw * d.mbh * bpm);
+    const uint32_t noct = (nblocks + 7) >> 3;
+    const int wave = t >> 6, lane = t & 63, lb = lane >> 3, r = lane & 7;
     // natural row r = zig-zag positions kZigOfNat[8r .. 8r+7] of the staged block (byte offsets)
     uint32_t zo[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) zo[j] = 2u * kZigOfNat[r * 8 + j];
-    const uint8_t* zrow = reinterpret_cast<const uint8_t*>(&zzb[lb][0]);
+    const uint8_t* zrow = reinterpret_cast<const uint8_t*>(&zzb[wave][lb][0]);
     const int16_t* A = ac + (int64_t)img * coef_cap * 64;
     const int32_t* D = dcv + (int64_t)img * coef_cap;
     uint8_t* P = planes + (int64_t)img * plane_cap;
     const bool small_mcu = bpm <= kSpecMaxBpm;
-    // lane position (block-in-MCU k, MCU column / row) advanced by the grid stride without
-    // divisions: step = q MCUs + rr blocks, q = qy MCU rows + qx MCU columns
-    const int64_t step = (int64_t)gridDim.x * 32;
-    const int64_t q = step / bpm;
-    const int rr = (int)(step - q * bpm);
-    const int64_t qy = q / mbw;
-    const int qx = (int)(q - qy * mbw);
-    // XCD-aware chunks: workgroups dispatched to one XCD (linear id % 8, gridDim.x a multiple
-    // of 8) take adjacent 32-block chunks, so the partial plane lines they write merge in that
-    // XCD's L2 (measured: k_idct -17%)
-    const int64_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    int64_t n = chunk0 * 32 + lb;
-    const int64_t mcu0 = n / bpm;
-    int k = (int)(n - mcu0 * bpm);
-    int64_t mby = mcu0 / mbw;
-    int mbx = (int)(mcu0 - mby * mbw);
-    for (int64_t base = chunk0 * 32; base < nblocks; base += step) {
-        const bool live = n < nblocks;
-        IdctGeo g;
-        if (small_mcu) {
-            g = geo[k];
-        } else {  // > 16 blocks per MCU: walk the component list
-            int sbx = 0, sby = 0;
-            const int ci = mcu_block_comp(d, k, sbx, sby);
-            const Comp& c = d.c[ci];
-            g = IdctGeo{comp_plane_off(d, ci), c.stride, sbx * 8, sby * 8, c.hs * 8, c.vs * 8, ci};
+    // XCD-aware order: workgroups dispatched to one XCD (linear id % 8, gridDim.x a multiple of
+    // 8) take adjacent octet ranges, so the partial plane lines they write merge in that XCD's L2
+    const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
+    for (uint32_t o0 = wid * kIdctU; o0 < noct; o0 += nw * kIdctU) {
+        int4 c[kIdctU];
+#pragma unroll
+        for (int u = 0; u < kIdctU; ++u) {
+            const uint32_t n = (o0 + u) * 8 + lb;
+            c[u] = n < nblocks ? *reinterpret_cast<const int4*>(A + (int64_t)n * 64 + r * 8) : make_int4(0, 0, 0, 0);
         }
-        if (live) zzb[lb][r] = *reinterpret_cast<const int4*>(A + n * 64 + r * 8);  // a block's 8 lanes share a wave
-        __builtin_amdgcn_wave_barrier();
-        if (live) {
+#pragma unroll
+        for (int u = 0; u < kIdctU; ++u) {
+            const uint32_t n = (o0 + u) * 8 + lb;
+            const bool live = n < nblocks;
+            zzb[wave][lb][r] = c[u];
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t mcu = n / (uint32_t)bpm, k = n - mcu * (uint32_t)bpm;
+            const uint32_t mby = mcu / (uint32_t)mbw, mbx = mcu - mby * (uint32_t)mbw;
+            IdctGeo g;
+            if (small_mcu) {
+                g = geo[k];
+            } else {  // > 16 blocks per MCU: walk the component list
+                int sbx = 0, sby = 0;
+                const int ci = mcu_block_comp(d, (int)k, sbx, sby);
+                const Comp& cc = d.c[ci];
+                g = IdctGeo{comp_plane_off(d, ci), cc.stride, sbx * 8, sby * 8, cc.hs * 8, cc.vs * 8, ci};
+            }
             int16_t s[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) s[j] = *reinterpret_cast<const int16_t*>(zrow + zo[j]);
             int32_t v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = m24(s[j], qn[g.ci][r * 8 + j]);  // int16 x 8-bit: exact
-            if (r == 0 && s[0] == kDcEscape) v[0] = wmul(D[n], qn[g.ci][0]);  // DC outside int16
+            if (r == 0 && s[0] == kDcEscape && live) v[0] = wmul(D[n], qn[g.ci][0]);  // DC outside int16
             if (idct_fast_ok(v)) idct_row<true>(v);
             else idct_row<false>(v);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) rows[lb][r][j] = v[j];
-        }
-        __syncthreads();
-        if (live) {
+            for (int j = 0; j < 8; ++j) rows[wave][lb][r][j] = v[j];
+            __builtin_amdgcn_wave_barrier();
             int32_t col[8];
             uint8_t o[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) col[j] = rows[lb][j][r];
+            for (int j = 0; j < 8; ++j) col[j] = rows[wave][lb][j][r];
             if (idct_fast_ok(col)) idct_col<true>(col, o);
             else idct_col<false>(col, o);
+            uint8_t* pb = reinterpret_cast<uint8_t*>(&pix[wave][lb][0]);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) pix[lb][j][r] = o[j];
+            for (int j = 0; j < 8; ++j) pb[j * 8 + r] = o[j];
+            __builtin_amdgcn_wave_barrier();
+            if (live) {
+                const int64_t y = (int64_t)mby * g.my + g.dy + r, x = (int64_t)mbx * g.mx + g.dx;
+                *reinterpret_cast<uint2*>(P + g.off + y * g.stride + x) = pix[wave][lb][r];
+            }
+            __builtin_amdgcn_wave_barrier();
         }
-        __syncthreads();
-        if (live) {
-            const int64_t y = mby * g.my + g.dy + r, x = (int64_t)mbx * g.mx + g.dx;
-            __builtin_memcpy(P + g.off + y * g.stride + x, &pix[lb][r][0], 8);
+    }
+}
+
+
+// The main IDCT kernel, for MCUs of up to kIdctUnitBlocks blocks (every sampling but the
+// exotic 8x-subsampled ones). A wave's unit of work is kUM horizontally adjacent MCUs of one MCU
+// row (kUM = the largest power of two with kUM * bpm <= 64: 8 MCUs = 48 blocks at 4:2:0). Its
+// blocks are transformed an octet at a time as in k_idct_any, but the pixel tiles land in the
+// wave's LDS copy of the unit's plane rectangles; the wave then writes those rectangles row by
+// row with 8-byte stores of consecutive lanes (128-byte luma rows at 4:2:0) instead of one
+// 8-byte piece per block row: the scattered pieces cost 2x their bytes in HBM writes (PMC).
+struct IdctComp {
+    int64_t off;
+    int32_t stride, mx, my, cpr;  // plane stride, MCU pitch (px), 8-byte chunks per unit row
+};
+__global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                              const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
+                                              int64_t coef_cap, int64_t plane_cap) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    // (bpm is 0 for a descriptor without a frame header: nothing to transform)
+    if (d.status != kOk || d.bpm <= 0 || d.bpm > kIdctUnitBlocks) return;
+    __shared__ int32_t qn[3][64];                // natural-order dequant table per component
+    __shared__ uint32_t bgeo[kIdctUnitBlocks];   // unit block q -> ci | LDS offset of its tile << 2
+    __shared__ IdctComp cg[3];
+    __shared__ int32_t roff[4];                  // LDS offset of each component's rectangle
+    __shared__ int4 zzb[4][8][8];                // per wave: the octet's blocks as stored (zig-zag)
+    __shared__ int32_t rows[4][8][8][9];         // per wave: row-pass output, padded
+    __shared__ uint2 pixu[4][kIdctUnitBlocks * 8];  // per wave: the unit's pixels (64 B per block)
+    const int t = threadIdx.x;
+    const int bpm = d.bpm, mbw = d.mbw, nc = d.nc;
+    int kum = 1;
+    while (kum * 2 * bpm <= kIdctUnitBlocks) kum *= 2;
+    if (t < 3 * 64) {
+        const int ci = t >> 6, n = t & 63;
+        qn[ci][n] = ci < nc ? d.q[d.c[ci].tq][kZigOfNat[n]] : 0;
+    }
+    if (t < 3) {
+        const int ci = t < nc ? t : 0;
+        const Comp& c = d.c[ci];
+        cg[t] = IdctComp{comp_plane_off(d, ci), c.stride, c.hs * 8, c.vs * 8, kum * c.hs};
+    }
+    if (t == 0) {  // rectangles: component c is (kum * 8 hs) x (8 vs) bytes
+        int o = 0;
+        for (int ci = 0; ci < 3; ++ci) {
+            roff[ci] = o;
+            if (ci < nc) o += kum * d.c[ci].hs * 8 * d.c[ci].vs * 8;
         }
-        __syncthreads();
-        n += step;
-        k += rr;
-        mbx += qx;
-        mby += qy;
-        if (k >= bpm) { k -= bpm; ++mbx; }
-        if (mbx >= mbw) { mbx -= mbw; ++mby; }
+        roff[3] = o;
+    }
+    __syncthreads();
+    if (t < kum * bpm) {
+        const int m = t / bpm, k = t - m * bpm;
+        int sbx, sby;
+        const int ci = mcu_block_comp(d, k, sbx, sby);
+        const int wc = kum * d.c[ci].hs * 8;
+        bgeo[t] = (uint32_t)ci | (uint32_t)(roff[ci] + sby * 8 * wc + m * d.c[ci].hs * 8 + sbx * 8) << 2;
+    }
+    __syncthreads();
+    const int wave = t >> 6, lane = t & 63, lb = lane >> 3, r = lane & 7;
+    uint32_t zo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zo[j] = 2u * kZigOfNat[r * 8 + j];
+    const uint8_t* zrow = reinterpret_cast<const uint8_t*>(&zzb[wave][lb][0]);
+    uint8_t* pb = reinterpret_cast<uint8_t*>(&pixu[wave][0]);
+    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
+    const int32_t* D = dcv + (int64_t)img * coef_cap;
+    uint8_t* P = planes + (int64_t)img * plane_cap;
+    const uint32_t ucols = (uint32_t)((mbw + kum - 1) / kum), nunits = ucols * (uint32_t)d.mbh;
+    const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
+    for (uint32_t u = wid; u < nunits; u += nw) {
+        const uint32_t mby = u / ucols, mbx0 = (u - mby * ucols) * (uint32_t)kum;
+        const int cnt = min(kum, mbw - (int)mbx0);            // MCUs in this unit
+        const int nb = cnt * bpm, noct = (nb + 7) >> 3;        // blocks, octets
+        const uint32_t b0 = ((uint32_t)mby * (uint32_t)mbw + mbx0) * (uint32_t)bpm;  // first block
+        for (int o0 = 0; o0 < noct; o0 += kIdctU) {
+            int4 c[kIdctU];
+#pragma unroll
+            for (int k = 0; k < kIdctU; ++k) {
+                const int q = (o0 + k) * 8 + lb;
+                c[k] = q < nb ? *reinterpret_cast<const int4*>(A + (int64_t)(b0 + q) * 64 + r * 8) : make_int4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < kIdctU; ++k) {
+                if (o0 + k >= noct) break;  // wave-uniform
+                const int q = (o0 + k) * 8 + lb;
+                const bool live = q < nb;
+                zzb[wave][lb][r] = c[k];
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t bg = bgeo[live ? q : 0];
+                const int ci = (int)(bg & 3);
+                int16_t s[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s[j] = *reinterpret_cast<const int16_t*>(zrow + zo[j]);
+                int32_t v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = m24(s[j], qn[ci][r * 8 + j]);  // int16 x 8-bit: exact
+                if (r == 0 && s[0] == kDcEscape && live) v[0] = wmul(D[b0 + q], qn[ci][0]);  // DC outside int16
+                if (idct_fast_ok(v)) idct_row<true>(v);
+                else idct_row<false>(v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rows[wave][lb][r][j] = v[j];
+                __builtin_amdgcn_wave_barrier();
+                int32_t col[8];
+                uint8_t ob[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) col[j] = rows[wave][lb][j][r];
+                if (idct_fast_ok(col)) idct_col<true>(col, ob);
+                else idct_col<false>(col, ob);
+                if (live) {
+                    const int wc = cg[ci].cpr * 8;
+                    uint8_t* dst = pb + (bg >> 2) + r;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) dst[j * wc] = ob[j];
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        // the unit's rectangles -> planes: consecutive lanes store consecutive 8-byte chunks
+        for (int ci = 0; ci < nc; ++ci) {
+            const IdctComp g = cg[ci];
+            const int cpr = cnt * (g.mx >> 3);  // live chunks per row (partial unit at a row end)
+            const int total = cpr * g.my;
+            uint8_t* base = P + g.off + (int64_t)mby * g.my * g.stride + (int64_t)mbx0 * g.mx;
+            const uint2* src = &pixu[wave][roff[ci] >> 3];
+            for (int i = lane; i < total; i += 64) {
+                const int row = i / cpr, col = i - row * cpr;
+                *reinterpret_cast<uint2*>(base + (int64_t)row * g.stride + col * 8) = src[row * g.cpr + col];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -799,9 +928,11 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     B(kStIdct);
     const int64_t maxblk = ws.coef_cap;
     // ~16K workgroups per launch in total; every kernel grid-strides over its image's work
-    int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 31) / 32, 16384 / n));
+    int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 32 * kIdctU - 1) / (32 * kIdctU), 16384 / n));
     if (gx >= 8) gx &= ~7;  // XCD-aware chunk order in k_idct needs a multiple of 8
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
+                       ws.plane_cap);
+    hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap);
     E(kStIdct);
     B(kStUpsample);

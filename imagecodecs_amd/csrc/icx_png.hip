@@ -383,69 +383,100 @@ __device__ __forceinline__ int match_len(const uint8_t* F, int64_t p, int64_t di
     return l;
 }
 
-// One workgroup per 256 KiB block, one lane per 4 KiB segment.
-__global__ __launch_bounds__(kSegPerBlock) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
-                                                 int bw, uint32_t* __restrict__ tok, uint32_t* __restrict__ ntok,
-                                                 uint32_t* __restrict__ hist, uint32_t* __restrict__ adl) {
+// One workgroup (4 waves) per 256 KiB block; each wave takes a 4 KiB segment at a time and
+// walks it in 64-position windows: every lane scores the position under it against the six
+// structural candidates (left pixel, up to two pixels back, the pixel above and its two
+// neighbours) with coalesced loads, then the wave parses the window greedily with ballots --
+// the literal run up to the first position with a match is emitted by all lanes at once, the
+// match by one. The tokens are those of a serial greedy parse (first match of length >= 3 per
+// position, longest over the candidates, never crossing the segment end).
+__global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
+                                                  int bw, uint32_t* __restrict__ tok, uint32_t* __restrict__ ntok,
+                                                  uint32_t* __restrict__ hist, uint32_t* __restrict__ adl) {
     __shared__ uint32_t h_ll[kNLL], h_d[kND];
     const int64_t blk = blockIdx.x;
-    for (int i = threadIdx.x; i < kNLL; i += kSegPerBlock) h_ll[i] = 0;
+    for (int i = threadIdx.x; i < kNLL; i += 256) h_ll[i] = 0;
     if (threadIdx.x < kND) h_d[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t seg = blk * kSegPerBlock + threadIdx.x;
-    if (seg < nseg) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t cand[6] = {1, bw, 2 * bw, rowlen, rowlen - bw, rowlen + bw};
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (cand[k] <= 0 || cand[k] > 32768) cand[k] = 0;
+    for (int sl = wave; sl < kSegPerBlock; sl += 4) {
+        const int64_t seg = blk * kSegPerBlock + sl;
+        if (seg >= nseg) break;  // wave-uniform
         const int64_t s0 = seg * kSeg, s1 = min(N, s0 + kSeg);
         uint32_t* T = tok + s0;
+        // Adler-32 partials: sum b, sum (N - g) b (reduced mod 65521 at the end)
+        uint64_t a1 = 0, a2 = 0;
+        for (int64_t q = s0 + lane; q < s1; q += 64) {
+            const uint32_t b = F[q];
+            a1 += b;
+            a2 += (uint64_t)(N - q) * b;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            a1 += __shfl_xor(a1, o);
+            a2 += __shfl_xor(a2, o);
+        }
+        if (lane == 0) {
+            adl[2 * seg] = (uint32_t)(a1 % kAdlerMod);
+            adl[2 * seg + 1] = (uint32_t)(a2 % kAdlerMod);
+        }
         uint32_t nt = 0;
-        int64_t cand[6] = {1, bw, 2 * bw, rowlen, rowlen - bw, rowlen + bw};
+        int64_t pos = s0;  // first position not yet covered by a token
+        for (int64_t p0 = s0; p0 < s1; p0 += 64) {
+            const int64_t q = p0 + lane;
+            int best = 0, bd = 0;
+            uint32_t lit = 0;
+            if (q < s1) {
+                lit = F[q];
+                const int64_t maxlen = min((int64_t)258, s1 - q);
+                if (maxlen >= 3 && q >= pos) {  // positions under a previous match need no score
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
-            if (cand[k] <= 0 || cand[k] > 32768) cand[k] = 0;
-        uint64_t a1 = 0, a2 = 0;  // Adler-32 partials: sum b, sum (N - g) b (reduced at the end)
-        uint32_t wgt = (uint32_t)((N - s0) % kAdlerMod);  // (N - g) mod 65521 for g = p
-        int64_t p = s0;
-        while (p < s1) {
-            const int64_t maxlen = min((int64_t)258, s1 - p);
-            int best = 0;
-            int64_t bd = 0;
-            if (maxlen >= 3) {
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    const int64_t dd = cand[k];
-                    if (dd == 0 || dd > p) continue;
-                    if (F[p] != F[p - dd] || F[p + 1] != F[p - dd + 1] || F[p + 2] != F[p - dd + 2]) continue;
-                    const int l = 3 + match_len(F, p + 3, dd, maxlen - 3);
-                    if (l > best) {
-                        best = l;
-                        bd = dd;
+                    for (int k = 0; k < 6; ++k) {
+                        const int64_t dd = cand[k];
+                        if (dd == 0 || dd > q) continue;
+                        if (F[q] != F[q - dd] || F[q + 1] != F[q - dd + 1] || F[q + 2] != F[q - dd + 2]) continue;
+                        const int l = 3 + match_len(F, q + 3, dd, maxlen - 3);
+                        if (l > best) {
+                            best = l;
+                            bd = (int)dd;
+                        }
                     }
                 }
             }
-            const int adv = best >= 3 ? best : 1;
-            for (int k = 0; k < adv; ++k) {
-                const uint32_t b = F[p + k];
-                a1 += b;
-                a2 += (uint64_t)wgt * b;
-                wgt = wgt ? wgt - 1 : kAdlerMod - 1;
+            const uint64_t cmask = __ballot(best >= 3);
+            const int wend = (int)min((int64_t)64, s1 - p0);  // live lanes of this window
+            while (pos < p0 + wend) {  // wave-uniform
+                const int li = (int)(pos - p0);
+                const uint64_t m = cmask & (~0ull << li);
+                const int mi = m ? __ffsll((unsigned long long)m) - 1 : 64;
+                const int le = min(mi, wend);
+                if (lane >= li && lane < le) {  // the literal run li .. le-1
+                    T[nt + (lane - li)] = lit;
+                    atomicAdd(&h_ll[lit], 1u);
+                }
+                nt += (uint32_t)(le - li);
+                pos = p0 + le;
+                if (mi < wend) {  // the match at lane mi
+                    const int len = __shfl(best, mi), dist = __shfl(bd, mi);
+                    if (lane == 0) {
+                        T[nt] = 0x80000000u | (uint32_t)(len - 3) << 15 | (uint32_t)(dist - 1);
+                        atomicAdd(&h_ll[257 + len_code(len)], 1u);
+                        atomicAdd(&h_d[dist_code(dist)], 1u);
+                    }
+                    ++nt;
+                    pos += len;
+                }
             }
-            if (best >= 3) {
-                T[nt++] = 0x80000000u | (uint32_t)(best - 3) << 15 | (uint32_t)(bd - 1);
-                atomicAdd(&h_ll[257 + len_code(best)], 1u);
-                atomicAdd(&h_d[dist_code((int)bd)], 1u);
-            } else {
-                const uint32_t b = F[p];
-                T[nt++] = b;
-                atomicAdd(&h_ll[b], 1u);
-            }
-            p += adv;
         }
-        ntok[seg] = nt;
-        adl[2 * seg] = (uint32_t)(a1 % kAdlerMod);
-        adl[2 * seg + 1] = (uint32_t)(a2 % kAdlerMod);
+        if (lane == 0) ntok[seg] = nt;
     }
     __syncthreads();
     uint32_t* H = hist + blk * (kNLL + kND);
-    for (int i = threadIdx.x; i < kNLL; i += kSegPerBlock) H[i] = h_ll[i] + (i == 256 ? 1u : 0u);  // + EOB
+    for (int i = threadIdx.x; i < kNLL; i += 256) H[i] = h_ll[i] + (i == 256 ? 1u : 0u);  // + EOB
     if (threadIdx.x < kND) H[kNLL + threadIdx.x] = h_d[threadIdx.x];
 }
 
@@ -673,91 +704,121 @@ __device__ __forceinline__ uint32_t token_bits(const BlockCodes& B, uint32_t t) 
     return B.ll_len[257 + lc] + kLenExtra[lc] + B.d_len[dc] + kDistExtra[dc];
 }
 
+// One wave per segment: lanes sum the bit lengths of every 64th token.
 __global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint32_t* __restrict__ tok,
                                                      const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
                                                      unsigned long long* __restrict__ bits) {
-    const int64_t seg = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (seg >= nseg) return;
+    const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (seg >= nseg) return;  // wave-uniform
     const int64_t blk = seg / kSegPerBlock;
     const BlockCodes& B = bc[blk];
     const uint32_t* T = tok + seg * kSeg;
     const uint32_t nt = ntok[seg];
-    unsigned long long b = 0;
-    if (seg % kSegPerBlock == 0) b += B.hdr_bits;
-    for (uint32_t i = 0; i < nt; ++i) b += token_bits(B, T[i]);
-    if (seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1) b += B.ll_len[256];  // EOB
-    bits[seg] = b;
+    uint32_t b = 0;
+    for (uint32_t i = lane; i < nt; i += 64) b += token_bits(B, T[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o);
+    if (lane == 0) {
+        unsigned long long t = b;
+        if (seg % kSegPerBlock == 0) t += B.hdr_bits;
+        if (seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1) t += B.ll_len[256];  // EOB
+        bits[seg] = t;
+    }
 }
 
-// Bit writer for one segment: words strictly inside the segment's range are stored, the two
-// boundary words are OR-ed in (shared with the neighbouring segments); `out` was zeroed.
-struct SegWriter {
-    uint32_t* out;
-    unsigned long long pos;  // bit position of acc's bit 0
-    uint64_t acc = 0;
-    int nacc = 0;
-    unsigned long long first_word, last_word;
-    __device__ void flush_word(uint32_t v) {
-        const unsigned long long wi = pos >> 5;
-        if (wi == first_word || wi == last_word) atomicOr(out + wi, v);
-        else out[wi] = v;
-        pos += 32;
+// Token -> (bits, count), LSB-first: code, length extra, distance code, distance extra
+// (at most 15 + 5 + 15 + 13 = 48 bits).
+__device__ __forceinline__ uint64_t token_code(const BlockCodes& B, uint32_t t, int& nb) {
+    if (!(t & 0x80000000u)) {
+        nb = B.ll_len[t];
+        return B.ll_code[t];
     }
-    __device__ void put(uint32_t v, int nb) {
-        if (!nb) return;
-        acc |= (uint64_t)v << nacc;
-        nacc += nb;
-        if (nacc >= 32) {
-            flush_word((uint32_t)acc);
-            acc >>= 32;
-            nacc -= 32;
-        }
-    }
-    __device__ void finish() {
-        if (nacc > 0) flush_word((uint32_t)acc);
-    }
-};
+    const int len = (int)((t >> 15) & 255) + 3, dist = (int)(t & 0x7FFF) + 1;
+    const int lc = len_code(len), dc = dist_code(dist);
+    uint64_t v = B.ll_code[257 + lc];
+    int n = B.ll_len[257 + lc];
+    v |= (uint64_t)(len - kLenBase[lc]) << n;
+    n += kLenExtra[lc];
+    v |= (uint64_t)B.d_code[dc] << n;
+    n += B.d_len[dc];
+    v |= (uint64_t)(dist - kDistBase[dc]) << n;
+    nb = n + kDistExtra[dc];
+    return v;
+}
 
+// One wave per segment: each round of 64 tokens gets bit offsets from a wave prefix sum and is
+// OR-ed into the wave's LDS image of the segment's output words (aligned to the output's word
+// grid), which then leaves with coalesced stores -- the two boundary words (shared with the
+// neighbouring segments) with atomicOr. Segments whose bits exceed the LDS image (pathological
+// token mixes only) OR their words straight into the output.
+constexpr int kEmitWords = 2048;  // 64 Kbit per wave (a 4 KiB segment averages ~22 Kbit)
+__device__ __forceinline__ void or_bits(uint32_t* w, unsigned long long bitpos, uint64_t v, int nb) {
+    if (!nb) return;
+    const unsigned long long wi = bitpos >> 5;
+    const int sh = (int)(bitpos & 31);
+    const uint64_t hi = sh ? (v >> (32 - sh)) : (v >> 32);  // the bits above word wi
+    atomicOr(w + wi, (uint32_t)(v << sh));
+    if (sh + nb > 32) atomicOr(w + wi + 1, (uint32_t)hi);
+    if (sh + nb > 64) atomicOr(w + wi + 2, (uint32_t)(hi >> 32));
+}
+// The segment's bits into W (word 0 = output word w0; zeroed), starting at bit `pos`.
+__device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos, const BlockCodes& B,
+                                             const uint32_t* T, uint32_t nt, bool head, bool eob, int lane) {
+    if (head) {  // the block header: its words, shifted into place
+        const uint32_t hb = B.hdr_bits;
+        for (uint32_t i = lane; i * 32 < hb; i += 64) {
+            const int n = (int)min(32u, hb - i * 32);
+            or_bits(W, pos + i * 32, n == 32 ? B.hdr[i] : (B.hdr[i] & ((1u << n) - 1u)), n);
+        }
+        pos += hb;
+    }
+    for (uint32_t i0 = 0; i0 < nt; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        int nb = 0;
+        const uint64_t v = i < nt ? token_code(B, T[i], nb) : 0;
+        uint32_t inc = (uint32_t)nb;  // inclusive scan of nb over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o);
+            if (lane >= o) inc += u;
+        }
+        or_bits(W, pos + inc - nb, v, nb);
+        pos += __shfl(inc, 63);
+    }
+    if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
+}
 __global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint32_t* __restrict__ tok,
                                                   const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
                                                   const unsigned long long* __restrict__ off,
                                                   const unsigned long long* __restrict__ bits, uint32_t* __restrict__ out,
                                                   unsigned long long base_bits) {
-    const int64_t seg = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (seg >= nseg) return;
-    const int64_t blk = seg / kSegPerBlock;
-    const BlockCodes& B = bc[blk];
+    __shared__ uint32_t img[4][kEmitWords];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t seg = (int64_t)blockIdx.x * 4 + wave;
+    if (seg >= nseg) return;  // wave-uniform; no block barriers below
+    const BlockCodes& B = bc[seg / kSegPerBlock];
     const uint32_t* T = tok + seg * kSeg;
     const uint32_t nt = ntok[seg];
     const unsigned long long o0 = base_bits + off[seg], o1 = o0 + bits[seg];
     if (o1 == o0) return;
-    SegWriter w;
-    w.out = out;
-    w.pos = o0 & ~31ull;
-    w.nacc = (int)(o0 & 31);
-    w.first_word = o0 >> 5;
-    w.last_word = (o1 - 1) >> 5;
-    if (seg % kSegPerBlock == 0)
-        for (uint32_t b = 0; b < B.hdr_bits; b += 16) {
-            const uint32_t n = min(16u, B.hdr_bits - b);
-            const uint32_t v = (B.hdr[b >> 5] >> (b & 31)) & ((1u << n) - 1u);  // 16-bit pieces stay in one word
-            w.put(v, (int)n);
-        }
-    for (uint32_t i = 0; i < nt; ++i) {
-        const uint32_t t = T[i];
-        if (!(t & 0x80000000u)) {
-            w.put(B.ll_code[t], B.ll_len[t]);
-        } else {
-            const int len = (int)((t >> 15) & 255) + 3, dist = (int)(t & 0x7FFF) + 1;
-            const int lc = len_code(len), dc = dist_code(dist);
-            w.put(B.ll_code[257 + lc], B.ll_len[257 + lc]);
-            w.put((uint32_t)(len - kLenBase[lc]), kLenExtra[lc]);
-            w.put(B.d_code[dc], B.d_len[dc]);
-            w.put((uint32_t)(dist - kDistBase[dc]), kDistExtra[dc]);
-        }
+    const unsigned long long w0 = o0 >> 5, wl = (o1 - 1) >> 5;  // first / last output word
+    const int nw = (int)(wl - w0 + 1);
+    const bool head = seg % kSegPerBlock == 0, eob = seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1;
+    if (nw > kEmitWords) {  // straight into the (zeroed) output
+        emit_segment(out + w0, o0 & 31, B, T, nt, head, eob, lane);
+        return;
     }
-    if (seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1) w.put(B.ll_code[256], B.ll_len[256]);
-    w.finish();
+    uint32_t* W = img[wave];
+    for (int i = lane; i < nw; i += 64) W[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    emit_segment(W, o0 & 31, B, T, nt, head, eob, lane);
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < nw; i += 64) {
+        const uint32_t v = W[i];
+        if (i == 0 || i == nw - 1) atomicOr(out + w0 + i, v);  // shared with the neighbours
+        else out[w0 + i] = v;
+    }
 }
 
 // ------------------------------------------------------------------------------- CRC-32
@@ -1108,13 +1169,13 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     size_t c11 = ws->small ? 64 : 0;
     if (!pgrow(ws->small, 64, c11)) return -1;
     mark(4);
-    hipLaunchKernelGGL(k_png_lz77, dim3((unsigned)nblk), dim3(kSegPerBlock), 0, st, ws->filt, N, nseg, 1 + M.lb, M.bw, ws->tok,
+    hipLaunchKernelGGL(k_png_lz77, dim3((unsigned)nblk), dim3(256), 0, st, ws->filt, N, nseg, 1 + M.lb, M.bw, ws->tok,
                        ws->ntok, ws->hist, ws->adl);
     mark(5);
     mark(6);
     hipLaunchKernelGGL(k_png_huff, dim3((unsigned)nblk), dim3(64), 0, st, ws->hist, nblk, ws->bc);
-    const unsigned gseg = (unsigned)((nseg + 255) / 256);
-    hipLaunchKernelGGL(k_png_segbits, dim3(gseg), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->bits);
+    const unsigned gwave = (unsigned)((nseg + 3) / 4);  // one wave per segment
+    hipLaunchKernelGGL(k_png_segbits, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->bits);
     size_t tb = 0;
     PNG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ws->bits, ws->off, (int)nseg, st));
     if (!pgrow(ws->tmp, tb, ws->tmp_cap)) return -1;
@@ -1141,7 +1202,7 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     const unsigned long long base_bits = (dstart - wbase) * 8;
     PNG_HIP(hipMemsetAsync(d_out + wbase, 0, ((dbytes + (dstart - wbase) + 3) & ~3ull) + 4, st));
     mark(8);
-    hipLaunchKernelGGL(k_png_emit, dim3(gseg), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->off, ws->bits,
+    hipLaunchKernelGGL(k_png_emit, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->off, ws->bits,
                        reinterpret_cast<uint32_t*>(d_out + wbase), base_bits);
     mark(9);
     // signature + IHDR/PLTE/tRNS + IDAT length/type + zlib header (78 01, :1932-1941)
