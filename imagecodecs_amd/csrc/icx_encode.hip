@@ -1,9 +1,10 @@
 // icx_encode.hip -- gfx950 JPEG encoder: tiny_jpeg-exact (jpeg_enc.h:786-1175) and the C4
 // extension (4:2:0 / 4:4:4, IJG quality; defined by oracle/tje_oracle.c or_jpeg_encode).
 //
-//   k_enc_units   gather + float RGB->YCbCr (+ 2x2 chroma mean for 4:2:0) + AAN float FDCT +
-//                 quantize, one lane per data unit in MCU order (jpeg_enc.h:1094-1126, 656-817)
-//   k_enc_count   Huffman bit length of every unit            (jpeg_enc.h:831-887)
+//   k_enc_units   gather + float RGB->YCbCr (+ 2x2 chroma mean for 4:2:0) staged in LDS per
+//                 512-pixel run, then one lane per data unit: AAN float FDCT + quantize + the
+//                 AC bit length (jpeg_enc.h:1094-1126, 656-817, 851-887)
+//   k_enc_count   adds the DC code length of every unit       (jpeg_enc.h:831-849)
 //   (scan)        exclusive prefix sum of unit bit lengths -> bit offsets (hipCUB)
 //   k_enc_emit    pack each unit's codes at its bit offset    (jpeg_enc.h:613-643)
 //   k_stuff_*     FF -> FF 00 byte stuffing by count/scan/copy (jpeg_enc.h:634-638)
@@ -42,11 +43,6 @@ __device__ __forceinline__ int64_t pred_unit(const EncLayout& L, int64_t u) {  /
     return m > 0 ? (m - 1) * L.upm + L.lastk[L.comp[k]] : -1;
 }
 
-__constant__ static const uint8_t kZigOfNatE[64] = {
-    0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43,
-    9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
-    21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
-
 // AAN float FDCT on 8 samples at stride S (tjei_fdct, jpeg_enc.h:667-712), in registers.
 template <int S>
 __device__ __forceinline__ void fdct8(float* p) {
@@ -72,57 +68,14 @@ __device__ __forceinline__ void fdct8(float* p) {
     p[7 * S] = z11 - z4;
 }
 
-__global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ src, int w, int h, int comps,
-                                                   EncLayout L, int64_t nunits, const EncTables* __restrict__ T,
-                                                   int16_t* __restrict__ zz) {
-    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nunits) return;
-    const int64_t m = u / L.upm;
-    const int k = (int)(u - m * L.upm);
-    const int c = L.comp[k];
-    const int mx = (int)(m % L.mbw), my = (int)(m / L.mbw);
-    auto pix = [&](int x, int y) {  // edge clamp (jpeg_enc.h:1106-1111)
-        return src + ((int64_t)min(y, h - 1) * w + min(x, w - 1)) * comps;
-    };
-    auto ycc = [&](const uint8_t* p) {  // jpeg_enc.h:1118-1120, evaluated left to right
-        const uint8_t r = p[0], g = p[1], b = p[2];
-        if (c == 0) return 0.299f * r + 0.587f * g + 0.114f * b - 128;
-        if (c == 1) return -0.1687f * r - 0.3313f * g + 0.5f * b;
-        return 0.5f * r - 0.4187f * g - 0.0813f * b;
-    };
-    float f[64];
-    if (c != 0 && L.sub) {  // 4:2:0 chroma: ((a + b) + (c + d)) * 0.25f of the per-pixel values
-        const int x0 = mx * L.ms, y0 = my * L.ms;
-#pragma unroll
-        for (int oy = 0; oy < 8; ++oy)
-#pragma unroll
-            for (int ox = 0; ox < 8; ++ox) {
-                const int x = x0 + 2 * ox, y = y0 + 2 * oy;
-                const float a = ycc(pix(x, y)), b = ycc(pix(x + 1, y));
-                const float cc = ycc(pix(x, y + 1)), d = ycc(pix(x + 1, y + 1));
-                f[oy * 8 + ox] = ((a + b) + (cc + d)) * 0.25f;
-            }
-    } else {
-        const int x0 = mx * L.ms + L.bx[k] * 8, y0 = my * L.ms + L.by[k] * 8;
-#pragma unroll
-        for (int oy = 0; oy < 8; ++oy)
-#pragma unroll
-            for (int ox = 0; ox < 8; ++ox) f[oy * 8 + ox] = ycc(pix(x0 + ox, y0 + oy));
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) fdct8<1>(f + 8 * r);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) fdct8<8>(f + q);
-    const float* pq = T->pq[c ? 1 : 0];
-    int16_t* o = zz + u * 64;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {  // jpeg_enc.h:806-817
-        float v = f[i];
-        v *= pq[i];
-        v = floorf(v + 1024 + 0.5f);
-        v -= 1024;
-        o[kZigOfNatE[i]] = (int16_t)(int)v;
-    }
+// Zig-zag position of natural index i as a compile-time function: after unrolling, every block
+// store index is a constant and the quantised block stays in registers.
+constexpr int zig_of_nat(int i) {
+    constexpr uint8_t t[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                               3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                               10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                               21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+    return t[i];
 }
 
 __device__ __forceinline__ void vli(int v, int& nb, uint32_t& bits) {  // jpeg_enc.h:598-610
@@ -130,6 +83,118 @@ __device__ __forceinline__ void vli(int v, int& nb, uint32_t& bits) {  // jpeg_e
     if (v < 0) --v;
     nb = mag ? 32 - __clz(mag) : 1;
     bits = (uint32_t)v & ((1u << nb) - 1u);
+}
+
+// A workgroup owns a 512-pixel run of one MCU row (64 MCUs at 4:4:4, 32 at 4:2:0; 192 data units
+// either way). Phase 1: all lanes read the run's pixels (coalesced, edge-clamped as
+// jpeg_enc.h:1106-1111) and write the samples the units use to LDS -- Y per pixel, Cb/Cr per pixel
+// (4:4:4) or per 2x2 mean (4:2:0), each with the reference's float expression and order
+// (:1118-1120). Phase 2: one lane per data unit: 8x8 samples from LDS, AAN FDCT, quantise
+// (:806-817), the zig-zag block as eight 16-byte stores, and the AC part of its Huffman bit length
+// (the DC part needs the previous unit's DC: k_enc_count adds it).
+constexpr int kRunPx = 512;
+__global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ src, int w, int h, int comps,
+                                                   EncLayout L, int runs_per_row, const EncTables* __restrict__ T,
+                                                   int16_t* __restrict__ zz, uint64_t* __restrict__ nbits) {
+    __shared__ float S[3 * 8 * kRunPx];  // 4:4:4: Y|Cb|Cr, 8 x 512 each; 4:2:0: Y 16 x 512 | Cb|Cr 8 x 256
+    __shared__ float pq[2][64];
+    __shared__ uint8_t aclen[2][256];
+    const int t = threadIdx.x;
+    if (t < 128) pq[t >> 6][t & 63] = T->pq[t >> 6][t & 63];
+    aclen[0][t] = T->len[1][t];
+    aclen[1][t] = T->len[3][t];
+    const int my = blockIdx.x / runs_per_row, rx = blockIdx.x - my * runs_per_row;
+    const int x0 = rx * kRunPx, y0 = my * L.ms;
+    const int mcu0 = x0 / L.ms, nm = min(kRunPx / L.ms, L.mbw - mcu0), wpx = nm * L.ms;
+    auto pix = [&](int x, int y) { return src + ((int64_t)min(y, h - 1) * w + min(x, w - 1)) * comps; };
+    auto ycc = [](const uint8_t* p, int c) {  // jpeg_enc.h:1118-1120, evaluated left to right
+        const uint8_t r = p[0], g = p[1], b = p[2];
+        if (c == 0) return 0.299f * r + 0.587f * g + 0.114f * b - 128;
+        if (c == 1) return -0.1687f * r - 0.3313f * g + 0.5f * b;
+        return 0.5f * r - 0.4187f * g - 0.0813f * b;
+    };
+    constexpr int kHalf = kRunPx / 2;
+    if (L.sub) {  // 2x2 quads; chroma = ((a + b) + (c + d)) * 0.25f of the per-pixel values
+        for (int qd = t; qd < kHalf * 8; qd += 256) {
+            const int qy = qd / kHalf, qx = qd - qy * kHalf;
+            if (2 * qx >= wpx) continue;
+            const int x = x0 + 2 * qx, y = y0 + 2 * qy;
+            const uint8_t *p00 = pix(x, y), *p10 = pix(x + 1, y), *p01 = pix(x, y + 1), *p11 = pix(x + 1, y + 1);
+            float* Y = S + 2 * qy * kRunPx + 2 * qx;
+            Y[0] = ycc(p00, 0);
+            Y[1] = ycc(p10, 0);
+            Y[kRunPx] = ycc(p01, 0);
+            Y[kRunPx + 1] = ycc(p11, 0);
+#pragma unroll
+            for (int c = 1; c < 3; ++c) {
+                const float a = ycc(p00, c), b = ycc(p10, c), cc = ycc(p01, c), d = ycc(p11, c);
+                S[16 * kRunPx + (c - 1) * 8 * kHalf + qy * kHalf + qx] = ((a + b) + (cc + d)) * 0.25f;
+            }
+        }
+    } else {
+        for (int i = t; i < kRunPx * 8; i += 256) {
+            const int yy = i / kRunPx, xx = i - yy * kRunPx;
+            if (xx >= wpx) continue;
+            const uint8_t* p = pix(x0 + xx, y0 + yy);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) S[c * 8 * kRunPx + yy * kRunPx + xx] = ycc(p, c);
+        }
+    }
+    __syncthreads();
+    if (t >= nm * L.upm) return;
+    const int ml = t / L.upm, k = t - ml * L.upm, c = L.comp[k];
+    const float* base;
+    int pitch = kRunPx;
+    if (!L.sub) base = S + c * 8 * kRunPx + ml * 8;
+    else if (c == 0) base = S + L.by[k] * 8 * kRunPx + ml * 16 + L.bx[k] * 8;
+    else { base = S + 16 * kRunPx + (c - 1) * 8 * kHalf + ml * 8; pitch = kHalf; }
+    float f[64];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const float4 lo = *reinterpret_cast<const float4*>(base + r * pitch);
+        const float4 hi = *reinterpret_cast<const float4*>(base + r * pitch + 4);
+        f[8 * r + 0] = lo.x; f[8 * r + 1] = lo.y; f[8 * r + 2] = lo.z; f[8 * r + 3] = lo.w;
+        f[8 * r + 4] = hi.x; f[8 * r + 5] = hi.y; f[8 * r + 6] = hi.z; f[8 * r + 7] = hi.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) fdct8<1>(f + 8 * r);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) fdct8<8>(f + q);
+    const float* pqc = pq[c ? 1 : 0];
+    int o[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {  // jpeg_enc.h:806-817
+        float v = f[i];
+        v *= pqc[i];
+        v = floorf(v + 1024 + 0.5f);
+        v -= 1024;
+        o[zig_of_nat(i)] = (int)v;
+    }
+    const int64_t u = ((int64_t)my * L.mbw + mcu0 + ml) * L.upm + k;
+    int4* dst = reinterpret_cast<int4*>(zz + u * 64);
+    auto pk = [](int a, int b) { return (int)(((uint32_t)a & 0xFFFFu) | ((uint32_t)b << 16)); };
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        dst[q] = make_int4(pk(o[8 * q], o[8 * q + 1]), pk(o[8 * q + 2], o[8 * q + 3]), pk(o[8 * q + 4], o[8 * q + 5]),
+                           pk(o[8 * q + 6], o[8 * q + 7]));
+    // AC codes (jpeg_enc.h:851-887): a ZRL per 16 zeros before a nonzero coefficient, (run, size)
+    // symbol + amplitude bits, EOB unless coefficient 63 is nonzero
+    const uint8_t* al = aclen[c ? 1 : 0];
+    uint32_t bits = 0;
+    int run = 0;
+#pragma unroll
+    for (int i = 1; i < 64; ++i) {
+        const int v = (int16_t)o[i];
+        if (v) {
+            const int mag = v < 0 ? -v : v, nb = 32 - __clz(mag);
+            bits += (uint32_t)((run >> 4) * al[0xF0] + al[((run & 15) << 4) | nb] + nb);
+            run = 0;
+        } else {
+            ++run;
+        }
+    }
+    if (!(int16_t)o[63]) bits += al[0];
+    nbits[u] = bits;
 }
 
 // Visit every (length, bits) code of one unit in stream order (jpeg_enc.h:831-887).
@@ -164,16 +229,19 @@ __device__ __forceinline__ void unit_codes(const int16_t* zz, int pred, const En
     if (last != 63) put(T->len[ta][0], T->code[ta][0]);
 }
 
+// Adds the DC code length (jpeg_enc.h:834-849) to the AC bits k_enc_units stored.
 __global__ __launch_bounds__(256) void k_enc_count(const int16_t* __restrict__ zz, int64_t nunits, EncLayout L,
                                                    const EncTables* __restrict__ T, uint64_t* __restrict__ nbits) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nunits) return;
-    const int c = L.comp[u % L.upm];
+    const int c = L.comp[u % L.upm], td = c ? 2 : 0;
     const int64_t pu = pred_unit(L, u);
     const int pred = pu >= 0 ? zz[pu * 64] : 0;  // DC predictor never resets (:834-835)
-    uint64_t total = 0;
-    unit_codes(zz + u * 64, pred, T, c, [&](int n, uint32_t) { total += (uint64_t)n; });
-    nbits[u] = total;
+    const int diff = zz[u * 64] - pred;
+    int nb = 0;
+    uint32_t bits;
+    if (diff) vli(diff, nb, bits);
+    nbits[u] += (uint64_t)(T->len[td][nb] + nb);
 }
 
 // Stream words hold bits MSB-first: word k covers stream bits [32k, 32k+32).
@@ -482,7 +550,9 @@ static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const 
         if (ev) (void)hipEventRecord(ws.ev[i], st);
     };
     mark(0);
-    hipLaunchKernelGGL(k_enc_units, dim3(gu), dim3(TB), 0, st, d_src, w, h, comps, L, nunits, ws.T, ws.zz);
+    const int runs_per_row = (L.mbw * L.ms + kRunPx - 1) / kRunPx;
+    hipLaunchKernelGGL(k_enc_units, dim3((unsigned)(runs_per_row * mbh)), dim3(TB), 0, st, d_src, w, h, comps, L,
+                       runs_per_row, ws.T, ws.zz, ws.nb);
     mark(1);
     mark(2);
     hipLaunchKernelGGL(k_enc_count, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.nb);
