@@ -197,38 +197,6 @@ __global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ s
     nbits[u] = bits;
 }
 
-// Visit every (length, bits) code of one unit in stream order (jpeg_enc.h:831-887).
-template <class F>
-__device__ __forceinline__ void unit_codes(const int16_t* zz, int pred, const EncTables* T, int c, F&& put) {
-    const int td = c ? 2 : 0, ta = c ? 3 : 1;
-    int nb;
-    uint32_t bits;
-    const int diff = zz[0] - pred;
-    if (diff) {
-        vli(diff, nb, bits);
-        put(T->len[td][nb], T->code[td][nb]);
-        put(nb, bits);
-    } else {
-        put(T->len[td][0], T->code[td][0]);
-    }
-    int last = 0;
-    for (int i = 63; i > 0; --i)
-        if (zz[i]) { last = i; break; }
-    for (int i = 1; i <= last; ++i) {
-        int run = 0;
-        while (zz[i] == 0) {
-            ++run;
-            ++i;
-            if (run == 16) { put(T->len[ta][0xF0], T->code[ta][0xF0]); run = 0; }
-        }
-        vli(zz[i], nb, bits);
-        const int sym = (run << 4) | nb;
-        put(T->len[ta][sym], T->code[ta][sym]);
-        put(nb, bits);
-    }
-    if (last != 63) put(T->len[ta][0], T->code[ta][0]);
-}
-
 // Adds the DC code length (jpeg_enc.h:834-849) to the AC bits k_enc_units stored.
 __global__ __launch_bounds__(256) void k_enc_count(const int16_t* __restrict__ zz, int64_t nunits, EncLayout L,
                                                    const EncTables* __restrict__ T, uint64_t* __restrict__ nbits) {
@@ -244,65 +212,158 @@ __global__ __launch_bounds__(256) void k_enc_count(const int16_t* __restrict__ z
     nbits[u] += (uint64_t)(T->len[td][nb] + nb);
 }
 
-// Stream words hold bits MSB-first: word k covers stream bits [32k, 32k+32).
+// Stream words hold bits MSB-first: word k covers stream bits [32k, 32k+32). One lane per unit:
+// its zig-zag block is loaded once (eight 16-byte loads) and walked with a fully unrolled
+// coefficient loop, so every coefficient is a register; code tables come from LDS. Codes are
+// appended to a 64-bit accumulator and every completed word is stored; only words shared with a
+// neighbouring unit (the first, when the unit starts mid-word, and the last) use atomicOr.
+// Code order as tjei_encode_and_write_MCU (jpeg_enc.h:831-887): DC diff (never reset), then per
+// nonzero AC coefficient a ZRL per 16 preceding zeros, the (run, size) symbol and its amplitude
+// bits, and EOB unless coefficient 63 is nonzero.
 __global__ __launch_bounds__(256) void k_enc_emit(const int16_t* __restrict__ zz, int64_t nunits, EncLayout L,
                                                   const EncTables* __restrict__ T, const uint64_t* __restrict__ off,
+                                                  const uint64_t* __restrict__ nbits, uint64_t cap_bits,
                                                   uint32_t* __restrict__ words) {
+    __shared__ uint32_t tab[4][256];  // code << 8 | len
+    for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i >> 8][i & 255] = (uint32_t)T->code[i >> 8][i & 255] << 8 | T->len[i >> 8][i & 255];
+    __syncthreads();
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nunits) return;
+    if (u >= nunits || off[u] + nbits[u] + 32 > cap_bits) return;  // past the words buffer: host re-runs
     const int c = L.comp[u % L.upm];
     const int64_t pu = pred_unit(L, u);
     const int pred = pu >= 0 ? zz[pu * 64] : 0;
-    uint64_t pos = off[u];
-    uint64_t wi = pos >> 5;
-    uint32_t acc = 0;
-    unit_codes(zz + u * 64, pred, T, c, [&](int n, uint32_t v) {
-        if (!n) return;
-        v &= (n == 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
-        while (n > 0) {
-            const int o = (int)(pos & 31);
-            const int take = min(n, 32 - o);
-            const uint32_t part = (v >> (n - take)) & ((take == 32) ? 0xFFFFFFFFu : ((1u << take) - 1u));
-            acc |= part << (32 - o - take);
-            pos += take;
-            n -= take;
-            if ((pos & 31) == 0) {
-                atomicOr(&words[wi], acc);
-                acc = 0;
-                ++wi;
-            }
+    const int4* src = reinterpret_cast<const int4*>(zz + u * 64);
+    uint32_t w[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int4 v = src[q];
+        w[4 * q] = (uint32_t)v.x; w[4 * q + 1] = (uint32_t)v.y; w[4 * q + 2] = (uint32_t)v.z; w[4 * q + 3] = (uint32_t)v.w;
+    }
+    auto coef = [&](int i) { return (int)(int16_t)(w[i >> 1] >> (16 * (i & 1))); };
+    const uint32_t* td = tab[c ? 2 : 0];
+    const uint32_t* ta = tab[c ? 3 : 1];
+    const uint64_t pos = off[u];
+    uint32_t* wp = words + (pos >> 5);
+    const int o0 = (int)(pos & 31);
+    uint64_t acc = 0;
+    int nacc = o0;        // the first o0 bits of the first word belong to the previous unit (zeros here)
+    bool first = true;
+    auto put = [&](int n, uint32_t v) {
+        acc = (acc << n) | (v & ((1u << n) - 1u));
+        nacc += n;
+        if (nacc >= 32) {
+            const uint32_t word = (uint32_t)(acc >> (nacc - 32));
+            if (first && o0) atomicOr(wp, word);
+            else *wp = word;
+            first = false;
+            ++wp;
+            nacc -= 32;
         }
-    });
-    if (pos & 31) atomicOr(&words[wi], acc);
+    };
+    auto code = [&](uint32_t e) { put((int)(e & 255), e >> 8); };
+    int nb;
+    uint32_t bits;
+    const int diff = coef(0) - pred;
+    if (diff) {
+        vli(diff, nb, bits);
+        code(td[nb]);
+        put(nb, bits);
+    } else {
+        code(td[0]);
+    }
+    int run = 0;
+#pragma unroll
+    for (int i = 1; i < 64; ++i) {
+        const int v = coef(i);
+        if (v) {
+            for (int z = run >> 4; z > 0; --z) code(ta[0xF0]);
+            vli(v, nb, bits);
+            code(ta[((run & 15) << 4) | nb]);
+            put(nb, bits);
+            run = 0;
+        } else {
+            ++run;
+        }
+    }
+    if (!coef(63)) code(ta[0]);
+    if (nacc > 0) atomicOr(wp, (uint32_t)(acc << (32 - nacc)));  // shared with the next unit
 }
 
-__device__ __forceinline__ uint8_t stream_byte(const uint32_t* words, uint64_t b) {
-    return (uint8_t)(words[b >> 2] >> (24 - 8 * (b & 3)));
+// 16 stream bytes (4 words, one 16-byte load) per lane: adjacent lanes write adjacent output.
+constexpr int kStuffChunk = 16;
+__device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t t, uint64_t nbytes, uint32_t (&w)[4]) {
+    const uint64_t b0 = (uint64_t)t * kStuffChunk;
+    if (b0 + kStuffChunk <= nbytes) {
+        const uint4 v = *reinterpret_cast<const uint4*>(words + (b0 >> 2));
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = b0 + 4 * q < nbytes ? words[(b0 >> 2) + q] : 0u;
+    }
 }
 
-constexpr int kStuffChunk = 64;  // stream bytes per lane
-
-__global__ __launch_bounds__(256) void k_stuff_count(const uint32_t* __restrict__ words, uint64_t nbytes,
+// info[0] = stream bytes (k_enc_size), info[1] = stuffed bytes (k_stuff_total)
+__global__ void k_enc_size(const uint64_t* __restrict__ off, const uint64_t* __restrict__ nbits, int64_t nunits,
+                           uint64_t* __restrict__ info) {
+    info[0] = (off[nunits - 1] + nbits[nunits - 1] + 7) / 8;  // final partial byte zero-padded (:1161-1165)
+}
+__global__ __launch_bounds__(256) void k_zero_words(uint32_t* __restrict__ words, uint64_t cap_words,
+                                                    const uint64_t* __restrict__ info) {
+    const uint64_t n = min<uint64_t>(cap_words, (info[0] + 3) / 4 + 1);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        words[i] = 0;
+}
+__global__ __launch_bounds__(256) void k_stuff_count(const uint32_t* __restrict__ words, const uint64_t* __restrict__ info,
                                                      uint32_t* __restrict__ cnt, int64_t nchunks) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nchunks) return;
-    const uint64_t b0 = (uint64_t)t * kStuffChunk, b1 = min<uint64_t>(b0 + kStuffChunk, nbytes);
+    const uint64_t nbytes = info[0];
+    const uint64_t b0 = (uint64_t)t * kStuffChunk;
+    if (b0 >= nbytes) { cnt[t] = 0; return; }
+    const int nb = (int)min<uint64_t>(kStuffChunk, nbytes - b0);
+    uint32_t w[4];
+    chunk_words(words, t, nbytes, w);
     uint32_t n = 0;
-    for (uint64_t b = b0; b < b1; ++b) n += stream_byte(words, b) == 0xFF;
+#pragma unroll
+    for (int i = 0; i < kStuffChunk; ++i) n += (i < nb && ((w[i >> 2] >> (24 - 8 * (i & 3))) & 255u) == 255u);
     cnt[t] = n;
 }
 
-__global__ __launch_bounds__(256) void k_stuff_write(const uint32_t* __restrict__ words, uint64_t nbytes,
-                                                     const uint32_t* __restrict__ base, int64_t nchunks,
-                                                     uint8_t* __restrict__ out) {
+__global__ void k_stuff_total(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ base, int64_t nchunks,
+                              uint64_t* __restrict__ info) {
+    info[1] = info[0] + base[nchunks - 1] + cnt[nchunks - 1];
+}
+// The file header (SOI .. SOS, < 1 KiB) as a kernel argument: written with the stream, only when
+// the whole file fits, without a host sync.
+struct HdrArg {
+    uint8_t b[1024];
+    int n;
+};
+__global__ void k_put_header(HdrArg h, uint8_t* __restrict__ file, const uint64_t* __restrict__ info, uint64_t cap_e,
+                             int eoi) {
+    if (info[1] + (eoi ? 2 : 0) > cap_e) return;
+    for (int i = threadIdx.x; i < h.n; i += blockDim.x) file[i] = h.b[i];
+}
+// Writes the stuffed stream only when it fits in `cap` bytes (and, with eoi, the EOI marker after it).
+__global__ __launch_bounds__(256) void k_stuff_write(const uint32_t* __restrict__ words, const uint64_t* __restrict__ info,
+                                                     const uint32_t* __restrict__ base, int64_t nchunks, uint64_t cap,
+                                                     int eoi, uint8_t* __restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nchunks) return;
-    const uint64_t b0 = (uint64_t)t * kStuffChunk, b1 = min<uint64_t>(b0 + kStuffChunk, nbytes);
-    uint64_t o = b0 + base[t];
-    for (uint64_t b = b0; b < b1; ++b) {
-        const uint8_t v = stream_byte(words, b);
-        out[o++] = v;
-        if (v == 0xFF) out[o++] = 0;
+    const uint64_t nbytes = info[0], total = info[1];
+    if (t >= nchunks || total + (eoi ? 2 : 0) > cap) return;
+    if (eoi && t == 0) { out[total] = 0xFF; out[total + 1] = 0xD9; }
+    const uint64_t b0 = (uint64_t)t * kStuffChunk;
+    if (b0 >= nbytes) return;
+    const int nb = (int)min<uint64_t>(kStuffChunk, nbytes - b0);
+    uint32_t w[4];
+    chunk_words(words, t, nbytes, w);
+    uint8_t* o = out + b0 + base[t];
+#pragma unroll
+    for (int i = 0; i < kStuffChunk; ++i) {
+        if (i >= nb) break;
+        const uint8_t v = (uint8_t)(w[i >> 2] >> (24 - 8 * (i & 3)));
+        *o++ = v;
+        if (v == 0xFF) *o++ = 0;  // jpeg_enc.h:634-638
     }
 }
 
@@ -477,6 +538,8 @@ struct EncWs {
     uint64_t words_cap = 0;  // bytes
     uint32_t *cnt = nullptr, *base = nullptr;
     int64_t chunks_cap = 0;
+    uint64_t* info = nullptr;  // device: stream bytes, stuffed bytes
+    uint64_t est_bytes = 0;    // words-buffer estimate from the images so far
     void* tmp = nullptr;
     size_t tmp_cap = 0;
     // per-stage HIP events of the last entropy pass (icx_encoder_stage_times): units, count,
@@ -487,7 +550,7 @@ struct EncWs {
     ~EncWs() {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
-        for (void* p : {(void*)T, (void*)zz, (void*)nb, (void*)off, (void*)words, (void*)cnt, (void*)base, tmp})
+        for (void* p : {(void*)T, (void*)zz, (void*)nb, (void*)off, (void*)words, (void*)cnt, (void*)base, (void*)info, tmp})
             if (p) (void)hipFree(p);
     }
 };
@@ -526,9 +589,11 @@ static bool grow(Ptr*& p, size_t need, size_t& cap_bytes) {
 }
 
 // Entropy-coded data of the image at d_src (device) -> d_out[0 .. *n) (stuffed bytes), using the
-// workspace. Returns false on a HIP failure; *n > cap means the output did not fit (not written).
+// workspace; with eoi, FF D9 follows it (when *n + 2 <= cap). Returns false on a HIP failure;
+// a result that does not fit in cap is not written.
 static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables& T, const uint8_t* d_src,
-                           int w, int h, int comps, uint8_t* d_out, uint64_t cap, uint64_t* n) {
+                           int w, int h, int comps, uint8_t* d_out, uint64_t cap, uint64_t* n, bool eoi = false,
+                           const HdrArg* hdr = nullptr) {
     const int64_t mbh = (h + L.ms - 1) / L.ms;
     const int64_t nunits = (int64_t)L.mbw * mbh * L.upm;
     *n = 0;
@@ -563,42 +628,53 @@ static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const 
     if (!grow(ws.tmp, tmp_b, ws.tmp_cap)) return false;
     ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b, ws.nb, ws.off, (int)nunits, st));
     mark(5);
-    uint64_t last_off = 0, last_nb = 0;
-    ENC_HIP(hipMemcpyAsync(&last_off, ws.off + nunits - 1, 8, hipMemcpyDeviceToHost, st));
-    ENC_HIP(hipMemcpyAsync(&last_nb, ws.nb + nunits - 1, 8, hipMemcpyDeviceToHost, st));
-    ENC_HIP(hipStreamSynchronize(st));
-    const uint64_t nbytes = (last_off + last_nb + 7) / 8;  // final partial byte zero-padded (:1161-1165)
-    const uint64_t wbytes = ((nbytes + 3) / 4 + 1) * 4;
-    if (!grow(ws.words, wbytes, ws.words_cap)) return false;
-    ENC_HIP(hipMemsetAsync(ws.words, 0, wbytes, st));
-    mark(6);
-    hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.off, ws.words);
-    mark(7);
-    mark(8);
-    const int64_t nchunks = (int64_t)((nbytes + kStuffChunk - 1) / kStuffChunk);
-    if (nchunks == 0) return true;
-    size_t cc = ws.chunks_cap * 4, cb = cc;
-    if (nchunks > ws.chunks_cap) {
-        if (!grow(ws.cnt, (size_t)nchunks * 4, cc) || !grow(ws.base, (size_t)nchunks * 4, cb)) return false;
-        ws.chunks_cap = nchunks;
+    // The stream's size is known on the device only. Emit into a words buffer sized from the
+    // previous images (first call: W*H*comps/4) and size the stuffing from it, so the image needs
+    // a single host sync at the end; an image whose stream outgrows the estimate is re-run with
+    // the exact size (then the estimate grows).
+    if (!ws.info && hipMalloc(&ws.info, 4 * sizeof(uint64_t)) != hipSuccess) return false;
+    hipLaunchKernelGGL(k_enc_size, dim3(1), dim3(1), 0, st, ws.off, ws.nb, nunits, ws.info);
+    uint64_t est = ws.est_bytes ? ws.est_bytes : std::max<uint64_t>(65536, (uint64_t)w * h * comps / 4);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const uint64_t wbytes = (est + 4 + 15) / 16 * 16;
+        if (!grow(ws.words, wbytes, ws.words_cap)) return false;
+        const int64_t nchunks = (int64_t)(wbytes / kStuffChunk);
+        size_t cc = ws.chunks_cap * 4, cb = cc;
+        if (nchunks > ws.chunks_cap) {
+            if (!grow(ws.cnt, (size_t)nchunks * 4, cc) || !grow(ws.base, (size_t)nchunks * 4, cb)) return false;
+            ws.chunks_cap = nchunks;
+        }
+        hipLaunchKernelGGL(k_zero_words, dim3(1024), dim3(TB), 0, st, ws.words, (uint64_t)(wbytes / 4), ws.info);
+        mark(6);
+        hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.off, ws.nb,
+                           (uint64_t)wbytes * 8, ws.words);
+        mark(7);
+        mark(8);
+        const int gc = (int)((nchunks + TB - 1) / TB);
+        hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.cnt, nchunks);
+        size_t tmp_b2 = 0;
+        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
+        if (!grow(ws.tmp, tmp_b2, ws.tmp_cap)) return false;
+        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
+        hipLaunchKernelGGL(k_stuff_total, dim3(1), dim3(1), 0, st, ws.cnt, ws.base, nchunks, ws.info);
+        hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.base, nchunks, cap,
+                           eoi ? 1 : 0, d_out);
+        if (hdr) hipLaunchKernelGGL(k_put_header, dim3(1), dim3(256), 0, st, *hdr, d_out - hdr->n, ws.info, cap, eoi ? 1 : 0);
+        ENC_HIP(hipGetLastError());
+        mark(9);
+        uint64_t info[2] = {0, 0};
+        ENC_HIP(hipMemcpyAsync(info, ws.info, sizeof info, hipMemcpyDeviceToHost, st));
+        ENC_HIP(hipStreamSynchronize(st));
+        if (info[0] + 4 <= wbytes) {  // every unit was emitted
+            ws.est_bytes = std::max(ws.est_bytes, info[0] + info[0] / 4);
+            *n = info[1];
+            ws.timed = ev;
+            return true;
+        }
+        est = info[0] + info[0] / 4;
+        ws.est_bytes = est;
     }
-    const int gc = (int)((nchunks + TB - 1) / TB);
-    hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, ws.words, nbytes, ws.cnt, nchunks);
-    size_t tmp_b2 = 0;
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
-    if (!grow(ws.tmp, tmp_b2, ws.tmp_cap)) return false;
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
-    uint32_t last_cnt = 0, last_base = 0;
-    ENC_HIP(hipMemcpyAsync(&last_cnt, ws.cnt + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
-    ENC_HIP(hipMemcpyAsync(&last_base, ws.base + nchunks - 1, 4, hipMemcpyDeviceToHost, st));
-    ENC_HIP(hipStreamSynchronize(st));
-    *n = nbytes + (uint64_t)last_cnt + last_base;
-    if (*n > cap) return true;
-    hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, ws.words, nbytes, ws.base, nchunks, d_out);
-    ENC_HIP(hipGetLastError());
-    mark(9);
-    ws.timed = ev;
-    return true;
+    return false;
 }
 
 bool encode_host_image(hipStream_t st, const EncLayout& L, const EncTables& T, int w, int h, int comps,
@@ -684,17 +760,27 @@ int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, 
     std::vector<uint8_t> head;
     ext_header(head, w, h, qnl, qnc, subsampling);
     const uint64_t hn = head.size();
+    if (hn > sizeof(HdrArg::b)) return -1;
+    HdrArg ha;
+    std::memcpy(ha.b, head.data(), hn);
+    ha.n = (int)hn;
+    if (w == 0 || h == 0) {  // no data units: header + EOI only
+        *size = hn + 2;
+        if (*size > cap) return 1;
+        static const uint8_t eoi[2] = {0xFF, 0xD9};
+        if (hipMemcpyAsync(d_out, head.data(), hn, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_out + hn, eoi, 2, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return -1;
+        return 0;
+    }
     uint64_t n = 0;
-    if (!encode_entropy(st, *ws, make_layout(subsampling, w), T, d_src, w, h, comps,
-                        cap > hn ? d_out + hn : d_out, cap > hn ? cap - hn : 0, &n))
+    // the whole file (header, stuffed stream, EOI) is written on the device, only if it fits
+    if (!encode_entropy(st, *ws, make_layout(subsampling, w), T, d_src, w, h, comps, d_out + hn, cap > hn ? cap - hn : 0,
+                        &n, true, &ha))
         return -1;
     *size = hn + n + 2;
     if (*size > cap) return 1;
-    static const uint8_t eoi[2] = {0xFF, 0xD9};
-    if (hipMemcpyAsync(d_out, head.data(), hn, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_out + hn + n, eoi, 2, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return -1;
     if (ws->timed) {
         for (int i = 0; i < 5; ++i) {
             float t = 0.f;
