@@ -521,6 +521,7 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1),
                     help="CPU-baseline workers (default: the 16-core share of a GPU box)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive sub-batch (decode workloads)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -623,6 +624,32 @@ def main():
                 checked += 1
                 mismatches += got != cpu_hashes[key]
 
+    # PCIe-inclusive rate (rank 0, reported beside `value`, never as it): a bounded sub-batch goes
+    # host (pinned) -> HBM, is decoded, and its RGB comes back to pinned host memory, serially
+    pcie = None
+    if rank == 0 and not args.no_pcie:
+        m = min(n, 64)
+        nb_in = int(offs[m - 1] + sizes[m - 1])
+        h_in = torch.from_numpy(blob[:nb_in]).pin_memory()
+        h_out = torch.empty(m * stride, dtype=torch.uint8).pin_memory()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        d_data[:nb_in].copy_(h_in, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        batch.decode_device(m, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out.data_ptr(), stride,
+                            d_st.data_ptr(), d_dims.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        h_out.copy_(d_out[: m * stride], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        pcie = {"value": round(m * W * H / 1e6 / (t3 - t0), 2), "unit": "megapixels/s", "images": m,
+                "h2d_ms": round((t1 - t0) * 1e3, 3), "decode_ms": round((t2 - t1) * 1e3, 3),
+                "d2h_ms": round((t3 - t2) * 1e3, 3),
+                "note": "serial H2D (pinned) -> decode -> D2H (pinned) of a sub-batch; not overlapped"}
+        del h_in, h_out
+
     comp_bytes = float(sizes.sum())
     alg_bytes = comp_bytes + n * W * H * 3.0  # compressed + W*H*3 per image
     mpx = n * W * H / 1e6
@@ -663,6 +690,7 @@ def main():
         "cpu_baseline": cpu,
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
         "entropy_paths": paths,
+        "pcie_inclusive": pcie,
         "gen_seconds": round(gen_s, 1),
     }
     if rank == 0:
