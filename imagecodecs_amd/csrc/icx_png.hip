@@ -377,23 +377,55 @@ __global__ __launch_bounds__(256) void k_png_filter(const uint8_t* __restrict__ 
 
 // ------------------------------------------------------------------------------- LZ77
 // Token: literal = byte value (< 256); match = 1<<31 | (len-3) << 15 | (dist-1).
-__device__ __forceinline__ int match_len(const uint8_t* F, int64_t p, int64_t dist, int64_t maxlen) {
+// A wave's view of the filtered stream around its segment, staged in LDS: `near` covers
+// [s0 - kNear, s1) (the segment and the short candidate distances), `far` covers
+// [s0 - rowlen - kNear, s1 - rowlen + kNear) (the row above +- one pixel). Both start at a
+// 16-byte-aligned stream index so the staging is 16-byte loads. Every source byte a candidate
+// can compare (q - d + l with q + l < s1) lies in one of them: indices >= s0 - kNear in `near`,
+// the others (distances rowlen - bw .. rowlen + bw only) in `far`.
+constexpr int kNear = 16;                        // >= 2 * bw (bw <= 8)
+constexpr int kStage = kSeg + 2 * kNear + 16;    // bytes per staged view, 16-byte multiple
+struct SegView {
+    const uint8_t* nearp;  // LDS base, = stream index nb0
+    const uint8_t* farp;   // LDS base, = stream index fb0
+    int64_t nb0, fb0, nlo; // nlo = s0 - kNear: lowest index served by `near`
+    __device__ __forceinline__ uint8_t at(int64_t i) const {
+        return i >= nlo ? nearp[i - nb0] : farp[i - fb0];
+    }
+};
+__device__ __forceinline__ void stage_view(const uint8_t* __restrict__ F, int64_t N, int64_t b0, uint8_t* lds, int lane) {
+    for (int k = lane; k < kStage / 16; k += 64) {
+        const int64_t g = b0 + 16 * k;
+        uint4 v;
+        if (g >= 0 && g + 16 <= N) {
+            v = *reinterpret_cast<const uint4*>(F + g);
+        } else {
+            uint8_t t[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) t[j] = (g + j >= 0 && g + j < N) ? F[g + j] : 0;
+            __builtin_memcpy(&v, t, 16);
+        }
+        *reinterpret_cast<uint4*>(lds + 16 * k) = v;
+    }
+}
+__device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t dist, int64_t maxlen) {
     int l = 0;
-    while (l < maxlen && F[p + l] == F[p - dist + l]) ++l;
+    while (l < maxlen && V.nearp[p + l - V.nb0] == V.at(p - dist + l)) ++l;
     return l;
 }
 
-// One workgroup (4 waves) per 256 KiB block; each wave takes a 4 KiB segment at a time and
-// walks it in 64-position windows: every lane scores the position under it against the six
-// structural candidates (left pixel, up to two pixels back, the pixel above and its two
-// neighbours) with coalesced loads, then the wave parses the window greedily with ballots --
-// the literal run up to the first position with a match is emitted by all lanes at once, the
-// match by one. The tokens are those of a serial greedy parse (first match of length >= 3 per
+// One workgroup (4 waves) per 256 KiB block; each wave takes a 4 KiB segment at a time, stages
+// its two views in LDS, and walks it in 64-position windows: every lane scores the position
+// under it against the six structural candidates (left pixel, up to two pixels back, the pixel
+// above and its two neighbours), then the wave parses the window greedily with ballots -- the
+// literal run up to the first position with a match is emitted by all lanes at once, the match
+// by one. The tokens are those of a serial greedy parse (first match of length >= 3 per
 // position, longest over the candidates, never crossing the segment end).
 __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
                                                   int bw, uint32_t* __restrict__ tok, uint32_t* __restrict__ ntok,
                                                   uint32_t* __restrict__ hist, uint32_t* __restrict__ adl) {
     __shared__ uint32_t h_ll[kNLL], h_d[kND];
+    __shared__ __attribute__((aligned(16))) uint8_t views[4][2][kStage];
     const int64_t blk = blockIdx.x;
     for (int i = threadIdx.x; i < kNLL; i += 256) h_ll[i] = 0;
     if (threadIdx.x < kND) h_d[threadIdx.x] = 0;
@@ -408,10 +440,20 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
         if (seg >= nseg) break;  // wave-uniform
         const int64_t s0 = seg * kSeg, s1 = min(N, s0 + kSeg);
         uint32_t* T = tok + s0;
+        SegView V;
+        V.nlo = s0 - kNear;
+        V.nb0 = V.nlo & ~(int64_t)15;
+        V.fb0 = (s0 - rowlen - kNear) & ~(int64_t)15;
+        V.nearp = views[wave][0];
+        V.farp = views[wave][1];
+        __builtin_amdgcn_wave_barrier();
+        stage_view(F, N, V.nb0, views[wave][0], lane);
+        stage_view(F, N, V.fb0, views[wave][1], lane);
+        __builtin_amdgcn_wave_barrier();
         // Adler-32 partials: sum b, sum (N - g) b (reduced mod 65521 at the end)
         uint64_t a1 = 0, a2 = 0;
         for (int64_t q = s0 + lane; q < s1; q += 64) {
-            const uint32_t b = F[q];
+            const uint32_t b = V.nearp[q - V.nb0];
             a1 += b;
             a2 += (uint64_t)(N - q) * b;
         }
@@ -431,15 +473,16 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
             int best = 0, bd = 0;
             uint32_t lit = 0;
             if (q < s1) {
-                lit = F[q];
+                const uint8_t* tq = V.nearp + (q - V.nb0);
+                lit = tq[0];
                 const int64_t maxlen = min((int64_t)258, s1 - q);
                 if (maxlen >= 3 && q >= pos) {  // positions under a previous match need no score
 #pragma unroll
                     for (int k = 0; k < 6; ++k) {
                         const int64_t dd = cand[k];
                         if (dd == 0 || dd > q) continue;
-                        if (F[q] != F[q - dd] || F[q + 1] != F[q - dd + 1] || F[q + 2] != F[q - dd + 2]) continue;
-                        const int l = 3 + match_len(F, q + 3, dd, maxlen - 3);
+                        if (tq[0] != V.at(q - dd) || tq[1] != V.at(q - dd + 1) || tq[2] != V.at(q - dd + 2)) continue;
+                        const int l = 3 + match_len(V, q + 3, dd, maxlen - 3);
                         if (l > best) {
                             best = l;
                             bd = (int)dd;
