@@ -526,12 +526,31 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
 // ------------------------------------------------------------------------------ Huffman
 // Code lengths for freq[0..n) limited to maxbits (Huffman by sorting + JPEG Annex K.3
 // "adjust bits" length limiting, which keeps the code complete). Single thread; scratch in LDS.
+// The used symbols of freq[0..n) in (freq, symbol) ascending order, by rank counting over all
+// lanes of the workgroup (blockDim.x lanes; the caller synchronises before and after).
+__device__ void rank_order(const uint32_t* freq, int n, uint16_t* order) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t f = freq[i];
+        if (!f) continue;
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            const uint32_t g = freq[j];
+            r += g && (g < f || (g == f && j < i));
+        }
+        order[r] = (uint16_t)i;
+    }
+}
+
+// presorted: order[] already holds the used symbols sorted (rank_order).
 __device__ void huff_lengths(const uint32_t* freq, int n, int maxbits, uint8_t* len, uint16_t* order, uint32_t* wt,
-                             int16_t* parent, int* nused_out) {
+                             int16_t* parent, int* nused_out, bool presorted = false) {
     int m = 0;
     for (int i = 0; i < n; ++i) {
         len[i] = 0;
-        if (freq[i]) order[m++] = (uint16_t)i;
+        if (freq[i]) {
+            if (!presorted) order[m] = (uint16_t)i;
+            ++m;
+        }
     }
     *nused_out = m;
     if (m == 0) return;
@@ -540,7 +559,7 @@ __device__ void huff_lengths(const uint32_t* freq, int n, int maxbits, uint8_t* 
         return;
     }
     // insertion sort by (freq, symbol) ascending
-    for (int a = 1; a < m; ++a) {
+    for (int a = 1; a < m && !presorted; ++a) {
         const uint16_t v = order[a];
         int b = a - 1;
         while (b >= 0 && (freq[order[b]] > freq[v] || (freq[order[b]] == freq[v] && order[b] > v))) {
@@ -625,7 +644,7 @@ struct BitW {
 // One workgroup per block, thread 0 builds everything (deterministic, tiny).
 __global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hist, int64_t nblk, BlockCodes* __restrict__ bc) {
     __shared__ uint32_t f_ll[kNLL], f_d[kND];
-    __shared__ uint16_t order[kNLL];
+    __shared__ uint16_t order[kNLL], order_d[kND];
     __shared__ uint32_t wt[2 * kNLL];
     __shared__ int16_t parent[2 * kNLL];
     __shared__ uint8_t l_ll[kNLL], l_d[kND];
@@ -638,9 +657,7 @@ __global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hi
     BlockCodes& B = bc[blk];
     for (int i = threadIdx.x; i < kHdrWords; i += 64) B.hdr[i] = 0;
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    // at least two codes per tree keeps every code complete
-    {
+    if (threadIdx.x == 0) {  // at least two codes per tree keeps every code complete
         int u = 0;
         for (int i = 0; i < kNLL; ++i) u += f_ll[i] != 0;
         if (u < 2) f_ll[f_ll[0] ? 1 : 0] = 1;
@@ -651,9 +668,14 @@ __global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hi
             if (!f_d[1]) f_d[1] = 1;
         }
     }
+    __syncthreads();
+    rank_order(f_ll, kNLL, order);
+    rank_order(f_d, kND, order_d);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     int used;
-    huff_lengths(f_ll, kNLL, 15, l_ll, order, wt, parent, &used);
-    huff_lengths(f_d, kND, 15, l_d, order, wt, parent, &used);
+    huff_lengths(f_ll, kNLL, 15, l_ll, order, wt, parent, &used, true);
+    huff_lengths(f_d, kND, 15, l_d, order_d, wt, parent, &used, true);
     canon_codes(l_ll, kNLL, B.ll_code);
     canon_codes(l_d, kND, B.d_code);
     for (int i = 0; i < kNLL; ++i) B.ll_len[i] = l_ll[i];
