@@ -762,6 +762,14 @@ __global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hi
     B.hdr_bits = bw.n;
 }
 
+// The workgroup's block code tables -> LDS (every lane reaches the barrier).
+__device__ __forceinline__ void stage_codes(const BlockCodes* __restrict__ bc, BlockCodes& B) {
+    static_assert(sizeof(BlockCodes) % 4 == 0 && kSegPerBlock % 4 == 0, "staging layout");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(bc + (int64_t)blockIdx.x * 4 / kSegPerBlock);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&B);
+    for (int i = threadIdx.x; i < (int)(sizeof(BlockCodes) / 4); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
 __device__ __forceinline__ uint32_t token_bits(const BlockCodes& B, uint32_t t) {
     if (!(t & 0x80000000u)) return B.ll_len[t];
     const int len = (int)((t >> 15) & 255) + 3, dist = (int)(t & 0x7FFF) + 1;
@@ -773,11 +781,11 @@ __device__ __forceinline__ uint32_t token_bits(const BlockCodes& B, uint32_t t) 
 __global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint32_t* __restrict__ tok,
                                                      const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
                                                      unsigned long long* __restrict__ bits) {
+    __shared__ BlockCodes B;  // the four waves' segments share one block (kSegPerBlock % 4 == 0)
+    stage_codes(bc, B);
     const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (seg >= nseg) return;  // wave-uniform
-    const int64_t blk = seg / kSegPerBlock;
-    const BlockCodes& B = bc[blk];
     const uint32_t* T = tok + seg * kSeg;
     const uint32_t nt = ntok[seg];
     uint32_t b = 0;
@@ -859,10 +867,11 @@ __global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint32_t* 
                                                   const unsigned long long* __restrict__ bits, uint32_t* __restrict__ out,
                                                   unsigned long long base_bits) {
     __shared__ uint32_t img[4][kEmitWords];
+    __shared__ BlockCodes B;  // the four waves' segments share one block
+    stage_codes(bc, B);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t seg = (int64_t)blockIdx.x * 4 + wave;
     if (seg >= nseg) return;  // wave-uniform; no block barriers below
-    const BlockCodes& B = bc[seg / kSegPerBlock];
     const uint32_t* T = tok + seg * kSeg;
     const uint32_t nt = ntok[seg];
     const unsigned long long o0 = base_bits + off[seg], o1 = o0 + bits[seg];
