@@ -340,8 +340,8 @@ struct HdrArg {
     int n;
 };
 __global__ void k_put_header(HdrArg h, uint8_t* __restrict__ file, const uint64_t* __restrict__ info, uint64_t cap_e,
-                             int eoi) {
-    if (info[1] + (eoi ? 2 : 0) > cap_e) return;
+                             int eoi, uint64_t wbytes) {
+    if (info[1] + (eoi ? 2 : 0) > cap_e || info[0] + 4 > wbytes) return;
     for (int i = threadIdx.x; i < h.n; i += blockDim.x) file[i] = h.b[i];
 }
 // Writes the stuffed stream only when it fits in `cap` bytes (and, with eoi, the EOI marker after it).
@@ -350,7 +350,8 @@ __global__ __launch_bounds__(256) void k_stuff_write(const uint32_t* __restrict_
                                                      int eoi, uint8_t* __restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nbytes = info[0], total = info[1];
-    if (t >= nchunks || total + (eoi ? 2 : 0) > cap) return;
+    // nothing is written unless the whole stream fits in cap and every unit was emitted
+    if (t >= nchunks || total + (eoi ? 2 : 0) > cap || nbytes + 4 > (uint64_t)nchunks * kStuffChunk) return;
     if (eoi && t == 0) { out[total] = 0xFF; out[total + 1] = 0xD9; }
     const uint64_t b0 = (uint64_t)t * kStuffChunk;
     if (b0 >= nbytes) return;
@@ -659,7 +660,9 @@ static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const 
         hipLaunchKernelGGL(k_stuff_total, dim3(1), dim3(1), 0, st, ws.cnt, ws.base, nchunks, ws.info);
         hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.base, nchunks, cap,
                            eoi ? 1 : 0, d_out);
-        if (hdr) hipLaunchKernelGGL(k_put_header, dim3(1), dim3(256), 0, st, *hdr, d_out - hdr->n, ws.info, cap, eoi ? 1 : 0);
+        if (hdr)
+            hipLaunchKernelGGL(k_put_header, dim3(1), dim3(256), 0, st, *hdr, d_out - hdr->n, ws.info, cap, eoi ? 1 : 0,
+                               (uint64_t)wbytes);
         ENC_HIP(hipGetLastError());
         mark(9);
         uint64_t info[2] = {0, 0};

@@ -99,3 +99,28 @@ def test_ext_rejects(ctx):
     assert ctx.jpeg_encode(90, 422, 8, 8, 3, px) is None
     assert ctx.jpeg_encode(90, 420, 8, 8, 2, px) is None
     assert ctx.jpeg_encode(90, 420, 0, 0, 3, b"") == O.jpeg_encode(90, 420, 0, 0, 3, b"")  # header + EOI
+
+
+def test_ext_device_estimate_regrowth(ctx):
+    """The device encoder sizes its stream buffer from the images before; a much larger stream is
+    re-run at its exact size (same bytes), and an output that does not fit stays untouched."""
+    import torch
+    small, big = S.rgb(5, 64, 64, 3), S.rgb(6, 1024, 1024, 3)
+    d_out = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
+    enc = icx.Encoder(ctx)
+    for px, w, h in ((small, 64, 64), (big, 1024, 1024), (small, 64, 64)):
+        d_src = torch.from_numpy(px).cuda()
+        rc, n = enc.encode_device(100, 444, w, h, 3, d_src.data_ptr(), d_out.data_ptr(), d_out.numel())
+        assert rc == icx.OK
+        assert d_out[:n].cpu().numpy().tobytes() == O.jpeg_encode(100, 444, w, h, 3, px.tobytes())
+    enc.close()
+    enc2 = icx.Encoder(ctx)  # small estimate again, then a big image into a 4 KiB output
+    rc, _ = enc2.encode_device(100, 444, 64, 64, 3, torch.from_numpy(small).cuda().data_ptr(), d_out.data_ptr(),
+                               d_out.numel())
+    assert rc == icx.OK
+    d_big = torch.from_numpy(big).cuda()
+    d_out.fill_(0xAB)
+    rc, n = enc2.encode_device(100, 444, 1024, 1024, 3, d_big.data_ptr(), d_out.data_ptr(), 4096)
+    assert rc == icx.OUT_OF_MEM and n > 4096
+    assert bool((d_out == 0xAB).all())
+    enc2.close()

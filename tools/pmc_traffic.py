@@ -4,7 +4,7 @@
     python3 tools/pmc_traffic.py run  [--workload c3] [--kernel k_spec_write] [--out profiles/traffic.json]
     python3 tools/pmc_traffic.py parse FETCH_DIR WRITE_DIR [...]
 
-`run` profiles `bench.py --steps 1 --warmup 0 --no-cpu` twice, once with --pmc FETCH_SIZE and once
+`run` profiles `bench.py --steps 1 --warmup 0 --no-cpu --no-pcie` twice, once with --pmc FETCH_SIZE and once
 with --pmc WRITE_SIZE (the two cannot share a pass on gfx950; counters are collected in runs of their
 own, never together with tracing domains), then parses both. Per MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE counts wide (16 B/lane) streaming reads at exactly half their bytes on gfx950, so it is
@@ -60,7 +60,7 @@ def run(args):
     os.environ.setdefault("TMPDIR", "/tmp")
     out = os.path.join(ROOT, "gpurun_out", "pmc")
     bench = ["python3", os.path.join(ROOT, "bench.py"), "--workload", args.workload, "--steps", "1",
-             "--warmup", "0", "--no-cpu"]
+             "--warmup", "0", "--no-cpu", "--no-pcie"]
     if args.images:
         bench += ["--images", str(args.images)]
     dirs = []
