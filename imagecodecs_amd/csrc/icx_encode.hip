@@ -540,19 +540,24 @@ struct EncWs {
     uint32_t *cnt = nullptr, *base = nullptr;
     int64_t chunks_cap = 0;
     uint64_t* info = nullptr;  // device: stream bytes, stuffed bytes
+    uint64_t* hinfo = nullptr; // pinned host copy of info, valid when `fin` completes
+    hipEvent_t fin = nullptr;
     uint64_t est_bytes = 0;    // words-buffer estimate from the images so far
+    uint64_t wbytes = 0;       // words buffer of the job in flight
+    int64_t nunits = 0;        // data units of the job in flight
     void* tmp = nullptr;
     size_t tmp_cap = 0;
     // per-stage HIP events of the last entropy pass (icx_encoder_stage_times): units, count,
     // scan, emit, stuff; ms[] accumulates over calls until read
     hipEvent_t ev[10] = {};  // stage i spans ev[2i] .. ev[2i+1]
-    bool timed = false;
     float ms[5] = {};
     ~EncWs() {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         for (void* p : {(void*)T, (void*)zz, (void*)nb, (void*)off, (void*)words, (void*)cnt, (void*)base, (void*)info, tmp})
             if (p) (void)hipFree(p);
+        if (hinfo) (void)hipHostFree(hinfo);
+        if (fin) (void)hipEventDestroy(fin);
     }
 };
 EncWs* enc_ws_create() {
@@ -589,26 +594,34 @@ static bool grow(Ptr*& p, size_t need, size_t& cap_bytes) {
     return true;
 }
 
-// Entropy-coded data of the image at d_src (device) -> d_out[0 .. *n) (stuffed bytes), using the
-// workspace; with eoi, FF D9 follows it (when *n + 2 <= cap). Returns false on a HIP failure;
-// a result that does not fit in cap is not written.
-static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables& T, const uint8_t* d_src,
-                           int w, int h, int comps, uint8_t* d_out, uint64_t cap, uint64_t* n, bool eoi = false,
-                           const HdrArg* hdr = nullptr) {
+// One image's entropy-coded data is produced in two launches-only phases and one collect:
+//   enc_front  units, bit counts, scan, stream size (info[0], device)
+//   enc_tail   words (sized from the images before: the stream's size is known on the device
+//              only), emit, stuffing, stuffed size (info[1]); writes d_out only when the whole
+//              result fits in cap (and, with hdr / eoi, the header before it and EOI after it);
+//              info -> pinned host memory, event `fin`
+//   enc_collect  waits for `fin`: 1 = done (*n = stuffed bytes), 0 = the stream outgrew the words
+//              buffer (nothing written; run enc_tail again: est_bytes now holds its size), -1 = HIP
+//              failure
+// So an image costs one host wait, and a caller with two workspaces on two streams can issue
+// image i+1 before waiting for image i.
+static bool enc_front(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables* T, const uint8_t* d_src, int w,
+                      int h, int comps) {
     const int64_t mbh = (h + L.ms - 1) / L.ms;
     const int64_t nunits = (int64_t)L.mbw * mbh * L.upm;
-    *n = 0;
-    if (nunits == 0 || w == 0 || h == 0) return true;
+    ws.nunits = nunits;
     size_t c0 = ws.units_cap * 128, c1 = ws.units_cap * 8, c2 = c1;
     if (nunits > ws.units_cap) {
-        size_t tcap = ws.T ? sizeof(EncTables) : 0;
-        if (!grow(ws.T, sizeof(EncTables), tcap)) return false;
         if (!grow(ws.zz, (size_t)nunits * 128, c0) || !grow(ws.nb, (size_t)nunits * 8, c1) ||
             !grow(ws.off, (size_t)nunits * 8, c2))
             return false;
         ws.units_cap = nunits;
     }
-    ENC_HIP(hipMemcpyAsync(ws.T, &T, sizeof T, hipMemcpyHostToDevice, st));
+    if (!ws.T) ENC_HIP(hipMalloc(&ws.T, sizeof(EncTables)));
+    if (!ws.info) ENC_HIP(hipMalloc(&ws.info, 4 * sizeof(uint64_t)));
+    if (!ws.hinfo) ENC_HIP(hipHostMalloc(&ws.hinfo, 4 * sizeof(uint64_t)));
+    if (!ws.fin) ENC_HIP(hipEventCreateWithFlags(&ws.fin, hipEventDisableTiming));
+    if (T) ENC_HIP(hipMemcpyAsync(ws.T, T, sizeof *T, hipMemcpyHostToDevice, st));
     const int TB = 256;
     const int gu = (int)((nunits + TB - 1) / TB);
     const bool ev = ws.ev[9] != nullptr;
@@ -629,53 +642,87 @@ static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const 
     if (!grow(ws.tmp, tmp_b, ws.tmp_cap)) return false;
     ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b, ws.nb, ws.off, (int)nunits, st));
     mark(5);
-    // The stream's size is known on the device only. Emit into a words buffer sized from the
-    // previous images (first call: W*H*comps/4) and size the stuffing from it, so the image needs
-    // a single host sync at the end; an image whose stream outgrows the estimate is re-run with
-    // the exact size (then the estimate grows).
-    if (!ws.info && hipMalloc(&ws.info, 4 * sizeof(uint64_t)) != hipSuccess) return false;
     hipLaunchKernelGGL(k_enc_size, dim3(1), dim3(1), 0, st, ws.off, ws.nb, nunits, ws.info);
-    uint64_t est = ws.est_bytes ? ws.est_bytes : std::max<uint64_t>(65536, (uint64_t)w * h * comps / 4);
+    return hipGetLastError() == hipSuccess;
+}
+
+static bool enc_tail(hipStream_t st, EncWs& ws, const EncLayout& L, int w, int h, int comps, uint8_t* d_out,
+                     uint64_t cap, bool eoi, const HdrArg* hdr) {
+    const int TB = 256;
+    const int64_t nunits = ws.nunits;
+    const int gu = (int)((nunits + TB - 1) / TB);
+    const bool ev = ws.ev[9] != nullptr;
+    auto mark = [&](int i) {
+        if (ev) (void)hipEventRecord(ws.ev[i], st);
+    };
+    const uint64_t est = ws.est_bytes ? ws.est_bytes : std::max<uint64_t>(65536, (uint64_t)w * h * comps / 4);
+    const uint64_t wbytes = (est + 4 + 15) / 16 * 16;
+    if (!grow(ws.words, wbytes, ws.words_cap)) return false;
+    ws.wbytes = wbytes;
+    const int64_t nchunks = (int64_t)(wbytes / kStuffChunk);
+    size_t cc = ws.chunks_cap * 4, cb = cc;
+    if (nchunks > ws.chunks_cap) {
+        if (!grow(ws.cnt, (size_t)nchunks * 4, cc) || !grow(ws.base, (size_t)nchunks * 4, cb)) return false;
+        ws.chunks_cap = nchunks;
+    }
+    hipLaunchKernelGGL(k_zero_words, dim3(1024), dim3(TB), 0, st, ws.words, (uint64_t)(wbytes / 4), ws.info);
+    mark(6);
+    hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.off, ws.nb,
+                       (uint64_t)wbytes * 8, ws.words);
+    mark(7);
+    mark(8);
+    const int gc = (int)((nchunks + TB - 1) / TB);
+    hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.cnt, nchunks);
+    size_t tmp_b2 = 0;
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
+    if (!grow(ws.tmp, tmp_b2, ws.tmp_cap)) return false;
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
+    hipLaunchKernelGGL(k_stuff_total, dim3(1), dim3(1), 0, st, ws.cnt, ws.base, nchunks, ws.info);
+    hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.base, nchunks, cap,
+                       eoi ? 1 : 0, d_out);
+    if (hdr)
+        hipLaunchKernelGGL(k_put_header, dim3(1), dim3(256), 0, st, *hdr, d_out - hdr->n, ws.info, cap, eoi ? 1 : 0,
+                           (uint64_t)wbytes);
+    mark(9);
+    ENC_HIP(hipGetLastError());
+    ENC_HIP(hipMemcpyAsync(ws.hinfo, ws.info, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipEventRecord(ws.fin, st));
+    return true;
+}
+
+static int enc_collect(EncWs& ws, uint64_t* n) {
+    if (hipEventSynchronize(ws.fin) != hipSuccess) return -1;
+    const uint64_t nbytes = ws.hinfo[0];
+    if (nbytes + 4 > ws.wbytes) {  // the stream outgrew the words buffer: nothing was written
+        ws.est_bytes = nbytes + nbytes / 4;
+        return 0;
+    }
+    ws.est_bytes = std::max(ws.est_bytes, nbytes + nbytes / 4);
+    *n = ws.hinfo[1];
+    if (ws.ev[9]) {
+        for (int i = 0; i < 5; ++i) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, ws.ev[2 * i], ws.ev[2 * i + 1]) == hipSuccess) ws.ms[i] += t;
+        }
+    }
+    return 1;
+}
+
+// Entropy-coded data of the image at d_src (device) -> d_out[0 .. *n) (stuffed bytes); with eoi,
+// FF D9 follows it, with hdr the header precedes it (all only when they fit in cap). Returns false
+// on a HIP failure.
+static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables& T, const uint8_t* d_src,
+                           int w, int h, int comps, uint8_t* d_out, uint64_t cap, uint64_t* n, bool eoi = false,
+                           const HdrArg* hdr = nullptr) {
+    *n = 0;
+    const int64_t mbh = (h + L.ms - 1) / L.ms;
+    if ((int64_t)L.mbw * mbh * L.upm == 0 || w == 0 || h == 0) return true;
+    if (!enc_front(st, ws, L, &T, d_src, w, h, comps)) return false;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        const uint64_t wbytes = (est + 4 + 15) / 16 * 16;
-        if (!grow(ws.words, wbytes, ws.words_cap)) return false;
-        const int64_t nchunks = (int64_t)(wbytes / kStuffChunk);
-        size_t cc = ws.chunks_cap * 4, cb = cc;
-        if (nchunks > ws.chunks_cap) {
-            if (!grow(ws.cnt, (size_t)nchunks * 4, cc) || !grow(ws.base, (size_t)nchunks * 4, cb)) return false;
-            ws.chunks_cap = nchunks;
-        }
-        hipLaunchKernelGGL(k_zero_words, dim3(1024), dim3(TB), 0, st, ws.words, (uint64_t)(wbytes / 4), ws.info);
-        mark(6);
-        hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.off, ws.nb,
-                           (uint64_t)wbytes * 8, ws.words);
-        mark(7);
-        mark(8);
-        const int gc = (int)((nchunks + TB - 1) / TB);
-        hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.cnt, nchunks);
-        size_t tmp_b2 = 0;
-        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
-        if (!grow(ws.tmp, tmp_b2, ws.tmp_cap)) return false;
-        ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
-        hipLaunchKernelGGL(k_stuff_total, dim3(1), dim3(1), 0, st, ws.cnt, ws.base, nchunks, ws.info);
-        hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.base, nchunks, cap,
-                           eoi ? 1 : 0, d_out);
-        if (hdr)
-            hipLaunchKernelGGL(k_put_header, dim3(1), dim3(256), 0, st, *hdr, d_out - hdr->n, ws.info, cap, eoi ? 1 : 0,
-                               (uint64_t)wbytes);
-        ENC_HIP(hipGetLastError());
-        mark(9);
-        uint64_t info[2] = {0, 0};
-        ENC_HIP(hipMemcpyAsync(info, ws.info, sizeof info, hipMemcpyDeviceToHost, st));
-        ENC_HIP(hipStreamSynchronize(st));
-        if (info[0] + 4 <= wbytes) {  // every unit was emitted
-            ws.est_bytes = std::max(ws.est_bytes, info[0] + info[0] / 4);
-            *n = info[1];
-            ws.timed = ev;
-            return true;
-        }
-        est = info[0] + info[0] / 4;
-        ws.est_bytes = est;
+        if (!enc_tail(st, ws, L, w, h, comps, d_out, cap, eoi, hdr)) return false;
+        const int rc = enc_collect(ws, n);
+        if (rc < 0) return false;
+        if (rc > 0) return true;
     }
     return false;
 }
@@ -783,15 +830,70 @@ int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, 
                         &n, true, &ha))
         return -1;
     *size = hn + n + 2;
-    if (*size > cap) return 1;
-    if (ws->timed) {
-        for (int i = 0; i < 5; ++i) {
-            float t = 0.f;
-            if (hipEventElapsedTime(&t, ws->ev[2 * i], ws->ev[2 * i + 1]) == hipSuccess) ws->ms[i] += t;
+    return *size > cap ? 1 : 0;
+}
+
+// A batch of device images, same geometry and settings: image i -> d_out + i*stride. Images
+// alternate between two workspaces on two streams, so image i+1's kernels are issued before the
+// host waits for image i. Per image: sizes[i] and status[i] (0 ok, 1 did not fit: nothing
+// written). Returns 0, or -1 on a HIP failure. Synchronous.
+int jpeg_encode_device_batch(hipStream_t st0, hipStream_t st1, EncWs* w0, EncWs* w1, int n, int quality,
+                             int subsampling, int w, int h, int comps, const uint8_t* const* d_srcs, uint8_t* d_out,
+                             uint64_t stride, uint64_t* sizes, int32_t* status) {
+    if (n <= 0) return 0;
+    if (w == 0 || h == 0) {
+        for (int i = 0; i < n; ++i) {
+            const int rc = jpeg_encode_device(st0, w0, quality, subsampling, w, h, comps, d_srcs[i],
+                                              d_out + (uint64_t)i * stride, stride, &sizes[i]);
+            if (rc < 0) return -1;
+            status[i] = rc;
         }
-        ws->timed = false;
+        return 0;
     }
-    return 0;
+    uint8_t qnl[64], qnc[64];
+    ijg_table(kLumaQ, quality, qnl);
+    ijg_table(kK2Chroma, quality, qnc);
+    EncTables T;
+    build_tables(T, qnl, qnc);
+    std::vector<uint8_t> head;
+    ext_header(head, w, h, qnl, qnc, subsampling);
+    const uint64_t hn = head.size();
+    if (hn > sizeof(HdrArg::b)) return -1;
+    HdrArg ha;
+    std::memcpy(ha.b, head.data(), hn);
+    ha.n = (int)hn;
+    const EncLayout L = make_layout(subsampling, w);
+    EncWs* W[2] = {w0, w1};
+    hipStream_t S[2] = {st0, st1};
+    const uint64_t cap = stride > hn ? stride - hn : 0;
+    hipEvent_t fork = nullptr;
+    if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) return -1;
+    bool ok = hipEventRecord(fork, st0) == hipSuccess && hipStreamWaitEvent(st1, fork, 0) == hipSuccess;
+    auto finish = [&](int i) {  // wait for image i; re-run its tail once if its stream outgrew the buffer
+        EncWs& ws = *W[i & 1];
+        uint64_t nn = 0;
+        int rc = enc_collect(ws, &nn);
+        if (rc == 0) {
+            rc = enc_tail(S[i & 1], ws, L, w, h, comps, d_out + (uint64_t)i * stride + hn, cap, true, &ha) ? enc_collect(ws, &nn)
+                                                                                                       : -1;
+        }
+        if (rc <= 0) return false;
+        sizes[i] = hn + nn + 2;
+        status[i] = sizes[i] > stride ? 1 : 0;
+        return true;
+    };
+    for (int i = 0; ok && i < n + 2; ++i) {
+        if (i >= 2) ok = finish(i - 2);
+        if (ok && i < n) {
+            EncWs& ws = *W[i & 1];
+            ok = enc_front(S[i & 1], ws, L, i < 2 ? &T : nullptr, d_srcs[i], w, h, comps) &&
+                 enc_tail(S[i & 1], ws, L, w, h, comps, d_out + (uint64_t)i * stride + hn, cap, true, &ha);
+        }
+    }
+    // the caller's stream (st0) resumes after both
+    ok = ok && hipEventRecord(fork, st1) == hipSuccess && hipStreamWaitEvent(st0, fork, 0) == hipSuccess;
+    (void)hipEventDestroy(fork);
+    return ok ? 0 : -1;
 }
 
 }  // namespace icx

@@ -147,6 +147,15 @@ void icx_encoder_destroy(icx_encoder* enc);
 int icx_jpeg_encode_device(icx_encoder* enc, int quality, int subsampling, int width, int height,
                            int num_components, const uint8_t* d_src, uint8_t* d_out, uint64_t out_cap,
                            uint64_t* out_size, void* hip_stream);
+/* A batch of n device images of one geometry and setting (d_srcs: host array of device
+ * pointers) -> JPEG files at d_out + i*out_stride; out_sizes[i] and status[i] (ICX_OK, or
+ * ICX_OUT_OF_MEM when out_stride < out_sizes[i]: nothing written) on the host. Images alternate
+ * between two workspaces on two streams (hip_stream and an internal one), so each image's host
+ * wait overlaps the next image's kernels. Synchronous; returns ICX_OK, ICX_UNSUPPORTED or
+ * ICX_INTERNAL_ERR. Replaces a loop of icx_jpeg_encode_device calls (same bytes). */
+int icx_jpeg_encode_device_batch(icx_encoder* enc, int n, int quality, int subsampling, int width, int height,
+                                 int num_components, const uint8_t* const* d_srcs, uint8_t* d_out,
+                                 uint64_t out_stride, uint64_t* out_sizes, int32_t* status, void* hip_stream);
 /* Per-stage GPU time (HIP events) of the encodes since the previous call, summed: units
  * (DCT+quantise), count, scan, emit, stuff. Returns the number of stages filled (<= cap). */
 int icx_encoder_stage_times(icx_encoder* enc, const char** names, float* ms, int cap);

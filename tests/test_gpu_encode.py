@@ -124,3 +124,27 @@ def test_ext_device_estimate_regrowth(ctx):
     assert rc == icx.OUT_OF_MEM and n > 4096
     assert bool((d_out == 0xAB).all())
     enc2.close()
+
+
+@pytest.mark.parametrize("q,sub,w,h", [(90, 420, 640, 480), (50, 444, 333, 251), (100, 420, 1024, 768)])
+def test_ext_device_batch(ctx, q, sub, w, h):
+    """icx_jpeg_encode_device_batch (two workspaces on two streams) gives each image the oracle's
+    bytes; an image whose file exceeds the stride reports OUT_OF_MEM and leaves its slot alone."""
+    import torch
+    imgs = [S.rgb(300 + k, w, h, 3) for k in range(5)]
+    d_src = [torch.from_numpy(px).cuda() for px in imgs]
+    want = [O.jpeg_encode(q, sub, w, h, 3, px.tobytes()) for px in imgs]
+    stride = max(len(x) for x in want) + 64
+    d_out = torch.full((5 * stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    enc = icx.Encoder(ctx)
+    st, sizes = enc.encode_device_batch(q, sub, w, h, 3, [t.data_ptr() for t in d_src], d_out.data_ptr(), stride)
+    assert list(st) == [icx.OK] * 5 and list(sizes) == [len(x) for x in want]
+    out = d_out.cpu().numpy()
+    for k in range(5):
+        assert out[k * stride: k * stride + sizes[k]].tobytes() == want[k]
+    small = min(len(x) for x in want) - 1  # every image too large
+    d_out.fill_(0xAB)
+    st, sizes = enc.encode_device_batch(q, sub, w, h, 3, [t.data_ptr() for t in d_src], d_out.data_ptr(), small)
+    assert list(st) == [icx.OUT_OF_MEM] * 5 and list(sizes) == [len(x) for x in want]
+    assert bool((d_out == 0xAB).all())
+    enc.close()
