@@ -324,29 +324,62 @@ __device__ __forceinline__ uint32_t filt(int type, uint32_t s, uint32_t left, ui
     }
 }
 
+// Bytes [s, s+4) of row R packed little-endian (bytes before the row start read 0): the left
+// (or upper-left) neighbours of 4 consecutive positions at filter byte width bw.
+__device__ __forceinline__ uint32_t row_bytes4(const uint32_t* R, int64_t s) {
+    if (s >= 0) {
+        const int64_t j = s >> 2;
+        const int o = (int)(s & 3);
+        const uint32_t lo = R[j];
+        return o ? __builtin_amdgcn_alignbyte(R[j + 1], lo, (uint32_t)o) : lo;  // byte shift o
+    }
+    uint32_t v = 0;
+    for (int b = 0; b < 4; ++b)
+        if (s + b >= 0) v |= ((R[(s + b) >> 2] >> (8 * ((s + b) & 3))) & 255u) << (8 * b);
+    return v;
+}
+
 // One workgroup per row (grid-stride): MINSUM over the five filters, ties to the lower type
 // (`sum < smallest`, :3968), type 0 scored unsigned; palette / < 8 bits: type 0 (:3950).
+// Rows of whole dwords (lb % 4 == 0, the RGBA / 16-bit cases) are read a dword per lane:
+// the pixel, the pixel above and the left / upper-left neighbours (one alignbyte each).
 __global__ __launch_bounds__(256) void k_png_filter(const uint8_t* __restrict__ img, int h, const Mode* __restrict__ mode,
                                                     uint8_t* __restrict__ out) {
     const Mode& M = *mode;
     const int64_t lb = M.lb;
     const int bw = M.bw;
     const bool zero = M.colortype == kPalette || M.bitdepth < 8;
+    const bool wide = (lb & 3) == 0 && (reinterpret_cast<uintptr_t>(img) & 3) == 0;
     __shared__ uint32_t s_sum[5][4];
     for (int y = blockIdx.x; y < h; y += gridDim.x) {
         const uint8_t* cur = img + (int64_t)y * lb;
         const uint8_t* prv = y ? cur - lb : nullptr;
+        const uint32_t* C4 = reinterpret_cast<const uint32_t*>(cur);
+        const uint32_t* P4 = reinterpret_cast<const uint32_t*>(prv);
         int best = 0;
         if (!zero) {
             uint32_t sum[5] = {0, 0, 0, 0, 0};
-            for (int64_t i = threadIdx.x; i < lb; i += 256) {
-                const uint32_t s = cur[i], left = i >= bw ? cur[i - bw] : 0, up = prv ? prv[i] : 0,
-                               ul = (prv && i >= bw) ? prv[i - bw] : 0;
+            auto score = [&](uint32_t s, uint32_t left, uint32_t up, uint32_t ul) {
                 sum[0] += s;
 #pragma unroll
                 for (int tt = 1; tt < 5; ++tt) {
                     const uint32_t f = filt(tt, s, left, up, ul);
                     sum[tt] += f < 128 ? f : 255u - f;
+                }
+            };
+            if (wide) {
+                for (int64_t i = 4 * (int64_t)threadIdx.x; i < lb; i += 1024) {
+                    const uint32_t s4 = C4[i >> 2], l4 = row_bytes4(C4, i - bw);
+                    const uint32_t u4 = prv ? P4[i >> 2] : 0u, ul4 = prv ? row_bytes4(P4, i - bw) : 0u;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        score((s4 >> (8 * b)) & 255u, (l4 >> (8 * b)) & 255u, (u4 >> (8 * b)) & 255u, (ul4 >> (8 * b)) & 255u);
+                }
+            } else {
+                for (int64_t i = threadIdx.x; i < lb; i += 256) {
+                    const uint32_t s = cur[i], left = i >= bw ? cur[i - bw] : 0, up = prv ? prv[i] : 0,
+                                   ul = (prv && i >= bw) ? prv[i - bw] : 0;
+                    score(s, left, up, ul);
                 }
             }
 #pragma unroll
@@ -367,10 +400,27 @@ __global__ __launch_bounds__(256) void k_png_filter(const uint8_t* __restrict__ 
         }
         uint8_t* o = out + (int64_t)y * (lb + 1);
         if (threadIdx.x == 0) o[0] = (uint8_t)best;
-        for (int64_t i = threadIdx.x; i < lb; i += 256) {
-            const uint32_t s = cur[i], left = i >= bw ? cur[i - bw] : 0, up = prv ? prv[i] : 0,
-                           ul = (prv && i >= bw) ? prv[i - bw] : 0;
-            o[1 + i] = (uint8_t)filt(best, s, left, up, ul);
+        if (wide) {
+            for (int64_t i = 4 * (int64_t)threadIdx.x; i < lb; i += 1024) {
+                const uint32_t s4 = C4[i >> 2];
+                if (best == 0) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) o[1 + i + b] = (uint8_t)(s4 >> (8 * b));
+                    continue;
+                }
+                const uint32_t l4 = row_bytes4(C4, i - bw);
+                const uint32_t u4 = prv ? P4[i >> 2] : 0u, ul4 = prv ? row_bytes4(P4, i - bw) : 0u;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    o[1 + i + b] = (uint8_t)filt(best, (s4 >> (8 * b)) & 255u, (l4 >> (8 * b)) & 255u,
+                                                 (u4 >> (8 * b)) & 255u, (ul4 >> (8 * b)) & 255u);
+            }
+        } else {
+            for (int64_t i = threadIdx.x; i < lb; i += 256) {
+                const uint32_t s = cur[i], left = i >= bw ? cur[i - bw] : 0, up = prv ? prv[i] : 0,
+                               ul = (prv && i >= bw) ? prv[i - bw] : 0;
+                o[1 + i] = (uint8_t)filt(best, s, left, up, ul);
+            }
         }
     }
 }
