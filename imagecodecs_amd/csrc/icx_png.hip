@@ -434,13 +434,21 @@ __global__ __launch_bounds__(256) void k_png_filter(const uint8_t* __restrict__ 
 // can compare (q - d + l with q + l < s1) lies in one of them: indices >= s0 - kNear in `near`,
 // the others (distances rowlen - bw .. rowlen + bw only) in `far`.
 constexpr int kNear = 16;                        // >= 2 * bw (bw <= 8)
-constexpr int kStage = kSeg + 2 * kNear + 16;    // bytes per staged view, 16-byte multiple
+constexpr int kStage = kSeg + 2 * kNear + 32;    // bytes per staged view, 16-byte multiple (dword-read slack)
 struct SegView {
     const uint8_t* nearp;  // LDS base, = stream index nb0
     const uint8_t* farp;   // LDS base, = stream index fb0
     int64_t nb0, fb0, nlo; // nlo = s0 - kNear: lowest index served by `near`
     __device__ __forceinline__ uint8_t at(int64_t i) const {
         return i >= nlo ? nearp[i - nb0] : farp[i - fb0];
+    }
+    // bytes i .. i+3, byte i lowest (a far-view read never crosses the end of that view: far
+    // candidates compare below s1 - rowlen + bw, and the view runs 2 kNear + 32 bytes past it)
+    __device__ __forceinline__ uint32_t dword(int64_t i) const {
+        const bool nr = i >= nlo;
+        const int64_t o = nr ? i - nb0 : i - fb0;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(nr ? nearp : farp) + (o >> 2);
+        return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(o & 3));
     }
 };
 __device__ __forceinline__ void stage_view(const uint8_t* __restrict__ F, int64_t N, int64_t b0, uint8_t* lds, int lane) {
@@ -458,10 +466,16 @@ __device__ __forceinline__ void stage_view(const uint8_t* __restrict__ F, int64_
         *reinterpret_cast<uint4*>(lds + 16 * k) = v;
     }
 }
-__device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t dist, int64_t maxlen) {
+// Length of the match at p against p - dist, at most maxlen: four bytes per step, the first
+// differing byte from the lowest set bit of the XOR.
+__device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t dist, int maxlen) {
     int l = 0;
-    while (l < maxlen && V.nearp[p + l - V.nb0] == V.at(p - dist + l)) ++l;
-    return l;
+    while (l < maxlen) {
+        const uint32_t x = V.dword(p + l) ^ V.dword(p - dist + l);
+        if (x) return min(l + (int)(__builtin_ctz(x) >> 3), maxlen);
+        l += 4;
+    }
+    return maxlen;
 }
 
 // One workgroup (4 waves) per 256 KiB block; each wave takes a 4 KiB segment at a time, stages
@@ -523,15 +537,15 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
             int best = 0, bd = 0;
             uint32_t lit = 0;
             if (q < s1) {
-                const uint8_t* tq = V.nearp + (q - V.nb0);
-                lit = tq[0];
-                const int64_t maxlen = min((int64_t)258, s1 - q);
+                const uint32_t t4 = V.dword(q);
+                lit = t4 & 255u;
+                const int maxlen = (int)min((int64_t)258, s1 - q);
                 if (maxlen >= 3 && q >= pos) {  // positions under a previous match need no score
 #pragma unroll
                     for (int k = 0; k < 6; ++k) {
                         const int64_t dd = cand[k];
                         if (dd == 0 || dd > q) continue;
-                        if (tq[0] != V.at(q - dd) || tq[1] != V.at(q - dd + 1) || tq[2] != V.at(q - dd + 2)) continue;
+                        if (((V.dword(q - dd) ^ t4) & 0xFFFFFFu) != 0) continue;  // first three bytes
                         const int l = 3 + match_len(V, q + 3, dd, maxlen - 3);
                         if (l > best) {
                             best = l;
