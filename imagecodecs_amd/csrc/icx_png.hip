@@ -914,12 +914,10 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
         const uint32_t i = i0 + lane;
         int nb = 0;
         const uint64_t v = i < nt ? token_code(B, T[i], nb) : 0;
-        uint32_t inc = (uint32_t)nb;  // inclusive scan of nb over the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(inc, o);
-            if (lane >= o) inc += u;
-        }
+        uint32_t inc;  // inclusive scan of nb over the wave (rocprim's DPP cross-lane scan)
+        using WScan = rocprim::warp_scan<uint32_t, 64>;
+        typename WScan::storage_type wst;  // empty for the cross-lane implementation
+        WScan().inclusive_scan((uint32_t)nb, inc, wst);
         or_bits(W, pos + inc - nb, v, nb);
         pos += __shfl(inc, 63);
     }
