@@ -21,6 +21,7 @@
 //                   writes quantized coefficients; true-path errors flag the image
 // A lane's state is (bit position in U, block-in-MCU b, coefficient cursor z).
 #include <hip/hip_runtime.h>
+#include <rocprim/warp/warp_scan.hpp>
 
 #include "icx_spec_core.h"
 
@@ -122,14 +123,12 @@ __device__ __forceinline__ int find_image(const int32_t* pre, int n, int x) {
 // flat tile list, so the owning image only ever advances (no per-tile search).
 constexpr int kLaneRaw = kTileBytes / 64;
 
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o);
-        if (lane >= o) v += t;
-    }
-    return v;
+__device__ __forceinline__ int wave_incl_scan(int v) {  // rocprim's DPP cross-lane scan
+    using WScan = rocprim::warp_scan<int, 64>;
+    typename WScan::storage_type st;  // empty for the cross-lane implementation
+    int r;
+    WScan().inclusive_scan(v, r, st);
+    return r;
 }
 __device__ __forceinline__ long long wave_min_ll(long long v) {
 #pragma unroll
