@@ -487,8 +487,10 @@ __device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t di
 // position, longest over the candidates, never crossing the segment end).
 __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
                                                   int bw, uint32_t* __restrict__ tok, uint32_t* __restrict__ ntok,
-                                                  uint32_t* __restrict__ hist, uint32_t* __restrict__ adl) {
+                                                  uint32_t* __restrict__ hist, uint32_t* __restrict__ adl,
+                                                  uint16_t* __restrict__ seghist, uint32_t* __restrict__ segx) {
     __shared__ uint32_t h_ll[kNLL], h_d[kND];
+    __shared__ uint32_t s_h[4][kNLL + kND];  // per wave: the current segment's symbol counts
     __shared__ __attribute__((aligned(16))) uint8_t views[4][2][kStage];
     const int64_t blk = blockIdx.x;
     for (int i = threadIdx.x; i < kNLL; i += 256) h_ll[i] = 0;
@@ -504,6 +506,9 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
         if (seg >= nseg) break;  // wave-uniform
         const int64_t s0 = seg * kSeg, s1 = min(N, s0 + kSeg);
         uint32_t* T = tok + s0;
+        uint32_t* SH = s_h[wave];
+        for (int i = lane; i < kNLL + kND; i += 64) SH[i] = 0;
+        uint32_t xbits = 0;  // length / distance extra bits of the segment's matches (lane 0)
         SegView V;
         V.nlo = s0 - kNear;
         V.nb0 = V.nlo & ~(int64_t)15;
@@ -563,7 +568,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
                 const int le = min(mi, wend);
                 if (lane >= li && lane < le) {  // the literal run li .. le-1
                     T[nt + (lane - li)] = lit;
-                    atomicAdd(&h_ll[lit], 1u);
+                    atomicAdd(&SH[lit], 1u);
                 }
                 nt += (uint32_t)(le - li);
                 pos = p0 + le;
@@ -571,15 +576,29 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
                     const int len = __shfl(best, mi), dist = __shfl(bd, mi);
                     if (lane == 0) {
                         T[nt] = 0x80000000u | (uint32_t)(len - 3) << 15 | (uint32_t)(dist - 1);
-                        atomicAdd(&h_ll[257 + len_code(len)], 1u);
-                        atomicAdd(&h_d[dist_code(dist)], 1u);
+                        const int lc = len_code(len), dc = dist_code(dist);
+                        SH[257 + lc] += 1u;
+                        SH[kNLL + dc] += 1u;
+                        xbits += kLenExtra[lc] + kDistExtra[dc];
                     }
                     ++nt;
                     pos += len;
                 }
             }
         }
-        if (lane == 0) ntok[seg] = nt;
+        if (lane == 0) {
+            ntok[seg] = nt;
+            segx[seg] = xbits;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the segment's counts: to HBM for k_png_segbits, into the block histogram for k_png_huff
+        uint16_t* G = seghist + seg * (kNLL + kND);
+        for (int i = lane; i < kNLL + kND; i += 64) {
+            const uint32_t c = SH[i];
+            G[i] = (uint16_t)c;
+            if (c) atomicAdd(i < kNLL ? &h_ll[i] : &h_d[i - kNLL], c);
+        }
+        __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
     uint32_t* H = hist + blk * (kNLL + kND);
@@ -834,30 +853,24 @@ __device__ __forceinline__ void stage_codes(const BlockCodes* __restrict__ bc, B
     for (int i = threadIdx.x; i < (int)(sizeof(BlockCodes) / 4); i += blockDim.x) dst[i] = src[i];
     __syncthreads();
 }
-__device__ __forceinline__ uint32_t token_bits(const BlockCodes& B, uint32_t t) {
-    if (!(t & 0x80000000u)) return B.ll_len[t];
-    const int len = (int)((t >> 15) & 255) + 3, dist = (int)(t & 0x7FFF) + 1;
-    const int lc = len_code(len), dc = dist_code(dist);
-    return B.ll_len[257 + lc] + kLenExtra[lc] + B.d_len[dc] + kDistExtra[dc];
-}
 
-// One wave per segment: lanes sum the bit lengths of every 64th token.
-__global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint32_t* __restrict__ tok,
-                                                     const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
+// One wave per segment: the segment's symbol counts (from k_png_lz77) times the block's code
+// lengths, plus the extra bits of its matches -- no pass over the tokens.
+__global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint16_t* __restrict__ seghist,
+                                                     const uint32_t* __restrict__ segx, const BlockCodes* __restrict__ bc,
                                                      unsigned long long* __restrict__ bits) {
     __shared__ BlockCodes B;  // the four waves' segments share one block (kSegPerBlock % 4 == 0)
     stage_codes(bc, B);
     const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (seg >= nseg) return;  // wave-uniform
-    const uint32_t* T = tok + seg * kSeg;
-    const uint32_t nt = ntok[seg];
+    const uint16_t* G = seghist + seg * (kNLL + kND);
     uint32_t b = 0;
-    for (uint32_t i = lane; i < nt; i += 64) b += token_bits(B, T[i]);
+    for (int i = lane; i < kNLL + kND; i += 64) b += (uint32_t)G[i] * (i < kNLL ? B.ll_len[i] : B.d_len[i - kNLL]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o);
     if (lane == 0) {
-        unsigned long long t = b;
+        unsigned long long t = (unsigned long long)b + segx[seg];
         if (seg % kSegPerBlock == 0) t += B.hdr_bits;
         if (seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1) t += B.ll_len[256];  // EOB
         bits[seg] = t;
@@ -1075,6 +1088,9 @@ struct PngWs {
     size_t tok_cap = 0, seg_cap = 0, blk_cap = 0, hist_cap = 0, crc_cap = 0;
     BlockCodes* bc = nullptr;
     unsigned long long *bits = nullptr, *off = nullptr;
+    uint16_t* seghist = nullptr;  // per segment: literal/length and distance symbol counts
+    uint32_t* segx = nullptr;     // per segment: extra bits of its matches
+    size_t seghist_cap = 0, segx_cap = 0;
     void* tmp = nullptr;
     size_t tmp_cap = 0;
     // per-stage HIP events (icx_png_encoder_stage_times): stage i spans ev[2i] .. ev[2i+1];
@@ -1087,7 +1103,7 @@ struct PngWs {
             if (e) (void)hipEventDestroy(e);
         for (void* p : {(void*)st, (void*)set_key, (void*)set_idx, (void*)mode, (void*)conv, (void*)filt, (void*)tok,
                         (void*)ntok, (void*)hist, (void*)adl, (void*)crc, (void*)small, (void*)bc, (void*)bits,
-                        (void*)off, tmp})
+                        (void*)off, (void*)seghist, (void*)segx, tmp})
             if (p) (void)hipFree(p);
     }
 };
@@ -1305,13 +1321,16 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     size_t c11 = ws->small ? 64 : 0;
     if (!pgrow(ws->small, 64, c11)) return -1;
     mark(4);
+    if (!pgrow(ws->seghist, (size_t)nseg * (kNLL + kND) * 2, ws->seghist_cap) ||
+        !pgrow(ws->segx, (size_t)nseg * 4, ws->segx_cap))
+        return -1;
     hipLaunchKernelGGL(k_png_lz77, dim3((unsigned)nblk), dim3(256), 0, st, ws->filt, N, nseg, 1 + M.lb, M.bw, ws->tok,
-                       ws->ntok, ws->hist, ws->adl);
+                       ws->ntok, ws->hist, ws->adl, ws->seghist, ws->segx);
     mark(5);
     mark(6);
     hipLaunchKernelGGL(k_png_huff, dim3((unsigned)nblk), dim3(64), 0, st, ws->hist, nblk, ws->bc);
     const unsigned gwave = (unsigned)((nseg + 3) / 4);  // one wave per segment
-    hipLaunchKernelGGL(k_png_segbits, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->bits);
+    hipLaunchKernelGGL(k_png_segbits, dim3(gwave), dim3(256), 0, st, nseg, ws->seghist, ws->segx, ws->bc, ws->bits);
     size_t tb = 0;
     PNG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ws->bits, ws->off, (int)nseg, st));
     if (!pgrow(ws->tmp, tb, ws->tmp_cap)) return -1;
