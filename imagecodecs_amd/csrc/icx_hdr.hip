@@ -5,6 +5,7 @@
 // scanline was coded. The common files are located in parallel and only the rest is walked:
 //   k_hdr_parse      header walk (:713-750), one lane per image
 //   k_hdr_scan       every byte of the pixel data: new-style scanline starts "2 2 w>>8 w&255"
+//   k_hdr_candwalk   one lane per start found: walk that scanline to its end
 //                    (their ends found by walking the 4 run-length coded components), and
 //                    old-style run markers R=G=B=1 (:643-645)
 //   k_hdr_flatcheck  flat files: is row y, at ds + 4*w*y, a plain RGBE row?
@@ -149,7 +150,6 @@ __global__ __launch_bounds__(256) void k_hdr_scan(const uint8_t* __restrict__ da
     const int64_t n = dd.size, ds = dd.ds;
     const int w = dd.w;
     const bool newfmt = w >= 8 && w <= 0x7fff;
-    const int64_t cap = 16 * (int64_t)w + 64;
     bool marker = false;
     for (int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; ds + q < n; q += (int64_t)gridDim.x * blockDim.x * 4) {
         const int64_t p = ds + q;
@@ -162,16 +162,30 @@ __global__ __launch_bounds__(256) void k_hdr_scan(const uint8_t* __restrict__ da
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (k < nb && p + k + 3 < n && b[k] == 2 && b[k + 1] == 2 && b[k + 2] == (w >> 8) && b[k + 3] == (w & 255)) {
-                const int64_t e = hdr_walk_new(d, n, p + k, w, cap);
-                const int s = atomicAdd(&dd.ncand, 1);
-                if (s < kHdrCandCap) {
-                    cq[(int64_t)i * kHdrCandCap + s] = (int32_t)(q + k);
-                    ce[(int64_t)i * kHdrCandCap + s] = e >= 0 ? (int32_t)(e - ds) : (int32_t)e;
-                }
+                const int s = atomicAdd(&dd.ncand, 1);  // its end: k_hdr_candwalk
+                if (s < kHdrCandCap) cq[(int64_t)i * kHdrCandCap + s] = (int32_t)(q + k);
             }
         }
     }
     if (__any(marker) && (threadIdx.x & 63) == 0) atomicOr(&dd.has_marker, 1);
+}
+
+// grid (x: candidate chunks, y: image): one lane per scanline start k_hdr_scan found walks that
+// scanline's four run-length coded components to its end (hdr_walk_new). Walking in the scan
+// itself left 63 of 64 lanes idle behind each walking lane; here every lane walks.
+__global__ __launch_bounds__(256) void k_hdr_candwalk(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                      const HdrDesc* __restrict__ desc, const int32_t* __restrict__ cq,
+                                                      int32_t* __restrict__ ce) {
+    const int i = blockIdx.y;
+    const HdrDesc& dd = desc[i];
+    if (dd.status != kHdrPending) return;
+    const int nc = min(dd.ncand, kHdrCandCap);
+    const uint8_t* d = data + off[i];
+    const int64_t n = dd.size, ds = dd.ds, cap = 16 * (int64_t)dd.w + 64;
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nc; s += gridDim.x * blockDim.x) {
+        const int64_t e = hdr_walk_new(d, n, ds + cq[(int64_t)i * kHdrCandCap + s], dd.w, cap);
+        ce[(int64_t)i * kHdrCandCap + s] = e >= 0 ? (int32_t)(e - ds) : (int32_t)e;
+    }
 }
 
 // grid (x: row chunks, y: image). Row y of a flat file starts at ds + 4*w*y; it is decoded as a
@@ -463,6 +477,8 @@ void launch_hdr_decode(const HdrWs& ws, int n, const uint8_t* d_data, const uint
     E(kStParse);
     B(kStUnstuff);  // locating the scanlines
     hipLaunchKernelGGL(k_hdr_scan, dim3(gx, n), dim3(256), 0, st, d_data, d_off, ws.desc, ws.cq, ws.ce);
+    hipLaunchKernelGGL(k_hdr_candwalk, dim3(kHdrCandCap / 256, n), dim3(256), 0, st, d_data, d_off, ws.desc, ws.cq,
+                       ws.ce);
     hipLaunchKernelGGL(k_hdr_flatcheck, dim3(std::max(1, std::min(gx, (ws.max_h + 255) / 256)), n), dim3(256), 0, st,
                        d_data, d_off, ws.desc);
     hipLaunchKernelGGL(k_hdr_link, dim3(n), dim3(1024), 0, st, ws.desc, ws.cq, ws.ce, ws.start, ws.max_h);
