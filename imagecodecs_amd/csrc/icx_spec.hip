@@ -481,7 +481,7 @@ __device__ __forceinline__ int slot_elem(int t, int n) { return (((n >> 3) ^ (t 
 // NL lanes per workgroup; `wpre` numbers the image's lanes in NL-lane groups (wgpre for 256,
 // wg2pre for kWriteLanesBig), `total` = totals[1] or totals[2].
 template <int NL>
-__global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+__global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                     const uint8_t* __restrict__ U, int64_t ucap,
                                                     const uint64_t* __restrict__ X, const LaneEntry* __restrict__ ent,
@@ -500,7 +500,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int n, const Desc* __restrict
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wpre, n, wg, cur, T, desc);
         SpecImg& s = spec[i];
-        if (s.mode != 1 && s.mode != 3) continue;  // uniform per workgroup
+        // uniform per workgroup; `want` (1 or 3) limits a launch to one mode
+        if ((s.mode != 1 && s.mode != 3) || (want && s.mode != want)) continue;
         const bool dri = s.mode == 3;
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         const Sel S = make_sel(desc[i]);
@@ -679,12 +680,18 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
     E(kStEntropy);
     B(kStWrite);
-    if ((int64_t)ws.max_w * ws.max_h >= (int64_t)2048 * 2048)  // >= 1 MB of entropy data per image
-        hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec,
+    if ((int64_t)ws.max_w * ws.max_h >= (int64_t)2048 * 2048) {  // >= 1 MB of entropy data per image
+        // 2 KiB subsequences: 512-lane workgroups (tables amortised); restart intervals (DRI,
+        // typically one per MCU row, so a few hundred long lanes per image): 256-lane workgroups,
+        // which a 512-lane numbering would leave half idle
+        hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, 1, n, ws.desc, ws.spec,
                            ws.wg2pre, ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
-    else
-        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
+        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
                            ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+    } else {
+        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 0, n, ws.desc, ws.spec, ws.wgpre,
+                           ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+    }
     E(kStWrite);
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
 }
