@@ -151,20 +151,49 @@ __global__ __launch_bounds__(256) void k_hdr_scan(const uint8_t* __restrict__ da
     const int w = dd.w;
     const bool newfmt = w >= 8 && w <= 0x7fff;
     bool marker = false;
-    for (int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; ds + q < n; q += (int64_t)gridDim.x * blockDim.x * 4) {
+    auto found = [&](int64_t qk) {  // a new-style scanline start at data offset qk
+        const int s = atomicAdd(&dd.ncand, 1);  // its end: k_hdr_candwalk
+        if (s < kHdrCandCap) cq[(int64_t)i * kHdrCandCap + s] = (int32_t)qk;
+    };
+    const uint32_t pat = 2u | 2u << 8 | (uint32_t)((w >> 8) & 255) << 16 | (uint32_t)(w & 255) << 24;
+    // 16 positions per lane: six aligned dwords, realigned to p with alignbyte, give the 19 bytes
+    // the four 4-byte groups and sixteen candidate windows need
+    for (int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; ds + q < n;
+         q += (int64_t)gridDim.x * blockDim.x * 16) {
         const int64_t p = ds + q;
-        const int nb = (int)min<int64_t>(4, n - p);
-        uint8_t b[7];
+        if (p + 24 <= n) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(d + p);
+            const uint32_t mis = (uint32_t)(a & 3);
+            const uint32_t* g = reinterpret_cast<const uint32_t*>(a - mis);
+            uint32_t W[6], A[5];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) b[k] = p + k < n ? d[p + k] : 0;
-        marker |= nb == 4 && b[0] == 1 && b[1] == 1 && b[2] == 1;  // aligned groups (oldDecrunchHDR :644)
-        if (!newfmt) continue;
+            for (int k = 0; k < 6; ++k) W[k] = g[k];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < nb && p + k + 3 < n && b[k] == 2 && b[k + 1] == 2 && b[k + 2] == (w >> 8) && b[k + 3] == (w & 255)) {
-                const int s = atomicAdd(&dd.ncand, 1);  // its end: k_hdr_candwalk
-                if (s < kHdrCandCap) cq[(int64_t)i * kHdrCandCap + s] = (int32_t)(q + k);
+            for (int k = 0; k < 5; ++k) A[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], mis);  // bytes p+4k..
+#pragma unroll
+            for (int k = 0; k < 4; ++k) marker |= (A[k] & 0xFFFFFFu) == 0x010101u;  // aligned groups (:644)
+            if (!newfmt) continue;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t v = (k & 3) ? __builtin_amdgcn_alignbyte(A[(k >> 2) + 1], A[k >> 2], (uint32_t)(k & 3))
+                                           : A[k >> 2];
+                if (v == pat) found(q + k);
             }
+            continue;
+        }
+        for (int grp = 0; grp < 4; ++grp) {  // the file's last bytes, one at a time
+            const int64_t qq = q + 4 * grp, pp = ds + qq;
+            if (pp >= n) break;
+            const int nb = (int)min<int64_t>(4, n - pp);
+            uint8_t b[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) b[k] = pp + k < n ? d[pp + k] : 0;
+            marker |= nb == 4 && b[0] == 1 && b[1] == 1 && b[2] == 1;  // aligned groups (oldDecrunchHDR :644)
+            if (!newfmt) continue;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < nb && pp + k + 3 < n && b[k] == 2 && b[k + 1] == 2 && b[k + 2] == (w >> 8) && b[k + 3] == (w & 255))
+                    found(qq + k);
         }
     }
     if (__any(marker) && (threadIdx.x & 63) == 0) atomicOr(&dd.has_marker, 1);
