@@ -436,11 +436,24 @@ __global__ __launch_bounds__(256) void k_hdr_convert(const uint8_t* __restrict__
         if (dd.mode == 2) k = kRowNew;
         else if (dd.mode == 3) { k = kind[(int64_t)i * max_h + y]; s = start[(int64_t)i * max_h + y]; }
         const uint8_t* plane = planes + ((int64_t)i * max_h + y) * 4 * max_w;
+        // flat rows: one aligned dword (two when the row is not 4-byte aligned, realigned with
+        // alignbyte) per pixel instead of four byte loads; the row's last pixel may not read past
+        // the file
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(d + s) & 3);
+        const uint32_t* g4 = reinterpret_cast<const uint32_t*>(d + s - mis);
+        const int xfast = mis && s + 4 * (int64_t)w + 4 > dd.size ? w - 1 : w;  // pixels with a safe 2nd dword
         for (int x = threadIdx.x; x < w; x += blockDim.x) {
             uint32_t r, g, b, e;
             if (k == kRowFlat) {
-                const uint8_t* p = d + s + 4 * (int64_t)x;
-                r = p[0]; g = p[1]; b = p[2]; e = p[3];
+                uint32_t v;
+                if (x < xfast) {
+                    v = g4[x];
+                    if (mis) v = __builtin_amdgcn_alignbyte(g4[x + 1], v, mis);
+                } else {
+                    const uint8_t* p = d + s + 4 * (int64_t)x;
+                    v = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+                }
+                r = v & 255u; g = (v >> 8) & 255u; b = (v >> 16) & 255u; e = v >> 24;
             } else {
                 r = plane[x]; g = plane[w + x]; b = plane[2 * w + x]; e = plane[3 * w + x];
             }
