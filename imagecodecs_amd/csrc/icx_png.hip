@@ -486,7 +486,7 @@ __device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t di
 // by one. The tokens are those of a serial greedy parse (first match of length >= 3 per
 // position, longest over the candidates, never crossing the segment end).
 __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
-                                                  int bw, uint32_t* __restrict__ tok, uint32_t* __restrict__ ntok,
+                                                  int bw, uint16_t* __restrict__ tok, uint32_t* __restrict__ ntok,
                                                   uint32_t* __restrict__ hist, uint32_t* __restrict__ adl,
                                                   uint16_t* __restrict__ seghist, uint32_t* __restrict__ segx) {
     __shared__ uint32_t h_ll[kNLL], h_d[kND];
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
         const int64_t seg = blk * kSegPerBlock + sl;
         if (seg >= nseg) break;  // wave-uniform
         const int64_t s0 = seg * kSeg, s1 = min(N, s0 + kSeg);
-        uint32_t* T = tok + s0;
+        uint16_t* T = tok + s0;
         uint32_t* SH = s_h[wave];
         for (int i = lane; i < kNLL + kND; i += 64) SH[i] = 0;
         uint32_t xbits = 0;  // length / distance extra bits of the segment's matches (lane 0)
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
                 const int mi = m ? __ffsll((unsigned long long)m) - 1 : 64;
                 const int le = min(mi, wend);
                 if (lane >= li && lane < le) {  // the literal run li .. le-1
-                    T[nt + (lane - li)] = lit;
+                    T[nt + (lane - li)] = (uint16_t)lit;
                     atomicAdd(&SH[lit], 1u);
                 }
                 nt += (uint32_t)(le - li);
@@ -575,13 +575,14 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
                 if (mi < wend) {  // the match at lane mi
                     const int len = __shfl(best, mi), dist = __shfl(bd, mi);
                     if (lane == 0) {
-                        T[nt] = 0x80000000u | (uint32_t)(len - 3) << 15 | (uint32_t)(dist - 1);
+                        T[nt] = (uint16_t)(0x4000u | (uint32_t)(len - 3));    // match: length slot,
+                        T[nt + 1] = (uint16_t)(0x8000u | (uint32_t)(dist - 1));  // then distance slot
                         const int lc = len_code(len), dc = dist_code(dist);
                         SH[257 + lc] += 1u;
                         SH[kNLL + dc] += 1u;
                         xbits += kLenExtra[lc] + kDistExtra[dc];
                     }
-                    ++nt;
+                    nt += 2;
                     pos += len;
                 }
             }
@@ -877,14 +878,20 @@ __global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint16_
     }
 }
 
-// Token -> (bits, count), LSB-first: code, length extra, distance code, distance extra
-// (at most 15 + 5 + 15 + 13 = 48 bits).
-__device__ __forceinline__ uint64_t token_code(const BlockCodes& B, uint32_t t, int& nb) {
-    if (!(t & 0x80000000u)) {
+// Token slot i -> (bits, count), LSB-first: a literal; or, at a match's length slot, code, length
+// extra, distance code, distance extra (at most 15 + 5 + 15 + 13 = 48 bits); a distance slot
+// emits nothing (its match's length slot took it).
+__device__ __forceinline__ uint64_t token_code(const BlockCodes& B, const uint16_t* T, uint32_t i, int& nb) {
+    const uint32_t t = T[i];
+    if (t < 256) {
         nb = B.ll_len[t];
         return B.ll_code[t];
     }
-    const int len = (int)((t >> 15) & 255) + 3, dist = (int)(t & 0x7FFF) + 1;
+    if (t & 0x8000u) {
+        nb = 0;
+        return 0;
+    }
+    const int len = (int)(t & 255) + 3, dist = (int)(T[i + 1] & 0x7FFFu) + 1;
     const int lc = len_code(len), dc = dist_code(dist);
     uint64_t v = B.ll_code[257 + lc];
     int n = B.ll_len[257 + lc];
@@ -914,7 +921,7 @@ __device__ __forceinline__ void or_bits(uint32_t* w, unsigned long long bitpos, 
 }
 // The segment's bits into W (word 0 = output word w0; zeroed), starting at bit `pos`.
 __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos, const BlockCodes& B,
-                                             const uint32_t* T, uint32_t nt, bool head, bool eob, int lane) {
+                                             const uint16_t* T, uint32_t nt, bool head, bool eob, int lane) {
     if (head) {  // the block header: its words, shifted into place
         const uint32_t hb = B.hdr_bits;
         for (uint32_t i = lane; i * 32 < hb; i += 64) {
@@ -926,7 +933,7 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
     for (uint32_t i0 = 0; i0 < nt; i0 += 64) {
         const uint32_t i = i0 + lane;
         int nb = 0;
-        const uint64_t v = i < nt ? token_code(B, T[i], nb) : 0;
+        const uint64_t v = i < nt ? token_code(B, T, i, nb) : 0;
         uint32_t inc;  // inclusive scan of nb over the wave (rocprim's DPP cross-lane scan)
         using WScan = rocprim::warp_scan<uint32_t, 64>;
         typename WScan::storage_type wst;  // empty for the cross-lane implementation
@@ -936,7 +943,7 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
     }
     if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
 }
-__global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint32_t* __restrict__ tok,
+__global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint16_t* __restrict__ tok,
                                                   const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
                                                   const unsigned long long* __restrict__ off,
                                                   const unsigned long long* __restrict__ bits, uint32_t* __restrict__ out,
@@ -947,7 +954,7 @@ __global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint32_t* 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t seg = (int64_t)blockIdx.x * 4 + wave;
     if (seg >= nseg) return;  // wave-uniform; no block barriers below
-    const uint32_t* T = tok + seg * kSeg;
+    const uint16_t* T = tok + seg * kSeg;
     const uint32_t nt = ntok[seg];
     const unsigned long long o0 = base_bits + off[seg], o1 = o0 + bits[seg];
     if (o1 == o0) return;
@@ -1084,7 +1091,8 @@ struct PngWs {
     Mode* mode = nullptr;
     uint8_t *conv = nullptr, *filt = nullptr;
     size_t conv_cap = 0, filt_cap = 0;
-    uint32_t *tok = nullptr, *ntok = nullptr, *hist = nullptr, *adl = nullptr, *crc = nullptr, *small = nullptr;
+    uint16_t* tok = nullptr;  // token slots: literal byte, or a match's length slot + distance slot
+    uint32_t *ntok = nullptr, *hist = nullptr, *adl = nullptr, *crc = nullptr, *small = nullptr;
     size_t tok_cap = 0, seg_cap = 0, blk_cap = 0, hist_cap = 0, crc_cap = 0;
     BlockCodes* bc = nullptr;
     unsigned long long *bits = nullptr, *off = nullptr;
@@ -1306,7 +1314,7 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     // ---- P3/P4: deflate
     const int64_t nseg = (N + kSeg - 1) / kSeg, nblk = (nseg + kSegPerBlock - 1) / kSegPerBlock;
     size_t c5 = ws->seg_cap, c6 = ws->seg_cap, c7 = ws->seg_cap, c8 = ws->seg_cap, c9 = ws->blk_cap, c10 = ws->blk_cap;
-    if (!pgrow(ws->tok, (size_t)nseg * kSeg * 4, ws->tok_cap)) return -1;
+    if (!pgrow(ws->tok, (size_t)nseg * kSeg * 2, ws->tok_cap)) return -1;  // <= kSeg slots per segment
     if ((size_t)nseg * 8 > ws->seg_cap || !ws->ntok) {
         if (!pgrow(ws->ntok, (size_t)nseg * 8, c5) || !pgrow(ws->adl, (size_t)nseg * 8, c6) ||
             !pgrow(ws->bits, (size_t)nseg * 8, c7) || !pgrow(ws->off, (size_t)nseg * 8, c8))
