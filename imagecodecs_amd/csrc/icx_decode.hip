@@ -259,8 +259,10 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
     __shared__ uint32_t bgeo[kIdctUnitBlocks];   // unit block q -> ci | LDS offset of its tile << 2
     __shared__ IdctComp cg[3];
     __shared__ int32_t roff[4];                  // LDS offset of each component's rectangle
-    __shared__ int4 zzb[4][8][8];                // per wave: the octet's blocks as stored (zig-zag)
-    __shared__ int32_t rows[4][8][8][9];         // per wave: row-pass output, padded
+    // per wave: row-pass output (padded); the octet's blocks as stored (zig-zag) share its space:
+    // they are read before the row pass writes (a wave's LDS accesses complete in order), and
+    // the 4 KB saved fits six workgroups per CU (6 waves/SIMD) instead of five
+    __shared__ __attribute__((aligned(16))) int32_t rows[4][8][8][9];
     __shared__ uint2 pixu[4][kIdctUnitBlocks * 8];  // per wave: the unit's pixels (64 B per block)
     const int t = threadIdx.x;
     const int bpm = d.bpm, mbw = d.mbw, nc = d.nc;
@@ -296,7 +298,9 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
     uint32_t zo[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) zo[j] = 2u * kZigOfNat[r * 8 + j];
-    const uint8_t* zrow = reinterpret_cast<const uint8_t*>(&zzb[wave][lb][0]);
+    static_assert(sizeof(rows[0]) % 16 == 0 && sizeof(rows[0]) >= sizeof(int4) * 64, "zig-zag stage fits");
+    int4* zzw = reinterpret_cast<int4*>(&rows[wave][0][0][0]);  // this wave's [8][8] stage
+    const uint8_t* zrow = reinterpret_cast<const uint8_t*>(zzw + lb * 8);
     uint8_t* pb = reinterpret_cast<uint8_t*>(&pixu[wave][0]);
     const int16_t* A = ac + (int64_t)img * coef_cap * 64;
     const int32_t* D = dcv + (int64_t)img * coef_cap;
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
                 if (o0 + k >= noct) break;  // wave-uniform
                 const int q = (o0 + k) * 8 + lb;
                 const bool live = q < nb;
-                zzb[wave][lb][r] = c[k];
+                zzw[lb * 8 + r] = c[k];
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t bg = bgeo[live ? q : 0];
                 const int ci = (int)(bg & 3);
