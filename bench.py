@@ -668,9 +668,10 @@ def main():
         kname = STAGE_KERNEL.get(dom, dom)
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
-            if tj.get("workload") == args.workload and tj.get("kernel") == kname and \
-                    tj.get("images_per_launch") == -(-n // launches):
-                traffic = tj.get("bytes_per_launch")
+            # PMC runs may group images differently (the profiler holds HBM, so fewer images fit a
+            # group): the per-image traffic is scaled to this run's images per launch
+            if tj.get("workload") == args.workload and tj.get("kernel") == kname and tj.get("images_per_launch"):
+                traffic = round(tj["bytes_per_launch"] / tj["images_per_launch"] * (-(-n // launches)))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": kname, "launches_per_step": launches,
