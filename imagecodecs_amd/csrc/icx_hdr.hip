@@ -380,32 +380,66 @@ __global__ void k_hdr_walk(int n, const uint8_t* __restrict__ data, const uint64
     dd.status = status;
 }
 
-// One wave per new-style row: packet headers are read wave-uniformly, literal bytes and runs are
-// written by the lanes into the row's 4 component planes. grid (x: row chunks of 4 waves, y: image)
+// One wave per new-style row: the row's packet stream is staged through a 4 KB LDS window per wave
+// (coalesced 16-byte loads), so the wave-uniform chain of packet headers runs at LDS latency
+// instead of one dependent global load per packet; literal bytes and runs are written by the
+// lanes into the row's 4 component planes. The window is refilled at the current packet whenever
+// fewer than 129 bytes (the longest packet: code 128 + 128 literals) remain in it; bytes past the
+// file end are never read. grid (x: row chunks of 4 waves, y: image)
+constexpr int kHdrWin = 4096;
 __global__ __launch_bounds__(256) void k_hdr_unpack(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                                                     const HdrDesc* __restrict__ desc, const int64_t* __restrict__ start,
                                                     const uint8_t* __restrict__ kind, uint8_t* __restrict__ planes,
                                                     int max_w, int max_h) {
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kHdrWin];
     const int i = blockIdx.y;
     const HdrDesc& dd = desc[i];
     if (dd.mode != 2 && dd.mode != 3) return;
     const uint8_t* d = data + off[i];
+    const int64_t fsize = dd.size;
     const int w = dd.w, lane = threadIdx.x & 63;
+    uint8_t* win = win_all[threadIdx.x >> 6];
     for (int y = blockIdx.x * 4 + (threadIdx.x >> 6); y < dd.rows; y += gridDim.x * 4) {
         if (dd.mode == 3 && kind[(int64_t)i * max_h + y] != kRowNew) continue;
         int64_t pos = start[(int64_t)i * max_h + y] + 4;
+        int64_t base = 0, lim = -1;  // window holds file bytes [base, base + kHdrWin); refill past lim
         uint8_t* plane = planes + ((int64_t)i * max_h + y) * 4 * max_w;
         for (int c = 0; c < 4; ++c) {
             uint8_t* pc = plane + (int64_t)c * w;
             for (int j = 0; j < w;) {
-                int code = d[pos];
+                if (pos > lim) {
+                    // base: pos rounded down so that d + base is 16-byte aligned
+                    base = pos - (int64_t)(reinterpret_cast<uintptr_t>(d + pos) & 15);
+                    lim = base + kHdrWin - 129;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int q = 0; q < kHdrWin / (64 * 16); ++q) {
+                        const int o = (q * 64 + lane) * 16;
+                        const int64_t a = base + o;
+                        uint4 v = make_uint4(0, 0, 0, 0);
+                        if (a >= 0 && a + 16 <= fsize) {
+                            v = *reinterpret_cast<const uint4*>(d + a);
+                        } else {
+                            uint32_t t[4] = {0, 0, 0, 0};
+                            for (int b = 0; b < 16; ++b)
+                                if (a + b >= 0 && a + b < fsize) t[b >> 2] |= (uint32_t)d[a + b] << (8 * (b & 3));
+                            v = make_uint4(t[0], t[1], t[2], t[3]);
+                        }
+                        *reinterpret_cast<uint4*>(win + o) = v;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+                const uint8_t* p = win + (pos - base);
+                int code = p[0];
                 if (code > 128) {
                     code &= 127;
-                    const uint8_t v = d[pos + 1];
+                    const uint8_t v = p[1];
                     for (int k = lane; k < code; k += 64) pc[j + k] = v;
                     pos += 2;
                 } else {
-                    for (int k = lane; k < code; k += 64) pc[j + k] = d[pos + 1 + k];
+                    for (int k = lane; k < code; k += 64) pc[j + k] = p[1 + k];
                     pos += 1 + code;
                 }
                 j += code;
