@@ -46,6 +46,7 @@ struct icx_batch {
     hipEvent_t fork = nullptr, join[kMaxPipes] = {};
     uint8_t* d_hin = nullptr;  // staging for icx_jpeg_batch_decode_host
     size_t d_hin_cap = 0;
+    hipStream_t last_st = nullptr;  // the stream the last decode was ordered on
     std::unique_ptr<EventHook> hook;
 };
 
@@ -177,7 +178,15 @@ static void ws_free(GroupWs& ws) {
     ws = GroupWs{};
 }
 
+static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int max_h);
+// All or nothing: a failure part-way frees this workspace's buffers before returning.
 static bool ws_alloc(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int max_h) {
+    if (ws_alloc_all(ctx, ws, group, max_w, max_h)) return true;
+    ws_free(ws);
+    return false;
+}
+
+static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int max_h) {
     (void)ws_per_slot(ws, max_w, max_h);
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
@@ -218,7 +227,9 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
         return nullptr;
     }
     ICX_HIP(ctx, hipSetDevice(ctx->device), nullptr);
-    auto b = std::make_unique<icx_batch>();
+    // Every early return below (an allocation or stream/event creation failing part-way) frees
+    // what was already created: the deleter is icx_batch_destroy, which skips null members.
+    std::unique_ptr<icx_batch, void (*)(icx_batch*)> b(new icx_batch(), icx_batch_destroy);
     b->ctx = ctx;
     b->max_images = max_images;
     // pipelines: ICX_PIPES (1..2, default 2) when the batch holds at least two images
@@ -270,6 +281,7 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     if (!d_data || !d_off || !d_size || !d_out || !d_status || !d_dims) { ctx->err = "null pointer"; return ICX_INTERNAL_ERR; }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    b->last_st = st;
     b->hook->reset();
     for (int p = 0; p < b->pipes; ++p)
         ICX_HIP(ctx, hipMemsetAsync(b->ws[p].stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
@@ -301,6 +313,12 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
 int icx_batch_path_stats(const icx_batch* b, int32_t* parallel, int32_t* fallback, int32_t* sequential) {
     if (!b) return ICX_INTERNAL_ERR;
     int32_t h[4] = {0, 0, 0, 0};
+    // The decode ran on non-blocking streams, which the null stream does not order against:
+    // wait for them (every pipe joins into last_st) before reading the counters.
+    ICX_HIP(b->ctx, hipSetDevice(b->ctx->device), ICX_INTERNAL_ERR);
+    if (b->last_st) ICX_HIP(b->ctx, hipStreamSynchronize(b->last_st), ICX_INTERNAL_ERR);
+    for (int p = 1; p < b->pipes; ++p)
+        if (b->pst[p]) ICX_HIP(b->ctx, hipStreamSynchronize(b->pst[p]), ICX_INTERNAL_ERR);
     for (int p = 0; p < b->pipes; ++p) {
         int32_t q[4];
         ICX_HIP(b->ctx, hipMemcpy(q, b->ws[p].stats, sizeof q, hipMemcpyDeviceToHost), ICX_INTERNAL_ERR);

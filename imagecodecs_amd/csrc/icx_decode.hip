@@ -511,7 +511,8 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
     const int ntiles = ntx * nty;
     const uint8_t* P[3] = {P0, P0 + comp_plane_off(d, 1), P0 + comp_plane_off(d, 2)};
     const int kind[2] = {fused_kind(d, 1), fused_kind(d, 2)};
-    const bool aligned_out = ((W * 3) & 3) == 0;
+    // dword stores need 4-byte aligned rows: the row pitch and the image base (out_stride may be odd)
+    const bool aligned_out = ((W * 3) & 3) == 0 && (reinterpret_cast<uintptr_t>(o) & 3) == 0;
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int ty = tile / ntx, tx = tile - ty * ntx;
         const int X0 = tx * kTW, Y0 = ty * kTH;

@@ -890,10 +890,13 @@ int jpeg_encode_device_batch(hipStream_t st0, hipStream_t st1, EncWs* w0, EncWs*
                  enc_tail(S[i & 1], ws, L, w, h, comps, d_out + (uint64_t)i * stride + hn, cap, true, &ha);
         }
     }
-    // the caller's stream (st0) resumes after both
-    ok = ok && hipEventRecord(fork, st1) == hipSuccess && hipStreamWaitEvent(st0, fork, 0) == hipSuccess;
+    // The caller's stream (st0) resumes after both -- on the error path too: an image may still
+    // be running on st1, writing d_out and ws2, and a caller that reuses d_out on st0 must not
+    // overtake it. If the join itself cannot be recorded, wait for st1 on the host.
+    const bool joined = hipEventRecord(fork, st1) == hipSuccess && hipStreamWaitEvent(st0, fork, 0) == hipSuccess;
+    if (!joined) (void)hipStreamSynchronize(st1);
     (void)hipEventDestroy(fork);
-    return ok ? 0 : -1;
+    return ok && joined ? 0 : -1;
 }
 
 }  // namespace icx

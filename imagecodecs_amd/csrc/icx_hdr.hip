@@ -458,11 +458,22 @@ __global__ __launch_bounds__(256) void k_hdr_convert(const uint8_t* __restrict__
     if (dd.mode == 0) return;
     const uint8_t* d = data + off[i];
     const int w = dd.w;
-    float4* o = reinterpret_cast<float4*>(out + (int64_t)i * out_stride);
+    float* const fo = out + (int64_t)i * out_stride;
+    // 16-byte stores need a 16-byte aligned image base (out_stride is any number of floats)
+    const bool vec = (reinterpret_cast<uintptr_t>(fo) & 15) == 0;
+    float4* o = reinterpret_cast<float4*>(fo);
+    auto put = [&](float4* p, const float4& v) {
+        if (vec) {
+            *p = v;
+        } else {
+            float* q = reinterpret_cast<float*>(p);
+            q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
+        }
+    };
     for (int y = blockIdx.x; y < dd.h; y += gridDim.x) {
         float4* orow = o + (int64_t)y * w;
         if (y >= dd.rows) {  // rows after a failed scanline (uninitialised in the reference)
-            for (int x = threadIdx.x; x < w; x += blockDim.x) orow[x] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int x = threadIdx.x; x < w; x += blockDim.x) put(orow + x, make_float4(0.f, 0.f, 0.f, 0.f));
             continue;
         }
         int k = kRowFlat;
@@ -492,7 +503,7 @@ __global__ __launch_bounds__(256) void k_hdr_convert(const uint8_t* __restrict__
                 r = plane[x]; g = plane[w + x]; b = plane[2 * w + x]; e = plane[3 * w + x];
             }
             const int ex = (int)e - 136;
-            orow[x] = make_float4(ldexpf((float)r, ex), ldexpf((float)g, ex), ldexpf((float)b, ex), (float)e);
+            put(orow + x, make_float4(ldexpf((float)r, ex), ldexpf((float)g, ex), ldexpf((float)b, ex), (float)e));
         }
     }
 }

@@ -91,6 +91,59 @@ def test_batch_out_of_capacity_is_oom(ctx):
     assert res[0][4].tobytes() == O.decode(small)[4]
 
 
+@pytest.mark.parametrize("stride_extra", [1, 2, 3])
+def test_decode_host_unaligned_out_stride(ctx, stride_extra):
+    """An out_stride that is not a multiple of 4: images 1.. start at odd device addresses, so
+    the dword-storing convert paths must check the image base (tiny 4:2:0 chroma and 4:1:1 take
+    k_convert_fused / the generic passes)."""
+    # chroma planes of 3 samples (W or H = 5..6 at 4:2:0) are below k_convert_stream's minimum of 4
+    cases = [(6, 6, "420"), (5, 10, "420"), (10, 6, "420"), (12, 12, "420"), (36, 20, "411"), (64, 64, "422"),
+             (100, 52, "420"), (24, 16, "440"), (6, 40, "422")]
+    jpegs = [S.synth_jpeg(7000 + k, w, h, smp, 75) for k, (w, h, smp) in enumerate(cases)]
+    b = icx.Batch(ctx, len(jpegs), 100, 64)
+    res = b.decode_host(jpegs, out_stride=100 * 64 * 3 + stride_extra)
+    for j, (code, w, h, n, pix) in zip(jpegs, res):
+        ocode, ow, oh, on, opix = O.decode(j)
+        assert code == ocode == 0 and (w, h, n) == (ow, oh, on)
+        assert pix.tobytes() == opix
+    b.close()
+
+
+@pytest.mark.parametrize("group", [1200, 2400, 100000])
+def test_batch_create_failure_frees_device_memory(ctx, group):
+    """An explicit group too large for HBM fails part-way through the workspace allocation
+    (inside pipe 0, or in pipe 1 after pipe 0 succeeded): nothing may stay allocated."""
+    import torch
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    with pytest.raises(icx.ICXError):
+        icx.Batch(ctx, group, 4096, 4096, group)
+    free1 = torch.cuda.mem_get_info(0)[0]
+    assert free0 - free1 < 64 << 20, (free0, free1)
+
+
+def test_path_stats_after_device_decode_without_sync(ctx):
+    """path_stats right after an asynchronous device decode: it must order itself after the
+    decode's streams instead of reading stale counters."""
+    import torch
+    dev = torch.device("cuda", 0)
+    jpegs = [S.synth_jpeg(7100 + i, 640, 480, "420", 90) for i in range(6)]
+    sizes = [len(j) for j in jpegs]
+    offs = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
+    data = torch.from_numpy(np.frombuffer(b"".join(jpegs), np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_sz = torch.from_numpy(np.array(sizes, np.int64)).to(dev)
+    stride = 640 * 480 * 3
+    out = torch.zeros(len(jpegs) * stride, dtype=torch.uint8, device=dev)
+    st = torch.zeros((len(jpegs),), dtype=torch.int32, device=dev)
+    dims = torch.zeros((len(jpegs), 3), dtype=torch.int32, device=dev)
+    b = icx.Batch(ctx, len(jpegs), 640, 480, 2)
+    b.decode_device(len(jpegs), data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), out.data_ptr(), stride,
+                    st.data_ptr(), dims.data_ptr(), 0)
+    assert b.path_stats() == {"parallel": len(jpegs), "fallback": 0, "sequential": 0}
+    b.close()
+
+
 def test_device_resident_batch_torch(ctx):
     """The throughput API: device pointers in, device pointers out, per-image statuses."""
     import torch

@@ -55,7 +55,7 @@ def test_hdr_edge_files_single(ctx):
         _same(ctx.hdr_decode(data), O.hdr_decode(data), name)
 
 
-def _batch(ctx, files, max_w, max_h):
+def _batch(ctx, files, max_w, max_h, pad=0):
     import torch
     dev = torch.device("cuda", 0)
     n = len(files)
@@ -66,7 +66,7 @@ def _batch(ctx, files, max_w, max_h):
     data = torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).to(dev)
     d_off = torch.from_numpy(offs).to(dev)
     d_sz = torch.from_numpy(sizes).to(dev)
-    stride = 4 * max_w * max_h
+    stride = 4 * max_w * max_h + pad  # pad: floats, so images >= 1 may sit off 16-byte alignment
     out = torch.full((n * stride,), -7.0, dtype=torch.float32, device=dev)
     st = torch.full((n,), -9, dtype=torch.int32, device=dev)
     dims = torch.zeros((n, 3), dtype=torch.int32, device=dev)
@@ -117,6 +117,17 @@ def test_hdr_many_rows_beyond_candidate_cap(ctx):
     res, _ = _batch(ctx, [f], 16, 9000)
     assert res[0][0] == icx.HDR_OK
     np.testing.assert_array_equal(res[0][4].view(np.uint32), H.expected_floats(px).view(np.uint32))
+
+
+@pytest.mark.parametrize("pad", [1, 2, 3])
+def test_hdr_batch_unaligned_stride(ctx, pad):
+    """out_stride not a multiple of 4 floats: images 1.. start off 16-byte alignment, and the
+    convert kernel must fall back to scalar stores (same float bits)."""
+    imgs = [H.S.rgbe(60 + k, 33 + 7 * k, 21 + 3 * k) for k in range(3)]
+    files = [H.S.hdr(px, m) for px, m in zip(imgs, [H.RLE, H.FLAT, H.OLD])]
+    res, _ = _batch(ctx, files, 64, 40, pad)
+    for k, (f, got) in enumerate(zip(files, res)):
+        _same(got, O.hdr_decode(f), f"pad{pad}/{k}")
 
 
 def test_hdr_too_large_for_workspace(ctx):

@@ -44,7 +44,8 @@ def parse(fetch_dir, write_dir, kernel, workload, images):
     wv = _values(write_dir, "WRITE_SIZE", kernel)
     f_kib = sum(fv) / len(fv)
     w_kib = sum(wv) / len(wv)
-    fetch_b = 2.0 * f_kib * 1024.0  # gfx950: FETCH_SIZE = half the bytes of 16 B/lane reads
+    corr, src = fetch_correction()
+    fetch_b = corr * f_kib * 1024.0  # gfx950: FETCH_SIZE = half the bytes of 16 B/lane reads
     write_b = w_kib * 1024.0
     n_images = images or {"c3": 512, "c2": 1024}.get(workload)
     return {"workload": workload, "kernel": kernel, "images_per_bench_step": n_images,
@@ -52,8 +53,22 @@ def parse(fetch_dir, write_dir, kernel, workload, images):
             "launches": len(fv), "fetch_size_kib_raw": round(f_kib, 1), "write_size_kib_raw": round(w_kib, 1),
             "fetch_bytes": round(fetch_b), "write_bytes": round(write_b),
             "bytes_per_launch": round(fetch_b + write_b),
-            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs; FETCH_SIZE x2 "
-                      "(gfx950 wide-read correction, MI355X_MICROARCH.md HBM section); KiB -> bytes"}
+            "fetch_correction": corr, "fetch_correction_source": src,
+            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs; FETCH_SIZE x the "
+                      "correction measured by tools/pmc_calib.py (1 GiB of 16 B/lane reads); KiB -> bytes"}
+
+
+def fetch_correction():
+    """FETCH_SIZE -> bytes factor for 16 B/lane streaming reads, as measured in this repo by
+    tools/pmc_calib.py (profiles/r02_pmc_calibration.json); the guide's x2 if absent."""
+    p = os.path.join(ROOT, "profiles", "r02_pmc_calibration.json")
+    try:
+        c = json.load(open(p))["fetch_correction_read16"]
+        if c:
+            return float(c), os.path.relpath(p, ROOT)
+    except (OSError, KeyError, ValueError):
+        pass
+    return 2.0, "MI355X_MICROARCH.md HBM section (not yet calibrated here)"
 
 
 def run(args):
