@@ -15,6 +15,7 @@
 
 #include "../../include/icx.h"
 #include "icx_internal.h"
+#include "icx_step.h"
 
 using namespace icx;
 
@@ -58,6 +59,7 @@ static thread_local char g_msg[512];
     do {                                                                                    \
         hipError_t e_ = (call);                                                             \
         if (e_ != hipSuccess) {                                                             \
+            (void)hipGetLastError(); /* reported here: not left for the caller's next check */ \
             std::snprintf(g_msg, sizeof g_msg, "%s failed: %s", #call, hipGetErrorString(e_)); \
             if (ctx) (ctx)->err = g_msg;                                                    \
             return ret;                                                                     \
@@ -164,6 +166,7 @@ static int64_t ws_per_slot(GroupWs& ws, int max_w, int max_h) {
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
     return ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
+           (int64_t)sizeof(StepSet) +
            tiles_per_slot * 28 + ws.rst_cap * 8 +
            lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
 }
@@ -173,7 +176,7 @@ static void ws_free(GroupWs& ws) {
                     (void*)ws.tilepre, (void*)ws.wgpre, (void*)ws.wg2pre, (void*)ws.totals, (void*)ws.tiles,
                     (void*)ws.tile_obase, (void*)ws.U, (void*)ws.X, (void*)ws.sub, (void*)ws.rst, (void*)ws.tile_rbase,
                     (void*)ws.ent, (void*)ws.stats, (void*)ws.Y, (void*)ws.rec, (void*)ws.nrec, (void*)ws.guess_cnt,
-                    (void*)ws.repair})
+                    (void*)ws.repair, (void*)ws.steps})
         if (p) (void)hipFree(p);
     ws = GroupWs{};
 }
@@ -218,6 +221,7 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ICX_HIP(ctx, hipMalloc(&ws.nrec, sizeof(int32_t) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.guess_cnt, sizeof(int32_t) * 4 * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.repair, sizeof(int32_t) * kMaxRepair * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.steps, sizeof(StepSet) * group), false);
     return true;
 }
 

@@ -85,6 +85,7 @@ struct GroupWs {
     int64_t* rst = nullptr;     // [slots][rst_cap] (U byte index << 3) | marker number
     int32_t* tile_rbase = nullptr;  // [tiles_cap] restart markers before the tile (per image)
     LaneEntry* ent = nullptr;   // [lanes_cap]
+    struct StepSet* steps = nullptr;  // [slots] step tables (icx_step.h), built per group
     int32_t* stats = nullptr;   // [4] path counters, accumulated over a batch call
 };
 

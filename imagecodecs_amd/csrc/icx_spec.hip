@@ -320,69 +320,96 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
 }
 
 // -------------------------------------------------------------------- entropy lanes
-__device__ __forceinline__ void load_tables(LdsTables& T, const Desc& d) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&d.huff[0]);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&T.huff[0]);
-    for (int k = threadIdx.x; k < (int)(sizeof(Huff) * 4 / 4); k += blockDim.x) dst[k] = src[k];
-    if (threadIdx.x < 64) T.nat_of_zig[threadIdx.x] = kNatOfZig[threadIdx.x];
+// Step tables (icx_step.h), one set per image, built once per group from the parsed Huffman
+// tables; each workgroup below stages the format it decodes with into LDS.
+__global__ __launch_bounds__(256) void k_step_tabs(int n, const Desc* __restrict__ desc, StepSet* __restrict__ steps) {
+    __shared__ Huff h[4];
+    const int i = blockIdx.x;
+    if (i >= n || desc[i].status != kPending) return;
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&desc[i].huff[0]);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&h[0]);
+        for (int k = threadIdx.x; k < (int)(sizeof(h) / 4); k += blockDim.x) dst[k] = src[k];
+    }
+    __syncthreads();
+    StepSet& S = steps[i];
+    for (int k = threadIdx.x; k < ScanTab::entries(); k += blockDim.x) S.scan.fill(h, k);
+    for (int k = threadIdx.x; k < WriteTab::entries(); k += blockDim.x) S.write.fill(h, k);
 }
 
-__device__ __forceinline__ int wg_image_setup(const int32_t* wgpre, int n, int wg, int& cur, LdsTables& T,
-                                              const Desc* desc) {
-    const int i = find_image(wgpre, n, wg);
+template <class Tab>
+__device__ __forceinline__ void stage_tab(Tab& T, const Tab& src) {
+    static_assert(sizeof(Tab) % 16 == 0, "16-byte copies");
+    const uint4* s = reinterpret_cast<const uint4*>(&src);
+    uint4* d = reinterpret_cast<uint4*>(&T);
+    for (int k = threadIdx.x; k < (int)(sizeof(Tab) / 16); k += blockDim.x) d[k] = s[k];
+}
+__device__ __forceinline__ const ScanTab& set_part(const StepSet& S, const ScanTab*) { return S.scan; }
+__device__ __forceinline__ const WriteTab& set_part(const StepSet& S, const WriteTab*) { return S.write; }
+
+// Workgroup wg of a flat numbering (prefix pre over images): the image, with its tables staged.
+template <class Tab>
+__device__ __forceinline__ int wg_image_setup(const int32_t* pre, int n, int wg, int& cur, Tab& T,
+                                              const StepSet* steps) {
+    const int i = find_image(pre, n, wg);
     if (i != cur) {
         __syncthreads();
-        load_tables(T, desc[i]);
+        stage_tab(T, set_part(steps[i], (const Tab*)nullptr));
         __syncthreads();
         cur = i;
     }
     return i;
 }
 
-__global__ __launch_bounds__(256) void k_spec_guess(int n, const Desc* __restrict__ desc,
-                                                    const SpecImg* __restrict__ spec, const int32_t* __restrict__ wgpre,
-                                                    const int32_t* __restrict__ totals, const uint8_t* __restrict__ U,
-                                                    int64_t ucap, uint64_t* __restrict__ X, RecState* __restrict__ rec,
-                                                    int32_t* __restrict__ nrec, int32_t* __restrict__ gtot) {
-    __shared__ LdsTables T;
+// NL lanes per workgroup; `wpre` numbers each image's lanes in NL-lane groups (totals[tsel]).
+template <int NL>
+__global__ __launch_bounds__(NL) void k_spec_guess(int n, const Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
+                                                   const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
+                                                   int tsel, const StepSet* __restrict__ steps,
+                                                   const uint8_t* __restrict__ U, int64_t ucap, uint64_t* __restrict__ X,
+                                                   RecState* __restrict__ rec, int32_t* __restrict__ nrec,
+                                                   int32_t* __restrict__ gtot) {
+    __shared__ ScanTab T;
     int cur = -1;
-    const int total = totals[1];
+    const int total = totals[tsel];
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
-        const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
+        const int i = wg_image_setup(wpre, n, wg, cur, T, steps);
         const SpecImg& s = spec[i];
         if (s.mode != 1) continue;  // uniform per workgroup
-        const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
+        const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         if (j >= s.nsub - 1) continue;  // the last lane's exit is never needed
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
         const int64_t sb = (int64_t)kSubBytes * 8;
-        X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, make_sel(desc[i]), j * sb, (j + 1) * sb, 0, rec + f * kRec,
-                          nrec + f, gtot + 4 * f);
+        X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j * sb, (j + 1) * sb, 0,
+                          rec + f * kRec, nrec + f, gtot + 4 * f);
     }
 }
 
-__global__ __launch_bounds__(256) void k_spec_count(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
-                                                    const int32_t* __restrict__ wgpre, const int32_t* __restrict__ totals,
-                                                    const uint8_t* __restrict__ U, int64_t ucap,
-                                                    const uint64_t* __restrict__ X, uint64_t* __restrict__ Y,
-                                                    const RecState* __restrict__ rec, const int32_t* __restrict__ nrec,
-                                                    const int32_t* __restrict__ gtot, SubRec* __restrict__ sub,
-                                                    int32_t* __restrict__ repair) {
-    __shared__ LdsTables T;
+template <int NL>
+__global__ __launch_bounds__(NL) void k_spec_count(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                   const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
+                                                   int tsel, const StepSet* __restrict__ steps,
+                                                   const uint8_t* __restrict__ U, int64_t ucap,
+                                                   const uint64_t* __restrict__ X, uint64_t* __restrict__ Y,
+                                                   const RecState* __restrict__ rec, const int32_t* __restrict__ nrec,
+                                                   const int32_t* __restrict__ gtot, SubRec* __restrict__ sub,
+                                                   int32_t* __restrict__ repair) {
+    __shared__ ScanTab T;
     int cur = -1;
-    const int total = totals[1];
+    const int total = totals[tsel];
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
-        const int i = wg_image_setup(wgpre, n, wg, cur, T, desc);
+        const int i = wg_image_setup(wpre, n, wg, cur, T, steps);
         SpecImg& s = spec[i];
         if (s.mode != 1) continue;  // uniform per workgroup
-        const int64_t j = (int64_t)(wg - wgpre[i]) * kLanes + threadIdx.x;
+        const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         if (j >= s.nsub - 1) continue;
         const int64_t base = (int64_t)s.wg_base * kLanes, f = base + j;
         const int64_t sb = (int64_t)kSubBytes * 8;
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
         SubRec out;
         bool synced;
-        Y[f] = lane_count(U + (int64_t)i * ucap, s.ulen, T, make_sel(desc[i]), entry, j * sb, (j + 1) * sb, rec + f * kRec,
-                          nrec[f], gtot + 4 * f, X[f], out, synced);
+        Y[f] = lane_count(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), entry, j * sb, (j + 1) * sb,
+                          rec + f * kRec, nrec[f], gtot + 4 * f, X[f], out, synced);
         sub[f] = out;
         if (out.mism) {  // queue for the serial repair walk
             const int q = atomicAdd(&s.nrepair, 1);
@@ -394,15 +421,16 @@ __global__ __launch_bounds__(256) void k_spec_count(int n, const Desc* __restric
 // One workgroup per image with queued lanes; lane 0 walks them in order (they are rare:
 // a guess lane that never resynchronised inside its 2 KiB).
 __global__ __launch_bounds__(64) void k_spec_repair(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                    const StepSet* __restrict__ steps,
                                                     const uint8_t* __restrict__ U, int64_t ucap, uint64_t* __restrict__ X,
                                                     const uint64_t* __restrict__ Y, const RecState* __restrict__ rec,
                                                     const int32_t* __restrict__ nrec, const int32_t* __restrict__ gtot,
                                                     SubRec* __restrict__ sub, int32_t* __restrict__ repair) {
-    __shared__ LdsTables T;
+    __shared__ ScanTab T;
     const int i = blockIdx.x;
     SpecImg& s = spec[i];
     if (s.mode != 1 || s.nrepair == 0) return;
-    load_tables(T, desc[i]);
+    stage_tab(T, steps[i].scan);
     __syncthreads();
     if (threadIdx.x != 0) return;
     if (s.nrepair > kMaxRepair) { s.mode = 2; return; }
@@ -419,7 +447,7 @@ __global__ __launch_bounds__(64) void k_spec_repair(int n, const Desc* __restric
     for (int a = 0; a < nq; ++a) {
         const int64_t j = q[a];
         if (j <= done) continue;  // re-derived by an earlier walk
-        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, make_sel(desc[i]), j, s.nsub, (int64_t)kSubBytes * 8, X + base,
+        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j, s.nsub, (int64_t)kSubBytes * 8, X + base,
                            Y + base, rec + base * kRec, nrec + base, gtot + 4 * base, sub + base, 64);
         if (done < 0) { s.mode = 2; return; }  // pathological stream: sequential decode
     }
@@ -471,7 +499,7 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
     }
 }
 
-// One flat loop over codes per lane (lanes of a wave never wait for each other at block
+// One flat loop over lookups per lane (lanes of a wave never wait for each other at block
 // boundaries); each block is assembled in the lane's LDS slot and leaves as eight 16-byte
 // stores when it ends (scattered 2-byte global stores amplified HBM writes ~10x).
 // 128-byte lane slot; 16-byte chunk q of lane t lives at chunk q ^ (t & 7), so the b128 reads
@@ -483,11 +511,12 @@ __device__ __forceinline__ int slot_elem(int t, int n) { return (((n >> 3) ^ (t 
 template <int NL>
 __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
+                                                    const StepSet* __restrict__ steps,
                                                     const uint8_t* __restrict__ U, int64_t ucap,
                                                     const uint64_t* __restrict__ X, const LaneEntry* __restrict__ ent,
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                     int64_t coef_cap, const int64_t* __restrict__ rst, int64_t rst_cap) {
-    __shared__ LdsTables T;
+    __shared__ WriteTab T;
     __shared__ int4 slots[NL][8];
     __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
     int cur = -1;
@@ -498,13 +527,14 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 #pragma unroll
     for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
-        const int i = wg_image_setup(wpre, n, wg, cur, T, desc);
+        const int i = wg_image_setup(wpre, n, wg, cur, T, steps);
         SpecImg& s = spec[i];
         // uniform per workgroup; `want` (1 or 3) limits a launch to one mode
         if ((s.mode != 1 && s.mode != 3) || (want && s.mode != want)) continue;
         const bool dri = s.mode == 3;
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         const Sel S = make_sel(desc[i]);
+        const Huff* H = desc[i].huff;
         // DRI: lane j = restart interval j, from the byte after marker j-1, exactly R MCUs, DC 0
         const int64_t* RS = rst + (int64_t)i * rst_cap;
         const int64_t iblocks = (int64_t)desc[i].restart * desc[i].bpm;
@@ -525,12 +555,12 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
                                    : ((!act || j == 0) ? pack_state(0, 0, 0) : X[base + j - 1]);
         Reader r;
         r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
-        int b = st_b(entry), z = st_z(entry), coef, ci = 0;
-        int32_t val, pred[3] = {0, 0, 0};
+        int b = st_b(entry), z = st_z(entry), ci = 0;
+        int32_t pred[3] = {0, 0, 0};
         int64_t bi = 0, limit = 0;
         bool bad = false;
         // the block in progress at entry belongs to the previous lane
-        while (z != 0) decode_unit(r, T, S, b, z, coef, val);
+        while (z != 0) (void)write_step(r, T, H, S, b, z, false);
         // lane-relative 32-bit bounds: territory end and the first fetch that is a syntax error
         const int64_t e0 = st_pos(entry);
         const uint32_t kFar = 1u << 30;
@@ -556,38 +586,43 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         // waits for them at their first use inside the loop with vmcnt(0) -- i.e. for every
         // coefficient store and prefetch in flight -- on every DC code.
         asm volatile("" : "+v"(pred[0]), "+v"(pred[1]), "+v"(pred[2]));
-        r.phase();  // the prelude above ran a lane-dependent number of codes
-        // Wave-uniform loop: one code per active lane per iteration, then the wave flushes the
-        // blocks its lanes completed together -- eight 128-byte blocks per round, each lane
-        // moving one 16-byte chunk LDS -> HBM and zeroing it (coalesced full-line stores,
-        // no divergent per-lane flush).
+        r.phase();  // the prelude above ran a lane-dependent number of lookups
+        // Wave-uniform loop: one lookup (one symbol or a pair) per active lane per iteration,
+        // then the wave flushes the blocks its lanes completed together -- eight 128-byte blocks
+        // per round, each lane moving one 16-byte chunk LDS -> HBM and zeroing it (coalesced
+        // full-line stores, no divergent per-lane flush).
         while (__any(act)) {
             // The reader advances on every lane, active or not (an idle lane decodes harmless
             // garbage; its loads are clamped to U): keeping Reader updates out of divergent
             // branches stops the compiler from routing the in-flight chunk through loop-header
             // copies, which made every iteration wait for the newest load and all stores.
-            if (z == 0) {  // a block starts: stop at the next lane's territory
+            const bool dc = z == 0;
+            if (dc) {  // a block starts: stop at the next lane's territory
                 if (r.used >= lim_rel) act = false;
                 ci = S.comp(b);
             }
-            // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644)
-            const bool peek_bad = r.used + 16 > err_rel;
-            const int rc = decode_unit(r, T, S, b, z, coef, val);
+            // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644); a second
+            // symbol is only paired when its own peek stays clear of the error byte
+            const uint32_t u0 = r.used;
+            const bool peek_bad = u0 + 16 > err_rel;
+            const WriteOut o = write_step(r, T, H, S, b, z, u0 + 16 + WriteTab::kAcBits > err_rel);
             bool done = false;
             int64_t bdone = 0;
             if (act) {
-                if (peek_bad || rc != kUnitOk || r.used > err_rel) {
+                if (peek_bad || o.err || r.used > err_rel) {
                     bad = true;
                     act = false;
                 } else {
-                    if (coef == 0) {
-                        pred[ci] = wadd(pred[ci], val);
-                        const int16_t cell = dc_cell(pred[ci]);
-                        sv[slot_elem(threadIdx.x, 0)] = cell;
-                        if (cell == kDcEscape) D[bi] = pred[ci];
-                    } else if (coef > 0) {
-                        sv[slot_elem(threadIdx.x, coef)] = (int16_t)val;  // zig-zag order (k_idct reorders)
+                    int32_t v1 = o.v1;
+                    if (dc) {
+                        pred[ci] = wadd(pred[ci], v1);
+                        v1 = dc_cell(pred[ci]);
+                        if (v1 == kDcEscape) D[bi] = pred[ci];
                     }
+                    // zig-zag order (k_idct reorders); an error ends the lane before its slot
+                    // could be misused, so the positions are only masked into the slot
+                    if (o.w1) sv[slot_elem(threadIdx.x, o.c1 & 63)] = (int16_t)v1;
+                    if (o.w2) sv[slot_elem(threadIdx.x, o.c2 & 63)] = (int16_t)o.v2;
                     if (z == 0) {
                         done = true;
                         bdone = bi++;
@@ -663,6 +698,7 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
                        ws.totals, ws.ucap);
+    hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
     hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,
@@ -671,12 +707,13 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
                        ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.ucap, ws.rst, ws.rst_cap);
     E(kStUnstuff);
     B(kStEntropy);
-    hipLaunchKernelGGL(k_spec_guess, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
-                       ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt);
-    hipLaunchKernelGGL(k_spec_count, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.U,
-                       ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
-    hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.U, ws.ucap, ws.X, ws.Y, ws.rec,
-                       ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+    // guess / count: 512-lane workgroups (the 41 KB scan tables amortised over more lanes)
+    hipLaunchKernelGGL(k_spec_guess<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                       ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt);
+    hipLaunchKernelGGL(k_spec_count<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                       ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+    hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.ucap, ws.X, ws.Y,
+                       ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
     E(kStEntropy);
     B(kStWrite);
@@ -685,12 +722,12 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
         // typically one per MCU row, so a few hundred long lanes per image): 256-lane workgroups,
         // which a 512-lane numbering would leave half idle
         hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, 1, n, ws.desc, ws.spec,
-                           ws.wg2pre, ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.wg2pre, ws.totals, ws.steps, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.totals, ws.steps, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
     } else {
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 0, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.totals, ws.steps, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
     }
     E(kStWrite);
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);

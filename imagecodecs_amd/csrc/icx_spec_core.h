@@ -3,6 +3,7 @@
 // tests (tests/emu/spec_emu.cpp). No kernels here.
 #pragma once
 #include "icx_internal.h"
+#include "icx_step.h"
 
 namespace icx {
 
@@ -141,32 +142,23 @@ ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, i
     return kept;
 }
 
-struct LdsTables {
-    Huff huff[4];
-    uint8_t nat_of_zig[64];
-};
-
 // Per-image MCU layout in registers (wave-uniform): component of MCU block b (2 bits per
-// block) and the DC / AC table of block b (4 bits per block: DC in bits 0-1, AC in 2-3), so
-// the code-to-code dependency chain holds a single LDS access (the fast Huffman entry).
+// block) and the DC / AC table of block b (4 bits per block: DC in bits 0-1, AC in 2-3).
 struct Sel {
     int bpm;
     uint32_t comps;
     uint64_t tabs;
-    uint32_t b10[4];  // per table: bound[kFastBits], the first 16-bit window of a > 10-bit code
     ICX_HD int comp(int b) const { return (int)((comps >> (2 * b)) & 3u); }
     ICX_HD int tab(int b, bool dc) const { return (int)((tabs >> (4 * b + (dc ? 0 : 2))) & 3u); }
-    ICX_HD uint32_t bound10(int t) const { return (t & 2) ? ((t & 1) ? b10[3] : b10[2]) : ((t & 1) ? b10[1] : b10[0]); }
 };
 ICX_HD Sel make_sel(const Desc& d) {
-    Sel s{d.bpm, 0u, 0ull, {0u, 0u, 0u, 0u}};
+    Sel s{d.bpm, 0u, 0ull};
     for (int b = 0; b < d.bpm && b < kSpecMaxBpm; ++b) {
         int sbx, sby;
         const int ci = mcu_block_comp(d, b, sbx, sby);
         s.comps |= (uint32_t)ci << (2 * b);
         s.tabs |= (uint64_t)((d.c[ci].dc_tab & 3) | ((d.c[ci].ac_tab & 3) << 2)) << (4 * b);
     }
-    for (int t = 0; t < 4; ++t) s.b10[t] = d.huff[t].bound[kFastBits];
     return s;
 }
 
@@ -273,6 +265,11 @@ struct Reader {
         tick = 0;
     }
     ICX_HD int64_t pos() const { return base + used; }
+    ICX_HD void consume(uint32_t n) {
+        buf <<= n;
+        nb -= (int)n;
+        used += n;
+    }
     ICX_HD uint32_t peek16() const { return (uint32_t)(buf >> 48); }
     ICX_HD uint32_t take(int n) {
         const uint32_t v = n ? (uint32_t)(buf >> (64 - n)) : 0u;
@@ -283,67 +280,105 @@ struct Reader {
     }
 };
 
-enum : int { kUnitOk = 0, kUnitErr = 1 };
+ICX_HD uint32_t ubfe(uint32_t x, uint32_t off, uint32_t w) {  // bits [off, off + w) of x
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ubfe(x, off, w);
+#else
+    return w ? (x >> off) & ((1u << w) - 1u) : 0u;
+#endif
+}
+// njGetVLC's sign extension (jpeg_dec.h:653-654) of an nbx-bit magnitude (nbx = 0: 0).
+ICX_HD int32_t extend_mag(uint32_t raw, uint32_t nbx) {
+    const uint32_t mask = (1u << nbx) - 1u;
+    return (int32_t)(raw <= (mask >> 1) ? raw - mask : raw);
+}
 
-// One Huffman code + magnitude bits in the state (b, z); z == 0 expects the DC code.
-// On return: *coef = coefficient index written (0 = DC, 1..63 AC, -1 none), *val = value.
-// Errors (jpeg_dec.h:646, 667, 669) end the block deterministically so speculative lanes
-// keep going; on the true path any error makes the image NJ_SYNTAX_ERROR.
-ICX_HD int decode_unit(Reader& r, const LdsTables& T, const Sel& S, int& b, int& z, int& coef,
-                                           int32_t& val) {
-    // One table read, one variable shift for code + magnitude bits, one shift to consume them;
-    // the DC / EOB / ZRL / error / end-of-block cases are selects, not branches (the lanes of a
-    // wave take different ones on almost every code). Only codes longer than kFastBits branch.
-    const bool dc = z == 0;
-    const int tb = S.tab(b, dc);
-    const Huff& H = T.huff[tb];
+// One step-table lookup (icx_step.h): refill, peek, entry; long codes behind a wave-uniform
+// branch whose body is a select (a wave where no lane needs it skips it).
+template <class Tab>
+ICX_HD uint32_t step_lookup(Reader& r, const Tab& T, const Huff* H, int t, uint32_t& x) {
     r.refill();
-    const uint32_t win = r.peek16();
-    uint32_t e = H.fast[win >> (16 - kFastBits)];
-    // > 10-bit codes: the subtable entry sits at win - bound[10] (huff_fill_fast). Behind a
-    // wave-uniform branch whose body is a select, so a wave where no lane needs it skips it.
-    if (wave_any(e & kSubFlag)) {
-        const uint32_t q = win - S.bound10(tb);
-        constexpr uint32_t kSubN = kSubTabs << (16 - kFastBits);
-        const uint32_t es = H.sub[q < kSubN ? q : kSubN - 1];
-        e = (e & kSubFlag) ? es : e;
+    x = (uint32_t)(r.buf >> 32);
+    uint32_t e = T.look(t, x);
+    if (wave_any((e & kStSlow) != 0u)) {
+        const uint32_t es = T.resolve(t, x, e & kStSlow ? e : kStSub, H);
+        e = (e & kStSlow) ? es : e;
     }
-    int len = (int)(e >> 8), sym = (int)(e & 0xFF);
-    if (wave_any(e == 0)) {  // invalid codes, oversized tables (a wave-uniform branch: rare)
-        if (e == 0) len = huff_search(H, win, kFastBits + 1, sym);
-    }
-    const bool inv = len == 0;               // no such code: consume one bit (jpeg_dec.h:646)
-    const int nbx = inv ? 0 : (sym & 15);
-    const int tot = inv ? 1 : len + nbx;     // <= 31 bits, refill left >= 33
-    const uint32_t m = 1u << nbx;
-    const uint32_t raw = (uint32_t)(r.buf >> (64 - tot)) & (m - 1u);
-    const int32_t v = (int32_t)(raw < (m >> 1) ? raw - m + 1u : raw);  // njGetVLC sign extension (:653-654)
-    r.buf <<= tot;
-    r.nb -= tot;
-    r.used += (uint32_t)tot;
-    const bool eob = !dc && !inv && sym == 0;                              // :667
-    const int c = z + (sym >> 4);
-    const bool err = inv || (!dc && !eob && ((nbx == 0 && sym != 0xF0) || c > 63));  // :669, :671
-    const bool endb = err || eob || (!dc && c == 63);
-    const bool keep = !err && !eob;
-    coef = dc ? (inv ? -1 : 0) : (keep ? c : -1);
-    val = (keep || (dc && !inv)) ? v : 0;
+    return e;
+}
+
+// SCAN step (guess / count / repair): one lookup -- a run of symbols of the current block, or
+// the DC code -- in the state (b, z); z == 0 expects the DC code. *dcv = the DC value when
+// the lookup was a DC code (0 for an invalid one). Returns true on a decode error (jpeg_dec.h
+// :646, :669, :671), which ends the block deterministically so speculative lanes keep going;
+// on the true path an error makes the image NJ_SYNTAX_ERROR.
+ICX_HD bool scan_step(Reader& r, const ScanTab& T, const Huff* H, const Sel& S, int& b, int& z, int32_t& dcv) {
+    const bool dc = z == 0;
+    uint32_t x;
+    const uint32_t e = step_lookup(r, T, H, S.tab(b, dc), x);
+    const uint32_t zm = (e >> 21) & 127u;
+    const bool usem = (uint32_t)z + zm <= 64u;
+    const uint32_t tot = usem ? (e >> 16) & 31u : st_tot1(e);
+    const uint32_t zad = usem ? zm : st_zad1(e);
+    const bool eob = usem ? ((e >> 28) & 1u) != 0 : st_eob1(e) != 0;
+    const bool e1 = !usem && st_err1(e);
+    const uint32_t nbx = st_nbx1(e);
+    dcv = extend_mag(ubfe(x, 32u - st_tot1(e), nbx), nbx);
+    r.consume(tot);
+    const int zn = z + (int)zad;
+    const bool err = e1 || (zn > 64 && !eob);
+    const bool endb = eob || zn >= 64 || err;
     const int bn = b + 1 == S.bpm ? 0 : b + 1;
-    z = endb ? 0 : (dc ? 1 : c + 1);
     b = endb ? bn : b;
-    return err ? kUnitErr : kUnitOk;
+    z = endb ? 0 : zn;
+    return err;
+}
+
+// WRITE step: one lookup, one symbol or a pair, with their coefficient positions (zig-zag
+// order) and values. The DC code's value is the DC diff (v1, c1 = 0). `near_err`: a second
+// symbol whose 16-bit peek (:644) would fetch the error byte is not paired, so the error is
+// flagged exactly where NanoJPEG's sequential reader meets it.
+struct WriteOut {
+    int32_t v1, v2;
+    int c1, c2;
+    bool w1, w2;  // write v1 at c1 / v2 at c2
+    bool err;
+};
+ICX_HD WriteOut write_step(Reader& r, const WriteTab& T, const Huff* H, const Sel& S, int& b, int& z, bool near_err) {
+    const bool dc = z == 0;
+    uint32_t x;
+    const uint32_t e = step_lookup(r, T, H, S.tab(b, dc), x);
+    const uint32_t tot1 = st_tot1(e), nbx1 = st_nbx1(e), zad1 = st_zad1(e);
+    const uint32_t tot2 = (e >> 16) & 15u, nbx2 = (e >> 20) & 15u, zad2 = (e >> 24) & 31u, eob2 = (e >> 29) & 1u;
+    const bool pair = tot2 != 0u && (uint32_t)z + zad1 + zad2 + eob2 <= 64u && !near_err;
+    WriteOut o;
+    o.v1 = extend_mag(ubfe(x, 32u - tot1, nbx1), nbx1);
+    o.v2 = extend_mag(ubfe(x, 32u - tot1 - tot2, nbx2), nbx2);
+    r.consume(tot1 + (pair ? tot2 : 0u));
+    o.c1 = z + (int)zad1 - 1;
+    o.c2 = o.c1 + (int)zad2;
+    o.w1 = !st_eob1(e) && !st_err1(e);
+    o.w2 = pair && !eob2;
+    const bool eob = pair ? eob2 != 0 : st_eob1(e) != 0;
+    const int zn = z + (int)zad1 + (pair ? (int)zad2 : 0);
+    o.err = st_err1(e) || (zn > 64 && !eob);
+    const bool endb = eob || zn >= 64 || o.err;
+    const int bn = b + 1 == S.bpm ? 0 : b + 1;
+    b = endb ? bn : b;
+    z = endb ? 0 : zn;
+    return o;
 }
 
 // ------------------------------------------------------------------------ lane logic
 // Guess lane: decode [start, end) from the block-start guess (b0, z=0). Records the first
 // kRec MCU-start states (b == 0, z == 0) it passes through (rec, *nrec) and its totals tot = {DC codes,
-// DC-diff sums per component} over the whole lane. Returns the exit state: the first code
+// DC-diff sums per component} over the whole lane. Returns the exit state: the first lookup
 // boundary at or after `end`.
-ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, const Sel& S, int64_t start, int64_t end,
-                           int b0, RecState* rec, int32_t* nrec, int32_t* tot) {
+ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S, int64_t start,
+                           int64_t end, int b0, RecState* rec, int32_t* nrec, int32_t* tot) {
     Reader r;
     r.init(U, ulen, start);
-    int b = b0, z = 0, coef;
+    int b = b0, z = 0;
     int32_t val, cnt = 0, ds[3] = {0, 0, 0};
     int nr = 0;
     const uint32_t span = (uint32_t)(end - start);
@@ -359,7 +394,7 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, c
         }
         const int ci = S.comp(b);
         const bool dc = z == 0;
-        decode_unit(r, T, S, b, z, coef, val);
+        scan_step(r, T, H, S, b, z, val);
         if (dc) {
             ++cnt;
             ds[ci] = wadd(ds[ci], val);
@@ -377,12 +412,12 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const LdsTables& T, c
 // one the guess lane recorded, both decodes coincide from there on, so the lane's totals are
 // spliced from the guess lane's and its exit is the guess exit (synced = true). Otherwise the
 // whole lane is decoded and its own exit returned.
-ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, const Sel& S, uint64_t entry, int64_t start,
-                           int64_t end, const RecState* rec, int nrec, const int32_t* tot, uint64_t guess_exit,
-                           SubRec& out, bool& synced) {
+ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S,
+                           uint64_t entry, int64_t start, int64_t end, const RecState* rec, int nrec, const int32_t* tot,
+                           uint64_t guess_exit, SubRec& out, bool& synced) {
     Reader r;
     r.init(U, ulen, st_pos(entry));
-    int b = st_b(entry), z = st_z(entry), coef;
+    int b = st_b(entry), z = st_z(entry);
     int32_t val, cnt = 0, ds[3] = {0, 0, 0};
     int m = 0;
     synced = false;
@@ -403,7 +438,7 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, c
         }
         const int ci = S.comp(b);
         const bool dc = z == 0;
-        decode_unit(r, T, S, b, z, coef, val);
+        scan_step(r, T, H, S, b, z, val);
         if (dc) {
             ++cnt;
             ds[ci] = wadd(ds[ci], val);
@@ -421,16 +456,16 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const LdsTables& T, c
 // Serial repair of one unsynchronised lane j (its count pass derived the true exit Y[j]):
 // adopt it and re-derive the following lanes until one's exit agrees with its guess exit.
 // Returns the last lane touched, or -1 if the walk exceeded `max_walk` lanes.
-ICX_HD int64_t repair_walk(const uint8_t* U, int64_t ulen, const LdsTables& T, const Sel& S, int64_t j, int64_t nsub,
-                           int64_t sub_bits, uint64_t* X, const uint64_t* Y, const RecState* rec, const int32_t* nrec,
-                           const int32_t* tot, SubRec* sub, int max_walk) {
+ICX_HD int64_t repair_walk(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S, int64_t j,
+                           int64_t nsub, int64_t sub_bits, uint64_t* X, const uint64_t* Y, const RecState* rec,
+                           const int32_t* nrec, const int32_t* tot, SubRec* sub, int max_walk) {
     X[j] = Y[j];
     int64_t k = j + 1;
     for (int steps = 0; k < nsub - 1; ++k, ++steps) {
         if (steps >= max_walk) return -1;
         bool synced;
         SubRec out;
-        const uint64_t ex = lane_count(U, ulen, T, S, X[k - 1], k * sub_bits, (k + 1) * sub_bits, rec + k * kRec,
+        const uint64_t ex = lane_count(U, ulen, T, H, S, X[k - 1], k * sub_bits, (k + 1) * sub_bits, rec + k * kRec,
                                        nrec[k], tot + 4 * k, X[k], out, synced);
         sub[k] = out;
         if (ex == X[k]) break;

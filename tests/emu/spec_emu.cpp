@@ -81,12 +81,14 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
         }
     }
     if (giveup) { stats[1]++; return 1; }
-    // ---- tables
-    auto Tp = std::make_unique<LdsTables>();
-    LdsTables& T = *Tp;
-    std::memcpy(T.huff, d.huff, sizeof(T.huff));
-    for (int t = 0; t < 4; ++t) huff_fill_fast(T.huff[t], 0, 1);
-    for (int k = 0; k < 64; ++k) T.nat_of_zig[k] = (uint8_t)nat_of_zig(k);
+    // ---- tables (k_step_tabs)
+    auto SSp = std::make_unique<StepSet>();
+    StepSet& SS = *SSp;
+    for (int k = 0; k < ScanTab::entries(); ++k) SS.scan.fill(d.huff, k);
+    for (int k = 0; k < WriteTab::entries(); ++k) SS.write.fill(d.huff, k);
+    const ScanTab& T = SS.scan;
+    const WriteTab& TW = SS.write;
+    const Huff* H = d.huff;
     const int64_t S = sub_bytes;
     const int64_t nsub = ulen > 0 ? (ulen + S - 1) / S : 1;
     const Sel SL = make_sel(d);
@@ -96,7 +98,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     std::vector<RecState> rec(nsub * kRec);
     std::vector<int32_t> nrec(nsub, 0), tot(nsub * 4, 0);
     for (int64_t j = 0; j + 1 < nsub; ++j)
-        X[j] = lane_guess(U.data(), ulen, T, SL, j * sb, (j + 1) * sb, 0, rec.data() + j * kRec, &nrec[j], &tot[4 * j]);
+        X[j] = lane_guess(U.data(), ulen, T, H, SL, j * sb, (j + 1) * sb, 0, rec.data() + j * kRec, &nrec[j], &tot[4 * j]);
     // ---- count (k_spec_count)
     std::vector<SubRec> sub(nsub, SubRec{0, 0, 0, 0, 0});
     std::vector<int32_t> queue;
@@ -104,7 +106,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     for (int64_t j = 0; j + 1 < nsub; ++j) {
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[j - 1];
         bool synced;
-        Y[j] = lane_count(U.data(), ulen, T, SL, entry, j * sb, (j + 1) * sb, rec.data() + j * kRec, nrec[j],
+        Y[j] = lane_count(U.data(), ulen, T, H, SL, entry, j * sb, (j + 1) * sb, rec.data() + j * kRec, nrec[j],
                           &tot[4 * j], X[j], sub[j], synced);
         synced_lanes += synced;
         if (sub[j].mism) queue.push_back((int32_t)j);
@@ -116,7 +118,7 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     int64_t done = -1;
     for (int32_t j : queue) {
         if (j <= done) continue;
-        done = repair_walk(U.data(), ulen, T, SL, j, nsub, sb, X.data(), Y.data(), rec.data(), nrec.data(), tot.data(),
+        done = repair_walk(U.data(), ulen, T, H, SL, j, nsub, sb, X.data(), Y.data(), rec.data(), nrec.data(), tot.data(),
                            sub.data(), 64);
         if (done < 0) { stats[1]++; return 1; }
     }
@@ -142,25 +144,27 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
         const int64_t limit = last ? INT64_MAX : st_pos(X[j]);
         Reader r;
         r.init(U.data(), ulen, st_pos(entry));
-        int b = st_b(entry), z = st_z(entry), coefi;
-        int32_t val;
-        while (z != 0) decode_unit(r, T, SL, b, z, coefi, val);
+        int b = st_b(entry), z = st_z(entry);
+        while (z != 0) (void)write_step(r, TW, H, SL, b, z, false);
         int32_t pred[3] = {ent[j].p0, ent[j].p1, ent[j].p2};
         const int64_t errbits = errpos == INT64_MAX ? INT64_MAX : errpos * 8;
         bool bad = false;
         int64_t bi = ent[j].G;
         int ci = 0;
         while (bi < total) {  // k_spec_write's flat loop
-            if (z == 0) {
+            const bool dcl = z == 0;
+            if (dcl) {
                 if (r.pos() >= limit) break;
                 ci = SL.comp(b);
             }
-            if (r.pos() + 16 > errbits) bad = true;
-            const int rc = decode_unit(r, T, SL, b, z, coefi, val);
-            if (rc != kUnitOk || r.pos() > errbits) bad = true;
+            const int64_t p0 = r.pos();
+            if (p0 + 16 > errbits) bad = true;
+            const WriteOut o = write_step(r, TW, H, SL, b, z, p0 + 16 + WriteTab::kAcBits > errbits);
+            if (o.err || r.pos() > errbits) bad = true;
             if (bad) break;
-            if (coefi == 0) { pred[ci] = wadd(pred[ci], val); dc[bi] = pred[ci]; }
-            else if (coefi > 0) coef[bi * 64 + T.nat_of_zig[coefi]] = (int16_t)val;
+            if (dcl) { pred[ci] = wadd(pred[ci], o.v1); dc[bi] = pred[ci]; }
+            else if (o.w1) coef[bi * 64 + nat_of_zig(o.c1 & 63)] = (int16_t)o.v1;
+            if (o.w2) coef[bi * 64 + nat_of_zig(o.c2 & 63)] = (int16_t)o.v2;
             if (z == 0) ++bi;
         }
         anybad |= bad;
@@ -190,27 +194,26 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
         ulen += k;
         if (e >= 0) break;
     }
-    auto Tp = std::make_unique<LdsTables>();
-    LdsTables& T = *Tp;
-    std::memcpy(T.huff, d.huff, sizeof(T.huff));
-    for (int t = 0; t < 4; ++t) huff_fill_fast(T.huff[t], 0, 1);
-    for (int k = 0; k < 64; ++k) T.nat_of_zig[k] = (uint8_t)nat_of_zig(k);
+    auto SSp = std::make_unique<StepSet>();
+    for (int k = 0; k < ScanTab::entries(); ++k) SSp->scan.fill(d.huff, k);
+    const ScanTab& T = SSp->scan;
+    const Huff* H = d.huff;
     std::unordered_map<int64_t, int> truth;  // pos -> (b<<8|z)
     {
         Reader r; r.init(U.data(), ulen, 0);
-        int b = 0, z = 0, c; int32_t v;
+        int b = 0, z = 0; int32_t v;
         const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
         int64_t blocks = 0;
         truth[0] = 0;
-        while (blocks < total) { bool dc = z == 0; decode_unit(r, T, make_sel(d), b, z, c, v); if (dc) ++blocks; truth[r.pos()] = (b << 8) | z; }
+        while (blocks < total) { bool dc = z == 0; scan_step(r, T, H, make_sel(d), b, z, v); if (dc) ++blocks; truth[r.pos()] = (b << 8) | z; }
     }
     for (int s = 0; s < nstarts; ++s) {
         const int64_t start = (ulen * 8) * s / nstarts;
         Reader r; r.init(U.data(), ulen, start);
-        int b = guess_b, z = 0, c; int32_t v;
+        int b = guess_b, z = 0; int32_t v;
         out[s] = -1;
         while (r.pos() - start < maxbits) {
-            decode_unit(r, T, make_sel(d), b, z, c, v);
+            scan_step(r, T, H, make_sel(d), b, z, v);
             auto it = truth.find(r.pos());
             if (it != truth.end() && it->second == ((b << 8) | z)) { out[s] = r.pos() - start; break; }
         }
@@ -237,5 +240,127 @@ extern "C" int emu_huff_selftest(const uint8_t* counts17, const uint8_t* syms, i
         const int l1 = huff_lookup(t, w, s1), l2 = huff_search(t, w, 1, s2);
         if (l1 != l2 || (l1 && s1 != s2)) ++bad;
     }
+    return bad;
+}
+
+// ---- step-table self-check (tests/test_spec_emu.py) ----
+// One DC table (index 0) and one AC table (index 2) from counts/symbols; `nblocks` blocks of a
+// random bit stream (seed) are decoded three ways from the same start: symbol by symbol with the
+// canonical walk and NanoJPEG's block rules (the reference semantics), with scan_step and with
+// write_step. Returns the number of disagreements: block-start positions, DC values, error
+// flags, and every coefficient the write steps place.
+static uint64_t emu_rng(uint64_t& s) { s += 0x9E3779B97F4A7C15ull; uint64_t z = s; z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull; z = (z ^ (z >> 27)) * 0x94D049BB133111EBull; return z ^ (z >> 31); }
+extern "C" int emu_step_selftest(const uint8_t* dcc17, const uint8_t* dcs, int ndc, const uint8_t* acc17, const uint8_t* acs,
+                                 int nac, uint64_t seed, int nblocks, int64_t* stats /*[4]: blocks, symbols, lookups scan, lookups write*/) {
+    auto Hp = std::make_unique<Huff[]>(4);
+    Huff* H = Hp.get();
+    std::memset(H, 0, sizeof(Huff) * 4);
+    for (int i = 0; i < ndc && i < 256; ++i) H[0].sym[i] = dcs[i];
+    for (int i = 0; i < nac && i < 256; ++i) H[2].sym[i] = acs[i];
+    huff_finalize(H[0], dcc17);
+    huff_finalize(H[2], acc17);
+    uint8_t zero17[17] = {0};
+    huff_finalize(H[1], zero17);
+    huff_finalize(H[3], zero17);
+    auto SSp = std::make_unique<StepSet>();
+    for (int k = 0; k < ScanTab::entries(); ++k) SSp->scan.fill(H, k);
+    for (int k = 0; k < WriteTab::entries(); ++k) SSp->write.fill(H, k);
+    // random stream: mostly well-formed blocks would need an encoder; random bits exercise every
+    // entry kind (errors included) and the decoders must agree on all of them
+    const int64_t nbytes = (int64_t)nblocks * 64 + 64;
+    std::vector<uint8_t> U(nbytes + 64, 0xFF);
+    for (int64_t i = 0; i < nbytes; ++i) U[i] = (uint8_t)emu_rng(seed);
+    Desc d;
+    std::memset(&d, 0, sizeof d);
+    d.bpm = 1;
+    d.nc = 1;
+    d.c[0].nblk = 1; d.c[0].hs = 1; d.c[0].vs = 1; d.c[0].dc_tab = 0; d.c[0].ac_tab = 2;
+    const Sel SL = make_sel(d);
+    const int64_t ulen = nbytes;
+    int bad = 0;
+    // reference: symbol by symbol
+    std::vector<int64_t> starts;
+    std::vector<int32_t> dcs_ref;
+    std::vector<int> errs;
+    std::vector<int16_t> coefs;
+    {
+        int64_t pos = 0;
+        auto win = [&](int64_t p) { uint32_t v = 0; for (int i = 0; i < 4; ++i) v = (v << 8) | U[(p >> 3) + i]; return (uint32_t)(((uint64_t)v << (p & 7)) >> 8) >> 8; };
+        for (int blk = 0; blk < nblocks; ++blk) {
+            starts.push_back(pos);
+            std::vector<int16_t> c(64, 0);
+            int s = 0, err = 0;
+            int L = huff_search(H[0], win(pos) & 0xFFFF, 1, s);
+            int32_t v = 0;
+            if (!L) { err = 1; pos += 1; }
+            else { pos += L; int nb = s & 15; if (nb) { v = extend((int32_t)((win(pos) & 0xFFFF) >> (16 - nb)), nb); pos += nb; } stats[1]++; }
+            dcs_ref.push_back(v);
+            int k = 0;
+            while (!err) {
+                L = huff_search(H[2], win(pos) & 0xFFFF, 1, s);
+                if (!L) { err = 1; pos += 1; break; }
+                pos += L; stats[1]++;
+                if (!s) break;
+                if (!(s & 15) && s != 0xF0) { err = 1; break; }
+                int nb = s & 15; v = 0;
+                if (nb) { v = extend((int32_t)((win(pos) & 0xFFFF) >> (16 - nb)), nb); pos += nb; }
+                k += (s >> 4) + 1;
+                if (k > 63) { err = 1; break; }
+                c[k] = (int16_t)v;
+                if (k == 63) break;
+            }
+            errs.push_back(err);
+            coefs.insert(coefs.end(), c.begin(), c.end());
+        }
+        starts.push_back(pos);
+    }
+    // scan_step
+    {
+        Reader r; r.init(U.data(), ulen, 0);
+        int b = 0, z = 0;
+        for (int blk = 0; blk < nblocks; ++blk) {
+            if (r.pos() != starts[blk]) { ++bad; break; }
+            int err = 0;
+            int32_t dv = 0, v;
+            bool first = true;
+            do {
+                const bool dc = z == 0;
+                err |= scan_step(r, SSp->scan, H, SL, b, z, v);
+                if (dc && first) dv = v;
+                first = false;
+                stats[2]++;
+            } while (z != 0);
+            if (err != errs[blk]) ++bad;
+            if (!errs[blk] && dv != dcs_ref[blk]) ++bad;
+        }
+        if (r.pos() != starts[nblocks]) ++bad;
+    }
+    // write_step
+    {
+        Reader r; r.init(U.data(), ulen, 0);
+        int b = 0, z = 0;
+        for (int blk = 0; blk < nblocks; ++blk) {
+            if (r.pos() != starts[blk]) { ++bad; break; }
+            std::vector<int16_t> c(64, 0);
+            int err = 0;
+            int32_t dv = 0;
+            do {
+                const bool dc = z == 0;
+                const WriteOut o = write_step(r, SSp->write, H, SL, b, z, false);
+                err |= o.err;
+                if (dc) dv = o.v1;
+                else if (o.w1 && o.c1 < 64) c[o.c1] = (int16_t)o.v1;
+                if (o.w2 && o.c2 < 64) c[o.c2] = (int16_t)o.v2;
+                stats[3]++;
+            } while (z != 0);
+            if (err != errs[blk]) ++bad;
+            if (!errs[blk]) {
+                if (dv != dcs_ref[blk]) ++bad;
+                for (int k = 1; k < 64; ++k) bad += c[k] != coefs[(size_t)blk * 64 + k];
+            }
+        }
+        if (r.pos() != starts[nblocks]) ++bad;
+    }
+    stats[0] += nblocks;
     return bad;
 }

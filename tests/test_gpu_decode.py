@@ -120,6 +120,10 @@ def test_batch_create_failure_frees_device_memory(ctx, group):
         icx.Batch(ctx, group, 4096, 4096, group)
     free1 = torch.cuda.mem_get_info(0)[0]
     assert free0 - free1 < 64 << 20, (free0, free1)
+    # the failed hipMalloc is reported by icx, not left as HIP's sticky last error for torch
+    x = torch.ones(1 << 20, device="cuda")
+    torch.cuda.synchronize()
+    assert float(x.sum()) == float(1 << 20)
 
 
 def test_path_stats_after_device_decode_without_sync(ctx):

@@ -150,3 +150,59 @@ def test_two_level_huffman_random_tables():
         assert bad == 0, counts
         over_budget += nsub > 8
     assert over_budget > 0  # the exact-search fallback was exercised too
+
+
+def _step_selftest(dc_counts, dc_syms, ac_counts, ac_syms, seed, nblocks=3000):
+    L = emu_lib()
+    L.emu_step_selftest.restype = C.c_int
+    L.emu_step_selftest.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_uint64,
+                                    C.c_int, C.c_void_p]
+    stats = np.zeros(4, np.int64)
+    bad = L.emu_step_selftest(bytes([0] + dc_counts), bytes(dc_syms), len(dc_syms), bytes([0] + ac_counts),
+                              bytes(ac_syms), len(ac_syms), seed, nblocks, stats.ctypes.data)
+    return bad, stats
+
+
+def _ac_symbols(rng, n, invalid_rate=0.0):
+    valid = [0x00, 0xF0] + [(r << 4) | s for r in range(16) for s in range(1, 11)]
+    out = []
+    for _ in range(n):
+        if rng.random() < invalid_rate:
+            out.append(int(rng.integers(1, 16)) << 4)  # size 0, not ZRL: a syntax error (:669)
+        else:
+            out.append(valid[int(rng.integers(0, len(valid)))])
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_step_tables_annex_k(seed):
+    """Step tables (icx_step.h: multi-symbol scan runs, write pairs, long-code pool) decode
+    random streams exactly like the symbol-by-symbol canonical walk with NanoJPEG's block rules."""
+    rng = np.random.default_rng(seed)
+    dc_counts = _K1 if seed % 2 == 0 else _K2
+    ac_counts = _K3 if seed % 2 == 0 else _K5
+    dc_syms = list(range(sum(dc_counts)))
+    ac_syms = _ac_symbols(rng, sum(ac_counts), invalid_rate=0.02 * seed)
+    bad, stats = _step_selftest(dc_counts, dc_syms, ac_counts, ac_syms, 1000 + seed)
+    assert bad == 0, stats
+    assert stats[2] < stats[1] and stats[3] < stats[1]  # runs / pairs took several symbols per lookup
+
+
+def test_step_tables_random_tables():
+    rng = np.random.default_rng(21)
+    for t in range(120):
+        tabs = []
+        for _ in range(2):
+            counts, space, total = [0] * 16, 1 << 16, 0
+            for L in range(1, 17):
+                cap = min(space >> (16 - L), 256 - total)
+                c = int(rng.integers(0, cap + 1)) if cap > 0 and rng.random() < 0.6 else 0
+                counts[L - 1] = c
+                space -= c << (16 - L)
+                total += c
+            tabs.append((counts, total))
+        (dcc, ndc), (acc, nac) = tabs
+        dc_syms = [int(x) for x in rng.integers(0, 256, ndc)]
+        ac_syms = _ac_symbols(rng, nac, invalid_rate=0.05)
+        bad, stats = _step_selftest(dcc, dc_syms, acc, ac_syms, 7 + t, nblocks=400)
+        assert bad == 0, (t, dcc, acc)
