@@ -185,7 +185,14 @@ struct StepTab {
             const uint32_t i = soff[t] + (w - sbase[t]);
             return pool[i < (uint32_t)POOL ? i : POOL - 1];  // (clamped for lanes that only ride along)
         }
-        return exact(h[t], t, w);
+        const uint32_t r = exact(h[t], t, w);
+#if defined(__HIP_DEVICE_COMPILE__)
+        // The walk's global loads complete here (vmcnt(0); lgkmcnt / expcnt untouched): without
+        // it the compiler's wait tracking keeps them "in flight" past the join of this rare path
+        // and puts an s_waitcnt vmcnt(0) -- for every prefetch and store -- into every lookup.
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
+        return r;
     }
 };
 
