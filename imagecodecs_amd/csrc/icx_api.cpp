@@ -45,6 +45,9 @@ struct icx_batch {
     GroupWs ws[kMaxPipes];
     hipStream_t pst[kMaxPipes] = {};  // pst[0] unused: pipe 0 runs on the caller's stream
     hipEvent_t fork = nullptr, join[kMaxPipes] = {};
+    std::vector<hipEvent_t> front_done;  // per group of a call: its front half has run
+    int min_groups = 1;                  // a call is cut into at least this many groups
+    bool stagger = false;                // group g's front waits for group g-1's front (ICX_STAGGER=1; measured slower)
     uint8_t* d_hin = nullptr;  // staging for icx_jpeg_batch_decode_host
     size_t d_hin_cap = 0;
     hipStream_t last_st = nullptr;  // the stream the last decode was ordered on
@@ -251,6 +254,8 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     group = std::min(group, max_images);
     if (group < 2) pipes = 1;
     b->pipes = pipes;
+    if (const char* e = std::getenv("ICX_GROUPS")) b->min_groups = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("ICX_STAGGER")) b->stagger = std::atoi(e) != 0;
     for (int p = 0; p < pipes; ++p) {
         // `group` images in flight over all pipes: each workspace holds its share
         const int slots = (group + pipes - 1) / pipes;
@@ -272,6 +277,7 @@ void icx_batch_destroy(icx_batch* b) {
         if (b->join[p]) (void)hipEventDestroy(b->join[p]);
     }
     if (b->fork) (void)hipEventDestroy(b->fork);
+    for (auto e : b->front_done) (void)hipEventDestroy(e);
     if (b->d_hin) (void)hipFree(b->d_hin);
     delete b;
 }
@@ -292,19 +298,34 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     // equal-sized groups (512 images on 361 slots -> 256 + 256, not 361 + 151): every kernel's
     // grid is sized by the work of its group, so a small tail group leaves the GPU half idle
     const int slots = b->ws[0].slots;
-    const int ngroups = (n + slots - 1) / slots;
+    const int ngroups = std::min(n, std::max((n + slots - 1) / slots, b->min_groups));
     const int per = (n + ngroups - 1) / ngroups;
-    const int used = std::min(b->pipes, ngroups);
+    const int used = std::min(b->pipes, (n + per - 1) / per);
     if (used > 1) {  // the other pipes start after the caller's prior work on `st`
         ICX_HIP(ctx, hipEventRecord(b->fork, st), ICX_INTERNAL_ERR);
         for (int p = 1; p < used; ++p) ICX_HIP(ctx, hipStreamWaitEvent(b->pst[p], b->fork, 0), ICX_INTERNAL_ERR);
+    }
+    // Software pipeline over the groups, alternating pipes: group g's front half (parse, unstuff,
+    // entropy decode: latency-bound) starts when group g-1's front half is done, on the other
+    // pipe's stream, so it runs beside group g-1's back half (IDCT, convert: HBM-bound) instead
+    // of in lockstep with it.
+    const bool stagger = b->stagger && used > 1;
+    const int ng = (n + per - 1) / per;
+    while (stagger && (int)b->front_done.size() < ng) {
+        hipEvent_t e;
+        ICX_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), ICX_INTERNAL_ERR);
+        b->front_done.push_back(e);
     }
     int gi = 0;
     for (int g0 = 0; g0 < n; g0 += per, ++gi) {
         const int gn = std::min(per, n - g0);
         const int p = gi % used;
-        launch_decode_group(b->ws[p], gn, d_data, d_off + g0, d_size + g0, d_out + (uint64_t)g0 * out_stride, out_stride,
-                            d_status + g0, d_dims + 3 * g0, p == 0 ? st : b->pst[p], b->hook.get());
+        hipStream_t ps = p == 0 ? st : b->pst[p];
+        if (stagger && gi > 0) ICX_HIP(ctx, hipStreamWaitEvent(ps, b->front_done[gi - 1], 0), ICX_INTERNAL_ERR);
+        launch_decode_front(b->ws[p], gn, d_data, d_off + g0, d_size + g0, out_stride, ps, b->hook.get());
+        if (stagger) ICX_HIP(ctx, hipEventRecord(b->front_done[gi], ps), ICX_INTERNAL_ERR);
+        launch_decode_back(b->ws[p], gn, d_out + (uint64_t)g0 * out_stride, out_stride, d_status + g0, d_dims + 3 * g0,
+                           ps, b->hook.get());
     }
     for (int p = 1; p < used; ++p) {  // the caller's stream waits for every pipe
         ICX_HIP(ctx, hipEventRecord(b->join[p], b->pst[p]), ICX_INTERNAL_ERR);

@@ -623,6 +623,12 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
 // registers; YCbCr->RGB (:834-853) is stored as one 12-byte write per lane. No LDS, no barriers.
 // Vertical edge rows are wave-uniform branches; horizontal edge lanes take the generic taps.
 constexpr int kSH = 64;
+// rows (row pairs) whose loads are in flight ahead of the one being converted: one row pair per
+// wave left ~30 KB of loads in flight per CU, below what the HBM latency needs
+#ifndef ICX_CONV_PD
+#define ICX_CONV_PD 2
+#endif
+constexpr int kPD = ICX_CONV_PD;
 
 // 4 = gray; 0..3 = the shared chroma kind; -1 = left to k_convert_fused / the generic passes.
 __device__ __forceinline__ int stream_kind(const Desc& d) {
@@ -782,9 +788,10 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
         // interior horizontal taps for all 4 outputs, reads inside the row (chroma_make<true>)
         const bool f1 = M >= 1 && x0 + 3 <= 2 * c1.w - 4 && 2 * M + 5 < c1.s;
         const bool f2 = M >= 1 && x0 + 3 <= 2 * c2.w - 4 && 2 * M + 5 < c2.s;
-        // Software pipelining, unrolled by two with alternating buffers P/Q: the loads of the
-        // next row (pair) are in flight while the current one is computed; the scheduling
-        // barriers keep each buffer's reload after its last use so no in-flight value is copied.
+        // Software pipelining over a ring of kPD + 1 buffers, unrolled so every buffer index is a
+        // constant: the loads of the next kPD rows (row pairs) are in flight while the current one
+        // is computed; the scheduling barriers keep each buffer's reload after its last use so no
+        // in-flight value is copied.
         struct Pre {
             CRaw a, e;
             uint32_t y0, y1;
@@ -802,15 +809,17 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
             auto step = [&](int y, const Pre& p) {
                 emit(y, p.y0, chroma_make<KH>(c1, y, M, f1, p.a), chroma_make<KH>(c2, y, M, f2, p.e));
             };
-            Pre P = fetch(Y0);
-            for (int y = Y0; y < Y1; y += 2) {
-                const Pre Q = fetch(y + 1);
-                step(y, P);
-                __builtin_amdgcn_sched_barrier(0);
-                if (y + 1 >= Y1) break;
-                P = fetch(y + 2);
-                step(y + 1, Q);
-                __builtin_amdgcn_sched_barrier(0);
+            Pre B[kPD + 1];
+#pragma unroll
+            for (int u = 0; u < kPD; ++u) B[u] = fetch(Y0 + u);
+            for (int y = Y0; y < Y1; y += kPD + 1) {
+#pragma unroll
+                for (int u = 0; u <= kPD; ++u) {
+                    if (y + u >= Y1) break;  // wave-uniform
+                    B[(u + kPD) % (kPD + 1)] = fetch(y + u + kPD);
+                    step(y + u, B[u]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
             continue;
         }
@@ -873,15 +882,17 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
             a0 = a1; a1 = a2; a2 = a3; a3 = a4;
             e0 = e1; e1 = e2; e2 = e3; e3 = e4;
         };
-        Pre P = fetch(k0);
-        for (int k = k0; 2 * k < Y1; k += 2) {
-            const Pre Q = fetch(k + 1);
-            step(k, P);
-            __builtin_amdgcn_sched_barrier(0);
-            if (2 * (k + 1) >= Y1) break;
-            P = fetch(k + 2);
-            step(k + 1, Q);
-            __builtin_amdgcn_sched_barrier(0);
+        Pre B[kPD + 1];
+#pragma unroll
+        for (int u = 0; u < kPD; ++u) B[u] = fetch(k0 + u);
+        for (int k = k0; 2 * k < Y1; k += kPD + 1) {
+#pragma unroll
+            for (int u = 0; u <= kPD; ++u) {
+                if (2 * (k + u) >= Y1) break;  // wave-uniform
+                B[(u + kPD) % (kPD + 1)] = fetch(k + u + kPD);
+                step(k + u, B[u]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     }
 }
@@ -914,9 +925,8 @@ __global__ void k_finalize(int n, const Desc* __restrict__ desc, int32_t* __rest
 }
 
 // ---------------------------------------------------------------------------- launcher
-void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
-                         const uint64_t* d_size, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
-                         int32_t* d_dims, hipStream_t st, StageHook* hook) {
+void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
+                         const uint64_t* d_size, uint64_t out_stride, hipStream_t st, StageHook* hook) {
     if (n <= 0) return;
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
@@ -930,6 +940,14 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_entropy_seq, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc,
                        ws.coef_cap);
     E(kStEntropy);
+}
+
+void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
+                        int32_t* d_dims, hipStream_t st, StageHook* hook) {
+    if (n <= 0) return;
+    auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
+    auto E = [&](Stage s) { if (hook) hook->end(s, st); };
+    const int tb = 64, nb = (n + tb - 1) / tb;
     B(kStIdct);
     const int64_t maxblk = ws.coef_cap;
     // ~16K workgroups per launch in total; every kernel grid-strides over its image's work
@@ -966,6 +984,13 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
                        ws.tmp_cap, d_out, out_stride);
     hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(tb), 0, st, n, ws.desc, d_status, d_dims);
     E(kStConvert);
+}
+
+void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
+                         const uint64_t* d_size, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
+                         int32_t* d_dims, hipStream_t st, StageHook* hook) {
+    launch_decode_front(ws, n, d_data, d_off, d_size, out_stride, st, hook);
+    launch_decode_back(ws, n, d_out, out_stride, d_status, d_dims, st, hook);
 }
 
 }  // namespace icx

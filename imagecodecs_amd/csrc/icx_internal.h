@@ -107,6 +107,13 @@ struct StageHook {
 void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
                          const uint64_t* d_size, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
                          int32_t* d_dims, hipStream_t st, StageHook* hook);
+// The same in two halves: front = parse, unstuff, entropy decode (latency-bound); back = IDCT,
+// upsample, convert, statuses (HBM-bound). The batch scheduler overlaps one group's back with the
+// next group's front on another stream.
+void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
+                         const uint64_t* d_size, uint64_t out_stride, hipStream_t st, StageHook* hook);
+void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
+                        int32_t* d_dims, hipStream_t st, StageHook* hook);
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
                          StageHook* hook);
 

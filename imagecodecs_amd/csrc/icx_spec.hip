@@ -23,6 +23,9 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/warp/warp_scan.hpp>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "icx_spec_core.h"
 
 namespace icx {
@@ -43,7 +46,8 @@ __device__ int block_exclusive_scan(int v, int* sh) {  // blockDim.x <= 1024, re
     return incl - v;
 }
 
-__global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+__global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                    Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     int32_t* __restrict__ tilepre, int32_t* __restrict__ wgpre,
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
                                                     int64_t ucap) {
@@ -67,7 +71,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, Desc* __restrict__ de
                 s.mode = d.restart == 0 ? 1 : 3;
                 s.scan_len = scan_len;
                 s.total_blocks = (int64_t)d.mbw * d.mbh * d.bpm;
-                nt = (int)((scan_len + kTileBytes - 1) / kTileBytes);
+                nt = (int)ustf_ntiles(scan_len, ustf_align(data + off[i] + d.scan_off));
                 // lanes: 2 KiB subsequences, or (DRI) one per restart interval
                 const int64_t nmcu = (int64_t)d.mbw * d.mbh;
                 const int64_t nsub = s.mode == 1 ? (scan_len + kSubBytes - 1) / kSubBytes
@@ -118,11 +122,11 @@ __device__ __forceinline__ int find_image(const int32_t* pre, int n, int x) {
 }
 
 // ---------------------------------------------------------------------------- unstuff
-// Unstuff tiles: one wave per 4 KiB raw tile, 64 raw bytes (four 16-byte chunks) per lane; wave
-// shuffles for the prefix / min, no block barriers. Each wave walks a contiguous range of the
+// Unstuff tiles: one wave per 4 KiB raw tile cut at 16-byte aligned addresses (icx_spec_core.h
+// ustf16), four rounds of 64 consecutive aligned 16-byte chunks, one per lane: every load is a
+// contiguous 1 KiB per wave instruction. Neighbouring bytes come from the adjacent lanes. Wave
+// shuffles give the prefix / min, no block barriers. Each wave walks a contiguous range of the
 // flat tile list, so the owning image only ever advances (no per-tile search).
-constexpr int kLaneRaw = kTileBytes / 64;
-
 __device__ __forceinline__ int wave_incl_scan(int v) {  // rocprim's DPP cross-lane scan
     using WScan = rocprim::warp_scan<int, 64>;
     typename WScan::storage_type st;  // empty for the cross-lane implementation
@@ -134,30 +138,6 @@ __device__ __forceinline__ long long wave_min_ll(long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
     return v;
-}
-
-// One lane's 64 raw bytes: kept bytes before the lane's first end event (written to `out` when
-// WRITE), that event's raw offset (-1: none) and whether it is an error.
-template <bool WRITE>
-__device__ __forceinline__ int ustf_lane(const uint8_t* R, int64_t L, int64_t a, int64_t& end_at, int& end_err,
-                                         uint8_t* out, int32_t& giveup, RstSink& rs) {
-    int kept = 0;
-    end_at = -1;
-    end_err = 0;
-    const int64_t ub = rs.ubase;
-#pragma unroll
-    for (int c = 0; c < kLaneRaw / kChunk; ++c) {
-        int64_t e;
-        int er;
-        rs.ubase = ub + kept;
-        kept += ustf_chunk<WRITE>(R, L, a + c * kChunk, &e, &er, WRITE ? out + kept : nullptr, &giveup, &rs);
-        if (e >= 0) {
-            end_at = e;
-            end_err = er;
-            break;
-        }
-    }
-    return kept;
 }
 
 struct TileRange {
@@ -173,39 +153,127 @@ __device__ __forceinline__ TileRange wave_tiles(const int32_t* tilepre, int n, i
     return r;
 }
 
+// A tile's four rounds of chunks, loaded up front (4 KiB per wave in flight): lane l of round r
+// holds R-relative chunk a = t0 + 1024 r + 16 l (an aligned address). Neighbour bytes of a
+// round come from the adjacent lanes, and across rounds from lane 0 / lane 63 of the next /
+// previous round; only the tile's first prev dword and last next dword are extra loads.
+struct ChunkIn {
+    uint32_t D[4];
+    int nx;    // R[a+16]
+    int prun;  // ff_run4: FF bytes ending at R[a-1]
+};
+struct TileChunks {
+    uint4 V0, V1, V2, V3;  // rounds r, r+1, r+2, r+3 (shifted down after each round)
+    uint32_t pw, nx3;      // lane 0: R[a-4 .. a) of the current round; lane 63: R[a+16 ..) of round 3
+    int r;
+    __device__ __forceinline__ void load(const uint8_t* R, int64_t L, int64_t t0, int lane) {
+        static_assert(kTileBytes == 4096, "four 1 KiB rounds");
+        // Unconditional loads from clamped addresses (the last aligned chunk holding scan bytes),
+        // zero-selected past the data: a load inside a branch gets its own vmcnt(0) at the join.
+        const int64_t alast = ((int64_t)(ustf_align(R) + L - 1) & ~(int64_t)15) - ustf_align(R);
+        auto ld = [&](int64_t a) {
+            const uint4 v = *reinterpret_cast<const uint4*>(R + (a < L ? a : alast));
+            return a < L ? v : make_uint4(0u, 0u, 0u, 0u);
+        };
+        const int64_t a0 = t0 + lane * 16;
+        V0 = ld(a0); V1 = ld(a0 + 1024); V2 = ld(a0 + 2048); V3 = ld(a0 + 3072);
+        // R[t0-4 .. t0) (headers before the scan when t0 < 1: inside the file, unused), and the
+        // dword after the tile
+        const uint32_t p = *reinterpret_cast<const uint32_t*>(R + t0 - 4);
+        pw = t0 >= 1 ? p : 0u;
+        const int64_t an = t0 + kTileBytes;
+        const uint32_t q = *reinterpret_cast<const uint32_t*>(R + (an < L ? an : alast));
+        nx3 = an < L ? q : 0u;
+        r = 0;
+    }
+    // the current round's chunk, then advance (wave-level: every lane calls it)
+    __device__ __forceinline__ ChunkIn next(int64_t a, int lane) {
+        ChunkIn c;
+        c.D[0] = V0.x; c.D[1] = V0.y; c.D[2] = V0.z; c.D[3] = V0.w;
+        uint32_t p = __shfl_up(V0.w, 1);
+        if (lane == 0) p = pw;
+        uint32_t nw = __shfl_down(V0.x, 1);
+        const uint32_t q = __shfl(V1.x, 0);  // the next round's first dword
+        if (lane == 63) nw = r == 3 ? nx3 : q;
+        pw = __shfl(V0.w, 63);
+        V0 = V1; V1 = V2; V2 = V3;
+        ++r;
+        c.nx = (int)(nw & 0xFFu);
+        c.prun = ff_run4(p, a);
+        return c;
+    }
+};
+__device__ __forceinline__ int wave_sum(int v) { return __shfl(wave_incl_scan(v), 63); }
+
+// The image owning the wave's current tile, with its scan parameters kept in registers (reloaded
+// only when the tile walk crosses into the next image; per-tile reloads were four dependent
+// global loads per 4 KiB tile).
+struct TileImg {
+    int i, t_first, t_end;  // image, its first flat tile, one past its last
+    const uint8_t* R;
+    int64_t L;
+    __device__ __forceinline__ void set(int img, const uint8_t* data, const uint64_t* off, const Desc* desc,
+                                        const SpecImg* spec, const int32_t* tilepre) {
+        i = __builtin_amdgcn_readfirstlane(img);
+        t_first = __builtin_amdgcn_readfirstlane(tilepre[i]);
+        t_end = __builtin_amdgcn_readfirstlane(tilepre[i + 1]);
+        R = data + off[i] + desc[i].scan_off;
+        L = spec[i].scan_len;
+    }
+    __device__ __forceinline__ int64_t t0(int t) const {  // R-relative start of flat tile t
+        return (int64_t)(t - t_first) * kTileBytes - ustf_align(R);
+    }
+};
+
 __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __restrict__ data,
                                                     const uint64_t* __restrict__ off, const Desc* __restrict__ desc,
                                                     SpecImg* __restrict__ spec, const int32_t* __restrict__ tilepre,
                                                     const int32_t* __restrict__ totals, TileRec* __restrict__ tiles) {
     const int lane = threadIdx.x & 63;
-    TileRange tr = wave_tiles(tilepre, n, totals[0]);
+    const TileRange tr = wave_tiles(tilepre, n, totals[0]);
+    TileImg im;
+    if (tr.t < tr.t1) im.set(tr.i, data, off, desc, spec, tilepre);
     for (int t = tr.t; t < tr.t1; ++t) {
-        while (t >= tilepre[tr.i + 1]) ++tr.i;
-        const int i = tr.i;
-        const uint8_t* R = data + off[i] + desc[i].scan_off;
-        const int64_t L = spec[i].scan_len;
-        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)lane * kLaneRaw;
-        int64_t end_at;
-        int end_err;
+        while (t >= im.t_end) im.set(im.i + 1, data, off, desc, spec, tilepre);
+        const int i = im.i;
+        const uint8_t* R = im.R;
+        const int64_t L = im.L;
+        const int64_t t0 = im.t0(t);
         int32_t giveup = 0;
-        RstSink rs{0, 0, nullptr, 0, 0};
-        const int kept = ustf_lane<false>(R, L, a, end_at, end_err, nullptr, giveup, rs);
-        if (giveup) atomicOr(&spec[i].err, kSpecGiveUp);
-        const long long tend = wave_min_ll(end_at >= 0 ? (long long)end_at : LLONG_MAX);
-        // kept bytes (and restart markers) before the tile's first end event
-        const bool before = end_at >= 0 ? end_at <= tend : a < tend;
-        const int incl = wave_incl_scan(before ? kept : 0);
-        const int rincl = wave_incl_scan(before ? rs.n : 0);
-        const uint64_t owner = __ballot(end_at >= 0 && end_at == tend);  // the unique lane owning that FF
-        const int err = __shfl(end_err, owner ? __ffsll((long long)owner) - 1 : 0);
-        if (lane == 63) {
-            TileRec r;
-            r.kept = incl;
-            r.end_at = tend == LLONG_MAX ? -1 : tend;
-            r.end_err = owner ? err : 0;
-            r.nrst = rincl;
-            r.pad_ = 0;
-            tiles[t] = r;
+        int kept = 0, nrst = 0, err = 0;  // per lane until the end of the tile
+        long long tend = LLONG_MAX;
+        TileChunks tc;
+        tc.load(R, L, t0, lane);
+        for (int r = 0; r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
+            const int64_t a = t0 + r * 1024 + lane * 16;
+            RstSink rs{0, 0, nullptr, 0, 0};
+            const ChunkIn c = tc.next(a, lane);
+            const Ustf16 u = ustf16<false>(R, L, a, c.D, c.nx, c.prun, &giveup, &rs);
+            if (__any(u.end_at >= 0)) {  // the tile's data ends in this round (wave-uniform, rare)
+                const long long e = wave_min_ll(u.end_at >= 0 ? (long long)u.end_at : LLONG_MAX);
+                // kept bytes (and restart markers) before the first end event
+                const bool before = u.end_at >= 0 ? u.end_at <= e : a < e;
+                kept += before ? u.kept : 0;
+                nrst += before ? rs.n : 0;
+                const uint64_t owner = __ballot(u.end_at >= 0 && u.end_at == e);
+                err = __shfl(u.end_err, __ffsll((long long)owner) - 1);
+                tend = e;
+                break;
+            }
+            kept += u.kept;
+            nrst += rs.n;
+        }
+        kept = wave_sum(kept);
+        nrst = __any(nrst) ? wave_sum(nrst) : 0;
+        if (__any(giveup) && lane == 0) atomicOr(&spec[i].err, kSpecGiveUp);
+        if (lane == 0) {
+            TileRec rec;
+            rec.kept = kept;
+            rec.end_at = tend == LLONG_MAX ? -1 : tend;
+            rec.end_err = tend == LLONG_MAX ? 0 : err;
+            rec.nrst = nrst;
+            rec.pad_ = 0;
+            tiles[t] = rec;
         }
     }
 }
@@ -266,41 +334,76 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
                                                     const int32_t* __restrict__ tile_obase,
                                                     const int32_t* __restrict__ tile_rbase, uint8_t* __restrict__ U,
                                                     int64_t ucap, int64_t* __restrict__ rst, int64_t rst_cap) {
-    __shared__ uint32_t sbuf_all[4][kTileBytes / 4 + 8];  // per wave: the tile's kept bytes
+    constexpr int kBufW = kTileBytes / 4 + 8;           // per wave: the tile's kept bytes (+ slack)
+    __shared__ uint32_t sbuf_all[4][kBufW];
     const int lane = threadIdx.x & 63;
     uint32_t* sbuf = sbuf_all[threadIdx.x >> 6];
-    uint8_t* sb = reinterpret_cast<uint8_t*>(sbuf);
-    TileRange tr = wave_tiles(tilepre, n, totals[0]);
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(sbuf);
+    const TileRange tr = wave_tiles(tilepre, n, totals[0]);
+    TileImg im;
+    int64_t ulen = 0;
+    int32_t obv = 0;  // lane k: tile_obase[tb + k] for the current block of 64 tiles
+    if (tr.t < tr.t1) {
+        im.set(tr.i, data, off, desc, spec, tilepre);
+        ulen = spec[im.i].ulen;
+    }
     for (int t = tr.t; t < tr.t1; ++t) {
-        while (t >= tilepre[tr.i + 1]) ++tr.i;
-        const int i = tr.i;
-        const SpecImg& s = spec[i];
-        const int64_t obase = tile_obase[t];  // == ulen for every tile past the first end event
-        if (obase >= s.ulen) continue;        // wave-uniform
-        const int64_t tend = tiles[t].end_at;
-        const uint8_t* R = data + off[i] + desc[i].scan_off;
-        const int64_t a = (int64_t)(t - tilepre[i]) * kTileBytes + (int64_t)lane * kLaneRaw;
-        int64_t end_at;
-        int end_err;
-        int32_t giveup = 0;
-        RstSink rs0{0, 0, nullptr, 0, 0};
-        const int kept = ustf_lane<false>(R, s.scan_len, a, end_at, end_err, nullptr, giveup, rs0);
-        const bool before = end_at >= 0 ? (tend < 0 || end_at <= tend) : (tend < 0 || a < tend);
-        const int k = before ? kept : 0;
-        const int incl = wave_incl_scan(k);
-        const int nr = before ? rs0.n : 0;
-        const int rincl = wave_incl_scan(nr);
-        if (k) {
-            // restart markers go to the image's list in stream order (ordinal = markers before)
-            RstSink rs{0, obase + (incl - k), nr ? rst + (int64_t)i * rst_cap : nullptr,
-                       tile_rbase[t] + rincl - nr, (int32_t)min<int64_t>(rst_cap, INT32_MAX)};
-            ustf_lane<true>(R, s.scan_len, a, end_at, end_err, sb + (incl - k), giveup, rs);
+        while (t >= im.t_end) {
+            im.set(im.i + 1, data, off, desc, spec, tilepre);
+            ulen = spec[im.i].ulen;
         }
-        const int tile_kept = __shfl(incl, 63);
+        if (t == tr.t || ((t - tr.t) & 63) == 0) obv = tr.t + ((t - tr.t) & ~63) + lane < tr.t1 ? tile_obase[t + lane] : 0;
+        const int i = im.i;
+        const int64_t obase = __shfl(obv, (t - tr.t) & 63);  // == ulen for every tile past the first end event
+        if (obase >= ulen) continue;                          // wave-uniform
+        const uint8_t* R = im.R;
+        const int64_t L = im.L;
+        const int64_t t0 = im.t0(t);
+        for (int k = lane; k < kBufW / 4; k += 64) reinterpret_cast<uint4*>(sbuf)[k] = make_uint4(0u, 0u, 0u, 0u);
+        __builtin_amdgcn_wave_barrier();
+        int32_t giveup = 0;
+        int kept = 0, nrst = 0;
+        TileChunks tc;
+        tc.load(R, L, t0, lane);
+        for (int r = 0; r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
+            const int64_t a = t0 + r * 1024 + lane * 16;
+            RstSink rs0{0, 0, nullptr, 0, 0};
+            const ChunkIn c = tc.next(a, lane);
+            const Ustf16 u = ustf16<true>(R, L, a, c.D, c.nx, c.prun, &giveup, &rs0);
+            const long long e = wave_min_ll(u.end_at >= 0 ? (long long)u.end_at : LLONG_MAX);
+            const bool before = u.end_at >= 0 ? u.end_at <= e : a < e;
+            const int k = before ? u.kept : 0;
+            const int incl = wave_incl_scan(k);
+            const int nr = before ? rs0.n : 0;
+            if (__any(nr)) {  // restart markers go to the image's list in stream order (DRI images)
+                const int rincl = wave_incl_scan(nr);
+                if (nr) {
+                    RstSink rs{0, obase + kept + (incl - k), rst + (int64_t)i * rst_cap, tile_rbase[t] + nrst + rincl - nr,
+                               (int32_t)min<int64_t>(rst_cap, INT32_MAX)};
+                    (void)ustf16<false>(R, L, a, c.D, c.nx, c.prun, &giveup, &rs);
+                }
+                nrst += __shfl(rincl, 63);
+            }
+            if (k) {  // the kept bytes at byte offset ob of the tile buffer (ORed into zeroed dwords)
+                const int ob = kept + incl - k, q = ob >> 2, sft = ob & 3;
+                const uint32_t* d = u.out;
+                if (sft == 0) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) atomicOr(&sbuf[q + j], d[j]);
+                } else {
+                    atomicOr(&sbuf[q], d[0] << (8 * sft));
+#pragma unroll
+                    for (int j = 1; j < 4; ++j) atomicOr(&sbuf[q + j], __builtin_amdgcn_alignbyte(d[j], d[j - 1], 4 - sft));
+                    atomicOr(&sbuf[q + 4], d[3] >> (32 - 8 * sft));
+                }
+            }
+            kept += __shfl(incl, 63);
+            if (e != LLONG_MAX) break;  // wave-uniform: the data ends in this round
+        }
         __builtin_amdgcn_wave_barrier();
         // copy out: bytes up to the first 16-byte boundary and after the last one byte-wise
         // (they may share a 16-byte unit with the neighbouring tiles), the rest as 16-byte units
-        const int64_t nout = min<int64_t>(tile_kept, s.ulen - obase);
+        const int64_t nout = min<int64_t>(kept, ulen - obase);
         uint8_t* dst = U + (int64_t)i * ucap + obase;  // U + i*ucap is 4 KiB aligned
         const int head = (int)min<int64_t>(nout, (16 - (obase & 15)) & 15);
         const int nunit = (int)((nout - head) >> 4);
@@ -694,9 +797,9 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
                          StageHook* hook) {
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
-    const int g = 2048;  // grid-stride launches: >> 256 CUs
+    static const int g = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
     B(kStUnstuff);
-    hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
+    hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
                        ws.totals, ws.ucap);
     hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,

@@ -14,11 +14,8 @@ ICX_HD int64_t st_pos(uint64_t s) { return (int64_t)(s >> 16); }
 ICX_HD int st_b(uint64_t s) { return (int)((s >> 8) & 0xFF); }
 ICX_HD int st_z(uint64_t s) { return (int)(s & 0xFF); }
 
-// Per-lane marker automaton over kChunk raw bytes. Returns kept-byte count before the
-// first end event; *end_at = raw offset of the FF that ends the data (or -1), *end_err =
-// whether that end is a syntax error (bad marker / FF at EOF) rather than FF D9.
-constexpr int kChunk = kTileBytes / 256;
-
+// Unstuff helpers (k_ustf_count / k_ustf_write). carry_after_ff: R[a-1] is the end of an FF run;
+// whether R[a] is the marker byte of its last FF (odd run: jpeg_dec.h:465-475 pair the bytes up).
 ICX_HD bool carry_after_ff(const uint8_t* R, int64_t a, int32_t* giveup) {
     int k = 0;
     while (a - 1 - k >= 0 && R[a - 1 - k] == 0xFF) {
@@ -41,105 +38,155 @@ struct RstSink {
     }
 };
 
-// Bytes R[a-1 .. a+19) as five little-endian words, read with aligned dword loads (the bytes
-// before R are the file's headers, a > 0; the bytes after stay inside the scan, a + 24 <= L).
-ICX_HD bool ustf_window(const uint8_t* R, int64_t L, int64_t a, uint32_t (&v)[5]) {
-    if (a < 1 || a + kChunk + 8 > L) return false;
-    const uintptr_t p = reinterpret_cast<uintptr_t>(R + a - 1);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(R + a - 1 - (p & 3));
-    const int sh = (int)(p & 3) * 8;
-    uint32_t e[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) e[k] = q[k];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) v[k] = (uint32_t)((((uint64_t)e[k + 1] << 32) | e[k]) >> sh);
-    return true;
-}
-ICX_HD int win_byte(const uint32_t (&v)[5], int i) {  // i = -1 .. 18 -> R[a+i]
-    return (int)((v[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFF);
-}
+// ---- coalesced unstuff: 16-byte chunks at 16-byte aligned addresses ----
+// A wave's round covers 1 KiB of consecutive aligned chunks, one per lane, so each load is one
+// 16-byte access of a contiguous 1 KiB (the 64-byte-per-lane layout of ustf_chunk touched 64
+// lines per load instruction). Tiles are cut at aligned addresses: tile t of an image covers
+// R-relative bytes [kTileBytes*t - sh, kTileBytes*(t+1) - sh), sh = R's address mod 16, so the
+// first chunk of tile 0 starts before the scan (those header bytes are skipped).
+ICX_HD int ustf_align(const uint8_t* R) { return (int)(reinterpret_cast<uintptr_t>(R) & 15u); }
+ICX_HD int64_t ustf_ntiles(int64_t L, int sh) { return (L + sh + kTileBytes - 1) / kTileBytes; }
 
+struct Ustf16 {
+    int kept;        // kept bytes before the chunk's first end event
+    int64_t end_at;  // R-relative position of the FF that ends the data (-1: none in the chunk)
+    int end_err;     // that end is a syntax error (bad marker / FF at EOF), not FF D9
+    uint32_t out[4]; // WRITE: the kept bytes, little-endian, zero-filled
+};
+ICX_HD bool has_ff(const uint32_t (&D)[4]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = ~D[k];  // a zero byte of x is an FF byte of D[k]
+        m |= (x - 0x01010101u) & ~x & 0x80808080u;
+    }
+    return m != 0;
+}
+// FF bytes ending at R[a-1] among the four bytes before the chunk (pw = R[a-4 .. a) as a
+// little-endian dword; a < 1: none): 0..3, or 4 = four or more (the run is walked in memory).
+ICX_HD int ff_run4(uint32_t pw, int64_t a) {
+    if (a < 1) return 0;
+    int k = 0;
+    while (k < 4 && ((pw >> (24 - 8 * k)) & 0xFFu) == 0xFFu) ++k;
+    return k;
+}
+// Chunk R[a .. a+16), given as four little-endian dwords D (a may be < 0: bytes before the scan
+// are not part of it; bytes at or past L are ignored). nx = R[a+16] when a+16 < L; prun =
+// ff_run4 of the bytes before it. NanoJPEG's marker rules (jpeg_dec.h:447-482).
 template <bool WRITE>
-ICX_HD int ustf_chunk(const uint8_t* R, int64_t L, int64_t a, int64_t* end_at, int* end_err,
-                                          uint8_t* out, int32_t* giveup, RstSink* rs = nullptr) {
-    *end_at = -1;
-    *end_err = 0;
-    if (a >= L) return 0;
-    uint32_t v[5];
-    if (ustf_window(R, L, a, v)) {
-        uint32_t ff = 0;
+ICX_HD Ustf16 ustf16(const uint8_t* R, int64_t L, int64_t a, const uint32_t (&D)[4], int nx, int prun,
+                     int32_t* giveup, RstSink* rs) {
+    Ustf16 o;
+    o.end_at = -1;
+    o.end_err = 0;
+    const bool prev_ff = prun > 0;
+    if (a >= 0 && a + 16 <= L && !prev_ff && !has_ff(D)) {  // the common case: 16 bytes kept unchanged
+        o.kept = 16;
+        if (WRITE) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o.out[k] = D[k];
+        }
+        return o;
+    }
+    // byte 0 is the marker byte of an FF before the chunk (an odd FF run ends at a-1)
+    const bool carry = prev_ff && (prun < 4 ? (prun & 1) != 0 : carry_after_ff(R, a, giveup));
+    if (a >= 0 && a + 16 < L) {
+        // Stuffing only (every FF is followed by 00 -- all an encoder writes between markers):
+        // the bytes after the FFs are dropped, bit masks instead of the byte automaton.
+        uint32_t ffm = 0, zm = (nx & 0xFF) == 0 ? 1u << 16 : 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t w = (v[k] >> 8) | (v[k + 1] << 24);  // R[a+4k .. a+4k+4)
-            const uint32_t x = ~w;                               // a zero byte of x is an FF byte of w
-            ff |= (x - 0x01010101u) & ~x & 0x80808080u;
+            const uint32_t w = D[k];
+            const uint32_t f = ((w & 0x7F7F7F7Fu) + 0x01010101u) & w & 0x80808080u;     // byte == FF
+            const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;  // byte == 00
+            ffm |= ((f >> 7) & 1u | (f >> 14) & 2u | (f >> 21) & 4u | (f >> 28) & 8u) << (4 * k);
+            zm |= ((z >> 7) & 1u | (z >> 14) & 2u | (z >> 21) & 4u | (z >> 28) & 8u) << (4 * k);
         }
-        bool after_ff = win_byte(v, -1) == 0xFF && carry_after_ff(R, a, giveup);
-        if (!ff && !after_ff) {  // no marker activity: all 16 bytes kept unchanged
+        // a carried byte 0 is no FF of its own; 00 / FF there are dropped (an RSTn byte is kept;
+        // anything else ended the data in the previous chunk, and this chunk is not counted)
+        uint32_t drop0 = 0;
+        if (carry) {
+            ffm &= ~1u;
+            const uint32_t c0 = D[0] & 0xFFu;
+            drop0 = (c0 == 0u || c0 == 0xFFu) ? 1u : 0u;
+        }
+        const uint32_t drop = (ffm << 1) | drop0;  // bit 16: the next chunk's byte 0 (it drops it itself)
+        if (((ffm << 1) & ~zm) == 0u) {
+            o.kept = 16 - __builtin_popcount(drop & 0xFFFFu);
             if (WRITE) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) out[k] = (uint8_t)win_byte(v, k);
+                uint64_t q0 = (uint64_t)D[0] | ((uint64_t)D[1] << 32), q1 = (uint64_t)D[2] | ((uint64_t)D[3] << 32);
+                for (uint32_t m = drop & 0xFFFFu; m;) {  // highest dropped byte first
+                    const int p = 31 - __builtin_clz(m);
+                    m &= ~(1u << p);
+                    const int b = 8 * (p & 7);
+                    const uint64_t keep = b ? (1ull << b) - 1ull : 0ull;  // bytes below p
+                    if (p >= 8) {
+                        q1 = (q1 & keep) | ((q1 >> 8) & ~keep);
+                    } else {
+                        q0 = (q0 & keep) | ((q0 >> 8) & ~keep) | (q1 << 56);
+                        q1 >>= 8;
+                    }
+                }
+                o.out[0] = (uint32_t)q0;
+                o.out[1] = (uint32_t)(q0 >> 32);
+                o.out[2] = (uint32_t)q1;
+                o.out[3] = (uint32_t)(q1 >> 32);
             }
-            return kChunk;
+            return o;
         }
-        // the automaton below, on the register window (R[a+16] is byte 16 of the window)
-        int kept = 0;
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-            if (after_ff) { after_ff = false; continue; }
-            const int c = win_byte(v, k);
-            if (c != 0xFF) {
-                if (WRITE) out[kept] = (uint8_t)c;
-                ++kept;
-                continue;
-            }
-            const int m = win_byte(v, k + 1);
-            if (m == 0x00 || m == 0xFF) {
-                if (WRITE) out[kept] = 0xFF;
-                ++kept;
-                after_ff = true;
-            } else if ((m & 0xF8) == 0xD0) {
-                if (WRITE) { out[kept] = 0xFF; out[kept + 1] = (uint8_t)m; }
-                if (rs) rs->hit(kept, m);
-                kept += 2;
-                after_ff = true;
-            } else {
-                *end_at = a + k;
-                *end_err = m != 0xD9;
-                break;
-            }
-        }
-        return kept;
     }
-    bool after_ff = carry_after_ff(R, a, giveup);
+    const int lo = a < 0 ? (int)-a : 0;
+    const int hi = a + 16 <= L ? 16 : (int)(L - a);
+    uint64_t w0 = 0, w1 = 0;
     int kept = 0;
-    const int64_t b = a + kChunk < L ? a + kChunk : L;
-    for (int64_t p = a; p < b; ++p) {
-        if (after_ff) { after_ff = false; continue; }  // marker byte, consumed with its FF
-        const uint8_t c = R[p];
-        if (c != 0xFF) {
-            if (WRITE) out[kept] = c;
-            ++kept;
-            continue;
+    auto keep = [&](uint32_t c) {
+        if (WRITE) {
+            if (kept < 8) w0 |= (uint64_t)c << (8 * kept);
+            else w1 |= (uint64_t)c << (8 * (kept - 8));
         }
-        if (p + 1 >= L) { *end_at = p; *end_err = 1; break; }  // FF ends the file (:477-478)
-        const uint8_t m = R[p + 1];
-        if (m == 0x00 || m == 0xFF) {  // :465-467
-            if (WRITE) out[kept] = 0xFF;
-            ++kept;
-            after_ff = true;
-        } else if ((m & 0xF8) == 0xD0) {  // RSTn: both bytes enter the bit buffer (:472-475)
-            if (WRITE) { out[kept] = 0xFF; out[kept + 1] = m; }
-            if (rs) rs->hit(kept, m);
-            kept += 2;
-            after_ff = true;
+        ++kept;
+    };
+    // Byte 0 follows an odd FF run (the previous chunk's last FF reads it as its marker byte):
+    // 00 / FF are dropped; an RSTn byte is kept HERE (the previous chunk kept only the FF, so a
+    // chunk never keeps more than 16 bytes); anything else ended the data in the previous chunk.
+    bool skip = false;  // this byte is the marker byte of the FF before it
+    if (lo == 0 && hi > 0 && carry) {
+        const uint32_t c0 = D[0] & 0xFFu;
+        if ((c0 & 0xF8u) == 0xD0u) keep(c0);
+        skip = true;
+    }
+    bool done = false;
+    // bytes by 64-bit shifts of two registers (an indexed D[k >> 2] would go to scratch)
+    const uint64_t q0 = (uint64_t)D[0] | ((uint64_t)D[1] << 32), q1 = (uint64_t)D[2] | ((uint64_t)D[3] << 32);
+    auto byte = [&](int k) { return (uint32_t)((k < 8 ? q0 >> (8 * k) : q1 >> (8 * (k - 8))) & 0xFFu); };
+    for (int k = lo; k < hi && !done; ++k) {
+        if (skip) { skip = false; continue; }  // marker byte, consumed with its FF
+        const uint32_t c = byte(k);
+        if (c != 0xFFu) { keep(c); continue; }
+        if (a + k + 1 >= L) { o.end_at = a + k; o.end_err = 1; done = true; continue; }  // FF ends the file (:477-478)
+        const uint32_t m = k < 15 ? byte(k + 1) : (uint32_t)nx;
+        if (m == 0x00u || m == 0xFFu) {  // :465-467
+            keep(0xFFu);
+            skip = true;
+        } else if ((m & 0xF8u) == 0xD0u) {  // RSTn: both bytes enter the bit buffer (:472-475)
+            if (rs) rs->hit(kept, (int)m);
+            keep(0xFFu);
+            if (k < 15) keep(m);  // (at k = 15 the next chunk keeps the marker byte)
+            skip = true;
         } else {  // D9 ends the data (:468); anything else is a syntax error (:470-471)
-            *end_at = p;
-            *end_err = m != 0xD9;
-            break;
+            o.end_at = a + k;
+            o.end_err = m != 0xD9u;
+            done = true;
         }
     }
-    return kept;
+    o.kept = kept;
+    if (WRITE) {
+        o.out[0] = (uint32_t)w0;
+        o.out[1] = (uint32_t)(w0 >> 32);
+        o.out[2] = (uint32_t)w1;
+        o.out[3] = (uint32_t)(w1 >> 32);
+    }
+    return o;
 }
 
 // Per-image MCU layout in registers (wave-uniform): component of MCU block b (2 bits per

@@ -12,6 +12,90 @@
 
 using namespace icx;
 
+// The unstuff pass as k_ustf_count / k_ustf_scan / k_ustf_write compute it, with tiles cut at
+// alignment `sh` (the GPU uses R's address mod 16): per tile, four rounds of 64 lanes x 16-byte
+// chunks, each round's kept bytes before its first end event. Returns ulen; U gets the data plus
+// the 0xFF reader padding; rst (optional) gets the restart-marker records in stream order.
+static int64_t emu_unstuff(const uint8_t* R, int64_t L, int sh, std::vector<uint8_t>& U, int64_t& errpos,
+                           int32_t& giveup, std::vector<int64_t>* rst) {
+    const int64_t ntiles = ustf_ntiles(L, sh);
+    struct Lane { Ustf16 u; int n; int64_t a; uint32_t D[4]; int nx; int pf; };
+    auto round = [&](int64_t t0, int r, Lane* ln) {
+        for (int l = 0; l < 64; ++l) {
+            Lane& x = ln[l];
+            x.a = t0 + r * 1024 + l * 16;
+            for (int k = 0; k < 4; ++k) {
+                x.D[k] = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const int64_t p = x.a + 4 * k + b;
+                    if (p >= 0 && p < L) x.D[k] |= (uint32_t)R[p] << (8 * b);
+                }
+            }
+            x.nx = x.a + 16 < L && x.a + 16 >= 0 ? R[x.a + 16] : 0;
+            uint32_t pw = 0;  // R[a-4 .. a) (bytes before the scan: not FF here, unused by ff_run4)
+            for (int b = 0; b < 4; ++b) {
+                const int64_t p = x.a - 4 + b;
+                if (p >= 0 && p < L) pw |= (uint32_t)R[p] << (8 * b);
+            }
+            x.pf = ff_run4(pw, x.a);
+            RstSink rs{0, 0, nullptr, 0, 0};
+            x.u = ustf16<true>(R, L, x.a, x.D, x.nx, x.pf, &giveup, &rs);
+            x.n = rs.n;
+        }
+        int64_t e = INT64_MAX;
+        for (int l = 0; l < 64; ++l) if (ln[l].u.end_at >= 0 && ln[l].u.end_at < e) e = ln[l].u.end_at;
+        return e;
+    };
+    auto before = [](const Lane& x, int64_t e) { return x.u.end_at >= 0 ? x.u.end_at <= e : x.a < e; };
+    std::vector<TileRec> tiles(ntiles);
+    Lane ln[64];
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int64_t t0 = t * kTileBytes - sh;
+        int kept = 0, nrst = 0, err = 0;
+        int64_t tend = -1;
+        for (int r = 0; r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
+            const int64_t e = round(t0, r, ln);
+            for (int l = 0; l < 64; ++l)
+                if (before(ln[l], e)) { kept += ln[l].u.kept; nrst += ln[l].n; }
+            if (e != INT64_MAX) {
+                for (int l = 0; l < 64; ++l) if (ln[l].u.end_at == e) err = ln[l].u.end_err;
+                tend = e;
+                break;
+            }
+        }
+        tiles[t] = TileRec{kept, err, tend, nrst, 0};
+    }
+    int64_t fe = -1;
+    for (int64_t t = 0; t < ntiles; ++t)
+        if (tiles[t].end_at >= 0) { fe = t; break; }
+    int64_t ulen = 0;
+    for (int64_t t = 0; t < ntiles; ++t)
+        if (fe < 0 || t <= fe) ulen += tiles[t].kept;
+    errpos = (fe >= 0 && tiles[fe].end_err) ? ulen : INT64_MAX;
+    U.assign((size_t)u_pad_end(ulen) + 64, 0xFF);  // reader padding (icx_spec_core.h u_pad_end)
+    int64_t o = 0;
+    for (int64_t t = 0; t < ntiles && o < ulen; ++t) {
+        const int64_t t0 = t * kTileBytes - sh;
+        for (int r = 0; r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
+            const int64_t e = round(t0, r, ln);
+            for (int l = 0; l < 64; ++l) {
+                if (!before(ln[l], e)) continue;
+                if (rst && ln[l].n) {
+                    std::vector<int64_t> tmp(8);
+                    RstSink rs{0, o, tmp.data(), 0, 8};
+                    (void)ustf16<false>(R, L, ln[l].a, ln[l].D, ln[l].nx, ln[l].pf, &giveup, &rs);
+                    for (int k = 0; k < rs.n && k < 8; ++k) rst->push_back(tmp[k]);
+                }
+                for (int k = 0; k < ln[l].u.kept; ++k)
+                    if (o + k < ulen) U[o + k] = (uint8_t)(ln[l].u.out[k >> 2] >> (8 * (k & 3)));
+                o += ln[l].u.kept;
+            }
+            if (e != INT64_MAX) break;
+        }
+    }
+    return ulen;
+}
+
 extern "C" {
 
 // Returns: 0 parallel path finished (status in *status), 1 image would fall back to the
@@ -30,56 +114,10 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     if (total > cap_blocks) return 2;
     const uint8_t* R = file + d.scan_off;
     // ---- unstuff (k_ustf_count / k_ustf_scan / k_ustf_write)
-    const int64_t ntiles = (scan_len + kTileBytes - 1) / kTileBytes;
-    std::vector<TileRec> tiles(ntiles);
+    std::vector<uint8_t> U;
+    int64_t errpos;
     int32_t giveup = 0;
-    for (int64_t t = 0; t < ntiles; ++t) {
-        int64_t tend = INT64_MAX;
-        int terr = 0;
-        std::vector<int> kept(256);
-        std::vector<int64_t> ends(256);
-        std::vector<int> errs(256);
-        for (int l = 0; l < 256; ++l) {
-            const int64_t a = t * kTileBytes + (int64_t)l * kChunk;
-            kept[l] = ustf_chunk<false>(R, scan_len, a, &ends[l], &errs[l], nullptr, &giveup);
-            if (ends[l] >= 0 && ends[l] < tend) { tend = ends[l]; terr = errs[l]; }
-        }
-        int sum = 0;
-        for (int l = 0; l < 256; ++l) {
-            const int64_t a = t * kTileBytes + (int64_t)l * kChunk;
-            const bool before = ends[l] >= 0 ? ends[l] <= tend : a < tend;
-            if (before) sum += kept[l];
-        }
-        tiles[t].kept = sum;
-        tiles[t].end_at = tend == INT64_MAX ? -1 : tend;
-        tiles[t].end_err = terr;
-    }
-    int64_t fe = -1;
-    for (int64_t t = 0; t < ntiles; ++t)
-        if (tiles[t].end_at >= 0) { fe = t; break; }
-    std::vector<int64_t> obase(ntiles);
-    int64_t ulen = 0;
-    for (int64_t t = 0; t < ntiles; ++t) {
-        obase[t] = ulen;
-        if (fe < 0 || t <= fe) ulen += tiles[t].kept;
-    }
-    const int64_t errpos = (fe >= 0 && tiles[fe].end_err) ? ulen : INT64_MAX;
-    std::vector<uint8_t> U(ulen + 64, 0xFF);  // reader padding (icx_spec_core.h u_pad_end)
-    for (int64_t t = 0; t < ntiles; ++t) {
-        if (obase[t] >= ulen) continue;
-        const int64_t tend = tiles[t].end_at;
-        int64_t o = obase[t];
-        for (int l = 0; l < 256; ++l) {
-            const int64_t a = t * kTileBytes + (int64_t)l * kChunk;
-            int64_t e;
-            int er;
-            const int k = ustf_chunk<false>(R, scan_len, a, &e, &er, nullptr, &giveup);
-            const bool before = e >= 0 ? (tend < 0 || e <= tend) : (tend < 0 || a < tend);
-            if (!before) continue;
-            if (k && o + k <= ulen) ustf_chunk<true>(R, scan_len, a, &e, &er, U.data() + o, &giveup);
-            o += k;
-        }
-    }
+    const int64_t ulen = emu_unstuff(R, scan_len, ustf_align(R), U, errpos, giveup, nullptr);
     if (giveup) { stats[1]++; return 1; }
     // ---- tables (k_step_tabs)
     auto SSp = std::make_unique<StepSet>();
@@ -186,14 +224,9 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
     if (parse_headers(file, size, d) != kPending || d.restart || d.bpm > kSpecMaxBpm) return -1;
     const uint8_t* R = file + d.scan_off;
     const int64_t L = d.size - d.scan_off;
-    std::vector<uint8_t> U(L + 64, 0xFF);  // reader padding (icx_spec_core.h u_pad_end)
-    int64_t e; int er; int32_t gu = 0;
-    int64_t ulen = 0;
-    for (int64_t a = 0; a < L; a += kChunk) {
-        int k = ustf_chunk<true>(R, L, a, &e, &er, U.data() + ulen, &gu);
-        ulen += k;
-        if (e >= 0) break;
-    }
+    std::vector<uint8_t> U;
+    int64_t errpos; int32_t gu = 0;
+    const int64_t ulen = emu_unstuff(R, L, ustf_align(R), U, errpos, gu, nullptr);
     auto SSp = std::make_unique<StepSet>();
     for (int k = 0; k < ScanTab::entries(); ++k) SSp->scan.fill(d.huff, k);
     const ScanTab& T = SSp->scan;
@@ -363,4 +396,27 @@ extern "C" int emu_step_selftest(const uint8_t* dcc17, const uint8_t* dcs, int n
     }
     stats[0] += nblocks;
     return bad;
+}
+
+// ---- unstuff at a forced tile alignment (tests/test_spec_emu.py) ----
+// The scan of `file` unstuffed with tiles cut at alignment sh (0..15); returns ulen (-1: no scan
+// or buffer too small), *errpos as the GPU's SpecImg::errpos, *giveup, and the restart records.
+extern "C" int64_t emu_unstuff_sh(const uint8_t* file, int64_t size, int sh, uint8_t* out, int64_t cap, int64_t* errpos,
+                                  int32_t* giveup, int64_t* rst, int64_t rst_cap, int64_t* nrst, int64_t* scan_off) {
+    auto dp = std::make_unique<Desc>();
+    Desc& d = *dp;
+    if (parse_headers(file, size, d) != kPending) return -1;
+    *scan_off = d.scan_off;
+    const int64_t L = d.size - d.scan_off;
+    if (L <= 0) return -1;
+    std::vector<uint8_t> U;
+    std::vector<int64_t> rs;
+    int32_t gu = 0;
+    const int64_t ulen = emu_unstuff(file + d.scan_off, L, sh, U, *errpos, gu, &rs);
+    *giveup = gu;
+    *nrst = (int64_t)rs.size();
+    for (int64_t k = 0; k < (int64_t)rs.size() && k < rst_cap; ++k) rst[k] = rs[k];
+    if (ulen > cap) return -1;
+    std::memcpy(out, U.data(), (size_t)ulen);
+    return ulen;
 }

@@ -206,3 +206,83 @@ def test_step_tables_random_tables():
         ac_syms = _ac_symbols(rng, nac, invalid_rate=0.05)
         bad, stats = _step_selftest(dcc, dc_syms, acc, ac_syms, 7 + t, nblocks=400)
         assert bad == 0, (t, dcc, acc)
+
+
+def ref_unstuff(R: bytes):
+    """NanoJPEG's byte rules (jpeg_dec.h:447-482) read sequentially: FF00 / FFFF -> FF, FFD0-7
+    kept (both bytes, position recorded), FFD9 ends the data, any other FFxx or FF at the end of
+    the file ends it with a syntax error (errpos = unstuffed length)."""
+    out, rst, p, err = bytearray(), [], 0, None
+    while p < len(R):
+        c = R[p]
+        if c != 0xFF:
+            out.append(c)
+            p += 1
+            continue
+        if p + 1 >= len(R):
+            err = len(out)
+            break
+        m = R[p + 1]
+        if m in (0x00, 0xFF):
+            out.append(0xFF)
+        elif m & 0xF8 == 0xD0:
+            rst.append((len(out) << 3) | (m & 7))
+            out += bytes([0xFF, m])
+        else:
+            err = len(out) if m != 0xD9 else None
+            break
+        p += 2
+    return bytes(out), err, rst
+
+
+def emu_unstuff(data: bytes, sh: int):
+    L = emu_lib()
+    L.emu_unstuff_sh.restype = C.c_int64
+    cap = len(data) + 64
+    out = C.create_string_buffer(cap)
+    rst = np.zeros(1 << 16, np.int64)
+    errpos, giveup, nrst, so = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int64()
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    n = L.emu_unstuff_sh(buf, C.c_int64(len(data)), sh, out, C.c_int64(cap), C.byref(errpos), C.byref(giveup),
+                         rst.ctypes.data_as(C.c_void_p), C.c_int64(len(rst)), C.byref(nrst), C.byref(so))
+    if n < 0:
+        return None
+    e = None if errpos.value == (1 << 63) - 1 else errpos.value
+    return out.raw[:n], e, list(rst[: nrst.value]), so.value
+
+
+def _stuffing_corpus():
+    files = [open(os.path.join(GOLDEN, n), "rb").read() for n in sorted(MANIFEST)]
+    # adversarial scans: FF runs of every length, stuffing / restart / end markers at every offset
+    # of a 16-byte chunk and across 1 KiB round and 4 KiB tile boundaries
+    rng = np.random.default_rng(77)
+    base = S.synth_jpeg(11, 64, 64, "420", 90)
+    sos = base.index(b"\xff\xda")
+    head = base[: sos + 2 + int.from_bytes(base[sos + 2: sos + 4], "big")]
+    pieces = [b"\xff\x00", b"\xff\xff", b"\xff\xd0", b"\xff\xd3", b"\xff\xd7", b"\xff" * 3 + b"\x00", b"\xff" * 5 + b"\xd1"]
+    for k in range(24):
+        body = bytearray()
+        while len(body) < 9000:
+            body += bytes(rng.integers(0, 255, int(rng.integers(0, 40)), dtype=np.uint8))
+            body += pieces[int(rng.integers(0, len(pieces)))]
+        tail = [b"\xff\xd9", b"\xff\xc4", b"\xff", b""][k % 4]
+        files.append(head + bytes(body) + tail)
+    return files
+
+
+def test_emulated_unstuff_every_alignment():
+    """k_ustf_count / k_ustf_write's aligned-tile unstuff (icx_spec_core.h ustf16) gives the same
+    stream, error position and restart records as NanoJPEG's sequential byte rules, for all 16
+    alignments of the scan start (the GPU takes the alignment from the data's address)."""
+    checked = 0
+    for data in _stuffing_corpus():
+        r0 = emu_unstuff(data, 0)
+        if r0 is None:
+            continue
+        so = r0[3]
+        ref = ref_unstuff(data[so:])
+        for sh in range(16):
+            u, e, rst, _ = emu_unstuff(data, sh)
+            assert (u, e, rst) == ref, sh
+        checked += 1
+    assert checked >= 140
