@@ -9,6 +9,9 @@
 // All integer math reproduces the reference bit for bit (icx_jpeg.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "icx_internal.h"
 
 namespace icx {
@@ -237,6 +240,91 @@ __global__ __launch_bounds__(256) void k_idct_any(const Desc* __restrict__ desc,
 }
 
 
+// Lane-pair IDCT helpers (k_idct420c, k_fused420): a block is transformed by two lanes in
+// registers -- lane h takes natural rows 4h..4h+3 in the row pass and columns 4h..4h+3 in the
+// column pass, the 4x4 quadrants changing hands by DPP. Full row / column formulas (no zero-AC
+// shortcuts) with 24-bit multiplies: exact whenever every dequantized coefficient is below 2^14
+// in magnitude (then no row output reaches 2^21); otherwise the reference code (idct_row /
+// idct_col, shortcuts and 32-bit wrap included) runs.
+namespace {
+constexpr uint8_t kZigOfNatC[64] = {
+    0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43,
+    9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+    21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+}
+// Full row / column formulas (no shortcuts) with 24-bit multiplies: exact on the fast path.
+__device__ __forceinline__ void idct_row_full(int32_t (&r)[8]) {
+    int32_t x0 = (r[0] << 11) + 128, x1 = r[4] << 11, x2 = r[6], x3 = r[2];
+    int32_t x4 = r[1], x5 = r[7], x6 = r[5], x7 = r[3], x8;
+    x8 = m24(kW7, x4 + x5);
+    x4 = x8 + m24(kW1 - kW7, x4);
+    x5 = x8 - m24(kW1 + kW7, x5);
+    x8 = m24(kW3, x6 + x7);
+    x6 = x8 - m24(kW3 - kW5, x6);
+    x7 = x8 - m24(kW3 + kW5, x7);
+    x8 = x0 + x1;
+    x0 -= x1;
+    x1 = m24(kW6, x3 + x2);
+    x2 = x1 - m24(kW2 + kW6, x2);
+    x3 = x1 + m24(kW2 - kW6, x3);
+    x1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = x0 + x2;
+    x0 -= x2;
+    x2 = (m24(181, x4 + x5) + 128) >> 8;
+    x4 = (m24(181, x4 - x5) + 128) >> 8;
+    r[0] = (x7 + x1) >> 8;
+    r[1] = (x3 + x2) >> 8;
+    r[2] = (x0 + x4) >> 8;
+    r[3] = (x8 + x6) >> 8;
+    r[4] = (x8 - x6) >> 8;
+    r[5] = (x0 - x4) >> 8;
+    r[6] = (x3 - x2) >> 8;
+    r[7] = (x7 - x1) >> 8;
+}
+__device__ __forceinline__ void idct_col_full(const int32_t (&v)[8], int32_t (&o)[8]) {
+    int32_t x0 = (v[0] << 8) + 8192, x1 = v[4] << 8, x2 = v[6], x3 = v[2];
+    int32_t x4 = v[1], x5 = v[7], x6 = v[5], x7 = v[3], x8;
+    x8 = m24(kW7, x4 + x5) + 4;
+    x4 = (x8 + m24(kW1 - kW7, x4)) >> 3;
+    x5 = (x8 - m24(kW1 + kW7, x5)) >> 3;
+    x8 = m24(kW3, x6 + x7) + 4;
+    x6 = (x8 - m24(kW3 - kW5, x6)) >> 3;
+    x7 = (x8 - m24(kW3 + kW5, x7)) >> 3;
+    x8 = x0 + x1;
+    x0 -= x1;
+    x1 = m24(kW6, x3 + x2) + 4;
+    x2 = (x1 - m24(kW2 + kW6, x2)) >> 3;
+    x3 = (x1 + m24(kW2 - kW6, x3)) >> 3;
+    x1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = x0 + x2;
+    x0 -= x2;
+    x2 = (m24(181, x4 + x5) + 128) >> 8;
+    x4 = (m24(181, x4 - x5) + 128) >> 8;
+    auto cl = [](int32_t x) { return min(max((x >> 14) + 128, 0), 255); };
+    o[0] = cl(x7 + x1);
+    o[1] = cl(x3 + x2);
+    o[2] = cl(x0 + x4);
+    o[3] = cl(x8 + x6);
+    o[4] = cl(x8 - x6);
+    o[5] = cl(x0 - x4);
+    o[6] = cl(x3 - x2);
+    o[7] = cl(x7 - x1);
+}
+__device__ __forceinline__ int32_t pair_swap(int32_t x) {  // the other lane of the pair (DPP quad_perm [1,0,3,2])
+    return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ bool fused420(const Desc& d);  // (k_fused420 below)
+
 // The main IDCT kernel, for MCUs of up to kIdctUnitBlocks blocks (every sampling but the
 // exotic 8x-subsampled ones). A wave's unit of work is kUM horizontally adjacent MCUs of one MCU
 // row (kUM = the largest power of two with kUM * bpm <= 64: 8 MCUs = 48 blocks at 4:2:0). Its
@@ -250,11 +338,11 @@ struct IdctComp {
 };
 __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                               const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
-                                              int64_t coef_cap, int64_t plane_cap) {
+                                              int64_t coef_cap, int64_t plane_cap, int fuse) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     // (bpm is 0 for a descriptor without a frame header: nothing to transform)
-    if (d.status != kOk || d.bpm <= 0 || d.bpm > kIdctUnitBlocks) return;
+    if (d.status != kOk || d.bpm <= 0 || d.bpm > kIdctUnitBlocks || (fuse && fused420(d))) return;
     __shared__ int32_t qn[3][64];                // natural-order dequant table per component
     __shared__ uint32_t bgeo[kIdctUnitBlocks];   // unit block q -> ci | LDS offset of its tile << 2
     __shared__ IdctComp cg[3];
@@ -622,7 +710,10 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
 // made from two dword loads per row; the vertical pass (:762-791) slides a 5-row window held in
 // registers; YCbCr->RGB (:834-853) is stored as one 12-byte write per lane. No LDS, no barriers.
 // Vertical edge rows are wave-uniform branches; horizontal edge lanes take the generic taps.
-constexpr int kSH = 64;
+#ifndef ICX_KSH
+#define ICX_KSH 64
+#endif
+constexpr int kSH = ICX_KSH;
 // rows (row pairs) whose loads are in flight ahead of the one being converted: one row pair per
 // wave left ~30 KB of loads in flight per CU, below what the HBM latency needs
 #ifndef ICX_CONV_PD
@@ -666,15 +757,14 @@ __device__ __forceinline__ uint32_t pmap(F f) {
 struct CRaw {
     uint32_t d0, d1;
 };
+// (The loads are unconditional -- edge lanes read the row start and ignore it: a load under a
+// per-lane branch gets an s_waitcnt vmcnt(0) at the join, which serialised every row fetch.)
 template <bool KH>
 __device__ __forceinline__ CRaw chroma_fetch(const CPl& c, int r, int M, bool fast) {
     const uint8_t* row = c.p + (int64_t)r * c.s;
     if (!KH) return CRaw{ld4(row + 4 * M), 0u};
-    if (fast) {
-        const int base = (2 * M - 2) & ~3;
-        return CRaw{ld4(row + base), ld4(row + base + 4)};
-    }
-    return CRaw{0u, 0u};  // edge lanes load inside chroma_make
+    const int base = fast ? (2 * M - 2) & ~3 : 0;  // edge lanes load inside chroma_make
+    return CRaw{ld4(row + base), ld4(row + base + 4)};
 }
 // The 4-tap kernel as one v_dot4 on four packed samples: samples are biased to int8 (x ^ 0x80
 // = x - 128) and, since the taps sum to 128, sum(k*x) + 64 = dot(k, x - 128) + 128*128 + 64.
@@ -746,6 +836,122 @@ struct StreamOut {
     }
 };
 
+// Data of one row (or row pair): the chroma loads of both components and the luma dwords.
+struct Pre {
+    CRaw a, e;
+    uint32_t y0, y1;
+};
+// Output rows [Y0, Y1) (Y0 even) of one lane's 4 columns (4M .. 4M+3) with vertical chroma
+// doubling (KV layouts, jpeg_dec.h:762-791): a 5-row chroma window slides down in registers;
+// luma(y) gives the lane's 4 luma samples of row y, emit(y, luma, cb, cr) converts and stores.
+// The sliding chroma window of rows_kv (both components): rows k-2..k+1 of the next row pair
+// k, and their biased column dwords (even-output taps).
+struct KvWin {
+    uint32_t a0, a1, a2, a3, e0, e1, e2, e3;
+    uint32_t ca[4], ce[4];
+};
+__device__ __forceinline__ uint32_t kv_column(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, int i) {
+    const uint32_t sel = 0x0c0c0400u | (uint32_t)(i * 0x0101);  // byte i of the low operand, byte i of the high
+    return __builtin_amdgcn_perm(r1, r0, sel) | (__builtin_amdgcn_perm(r3, r2, sel) << 16);
+}
+// Window for row pair k0: the first four rows, all eight rows' loads issued before any is used.
+template <bool KH>
+__device__ __forceinline__ void kv_init(KvWin& w, const CPl& c1, const CPl& c2, int M, bool f1, bool f2, int k0) {
+    auto cr1 = [&](int r) { return min(max(r, 0), c1.h - 1); };
+    auto cr2 = [&](int r) { return min(max(r, 0), c2.h - 1); };
+    CRaw ra[4], re[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ra[i] = chroma_fetch<KH>(c1, cr1(k0 - 2 + i), M, f1);
+        re[i] = chroma_fetch<KH>(c2, cr2(k0 - 2 + i), M, f2);
+    }
+    w.a0 = chroma_make<KH>(c1, cr1(k0 - 2), M, f1, ra[0]);
+    w.a1 = chroma_make<KH>(c1, cr1(k0 - 1), M, f1, ra[1]);
+    w.a2 = chroma_make<KH>(c1, cr1(k0), M, f1, ra[2]);
+    w.a3 = chroma_make<KH>(c1, cr1(k0 + 1), M, f1, ra[3]);
+    w.e0 = chroma_make<KH>(c2, cr2(k0 - 2), M, f2, re[0]);
+    w.e1 = chroma_make<KH>(c2, cr2(k0 - 1), M, f2, re[1]);
+    w.e2 = chroma_make<KH>(c2, cr2(k0), M, f2, re[2]);
+    w.e3 = chroma_make<KH>(c2, cr2(k0 + 1), M, f2, re[3]);
+    // per output column i, a dword of the 4 window rows' samples (biased)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        w.ca[i] = kv_column(w.a0, w.a1, w.a2, w.a3, i) ^ kBias8;
+        w.ce[i] = kv_column(w.e0, w.e1, w.e2, w.e3, i) ^ kBias8;
+    }
+}
+// Output rows [Y0, Y1) (Y0 even) of one lane's 4 columns (4M .. 4M+3) with vertical chroma
+// doubling (KV layouts, jpeg_dec.h:762-791), the window w set for row pair Y0 / 2 and left at
+// row pair Y1 / 2: luma(y) gives the lane's 4 luma samples of row y, emit(y, luma, cb, cr)
+// converts and stores.
+template <bool KH, class LumaF, class EmitF>
+__device__ __forceinline__ void kv_rows(KvWin& w, const CPl& c1, const CPl& c2, int M, bool f1, bool f2, int Y0, int Y1,
+                                        LumaF luma, EmitF emit) {
+    const int k0 = Y0 >> 1;
+    auto cr1 = [&](int r) { return min(max(r, 0), c1.h - 1); };
+    auto cr2 = [&](int r) { return min(max(r, 0), c2.h - 1); };
+    // data of row pair k: chroma row k+2, luma rows 2k and 2k+1
+    auto fetch = [&](int k) {
+        Pre p{};
+        if (2 * k < Y1) {
+            p.a = chroma_fetch<KH>(c1, cr1(k + 2), M, f1);
+            p.e = chroma_fetch<KH>(c2, cr2(k + 2), M, f2);
+            p.y0 = luma(2 * k);
+            if (2 * k + 1 < Y1) p.y1 = luma(2 * k + 1);
+        }
+        return p;
+    };
+    // E = rows k-2..k+1 (even output 2k: kTapRev), O = rows k-1..k+2 (odd 2k+1: kTapFwd);
+    // each row pair shifts one new row into the columns with one v_perm per column.
+    auto vsteps = [&](int k, uint32_t (&cc)[4], uint32_t nrow, int h, uint32_t w0, uint32_t w1, uint32_t w2,
+                      uint32_t w3, uint32_t& ev, uint32_t& od) {
+        const uint32_t nb = nrow ^ kBias8;
+        uint32_t oc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // O = (E >> 8) | new row's byte i << 24
+            oc[i] = __builtin_amdgcn_perm(nb, cc[i], 0x00030201u | ((uint32_t)(4 + i) << 24));
+        if (k >= 2 && k <= h - 3) {  // both outputs interior (wave-uniform)
+            ev = pack4(dtap(cc[0], kTapRev), dtap(cc[1], kTapRev), dtap(cc[2], kTapRev), dtap(cc[3], kTapRev));
+            od = pack4(dtap(oc[0], kTapFwd), dtap(oc[1], kTapFwd), dtap(oc[2], kTapFwd), dtap(oc[3], kTapFwd));
+        } else {
+            ev = vtap_even(k, h, w0, w1, w2, w3);
+            od = vtap_odd(k, h, w1, w2, w3, nrow);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cc[i] = oc[i];
+    };
+    auto step = [&](int k, const Pre& p) {
+        const uint32_t a4 = chroma_make<KH>(c1, cr1(k + 2), M, f1, p.a);
+        const uint32_t e4 = chroma_make<KH>(c2, cr2(k + 2), M, f2, p.e);
+        uint32_t ae, ao, ee, eo;
+        vsteps(k, w.ca, a4, c1.h, w.a0, w.a1, w.a2, w.a3, ae, ao);
+        vsteps(k, w.ce, e4, c2.h, w.e0, w.e1, w.e2, w.e3, ee, eo);
+        emit(2 * k, p.y0, ae, ee);
+        if (2 * k + 1 < Y1) emit(2 * k + 1, p.y1, ao, eo);
+        w.a0 = w.a1; w.a1 = w.a2; w.a2 = w.a3; w.a3 = a4;
+        w.e0 = w.e1; w.e1 = w.e2; w.e2 = w.e3; w.e3 = e4;
+    };
+    Pre B[kPD + 1];
+#pragma unroll
+    for (int u = 0; u < kPD; ++u) B[u] = fetch(k0 + u);
+    for (int k = k0; 2 * k < Y1; k += kPD + 1) {
+#pragma unroll
+        for (int u = 0; u <= kPD; ++u) {
+            if (2 * (k + u) >= Y1) break;  // wave-uniform
+            B[(u + kPD) % (kPD + 1)] = fetch(k + u + kPD);
+            step(k + u, B[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+template <bool KH, class LumaF, class EmitF>
+__device__ __forceinline__ void rows_kv(const CPl& c1, const CPl& c2, int M, bool f1, bool f2, int Y0, int Y1,
+                                        LumaF luma, EmitF emit) {
+    KvWin w;
+    kv_init<KH>(w, c1, c2, M, f1, f2, Y0 >> 1);
+    kv_rows<KH>(w, c1, c2, M, f1, f2, Y0, Y1, luma, emit);
+}
+
 template <int K>
 __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot, const StreamOut& so) {
     constexpr bool KH = (K & 1) != 0, KV = (K & 2) != 0;
@@ -792,10 +998,6 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
         // constant: the loads of the next kPD rows (row pairs) are in flight while the current one
         // is computed; the scheduling barriers keep each buffer's reload after its last use so no
         // in-flight value is copied.
-        struct Pre {
-            CRaw a, e;
-            uint32_t y0, y1;
-        };
         if (!KV) {
             auto fetch = [&](int y) {
                 Pre p{};
@@ -823,77 +1025,7 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
             }
             continue;
         }
-        const int k0 = Y0 >> 1;
-        auto cr1 = [&](int r) { return min(max(r, 0), c1.h - 1); };
-        auto cr2 = [&](int r) { return min(max(r, 0), c2.h - 1); };
-        uint32_t a0 = chroma_row<KH>(c1, cr1(k0 - 2), M, f1), a1 = chroma_row<KH>(c1, cr1(k0 - 1), M, f1);
-        uint32_t a2 = chroma_row<KH>(c1, cr1(k0), M, f1), a3 = chroma_row<KH>(c1, cr1(k0 + 1), M, f1);
-        uint32_t e0 = chroma_row<KH>(c2, cr2(k0 - 2), M, f2), e1 = chroma_row<KH>(c2, cr2(k0 - 1), M, f2);
-        uint32_t e2 = chroma_row<KH>(c2, cr2(k0), M, f2), e3 = chroma_row<KH>(c2, cr2(k0 + 1), M, f2);
-        // data of row pair k: chroma row k+2, luma rows 2k and 2k+1
-        auto fetch = [&](int k) {
-            Pre p{};
-            if (2 * k < Y1) {
-                p.a = chroma_fetch<KH>(c1, cr1(k + 2), M, f1);
-                p.e = chroma_fetch<KH>(c2, cr2(k + 2), M, f2);
-                p.y0 = luma(2 * k);
-                if (2 * k + 1 < Y1) p.y1 = luma(2 * k + 1);
-            }
-            return p;
-        };
-        // Interior rows: per output column i, a dword of the 4 window rows' samples (biased),
-        // E = rows k-2..k+1 (even output 2k: kTapRev), O = rows k-1..k+2 (odd 2k+1: kTapFwd);
-        // each row pair shifts one new row into the columns with one v_perm per column.
-        auto column = [](uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, int i) {
-            const uint32_t sel = 0x0c0c0400u | (uint32_t)(i * 0x0101);  // byte i of the low operand, byte i of the high
-            return __builtin_amdgcn_perm(r1, r0, sel) | (__builtin_amdgcn_perm(r3, r2, sel) << 16);
-        };
-        uint32_t ca[4], ce[4];  // E columns of components 1 and 2
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            ca[i] = column(a0, a1, a2, a3, i) ^ kBias8;
-            ce[i] = column(e0, e1, e2, e3, i) ^ kBias8;
-        }
-        auto vsteps = [&](int k, uint32_t (&cc)[4], uint32_t nrow, int h, uint32_t w0, uint32_t w1, uint32_t w2,
-                          uint32_t w3, uint32_t& ev, uint32_t& od) {
-            const uint32_t nb = nrow ^ kBias8;
-            uint32_t oc[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)  // O = (E >> 8) | new row's byte i << 24
-                oc[i] = __builtin_amdgcn_perm(nb, cc[i], 0x00030201u | ((uint32_t)(4 + i) << 24));
-            if (k >= 2 && k <= h - 3) {  // both outputs interior (wave-uniform)
-                ev = pack4(dtap(cc[0], kTapRev), dtap(cc[1], kTapRev), dtap(cc[2], kTapRev), dtap(cc[3], kTapRev));
-                od = pack4(dtap(oc[0], kTapFwd), dtap(oc[1], kTapFwd), dtap(oc[2], kTapFwd), dtap(oc[3], kTapFwd));
-            } else {
-                ev = vtap_even(k, h, w0, w1, w2, w3);
-                od = vtap_odd(k, h, w1, w2, w3, nrow);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) cc[i] = oc[i];
-        };
-        auto step = [&](int k, const Pre& p) {
-            const uint32_t a4 = chroma_make<KH>(c1, cr1(k + 2), M, f1, p.a);
-            const uint32_t e4 = chroma_make<KH>(c2, cr2(k + 2), M, f2, p.e);
-            uint32_t ae, ao, ee, eo;
-            vsteps(k, ca, a4, c1.h, a0, a1, a2, a3, ae, ao);
-            vsteps(k, ce, e4, c2.h, e0, e1, e2, e3, ee, eo);
-            emit(2 * k, p.y0, ae, ee);
-            if (2 * k + 1 < Y1) emit(2 * k + 1, p.y1, ao, eo);
-            a0 = a1; a1 = a2; a2 = a3; a3 = a4;
-            e0 = e1; e1 = e2; e2 = e3; e3 = e4;
-        };
-        Pre B[kPD + 1];
-#pragma unroll
-        for (int u = 0; u < kPD; ++u) B[u] = fetch(k0 + u);
-        for (int k = k0; 2 * k < Y1; k += kPD + 1) {
-#pragma unroll
-            for (int u = 0; u <= kPD; ++u) {
-                if (2 * (k + u) >= Y1) break;  // wave-uniform
-                B[(u + kPD) % (kPD + 1)] = fetch(k + u + kPD);
-                step(k + u, B[u]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
+        rows_kv<KH>(c1, c2, M, f1, f2, Y0, Y1, luma, emit);
     }
 }
 
@@ -901,14 +1033,231 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
 // every instantiation is launched and skips the images of other layouts.
 template <int K>
 __global__ __launch_bounds__(256) void k_convert_stream(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
-                                                        int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride) {
+                                                        int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride,
+                                                        int fuse) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk || stream_kind(d) != K) return;
+    if (d.status != kOk || stream_kind(d) != K || (K == 3 && fuse && fused420(d))) return;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     uint8_t* o = out + (int64_t)img * out_stride;
     const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
     stream_image<K>(d, pslot, so);
+}
+
+// ---------------------------------------------------- 4:2:0 chroma IDCT + fused luma IDCT/convert
+// The common 4:2:0 layout (Y 2x2, Cb and Cr 1x1 per MCU) skips k_idct and k_convert_stream<3>:
+// k_idct420c writes the two chroma planes, then k_fused420 transforms each MCU row's luma
+// blocks into LDS and converts those 16 rows from there -- the 16.8 MB luma plane per 4096^2
+// image never goes through HBM. Both use the lane-pair IDCT; the conversion is rows_kv, the same
+// code k_convert_stream runs, with the luma rows read from LDS.
+__device__ __forceinline__ bool fused420(const Desc& d) {
+    return d.status == kOk && d.nc == 3 && d.bpm == 6 && d.c[0].hs == 2 && d.c[0].vs == 2 && d.c[1].hs == 1 &&
+           d.c[1].vs == 1 && d.c[2].hs == 1 && d.c[2].vs == 1 && stream_kind(d) == 3;
+}
+
+// Lane-pair IDCT of one block: c = the block as stored (zig-zag int16), qw = its component's
+// dequant table (zig-zag, 4 bytes per register), h = the lane's half; rowd[r] = pixels 4h..4h+3
+// of row r. D / n: the int32 DC of a block whose cell 0 holds kDcEscape. Wave-level (the fast
+// path is a wave vote): every lane of the wave calls it.
+__device__ __forceinline__ void pair_idct(const int4 (&c)[8], const uint32_t (&qw)[16], int h, const int32_t* D, int64_t n,
+                                          uint32_t (&rowd)[8]) {
+    auto qt = [&](int z) { return (int32_t)((qw[z >> 2] >> (8 * (z & 3))) & 0xFFu); };
+    auto coef = [&](int z) {
+        const int4& w = c[z >> 3];
+        const int e = z & 7;
+        const uint32_t d32 = (uint32_t)(e < 2 ? w.x : e < 4 ? w.y : e < 6 ? w.z : w.w);
+        return (int32_t)(int16_t)(d32 >> (16 * (e & 1)));
+    };
+    // row pass: natural rows 4h + i (the two candidate positions are compile-time; h selects)
+    int32_t R[4][8];
+    int32_t hi = 0, lo = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int z0 = kZigOfNatC[8 * i + j], z1 = kZigOfNatC[8 * (4 + i) + j];
+            const int32_t v0 = m24(coef(z0), qt(z0)), v1 = m24(coef(z1), qt(z1));  // int16 x 8-bit: exact
+            R[i][j] = h ? v1 : v0;
+            hi = max(hi, R[i][j]);
+            lo = min(lo, R[i][j]);
+        }
+    }
+    if (h == 0 && (int16_t)c[0].x == kDcEscape) {  // DC outside int16 (corrupt streams only)
+        R[0][0] = wmul(D[n], qt(0));
+        hi = INT32_MAX;
+    }
+    const bool fast = __all(hi < (1 << 14) && lo > -(1 << 14));
+    if (fast) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) idct_row_full(R[i]);
+    } else {  // the reference code, shortcuts and 32-bit wrap-around included
+#pragma unroll
+        for (int i = 0; i < 4; ++i) idct_row<false>(R[i]);
+    }
+    // quadrant swap: lane h keeps columns 4h..4h+3 of its rows and gets the partner's
+    int32_t C[8][4];  // C[r][jj] = natural row r, column 4h + jj
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int32_t keep = h ? R[i][4 + jj] : R[i][jj];
+            const int32_t got = pair_swap(h ? R[i][jj] : R[i][4 + jj]);
+            C[i][jj] = h ? got : keep;
+            C[4 + i][jj] = h ? keep : got;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) rowd[r] = 0;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+        int32_t col[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) col[r] = C[r][jj];
+        if (fast) {
+            int32_t o[8];
+            idct_col_full(col, o);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) rowd[r] |= (uint32_t)o[r] << (8 * jj);
+        } else {
+            uint8_t o[8];
+            idct_col<false>(col, o);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) rowd[r] |= (uint32_t)o[r] << (8 * jj);
+        }
+    }
+}
+__device__ __forceinline__ void load_qw(const uint8_t* qz, uint32_t (&qw)[16]) {  // 64 bytes of LDS, 16-byte aligned
+    const uint4* qs = reinterpret_cast<const uint4*>(qz);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint4 w = qs[k];
+        qw[4 * k] = w.x; qw[4 * k + 1] = w.y; qw[4 * k + 2] = w.z; qw[4 * k + 3] = w.w;
+    }
+}
+__device__ __forceinline__ void load_block(const int16_t* A, int64_t n, int4 (&c)[8]) {
+    const int4* src = reinterpret_cast<const int4*>(A + n * 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = src[k];
+}
+
+// Chroma planes of fused420 images: a wave's unit is 16 MCUs of one MCU row; lane pair q < 16
+// takes Cb of MCU mx0 + q, q >= 16 Cr of MCU mx0 + q - 16, so each plane row of the unit is
+// 128 contiguous bytes written by one store instruction.
+__global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                                  const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
+                                                  int64_t coef_cap, int64_t plane_cap) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (!fused420(d)) return;
+    __shared__ __attribute__((aligned(16))) uint8_t qz[2][64];
+    const int t = threadIdx.x;
+    if (t < 128) qz[t >> 6][t & 63] = d.q[d.c[1 + (t >> 6)].tq][t & 63];
+    __syncthreads();
+    const int wave = t >> 6, lane = t & 63, q = lane >> 1, h = lane & 1, cc = q >> 4, mq = q & 15;
+    uint32_t qw[16];
+    load_qw(qz[cc], qw);
+    const int mbw = d.mbw, stride = d.c[1].stride;
+    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
+    const int32_t* D = dcv + (int64_t)img * coef_cap;
+    uint8_t* Pc = planes + (int64_t)img * plane_cap + comp_plane_off(d, 1 + cc);
+    const uint32_t ucols = (uint32_t)((mbw + 15) >> 4), nunits = ucols * (uint32_t)d.mbh;
+    const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
+    for (uint32_t u = wid; u < nunits; u += nw) {
+        const uint32_t mby = u / ucols;
+        const int mx = (int)((u - mby * ucols) << 4) + mq;
+        const bool live = mx < mbw;
+        const int64_t n = ((int64_t)mby * mbw + (live ? mx : mbw - 1)) * 6 + 4 + cc;
+        int4 c[8];
+        load_block(A, n, c);
+        uint32_t rowd[8];
+        pair_idct(c, qw, h, D, n, rowd);
+        if (live) {
+            uint8_t* dst = Pc + (int64_t)mby * 8 * stride + mx * 8 + 4 * h;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
+        }
+    }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global stores (__syncthreads would also wait vmcnt(0), i.e. for every RGB store in flight).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Luma IDCT + conversion of fused420 images. Each wave owns a strip of 16 MCUs (256 pixels) by
+// kFB MCU rows, like a k_convert_stream strip: per MCU row it transforms the row's 64 luma blocks
+// (two rounds of 32 lane pairs) into its own 16 x 256 luma rows in LDS, then converts those 16
+// rows with the chroma window carried in registers from the MCU row above (kv_rows: chroma
+// from the planes k_idct420c wrote, luma from LDS). No workgroup barriers.
+constexpr int kFB = 4;
+__global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                                  const int32_t* __restrict__ dcv, const uint8_t* __restrict__ planes,
+                                                  int64_t coef_cap, int64_t plane_cap, uint8_t* __restrict__ out,
+                                                  uint64_t out_stride) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (!fused420(d)) return;
+    __shared__ uint32_t Yl_all[4][16][64];  // per wave: its strip's 16 luma rows of the MCU row
+    __shared__ __attribute__((aligned(16))) uint8_t qz[64];
+    const int t = threadIdx.x;
+    if (t < 64) qz[t] = d.q[d.c[0].tq][t];
+    __syncthreads();
+    const int wave = t >> 6, lane = t & 63, h = lane & 1, k = (lane >> 1) & 3;
+    uint32_t (*Yl)[64] = Yl_all[wave];
+    int sbx, sby;
+    (void)mcu_block_comp(d, k, sbx, sby);
+    uint32_t qw[16];
+    load_qw(qz, qw);
+    const int W = d.W, H = d.H, mbw = d.mbw, mbh = d.mbh;
+    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
+    const int32_t* D = dcv + (int64_t)img * coef_cap;
+    const uint8_t* pslot = planes + (int64_t)img * plane_cap;
+    const CPl c1{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
+    const CPl c2{pslot + comp_plane_off(d, 2), d.c[2].w, d.c[2].h, d.c[2].stride};
+    uint8_t* o = out + (int64_t)img * out_stride;
+    const StreamOut so{o, W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (W & 3) == 0};
+    const int nsx = (mbw + 15) >> 4, nsy = (mbh + kFB - 1) / kFB, nstrip = nsx * nsy;
+    for (int strip = blockIdx.x * 4 + wave; strip < nstrip; strip += gridDim.x * 4) {
+        const int sy = strip / nsx, sx = strip - sy * nsx;
+        const int mx0 = sx << 4, mb0 = sy * kFB, mb1 = min(mbh, mb0 + kFB);
+        const int x0 = 256 * sx + 4 * lane, M = x0 >> 2;
+        const bool xl = x0 < W;
+        const int nb = min(4, W - x0) * 3;
+        const bool f1 = M >= 1 && x0 + 3 <= 2 * c1.w - 4 && 2 * M + 5 < c1.s;
+        const bool f2 = M >= 1 && x0 + 3 <= 2 * c2.w - 4 && 2 * M + 5 < c2.s;
+        KvWin w;
+        kv_init<true>(w, c1, c2, M, f1, f2, 8 * mb0);
+        for (int mby = mb0; mby < mb1; ++mby) {
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {  // the MCU row's 16 x 4 luma blocks, 32 per round
+                const int mq = (lane >> 3) + 8 * r2, mx = mx0 + mq;
+                const bool live = mx < mbw;
+                const int64_t n = ((int64_t)mby * mbw + (live ? mx : mbw - 1)) * 6 + k;
+                int4 c[8];
+                load_block(A, n, c);
+                uint32_t rowd[8];
+                pair_idct(c, qw, h, D, n, rowd);
+                if (live) {
+                    const int lc = mq * 4 + sbx * 2 + h;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) Yl[sby * 8 + r][lc] = rowd[r];
+                }
+            }
+            asm volatile("" ::: "memory");  // (a wave's LDS accesses execute in order)
+            const int Y0 = 16 * mby, Y1 = min(H, Y0 + 16);
+            if (xl) {
+                auto luma = [&](int y) { return Yl[y - Y0][lane]; };
+                auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
+                    uint8_t px[12];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
+                    so.put(y, x0, px, nb);
+                };
+                kv_rows<true>(w, c1, c2, M, f1, f2, Y0, Y1, luma, emit);
+            }
+            asm volatile("" ::: "memory");
+        }
+    }
 }
 
 // --------------------------------------------------------------------------- finalize
@@ -953,10 +1302,18 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     // ~16K workgroups per launch in total; every kernel grid-strides over its image's work
     int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 32 * kIdctU - 1) / (32 * kIdctU), 16384 / n));
     if (gx >= 8) gx &= ~7;  // XCD-aware chunk order in k_idct needs a multiple of 8
+    // ICX_FUSE420=1: 4:2:0 images take k_idct420c + k_fused420 (luma IDCT inside the conversion;
+    // bit-exact, measured slower beside the second pipeline: DESIGN.md §4)
+    const int fuse = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 0;
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
-                       ws.plane_cap);
+                       ws.plane_cap, fuse);
     hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap);
+    if (fuse) {  // 4:2:0: chroma planes only (the luma is transformed inside k_fused420)
+        const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;
+        hipLaunchKernelGGL(k_idct420c, dim3(std::max(cgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes,
+                           ws.coef_cap, ws.plane_cap);
+    }
     E(kStIdct);
     B(kStUpsample);
     const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, 16384 / (3 * n)));
@@ -969,15 +1326,21 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     const int sxg = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)(ws.max_w + 255) / 256) *
                                                                  ((ws.max_h + kSH - 1) / kSH) / 4 + 1, 16384 / n));
     hipLaunchKernelGGL(k_convert_stream<3>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride);
+                       out_stride, fuse);
+    const int fgx = (int)std::max<int64_t>(1, std::min<int64_t>((((int64_t)(ws.max_w + 255) / 256) *
+                                                                  ((ws.max_h + 16 * kFB - 1) / (16 * kFB)) + 3) / 4,
+                                                                 16384 / n));
+    if (fuse)
+        hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
+                           ws.plane_cap, d_out, out_stride);
     hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride);
+                       out_stride, fuse);
     hipLaunchKernelGGL(k_convert_stream<1>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride);
+                       out_stride, fuse);
     hipLaunchKernelGGL(k_convert_stream<2>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride);
+                       out_stride, fuse);
     hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride);
+                       out_stride, fuse);
     hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride);
     hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,

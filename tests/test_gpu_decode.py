@@ -242,3 +242,27 @@ def test_dri_corrupt_marker_falls_back_exactly(ctx):
         if code == 0:
             assert pix.tobytes() == opix
     b.close()
+
+
+def test_fused420_path_bit_exact(ctx, monkeypatch):
+    """ICX_FUSE420=1 (k_idct420c + k_fused420: the luma IDCT inside the conversion) decodes every
+    golden and odd-sized synthetic 4:2:0 images exactly as the default path / the oracle."""
+    monkeypatch.setenv("ICX_FUSE420", "1")
+    names = sorted(MANIFEST)
+    jpegs = [open(os.path.join(GOLDEN, n), "rb").read() for n in names]
+    b = icx.Batch(ctx, len(jpegs), 512, 512)
+    res = b.decode_host(jpegs)
+    for n, (code, w, h, c, pix) in zip(names, res):
+        exp = MANIFEST[n]
+        assert code == exp["code"], n
+        if code == icx.OK:
+            assert sha(pix) == exp["sha256"], n
+    rng = np.random.default_rng(420)
+    imgs = []
+    for k in range(6):
+        w, h = int(rng.integers(17, 1500)), int(rng.integers(17, 700))
+        imgs.append(S.synth_jpeg(900 + k, w, h, "420", int(rng.integers(30, 100))))
+    b2 = icx.Batch(ctx, len(imgs), 1500, 700)
+    for data, (code, w, h, c, pix) in zip(imgs, b2.decode_host(imgs)):
+        ocode, ow, oh, on, opix = O.decode(data)
+        assert (code, w, h) == (ocode, ow, oh) and pix.tobytes() == opix
