@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_convert_stream(const Desc* __restrict__
                                                         int fuse) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk || stream_kind(d) != K || (K == 3 && fuse && fused420(d))) return;
+    if (d.status != kOk || stream_kind(d) != K || (K == 3 && fuse == 1 && fused420(d))) return;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     uint8_t* o = out + (int64_t)img * out_stride;
     const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
@@ -1180,6 +1180,49 @@ __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc,
     }
 }
 
+// Luma planes of fused420 images when the conversion reads them from HBM (ICX_FUSE420 = 2): a
+// wave's unit is 8 MCUs of one MCU row; lane pair q takes luma block q & 3 of MCU mx0 + (q >> 2),
+// so each store instruction writes two whole 128-byte plane rows (the unit's upper and lower
+// block rows).
+__global__ __launch_bounds__(256) void k_idct420y(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                                  const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
+                                                  int64_t coef_cap, int64_t plane_cap) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (!fused420(d)) return;
+    __shared__ __attribute__((aligned(16))) uint8_t qz[64];
+    const int t = threadIdx.x;
+    if (t < 64) qz[t] = d.q[d.c[0].tq][t];
+    __syncthreads();
+    const int wave = t >> 6, lane = t & 63, q = lane >> 1, h = lane & 1, mq = q >> 2, k = q & 3;
+    int sbx, sby;
+    (void)mcu_block_comp(d, k, sbx, sby);
+    uint32_t qw[16];
+    load_qw(qz, qw);
+    const int mbw = d.mbw, stride = d.c[0].stride;
+    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
+    const int32_t* D = dcv + (int64_t)img * coef_cap;
+    uint8_t* Py = planes + (int64_t)img * plane_cap;  // component 0 is first in the slot
+    const uint32_t ucols = (uint32_t)((mbw + 7) >> 3), nunits = ucols * (uint32_t)d.mbh;
+    const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
+    for (uint32_t u = wid; u < nunits; u += nw) {
+        const uint32_t mby = u / ucols;
+        const int mx = (int)((u - mby * ucols) << 3) + mq;
+        const bool live = mx < mbw;
+        const int64_t n = ((int64_t)mby * mbw + (live ? mx : mbw - 1)) * 6 + k;
+        int4 c[8];
+        load_block(A, n, c);
+        uint32_t rowd[8];
+        pair_idct(c, qw, h, D, n, rowd);
+        if (live) {
+            uint8_t* dst = Py + ((int64_t)mby * 16 + sby * 8) * stride + mx * 16 + sbx * 8 + 4 * h;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
+        }
+    }
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // global stores (__syncthreads would also wait vmcnt(0), i.e. for every RGB store in flight).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -1302,17 +1345,25 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     // ~16K workgroups per launch in total; every kernel grid-strides over its image's work
     int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 32 * kIdctU - 1) / (32 * kIdctU), 16384 / n));
     if (gx >= 8) gx &= ~7;  // XCD-aware chunk order in k_idct needs a multiple of 8
-    // ICX_FUSE420=1: 4:2:0 images take k_idct420c + k_fused420 (luma IDCT inside the conversion;
-    // bit-exact, measured slower beside the second pipeline: DESIGN.md §4)
-    const int fuse = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 0;
+    // 4:2:0 images (fused420): mode 2 (default) transforms their planes with the lane-pair IDCT,
+    // k_idct420y / k_idct420c, whose stores are whole 128-byte plane rows (k_idct skips them);
+    // mode 1 takes k_idct420c + k_fused420 (the luma IDCT inside the conversion; bit-exact, but
+    // slower beside the second pipeline: DESIGN.md §4); mode 0 leaves them to k_idct. ICX_FUSE420
+    // overrides the mode (tests, experiments).
+    const int fuse = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 2;
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap, fuse);
     hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap);
-    if (fuse) {  // 4:2:0: chroma planes only (the luma is transformed inside k_fused420)
+    if (fuse) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
         const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;
         hipLaunchKernelGGL(k_idct420c, dim3(std::max(cgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes,
                            ws.coef_cap, ws.plane_cap);
+        if (fuse == 2) {
+            const int ygx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 8 + 31) / 32, 16384 / n)) & ~7;
+            hipLaunchKernelGGL(k_idct420y, dim3(std::max(ygx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc,
+                               ws.planes, ws.coef_cap, ws.plane_cap);
+        }
     }
     E(kStIdct);
     B(kStUpsample);
@@ -1330,7 +1381,7 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     const int fgx = (int)std::max<int64_t>(1, std::min<int64_t>((((int64_t)(ws.max_w + 255) / 256) *
                                                                   ((ws.max_h + 16 * kFB - 1) / (16 * kFB)) + 3) / 4,
                                                                  16384 / n));
-    if (fuse)
+    if (fuse == 1)
         hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                            ws.plane_cap, d_out, out_stride);
     hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,

@@ -244,10 +244,12 @@ def test_dri_corrupt_marker_falls_back_exactly(ctx):
     b.close()
 
 
-def test_fused420_path_bit_exact(ctx, monkeypatch):
-    """ICX_FUSE420=1 (k_idct420c + k_fused420: the luma IDCT inside the conversion) decodes every
-    golden and odd-sized synthetic 4:2:0 images exactly as the default path / the oracle."""
-    monkeypatch.setenv("ICX_FUSE420", "1")
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_420_plane_modes_bit_exact(ctx, monkeypatch, mode):
+    """Every 4:2:0 plane mode -- 0: k_idct, 1: k_idct420c + k_fused420 (luma IDCT inside the
+    conversion), 2 (default): k_idct420y + k_idct420c -- decodes every golden and odd-sized
+    synthetic 4:2:0 images exactly as the oracle."""
+    monkeypatch.setenv("ICX_FUSE420", mode)
     names = sorted(MANIFEST)
     jpegs = [open(os.path.join(GOLDEN, n), "rb").read() for n in names]
     b = icx.Batch(ctx, len(jpegs), 512, 512)
