@@ -752,7 +752,12 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
                         int4* sp = &slots[sl][0];
                         const int sq = q ^ (sl & 7);
 #ifndef ICX_EXP_NOSTORE  // timing experiment only: drop the coefficient stores
-                        A[(int64_t)bsrc * 8 + q] = sp[sq];
+                        {  // streaming (evict-first) stores: the lanes' U lines stay in L2 (fetch 6.3x -> 2.2x U)
+                            typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+                            const int4 v = sp[sq];
+                            const i32x4 vv = {v.x, v.y, v.z, v.w};
+                            __builtin_nontemporal_store(vv, reinterpret_cast<i32x4*>(A) + (int64_t)bsrc * 8 + q);
+                        }
 #endif
                         sp[sq] = make_int4(0, 0, 0, 0);
                     }
