@@ -952,80 +952,140 @@ __device__ __forceinline__ void rows_kv(const CPl& c1, const CPl& c2, int M, boo
     kv_rows<KH>(w, c1, c2, M, f1, f2, Y0, Y1, luma, emit);
 }
 
+// Chroma lanes whose horizontal taps leave the interior formulas (image border, stride-end
+// reads): f = the lane's 4 doubled outputs use the interior 4-tap formula and read inside the row.
+__device__ __forceinline__ bool interior_taps(const CPl& c, int M) {
+    return M >= 1 && 4 * M + 3 <= 2 * c.w - 4 && 2 * M + 5 < c.s;
+}
+// First lane of the right border (lanes 0 and [edge_from, ceil(W/4)) are border lanes).
+__device__ __forceinline__ int edge_from(const CPl& c1, const CPl& c2, int W) {
+    auto lim = [](const CPl& c) { return min((2 * c.w - 7) >> 2, (c.s - 6) >> 1) + 1; };  // first M failing
+    return max(1, min(min(lim(c1), lim(c2)), (W + 3) >> 2));
+}
+// One lane's columns 4M .. 4M+3, output rows [Y0, Y1) (Y0 even). The main kernel passes
+// f1 = f2 = true (constants: the border taps compile out of its loop); k_convert_edge passes the
+// real flags for the border lanes.
+template <int K>
+__device__ __forceinline__ void lane_strip(const CPl& c1, const CPl& c2, const uint8_t* P0, int s0, int W,
+                                           const StreamOut& so, int M, bool f1, bool f2, int Y0, int Y1) {
+    constexpr bool KH = (K & 1) != 0, KV = (K & 2) != 0;
+    const int x0 = 4 * M;
+    const int nb = min(4, W - x0) * 3;
+    auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
+        uint8_t px[12];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
+        so.put(y, x0, px, nb);
+    };
+    auto luma = [&](int y) { return ld4(P0 + (int64_t)y * s0 + x0); };
+    if (K == 4) {  // gray: stride removal (jpeg_dec.h:854-865)
+#pragma unroll 4
+        for (int y = Y0; y < Y1; ++y) {
+            const uint32_t v = luma(y);
+            uint8_t* dst = so.o + (int64_t)y * W + x0;
+            if (so.vec && nb == 12) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(dst));
+            else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (3 * i < nb) dst[i] = (uint8_t)bt(v, i);
+            }
+        }
+        return;
+    }
+    // Software pipelining over a ring of kPD + 1 buffers, unrolled so every buffer index is a
+    // constant: the loads of the next kPD rows (row pairs) are in flight while the current one
+    // is computed; the scheduling barriers keep each buffer's reload after its last use so no
+    // in-flight value is copied.
+    if (!KV) {
+        auto fetch = [&](int y) {
+            Pre p{};
+            if (y < Y1) {
+                p.a = chroma_fetch<KH>(c1, y, M, f1);
+                p.e = chroma_fetch<KH>(c2, y, M, f2);
+                p.y0 = luma(y);
+            }
+            return p;
+        };
+        auto step = [&](int y, const Pre& p) {
+            emit(y, p.y0, chroma_make<KH>(c1, y, M, f1, p.a), chroma_make<KH>(c2, y, M, f2, p.e));
+        };
+        Pre B[kPD + 1];
+#pragma unroll
+        for (int u = 0; u < kPD; ++u) B[u] = fetch(Y0 + u);
+        for (int y = Y0; y < Y1; y += kPD + 1) {
+#pragma unroll
+            for (int u = 0; u <= kPD; ++u) {
+                if (y + u >= Y1) break;  // wave-uniform
+                B[(u + kPD) % (kPD + 1)] = fetch(y + u + kPD);
+                step(y + u, B[u]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        return;
+    }
+    rows_kv<KH>(c1, c2, M, f1, f2, Y0, Y1, luma, emit);
+}
+
+struct ConvImg {
+    CPl c1, c2;
+    const uint8_t* P0;
+    int s0;
+};
+__device__ __forceinline__ ConvImg conv_img(const Desc& d, const uint8_t* pslot, int K) {
+    ConvImg ci{};
+    ci.P0 = pslot;
+    ci.s0 = d.c[0].stride;
+    if (K != 4) {
+        ci.c1 = CPl{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
+        ci.c2 = CPl{pslot + comp_plane_off(d, 2), d.c[2].w, d.c[2].h, d.c[2].stride};
+    }
+    return ci;
+}
+
 template <int K>
 __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot, const StreamOut& so) {
-    constexpr bool KH = (K & 1) != 0, KV = (K & 2) != 0;
-    const int W = d.W, H = d.H, s0 = d.c[0].stride;
-    const uint8_t* P0 = pslot;
-    CPl c1{}, c2{};
-    if (K != 4) {
-        c1 = CPl{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
-        c2 = CPl{pslot + comp_plane_off(d, 2), d.c[2].w, d.c[2].h, d.c[2].stride};
-    }
+    constexpr bool KH = (K & 1) != 0;
+    const int W = d.W, H = d.H;
+    const ConvImg ci = conv_img(d, pslot, K);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nsx = (W + 255) >> 8, nsy = (H + kSH - 1) / kSH, nstrip = nsx * nsy;
+    const int ef = KH ? edge_from(ci.c1, ci.c2, W) : 0;
     for (int strip = blockIdx.x * 4 + wv; strip < nstrip; strip += gridDim.x * 4) {
         const int sy = strip / nsx, sx = strip - sy * nsx;
-        const int M = sx * 64 + lane, x0 = 4 * M;
-        if (x0 >= W) continue;
-        const int nb = min(4, W - x0) * 3;
-        const int Y0 = sy * kSH, Y1 = min(H, Y0 + kSH);
-        auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
-            uint8_t px[12];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
-            so.put(y, x0, px, nb);
-        };
-        auto luma = [&](int y) { return ld4(P0 + (int64_t)y * s0 + x0); };
-        if (K == 4) {  // gray: stride removal (jpeg_dec.h:854-865)
-#pragma unroll 4
-            for (int y = Y0; y < Y1; ++y) {
-                const uint32_t v = luma(y);
-                uint8_t* dst = so.o + (int64_t)y * W + x0;
-                if (so.vec && nb == 12) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(dst));
-                else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (3 * i < nb) dst[i] = (uint8_t)bt(v, i);
-                }
-            }
-            continue;
-        }
-        // interior horizontal taps for all 4 outputs, reads inside the row (chroma_make<true>)
-        const bool f1 = M >= 1 && x0 + 3 <= 2 * c1.w - 4 && 2 * M + 5 < c1.s;
-        const bool f2 = M >= 1 && x0 + 3 <= 2 * c2.w - 4 && 2 * M + 5 < c2.s;
-        // Software pipelining over a ring of kPD + 1 buffers, unrolled so every buffer index is a
-        // constant: the loads of the next kPD rows (row pairs) are in flight while the current one
-        // is computed; the scheduling barriers keep each buffer's reload after its last use so no
-        // in-flight value is copied.
-        if (!KV) {
-            auto fetch = [&](int y) {
-                Pre p{};
-                if (y < Y1) {
-                    p.a = chroma_fetch<KH>(c1, y, M, f1);
-                    p.e = chroma_fetch<KH>(c2, y, M, f2);
-                    p.y0 = luma(y);
-                }
-                return p;
-            };
-            auto step = [&](int y, const Pre& p) {
-                emit(y, p.y0, chroma_make<KH>(c1, y, M, f1, p.a), chroma_make<KH>(c2, y, M, f2, p.e));
-            };
-            Pre B[kPD + 1];
-#pragma unroll
-            for (int u = 0; u < kPD; ++u) B[u] = fetch(Y0 + u);
-            for (int y = Y0; y < Y1; y += kPD + 1) {
-#pragma unroll
-                for (int u = 0; u <= kPD; ++u) {
-                    if (y + u >= Y1) break;  // wave-uniform
-                    B[(u + kPD) % (kPD + 1)] = fetch(y + u + kPD);
-                    step(y + u, B[u]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            continue;
-        }
-        rows_kv<KH>(c1, c2, M, f1, f2, Y0, Y1, luma, emit);
+        const int M = sx * 64 + lane;
+        if (4 * M >= W) continue;
+        // horizontally doubled layouts: the border lanes are k_convert_edge's
+        if (KH && (M == 0 || M >= ef)) continue;
+        lane_strip<K>(ci.c1, ci.c2, ci.P0, ci.s0, W, so, M, true, true, sy * kSH, min(H, sy * kSH + kSH));
+    }
+}
+
+// The border lanes of the horizontally doubled layouts (4:2:2, 4:2:0): lane 0 and the lanes from
+// edge_from on, with the generic taps (double_tap, stride-end reads). One thread per (lane,
+// kSH-row strip); a wave's 64 threads all take the generic path, so it runs with full lanes
+// instead of as a divergent tail inside k_convert_stream's waves (which cost it 4.2 of 14.6 ms).
+constexpr int kSHE = 16;  // rows per edge item (even): short strips, so the few border lanes fill the chip
+template <int K>
+__global__ __launch_bounds__(256) void k_convert_edge(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
+                                                      int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride,
+                                                      int fuse) {
+    static_assert(K & 1, "horizontally doubled layouts only");
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (d.status != kOk || stream_kind(d) != K || (K == 3 && fuse == 1 && fused420(d))) return;
+    const uint8_t* pslot = planes + (int64_t)img * plane_cap;
+    uint8_t* o = out + (int64_t)img * out_stride;
+    const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
+    const int W = d.W, H = d.H;
+    const ConvImg ci = conv_img(d, pslot, K);
+    const int nl = (W + 3) >> 2, ef = edge_from(ci.c1, ci.c2, W);
+    const int ne = 1 + max(0, nl - ef);  // lane 0, then lanes ef .. nl-1
+    const int nsy = (H + kSHE - 1) / kSHE, items = ne * nsy;
+    for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < items; it += gridDim.x * blockDim.x) {
+        const int sy = it / ne, e = it - sy * ne;
+        const int M = e == 0 ? 0 : ef + e - 1;
+        lane_strip<K>(ci.c1, ci.c2, ci.P0, ci.s0, W, so, M, interior_taps(ci.c1, M), interior_taps(ci.c2, M), sy * kSHE,
+                      min(H, sy * kSHE + kSHE));
     }
 }
 
@@ -1391,6 +1451,12 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     hipLaunchKernelGGL(k_convert_stream<2>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
     hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride, fuse);
+    // border lanes of the doubled layouts: ~3 lanes x (H / kSHE) strips per image
+    const int egx = (int)std::max<int64_t>(1, std::min<int64_t>((4 * ((ws.max_h + kSHE - 1) / kSHE) + 255) / 256, 16384 / n));
+    hipLaunchKernelGGL(k_convert_edge<3>, dim3(egx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride, fuse);
+    hipLaunchKernelGGL(k_convert_edge<1>, dim3(egx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
     hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride);
