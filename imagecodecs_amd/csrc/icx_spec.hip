@@ -690,50 +690,58 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         // coefficient store and prefetch in flight -- on every DC code.
         asm volatile("" : "+v"(pred[0]), "+v"(pred[1]), "+v"(pred[2]));
         r.phase();  // the prelude above ran a lane-dependent number of lookups
+#ifdef ICX_EXP_CYC  // timing experiment only: per-wave loop cycles and iterations (printf)
+        const uint64_t cyc0 = clock64();
+        int it_w = 0;
+#endif
         // Wave-uniform loop: one lookup (one symbol or a pair) per active lane per iteration,
         // then the wave flushes the blocks its lanes completed together -- eight 128-byte blocks
         // per round, each lane moving one 16-byte chunk LDS -> HBM and zeroing it (coalesced
         // full-line stores, no divergent per-lane flush).
         while (__any(act)) {
+#ifdef ICX_EXP_CYC
+            ++it_w;
+#endif
             // The reader advances on every lane, active or not (an idle lane decodes harmless
             // garbage; its loads are clamped to U): keeping Reader updates out of divergent
             // branches stops the compiler from routing the in-flight chunk through loop-header
             // copies, which made every iteration wait for the newest load and all stores.
             const bool dc = z == 0;
-            if (dc) {  // a block starts: stop at the next lane's territory
-                if (r.used >= lim_rel) act = false;
-                ci = S.comp(b);
-            }
+            // a block starts: stop at the next lane's territory
+            act = act && !(dc && r.used >= lim_rel);
+            ci = dc ? S.comp(b) : ci;
             // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644); a second
             // symbol is only paired when its own peek stays clear of the error byte
             const uint32_t u0 = r.used;
-            const bool peek_bad = u0 + 16 > err_rel;
+            const int z0 = z;
             const WriteOut o = write_step(r, T, H, S, b, z, u0 + 16 + WriteTab::kAcBits > err_rel);
-            bool done = false;
-            int64_t bdone = 0;
-            if (act) {
-                if (peek_bad || o.err || r.used > err_rel) {
-                    bad = true;
-                    act = false;
-                } else {
-                    int32_t v1 = o.v1;
-                    if (dc) {
-                        pred[ci] = wadd(pred[ci], v1);
-                        v1 = dc_cell(pred[ci]);
-                        if (v1 == kDcEscape) D[bi] = pred[ci];
-                    }
-                    // zig-zag order (k_idct reorders); an error ends the lane before its slot
-                    // could be misused, so the positions are only masked into the slot
-                    if (o.w1) sv[slot_elem(threadIdx.x, o.c1 & 63)] = (int16_t)v1;
-                    if (o.w2) sv[slot_elem(threadIdx.x, o.c2 & 63)] = (int16_t)o.v2;
-                    if (z == 0) {
-                        done = true;
-                        bdone = bi++;
-                        act = bi < bend;
-                        used_end = r.used;  // (the reader keeps moving once the lane is idle)
-                    }
-                }
-            }
+            // Bookkeeping by selects, not per-lane branches (each divergent `if` cost its exec-mask
+            // save / restore and a branch in every iteration).
+            const bool fail = u0 + 16 > err_rel || o.err || r.used > err_rel;
+            bad = bad || (act && fail);
+            const bool ok = act && !fail;
+            const bool okdc = ok && dc;
+            const int32_t pc = wadd(ci == 0 ? pred[0] : (ci == 1 ? pred[1] : pred[2]), o.v1);
+            pred[0] = okdc && ci == 0 ? pc : pred[0];
+            pred[1] = okdc && ci == 1 ? pc : pred[1];
+            pred[2] = okdc && ci == 2 ? pc : pred[2];
+            const int32_t cell = dc_cell(pc);
+            if (okdc && cell == kDcEscape) D[bi] = pc;  // DC outside int16 (corrupt streams only)
+            // Both slot writes always issue (zig-zag order; k_idct reorders). A symbol that writes
+            // nothing stores 0 at a coefficient the block has not reached: the cursor z0 (EOB), or
+            // the one after the first symbol (no pair) -- which is that symbol's own cell when it
+            // was coefficient 63, so the pair's cell is written first and the first symbol's
+            // value lands last. A lane that stopped scribbles in its own slot, which is zeroed
+            // before its next use.
+            const int n1 = o.w1 ? (o.c1 & 63) : min(z0, 63);
+            const int n2 = o.w2 ? (o.c2 & 63) : (o.w1 ? min(o.c1 + 1, 63) : min(z0, 63));
+            sv[slot_elem(threadIdx.x, n2)] = (int16_t)(o.w2 ? o.v2 : 0);
+            sv[slot_elem(threadIdx.x, n1)] = (int16_t)(o.w1 ? (dc ? cell : o.v1) : 0);
+            const bool done = ok && z == 0;
+            const int64_t bdone = bi;
+            bi += done ? 1 : 0;
+            act = ok && (!done || bi < bend);
+            used_end = done ? r.used : used_end;  // (the reader keeps moving once the lane is idle)
             const uint64_t m = __ballot(done);
             if (m) {  // wave-uniform; every lane takes part
                 if (done) {
@@ -765,11 +773,15 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
                 __builtin_amdgcn_wave_barrier();
             }
         }
-        if (bad) {
-            atomicOr(&s.err, kSpecSyntax);
+#ifdef ICX_EXP_CYC
+        if (lane == 0 && blockIdx.x % 64 == 0 && wg == (int)blockIdx.x && wave < 2)
+            printf("CYC wg %d wave %d iters %d per_iter %llu\n", wg, wave, it_w,
+                   (unsigned long long)((clock64() - cyc0) / max(1, it_w)));
+#endif
+        if (bad) atomicOr(&s.err, kSpecSyntax);
+        // stopped lanes scribbled in their slots: zero them for the next workgroup item
 #pragma unroll
-            for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
-        }
+        for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
         if (dri && j < s.nsub) {
             // NanoJPEG after R MCUs: byte-align, read 16 bits = FF D0+(j&7) (jpeg_dec.h:707-715).
             // The parallel result stands only if that is exactly marker j at the aligned end of

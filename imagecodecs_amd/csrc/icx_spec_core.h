@@ -99,8 +99,8 @@ ICX_HD Ustf16 ustf16(const uint8_t* R, int64_t L, int64_t a, const uint32_t (&D)
             const uint32_t w = D[k];
             const uint32_t f = ((w & 0x7F7F7F7Fu) + 0x01010101u) & w & 0x80808080u;     // byte == FF
             const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;  // byte == 00
-            ffm |= ((f >> 7) & 1u | (f >> 14) & 2u | (f >> 21) & 4u | (f >> 28) & 8u) << (4 * k);
-            zm |= ((z >> 7) & 1u | (z >> 14) & 2u | (z >> 21) & 4u | (z >> 28) & 8u) << (4 * k);
+            ffm |= (((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u)) << (4 * k);
+            zm |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
         }
         // a carried byte 0 is no FF of its own; 00 / FF there are dropped (an RSTn byte is kept;
         // anything else ended the data in the previous chunk, and this chunk is not counted)

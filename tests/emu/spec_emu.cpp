@@ -420,3 +420,51 @@ extern "C" int64_t emu_unstuff_sh(const uint8_t* file, int64_t size, int sh, uin
     std::memcpy(out, U.data(), (size_t)ulen);
     return ulen;
 }
+
+extern "C" {
+// Write-pass study (tuning aid): decode the whole scan with write_step and report, for a wave of
+// 64 lanes that each take 1/64 of the lookups in lockstep, out[0] lookups, out[1] lookups that
+// needed the long-code pool (SUB), out[2] wave iterations, out[3] iterations where some lane
+// needed the pool, out[4] iterations where some lane completed a block, out[5] blocks.
+int emu_write_study(const uint8_t* file, int64_t size, int64_t* out) {
+    auto dp = std::make_unique<Desc>();
+    Desc& d = *dp;
+    if (parse_headers(file, size, d) != kPending || d.restart || d.bpm > kSpecMaxBpm) return -1;
+    const uint8_t* R = file + d.scan_off;
+    std::vector<uint8_t> U;
+    int64_t errpos; int32_t gu = 0;
+    const int64_t ulen = emu_unstuff(R, d.size - d.scan_off, ustf_align(R), U, errpos, gu, nullptr);
+    auto SSp = std::make_unique<StepSet>();
+    for (int k = 0; k < WriteTab::entries(); ++k) SSp->write.fill(d.huff, k);
+    const WriteTab& TW = SSp->write;
+    const Sel SL = make_sel(d);
+    std::vector<uint8_t> ev;  // per lookup: bit0 SUB, bit1 block completed
+    Reader r; r.init(U.data(), ulen, 0);
+    int b = 0, z = 0;
+    const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
+    int64_t blocks = 0;
+    while (blocks < total) {
+        const bool dc = z == 0;
+        r.refill();  // (write_step refills again: harmless for the peek below)
+        const uint32_t e = TW.look(SL.tab(b, dc), (uint32_t)(r.buf >> 32));
+        (void)write_step(r, TW, d.huff, SL, b, z, false);
+        const bool done = z == 0;
+        blocks += done;
+        ev.push_back((uint8_t)(((e & kStSlow) ? 1 : 0) | (done ? 2 : 0)));
+    }
+    const int64_t n = (int64_t)ev.size(), per = (n + 63) / 64;
+    int64_t nsub = 0, it_sub = 0, it_done = 0;
+    for (uint8_t v : ev) nsub += v & 1;
+    for (int64_t i = 0; i < per; ++i) {
+        int any_s = 0, any_d = 0;
+        for (int l = 0; l < 64; ++l) {
+            const int64_t k = l * per + i;
+            if (k < n) { any_s |= ev[k] & 1; any_d |= (ev[k] >> 1) & 1; }
+        }
+        it_sub += any_s;
+        it_done += any_d;
+    }
+    out[0] = n; out[1] = nsub; out[2] = per; out[3] = it_sub; out[4] = it_done; out[5] = blocks;
+    return 0;
+}
+}
