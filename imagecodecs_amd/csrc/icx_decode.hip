@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void k_idct_any(const Desc* __restrict__ desc,
     __syncthreads();
     const uint32_t nblocks = (uint32_t)((int64_t)d.mbw * d.mbh * bpm);
     const uint32_t noct = (nblocks + 7) >> 3;
-    const int wave = t >> 6, lane = t & 63, lb = lane >> 3, r = lane & 7;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, lb = lane >> 3, r = lane & 7;
     // natural row r = zig-zag positions kZigOfNat[8r .. 8r+7] of the staged block (byte offsets)
     uint32_t zo[8];
 #pragma unroll
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
         bgeo[t] = (uint32_t)ci | (uint32_t)(roff[ci] + sby * 8 * wc + m * d.c[ci].hs * 8 + sbx * 8) << 2;
     }
     __syncthreads();
-    const int wave = t >> 6, lane = t & 63, lb = lane >> 3, r = lane & 7;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, lb = lane >> 3, r = lane & 7;
     uint32_t zo[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) zo[j] = 2u * kZigOfNat[r * 8 + j];
@@ -702,6 +702,11 @@ __global__ __launch_bounds__(256) void k_convert_fused(const Desc* __restrict__ 
 }
 
 
+// Wave index as a wave-uniform (SGPR) value: threadIdx.x >> 6 is uniform per wave, but the
+// compiler's divergence analysis cannot see it, so loops and branches on values derived from it
+// were compiled as divergent -- loads under exec masks, and an s_waitcnt vmcnt(0) at every join.
+__device__ __forceinline__ int wave_index() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 // ------------------------------------------------------------ streaming upsample + convert
 // The common layouts -- gray, and 3 components whose luma is full size and whose two chroma
 // components take the same doubling program (4:4:4, 4:2:2, 4:4:0, 4:2:0) -- are converted by
@@ -890,15 +895,15 @@ __device__ __forceinline__ void kv_rows(KvWin& w, const CPl& c1, const CPl& c2, 
     const int k0 = Y0 >> 1;
     auto cr1 = [&](int r) { return min(max(r, 0), c1.h - 1); };
     auto cr2 = [&](int r) { return min(max(r, 0), c2.h - 1); };
-    // data of row pair k: chroma row k+2, luma rows 2k and 2k+1
+    // data of row pair k: chroma row k+2, luma rows 2k and 2k+1. Unconditional loads (rows past
+    // the strip re-read its last row): a conditional fetch zero-initialised its registers, and
+    // that write had to wait for every load in flight (vmcnt(0)).
     auto fetch = [&](int k) {
-        Pre p{};
-        if (2 * k < Y1) {
-            p.a = chroma_fetch<KH>(c1, cr1(k + 2), M, f1);
-            p.e = chroma_fetch<KH>(c2, cr2(k + 2), M, f2);
-            p.y0 = luma(2 * k);
-            if (2 * k + 1 < Y1) p.y1 = luma(2 * k + 1);
-        }
+        Pre p;
+        p.a = chroma_fetch<KH>(c1, cr1(k + 2), M, f1);
+        p.e = chroma_fetch<KH>(c2, cr2(k + 2), M, f2);
+        p.y0 = luma(min(2 * k, Y1 - 1));
+        p.y1 = luma(min(2 * k + 1, Y1 - 1));
         return p;
     };
     // E = rows k-2..k+1 (even output 2k: kTapRev), O = rows k-1..k+2 (odd 2k+1: kTapFwd);
@@ -964,17 +969,24 @@ __device__ __forceinline__ int edge_from(const CPl& c1, const CPl& c2, int W) {
 }
 // One lane's columns 4M .. 4M+3, output rows [Y0, Y1) (Y0 even). The main kernel passes
 // f1 = f2 = true (constants: the border taps compile out of its loop); k_convert_edge passes the
-// real flags for the border lanes.
+// real flags for the border lanes. A lane that is not `live` runs along (with an in-range M) and
+// stores nothing, so the wave's loop has no per-lane exit.
 template <int K>
 __device__ __forceinline__ void lane_strip(const CPl& c1, const CPl& c2, const uint8_t* P0, int s0, int W,
-                                           const StreamOut& so, int M, bool f1, bool f2, int Y0, int Y1) {
+                                           const StreamOut& so, int M, bool f1, bool f2, int Y0, int Y1,
+                                           bool live = true) {
     constexpr bool KH = (K & 1) != 0, KV = (K & 2) != 0;
     const int x0 = 4 * M;
-    const int nb = min(4, W - x0) * 3;
+    const int nb = live ? min(4, W - x0) * 3 : 0;
     auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
         uint8_t px[12];
+#ifdef ICX_EXP_NOCOLOR  // timing experiment only: no colour conversion (wrong pixels)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { px[3 * i] = bt(yv, i); px[3 * i + 1] = bt(cb, i); px[3 * i + 2] = bt(cr, i); }
+#else
 #pragma unroll
         for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
+#endif
         so.put(y, x0, px, nb);
     };
     auto luma = [&](int y) { return ld4(P0 + (int64_t)y * s0 + x0); };
@@ -997,13 +1009,13 @@ __device__ __forceinline__ void lane_strip(const CPl& c1, const CPl& c2, const u
     // is computed; the scheduling barriers keep each buffer's reload after its last use so no
     // in-flight value is copied.
     if (!KV) {
-        auto fetch = [&](int y) {
-            Pre p{};
-            if (y < Y1) {
-                p.a = chroma_fetch<KH>(c1, y, M, f1);
-                p.e = chroma_fetch<KH>(c2, y, M, f2);
-                p.y0 = luma(y);
-            }
+        auto fetch = [&](int y) {  // unconditional (see kv_rows): rows past the strip re-read its last
+            Pre p;
+            const int yc = min(y, Y1 - 1);
+            p.a = chroma_fetch<KH>(c1, yc, M, f1);
+            p.e = chroma_fetch<KH>(c2, yc, M, f2);
+            p.y0 = luma(yc);
+            p.y1 = 0;
             return p;
         };
         auto step = [&](int y, const Pre& p) {
@@ -1047,16 +1059,18 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
     constexpr bool KH = (K & 1) != 0;
     const int W = d.W, H = d.H;
     const ConvImg ci = conv_img(d, pslot, K);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = wave_index();
     const int nsx = (W + 255) >> 8, nsy = (H + kSH - 1) / kSH, nstrip = nsx * nsy;
-    const int ef = KH ? edge_from(ci.c1, ci.c2, W) : 0;
-    for (int strip = blockIdx.x * 4 + wv; strip < nstrip; strip += gridDim.x * 4) {
+    const int nl = (W + 3) >> 2;                      // lanes (4 columns each) of a row
+    const int ef = KH ? edge_from(ci.c1, ci.c2, W) : nl;  // border lanes are k_convert_edge's
+    const int m0 = KH ? 1 : 0;
+    if (ef <= m0) return;  // every lane a border lane
+    for (int strip = blockIdx.x * 4 + wv; strip < nstrip; strip += gridDim.x * 4) {  // wave-uniform
         const int sy = strip / nsx, sx = strip - sy * nsx;
         const int M = sx * 64 + lane;
-        if (4 * M >= W) continue;
-        // horizontally doubled layouts: the border lanes are k_convert_edge's
-        if (KH && (M == 0 || M >= ef)) continue;
-        lane_strip<K>(ci.c1, ci.c2, ci.P0, ci.s0, W, so, M, true, true, sy * kSH, min(H, sy * kSH + kSH));
+        const bool live = M >= m0 && M < ef;
+        lane_strip<K>(ci.c1, ci.c2, ci.P0, ci.s0, W, so, min(max(M, m0), ef - 1), true, true, sy * kSH,
+                      min(H, sy * kSH + kSH), live);
     }
 }
 
@@ -1186,6 +1200,14 @@ __device__ __forceinline__ void pair_idct(const int4 (&c)[8], const uint32_t (&q
         }
     }
 }
+// A dequant table (64 bytes of Desc::q, 4-byte aligned) into registers straight from global
+// memory: the lane-pair IDCT kernels then use no LDS at all, so they can run beside the other
+// pipeline's LDS-bound entropy kernels.
+__device__ __forceinline__ void load_qw_g(const uint8_t* q, uint32_t (&qw)[16]) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(q);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) qw[k] = p[k];
+}
 __device__ __forceinline__ void load_qw(const uint8_t* qz, uint32_t (&qw)[16]) {  // 64 bytes of LDS, 16-byte aligned
     const uint4* qs = reinterpret_cast<const uint4*>(qz);
 #pragma unroll
@@ -1209,13 +1231,13 @@ __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc,
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     if (!fused420(d)) return;
-    __shared__ __attribute__((aligned(16))) uint8_t qz[2][64];
     const int t = threadIdx.x;
-    if (t < 128) qz[t >> 6][t & 63] = d.q[d.c[1 + (t >> 6)].tq][t & 63];
-    __syncthreads();
-    const int wave = t >> 6, lane = t & 63, q = lane >> 1, h = lane & 1, cc = q >> 4, mq = q & 15;
-    uint32_t qw[16];
-    load_qw(qz[cc], qw);
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, q = lane >> 1, h = lane & 1, cc = q >> 4, mq = q & 15;
+    uint32_t qw[16], qb[16];
+    load_qw_g(d.q[d.c[1].tq], qw);
+    load_qw_g(d.q[d.c[2].tq], qb);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) qw[k] = cc ? qb[k] : qw[k];
     const int mbw = d.mbw, stride = d.c[1].stride;
     const int16_t* A = ac + (int64_t)img * coef_cap * 64;
     const int32_t* D = dcv + (int64_t)img * coef_cap;
@@ -1250,15 +1272,12 @@ __global__ __launch_bounds__(256) void k_idct420y(const Desc* __restrict__ desc,
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     if (!fused420(d)) return;
-    __shared__ __attribute__((aligned(16))) uint8_t qz[64];
     const int t = threadIdx.x;
-    if (t < 64) qz[t] = d.q[d.c[0].tq][t];
-    __syncthreads();
-    const int wave = t >> 6, lane = t & 63, q = lane >> 1, h = lane & 1, mq = q >> 2, k = q & 3;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, q = lane >> 1, h = lane & 1, mq = q >> 2, k = q & 3;
     int sbx, sby;
     (void)mcu_block_comp(d, k, sbx, sby);
     uint32_t qw[16];
-    load_qw(qz, qw);
+    load_qw_g(d.q[d.c[0].tq], qw);
     const int mbw = d.mbw, stride = d.c[0].stride;
     const int16_t* A = ac + (int64_t)img * coef_cap * 64;
     const int32_t* D = dcv + (int64_t)img * coef_cap;
@@ -1305,7 +1324,7 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
     const int t = threadIdx.x;
     if (t < 64) qz[t] = d.q[d.c[0].tq][t];
     __syncthreads();
-    const int wave = t >> 6, lane = t & 63, h = lane & 1, k = (lane >> 1) & 3;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, h = lane & 1, k = (lane >> 1) & 3;
     uint32_t (*Yl)[64] = Yl_all[wave];
     int sbx, sby;
     (void)mcu_block_comp(d, k, sbx, sby);
@@ -1411,10 +1430,12 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     // slower beside the second pipeline: DESIGN.md §4); mode 0 leaves them to k_idct. ICX_FUSE420
     // overrides the mode (tests, experiments).
     const int fuse = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 2;
+#ifndef ICX_EXP_ONLY420  // timing experiment only: the 4:2:0 kernels alone (other samplings undecoded)
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap, fuse);
     hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap);
+#endif
     if (fuse) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
         const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;
         hipLaunchKernelGGL(k_idct420c, dim3(std::max(cgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes,
@@ -1428,9 +1449,11 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     E(kStIdct);
     B(kStUpsample);
     const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, 16384 / (3 * n)));
+#ifndef ICX_EXP_ONLY420
     for (int p = 0; p < 6; ++p)
         hipLaunchKernelGGL(k_upsample, dim3(ux, n * 3), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
                            ws.tmp_cap, p);
+#endif
     E(kStUpsample);
     B(kStConvert);
     const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 16384 / n));
@@ -1444,6 +1467,7 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     if (fuse == 1)
         hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                            ws.plane_cap, d_out, out_stride);
+#ifndef ICX_EXP_ONLY420
     hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
     hipLaunchKernelGGL(k_convert_stream<1>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
@@ -1452,16 +1476,19 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
                        out_stride, fuse);
     hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
+#endif
     // border lanes of the doubled layouts: ~3 lanes x (H / kSHE) strips per image
     const int egx = (int)std::max<int64_t>(1, std::min<int64_t>((4 * ((ws.max_h + kSHE - 1) / kSHE) + 255) / 256, 16384 / n));
     hipLaunchKernelGGL(k_convert_edge<3>, dim3(egx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
+#ifndef ICX_EXP_ONLY420
     hipLaunchKernelGGL(k_convert_edge<1>, dim3(egx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
     hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride);
     hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
                        ws.tmp_cap, d_out, out_stride);
+#endif
     hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(tb), 0, st, n, ws.desc, d_status, d_dims);
     E(kStConvert);
 }

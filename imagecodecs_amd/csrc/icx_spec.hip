@@ -607,7 +607,7 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
 // stores when it ends (scattered 2-byte global stores amplified HBM writes ~10x).
 // 128-byte lane slot; 16-byte chunk q of lane t lives at chunk q ^ (t & 7), so the b128 reads
 // of a 16-lane group hit distinct banks.
-__device__ __forceinline__ int slot_elem(int t, int n) { return (((n >> 3) ^ (t & 7)) << 3) | (n & 7); }
+__device__ __forceinline__ int slot_elem(int t, int n) { return n ^ ((t & 7) << 3); }  // = (n/8 ^ t%8)*8 + n%8
 
 // NL lanes per workgroup; `wpre` numbers the image's lanes in NL-lane groups (wgpre for 256,
 // wg2pre for kWriteLanesBig), `total` = totals[1] or totals[2].
