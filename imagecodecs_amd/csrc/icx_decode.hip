@@ -820,10 +820,52 @@ __device__ __forceinline__ uint32_t vtap_odd(int k, int h, uint32_t w1, uint32_t
     return pmap([&](int i) { return tap4(bt(w1, i), bt(w2, i), bt(w3, i), bt(w4, i)); });
 }
 
+// YCbCr -> RGB of a lane's 4 pixels (jpeg_dec.h:834-853, ycc_to_rgb) as three dwords of packed
+// RGB. Each channel is one or two v_dot2 on 16-bit pairs: (Y, cb) and (Y, cr) per pixel, with
+// the -128 offsets folded into the constant, e.g. R = 256*Y + 359*cr + (128 - 359*128) =
+// (Y << 8) + 359*(cr - 128) + 128. Clamping the numerator to [0, 65535] and taking its byte 1
+// equals clip8(numerator >> 8), so no shift is needed.
+typedef short icx_short2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ icx_short2 as_s2(uint32_t v) { return __builtin_bit_cast(icx_short2, v); }
+__device__ __forceinline__ void ycc4_to_rgb(uint32_t yv, uint32_t cb, uint32_t cr, uint32_t (&w)[3]) {
+    const icx_short2 kR = {256, 359}, kG1 = {256, -88}, kG2 = {0, -183}, kB = {256, 454};
+    uint32_t R[4], G[4], B[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t sel = (uint32_t)i | (0x0cu << 8) | ((uint32_t)(4 + i) << 16) | (0x0cu << 24);
+        const icx_short2 yb = as_s2(__builtin_amdgcn_perm(cb, yv, sel));  // (Y_i, cb_i)
+        const icx_short2 yr = as_s2(__builtin_amdgcn_perm(cr, yv, sel));  // (Y_i, cr_i)
+        const int rn = __builtin_amdgcn_sdot2(yr, kR, 128 - 359 * 128, false);
+        const int gn = __builtin_amdgcn_sdot2(yr, kG2, __builtin_amdgcn_sdot2(yb, kG1, 128 + (88 + 183) * 128, false), false);
+        const int bn = __builtin_amdgcn_sdot2(yb, kB, 128 - 454 * 128, false);
+        R[i] = (uint32_t)min(max(rn, 0), 65535);
+        G[i] = (uint32_t)min(max(gn, 0), 65535);
+        B[i] = (uint32_t)min(max(bn, 0), 65535);
+    }
+    // byte 1 of each: [R0 G0 B0 R1] [G1 B1 R2 G2] [B2 R3 G3 B3]
+    auto two = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x0c0c0501u); };  // (lo.b1, hi.b1)
+    auto cat = [](uint32_t lo2, uint32_t hi2) { return __builtin_amdgcn_perm(hi2, lo2, 0x05040100u); };
+    w[0] = cat(two(R[0], G[0]), two(B[0], R[1]));
+    w[1] = cat(two(G[1], B[1]), two(R[2], G[2]));
+    w[2] = cat(two(B[2], R[3]), two(G[3], B[3]));
+}
+
 struct StreamOut {
     uint8_t* o;
     int W;
     bool vec;  // rows 4-byte aligned
+    __device__ __forceinline__ void put3(int y, int x0, const uint32_t (&w)[3], int nb) const {
+        uint8_t* dst = o + ((int64_t)y * W + x0) * 3;
+        if (vec && nb == 12) {
+            typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+            const u32x3 v = {w[0], w[1], w[2]};
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x3*>(dst));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 12; ++i)
+                if (i < nb) dst[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        }
+    }
     __device__ __forceinline__ void put(int y, int x0, const uint8_t (&px)[12], int nb) const {
         uint8_t* dst = o + ((int64_t)y * W + x0) * 3;
         if (vec && nb == 12) {
@@ -979,15 +1021,9 @@ __device__ __forceinline__ void lane_strip(const CPl& c1, const CPl& c2, const u
     const int x0 = 4 * M;
     const int nb = live ? min(4, W - x0) * 3 : 0;
     auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
-        uint8_t px[12];
-#ifdef ICX_EXP_NOCOLOR  // timing experiment only: no colour conversion (wrong pixels)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { px[3 * i] = bt(yv, i); px[3 * i + 1] = bt(cb, i); px[3 * i + 2] = bt(cr, i); }
-#else
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
-#endif
-        so.put(y, x0, px, nb);
+        uint32_t w[3];
+        ycc4_to_rgb(yv, cb, cr, w);
+        so.put3(y, x0, w, nb);
     };
     auto luma = [&](int y) { return ld4(P0 + (int64_t)y * s0 + x0); };
     if (K == 4) {  // gray: stride removal (jpeg_dec.h:854-865)

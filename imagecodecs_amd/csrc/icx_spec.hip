@@ -144,7 +144,10 @@ struct TileRange {
     int t, t1, i;
 };
 __device__ __forceinline__ TileRange wave_tiles(const int32_t* tilepre, int n, int total) {
-    const int nw = gridDim.x * (blockDim.x >> 6), w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // w as a wave-uniform value (readfirstlane): derived from threadIdx.x, the compiler would
+    // treat the tile loops as divergent (exec-masked loads, vmcnt(0) at every join)
+    const int nw = gridDim.x * (blockDim.x >> 6),
+              w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int per = (total + nw - 1) / nw;
     TileRange r;
     r.t = min(total, w * per);
@@ -624,7 +627,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
     __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
     int cur = -1;
     const int total = totals[NL == kLanes ? 1 : 2];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int4* slot = &slots[threadIdx.x][0];
     int16_t* sv = reinterpret_cast<int16_t*>(slot);
 #pragma unroll
