@@ -866,21 +866,6 @@ struct StreamOut {
                 if (i < nb) dst[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
         }
     }
-    __device__ __forceinline__ void put(int y, int x0, const uint8_t (&px)[12], int nb) const {
-        uint8_t* dst = o + ((int64_t)y * W + x0) * 3;
-        if (vec && nb == 12) {
-            // one 12-byte store per lane (global_store_dwordx3): a wave writes 768 contiguous bytes
-            // per instruction instead of three strided dword passes over them
-            typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
-            u32x3 w;
-            __builtin_memcpy(&w, px, 12);
-            __builtin_nontemporal_store(w, reinterpret_cast<u32x3*>(dst));
-        } else {
-#pragma unroll
-            for (int i = 0; i < 12; ++i)
-                if (i < nb) dst[i] = px[i];
-        }
-    }
 };
 
 // Data of one row (or row pair): the chroma loads of both components and the luma dwords.
@@ -1258,6 +1243,39 @@ __device__ __forceinline__ void load_block(const int16_t* A, int64_t n, int4 (&c
     for (int k = 0; k < 8; ++k) c[k] = src[k];
 }
 
+// A wave's units wid, wid + nw, ... (wave-uniform loop): unit u's coefficient block is blk(u),
+// transformed and stored by unit(u, c). ICX_IDCT_PF: the next unit's block is loaded while the
+// current one is transformed (two register sets, the loop unrolled by two so neither is copied).
+#ifndef ICX_IDCT_PF  // measured: no gain (4:2:0 luma 6.12 -> 6.26 ms; 125 VGPRs, 4 waves/SIMD)
+#define ICX_IDCT_PF 0
+#endif
+template <class BlkF, class UnitF>
+__device__ __forceinline__ void idct_units(const int16_t* A, uint32_t wid, uint32_t nw, uint32_t nunits, BlkF blk,
+                                           UnitF unit) {
+#if ICX_IDCT_PF
+    if (wid >= nunits) return;
+    const uint32_t ulast = nunits - 1;
+    int4 c0[8], c1[8];
+    load_block(A, blk(wid), c0);
+    for (uint32_t u = wid;;) {
+        load_block(A, blk(min(u + nw, ulast)), c1);  // (past the end: a harmless reload)
+        unit(u, c0);
+        u += nw;
+        if (u >= nunits) break;
+        load_block(A, blk(min(u + nw, ulast)), c0);
+        unit(u, c1);
+        u += nw;
+        if (u >= nunits) break;
+    }
+#else
+    for (uint32_t u = wid; u < nunits; u += nw) {
+        int4 c[8];
+        load_block(A, blk(u), c);
+        unit(u, c);
+    }
+#endif
+}
+
 // Chroma planes of fused420 images: a wave's unit is 16 MCUs of one MCU row; lane pair q < 16
 // takes Cb of MCU mx0 + q, q >= 16 Cr of MCU mx0 + q - 16, so each plane row of the unit is
 // 128 contiguous bytes written by one store instruction.
@@ -1281,21 +1299,23 @@ __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc,
     const uint32_t ucols = (uint32_t)((mbw + 15) >> 4), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
-    for (uint32_t u = wid; u < nunits; u += nw) {
+    auto blk = [&](uint32_t u) {
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 4) + mq;
-        const bool live = mx < mbw;
-        const int64_t n = ((int64_t)mby * mbw + (live ? mx : mbw - 1)) * 6 + 4 + cc;
-        int4 c[8];
-        load_block(A, n, c);
+        return ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + 4 + cc;
+    };
+    auto unit = [&](uint32_t u, const int4 (&c)[8]) {
+        const uint32_t mby = u / ucols;
+        const int mx = (int)((u - mby * ucols) << 4) + mq;
         uint32_t rowd[8];
-        pair_idct(c, qw, h, D, n, rowd);
-        if (live) {
+        pair_idct(c, qw, h, D, blk(u), rowd);
+        if (mx < mbw) {
             uint8_t* dst = Pc + (int64_t)mby * 8 * stride + mx * 8 + 4 * h;
 #pragma unroll
             for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
         }
-    }
+    };
+    idct_units(A, wid, nw, nunits, blk, unit);
 }
 
 // Luma planes of fused420 images when the conversion reads them from HBM (ICX_FUSE420 = 2): a
@@ -1321,21 +1341,23 @@ __global__ __launch_bounds__(256) void k_idct420y(const Desc* __restrict__ desc,
     const uint32_t ucols = (uint32_t)((mbw + 7) >> 3), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
-    for (uint32_t u = wid; u < nunits; u += nw) {
+    auto blk = [&](uint32_t u) {
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 3) + mq;
-        const bool live = mx < mbw;
-        const int64_t n = ((int64_t)mby * mbw + (live ? mx : mbw - 1)) * 6 + k;
-        int4 c[8];
-        load_block(A, n, c);
+        return ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + k;
+    };
+    auto unit = [&](uint32_t u, const int4 (&c)[8]) {
+        const uint32_t mby = u / ucols;
+        const int mx = (int)((u - mby * ucols) << 3) + mq;
         uint32_t rowd[8];
-        pair_idct(c, qw, h, D, n, rowd);
-        if (live) {
+        pair_idct(c, qw, h, D, blk(u), rowd);
+        if (mx < mbw) {
             uint8_t* dst = Py + ((int64_t)mby * 16 + sby * 8) * stride + mx * 16 + sbx * 8 + 4 * h;
 #pragma unroll
             for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
         }
-    }
+    };
+    idct_units(A, wid, nw, nunits, blk, unit);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
@@ -1406,10 +1428,9 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
             if (xl) {
                 auto luma = [&](int y) { return Yl[y - Y0][lane]; };
                 auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
-                    uint8_t px[12];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) ycc_to_rgb(bt(yv, i), bt(cb, i), bt(cr, i), &px[3 * i]);
-                    so.put(y, x0, px, nb);
+                    uint32_t w[3];
+                    ycc4_to_rgb(yv, cb, cr, w);
+                    so.put3(y, x0, w, nb);
                 };
                 kv_rows<true>(w, c1, c2, M, f1, f2, Y0, Y1, luma, emit);
             }
