@@ -441,6 +441,11 @@ __global__ __launch_bounds__(256) void k_step_tabs(int n, const Desc* __restrict
     StepSet& S = steps[i];
     for (int k = threadIdx.x; k < ScanTab::entries(); k += blockDim.x) S.scan.fill(h, k);
     for (int k = threadIdx.x; k < WriteTab::entries(); k += blockDim.x) S.write.fill(h, k);
+    if (threadIdx.x == 0) {
+        const Sel sel = make_sel(desc[i]);
+        set_block_sel(S.scan, h, sel);
+        set_block_sel(S.write, h, sel);
+    }
 }
 
 template <class Tab>

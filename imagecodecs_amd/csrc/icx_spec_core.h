@@ -340,18 +340,32 @@ ICX_HD int32_t extend_mag(uint32_t raw, uint32_t nbx) {
     return (int32_t)(raw <= (mask >> 1) ? raw - mask : raw);
 }
 
-// One step-table lookup (icx_step.h): refill, peek, entry; long codes behind a wave-uniform
-// branch whose body is a select (a wave where no lane needs it skips it).
+// One step-table lookup (icx_step.h) for block b's DC (dc) or AC code: refill, peek, entry
+// (table chosen by T.bsel[b]); long codes behind wave-uniform branches whose bodies are selects
+// (a wave where no lane needs one skips it): the pool, and the canonical walk for windows the
+// pool does not hold (pathological tables only).
 template <class Tab>
-ICX_HD uint32_t step_lookup(Reader& r, const Tab& T, const Huff* H, int t, uint32_t& x) {
+ICX_HD uint32_t step_lookup(Reader& r, const Tab& T, const Huff* H, const Sel& S, int b, bool dc, uint32_t& x) {
     r.refill();
     x = (uint32_t)(r.buf >> 32);
-    uint32_t e = T.look(t, x);
+    uint32_t e = T.look_b(b, dc, x);
     if (wave_any((e & kStSlow) != 0u)) {
-        const uint32_t es = T.resolve(t, x, e & kStSlow ? e : kStSub, H);
-        e = (e & kStSlow) ? es : e;
+        const uint32_t ep = T.pool_b(b, dc, x);
+        if (wave_any((e & kStSearch) != 0u)) {
+            const uint32_t es = T.resolve(S.tab(b, dc), x, e & kStSearch ? e : kStSub, H);
+            e = (e & kStSearch) ? es : e;
+        }
+        e = (e & kStSub) ? ep : e;
     }
     return e;
+}
+static_assert(sizeof(ScanTab::bsel) / sizeof(ScanTab::bsel[0]) == kSpecMaxBpm, "bsel covers every block of an MCU");
+template <class Tab>
+ICX_HD void set_block_sel(Tab& T, const Huff* H, const Sel& S) {
+    for (int b = 0; b < kSpecMaxBpm; ++b) {
+        const int bb = b < S.bpm ? b : 0;
+        T.set_bsel(H, b, S.tab(bb, true), S.tab(bb, false));
+    }
 }
 
 // SCAN step (guess / count / repair): one lookup -- a run of symbols of the current block, or
@@ -362,7 +376,7 @@ ICX_HD uint32_t step_lookup(Reader& r, const Tab& T, const Huff* H, int t, uint3
 ICX_HD bool scan_step(Reader& r, const ScanTab& T, const Huff* H, const Sel& S, int& b, int& z, int32_t& dcv) {
     const bool dc = z == 0;
     uint32_t x;
-    const uint32_t e = step_lookup(r, T, H, S.tab(b, dc), x);
+    const uint32_t e = step_lookup(r, T, H, S, b, dc, x);
     const uint32_t zm = (e >> 21) & 127u;
     const bool usem = (uint32_t)z + zm <= 64u;
     const uint32_t tot = usem ? (e >> 16) & 31u : st_tot1(e);
@@ -394,7 +408,7 @@ struct WriteOut {
 ICX_HD WriteOut write_step(Reader& r, const WriteTab& T, const Huff* H, const Sel& S, int& b, int& z, bool near_err) {
     const bool dc = z == 0;
     uint32_t x;
-    const uint32_t e = step_lookup(r, T, H, S.tab(b, dc), x);
+    const uint32_t e = step_lookup(r, T, H, S, b, dc, x);
     const uint32_t tot1 = st_tot1(e), nbx1 = st_nbx1(e), zad1 = st_zad1(e);
     const uint32_t tot2 = (e >> 16) & 15u, nbx2 = (e >> 20) & 15u, zad2 = (e >> 24) & 31u, eob2 = (e >> 29) & 1u;
     const bool pair = tot2 != 0u && (uint32_t)z + zad1 + zad2 + eob2 <= 64u && !near_err;

@@ -90,6 +90,10 @@ struct StepTab {
     uint32_t pool[POOL];
     uint32_t sbase[4], soff[4], sn[4];  // per table: first pool window, pool offset, pool entries
     uint32_t pad_[4];                   // (16-byte multiple: staged into LDS with 16-byte copies)
+    // Per block-in-MCU b (set_bsel): byte offsets in this struct of b's DC and AC first-level
+    // tables, and their pool deltas soff[t] - sbase[t]. One LDS read of bsel[b] replaces the
+    // table selection arithmetic of every lookup (a 64-bit selector shift and ~12 VALU).
+    uint32_t bsel[16][4];  // 16 = kSpecMaxBpm (checked in icx_spec_core.h)
 
     static ICX_HD int bits(int t) { return t < 2 ? DB : AB; }
     // pool layout: tables in order, each gets what it needs while the pool lasts
@@ -173,6 +177,29 @@ struct StepTab {
         if (k < 4) sbase[k] = h[k].bound[bits(k)];
         else if (k < 8) soff[k - 4] = off[k - 4];
         else if (k < 12) sn[k - 8] = n[k - 8];
+    }
+    // bsel[b] for a block whose DC table is tdc (0, 1) and AC table tac (2, 3); tables come
+    // from fill(), so this only needs h (for the pool layout) and the table numbers.
+    ICX_HD void set_bsel(const Huff* h, int b, int tdc, int tac) {
+        uint32_t off[4], n[4];
+        layout(h, off, n);
+        const char* base = reinterpret_cast<const char*>(this);
+        bsel[b][0] = (uint32_t)(reinterpret_cast<const char*>(&dc[tdc & 1][0]) - base);
+        bsel[b][1] = (uint32_t)(reinterpret_cast<const char*>(&ac[(tac - 2) & 1][0]) - base);
+        bsel[b][2] = off[tdc & 3] - h[tdc & 3].bound[bits(tdc & 3)];
+        bsel[b][3] = off[tac & 3] - h[tac & 3].bound[bits(tac & 3)];
+    }
+    // First-level entry for block b's DC (dc) or AC code at peek x.
+    ICX_HD uint32_t look_b(int b, bool dc, uint32_t x) const {
+        const uint32_t off = dc ? bsel[b][0] : bsel[b][1];
+        const uint32_t idx = dc ? x >> (32 - DB) : x >> (32 - AB);
+        return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(this) + off + 4u * idx);
+    }
+    // The long-code pool entry of that window (meaningful when the first-level entry is SUB;
+    // clamped for lanes that only ride along).
+    ICX_HD uint32_t pool_b(int b, bool dc, uint32_t x) const {
+        const uint32_t i = (x >> 16) + (dc ? bsel[b][2] : bsel[b][3]);
+        return pool[i < (uint32_t)POOL ? i : POOL - 1];
     }
     // Entry of table t for the peek x (32 bits); SUB / SEARCH entries resolved (the caller
     // decides whether to look: a wave-uniform branch on the GPU).

@@ -124,6 +124,8 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     StepSet& SS = *SSp;
     for (int k = 0; k < ScanTab::entries(); ++k) SS.scan.fill(d.huff, k);
     for (int k = 0; k < WriteTab::entries(); ++k) SS.write.fill(d.huff, k);
+    set_block_sel(SS.scan, d.huff, make_sel(d));
+    set_block_sel(SS.write, d.huff, make_sel(d));
     const ScanTab& T = SS.scan;
     const WriteTab& TW = SS.write;
     const Huff* H = d.huff;
@@ -229,6 +231,7 @@ int emu_sync_study(const uint8_t* file, int64_t size, int nstarts, int guess_b, 
     const int64_t ulen = emu_unstuff(R, L, ustf_align(R), U, errpos, gu, nullptr);
     auto SSp = std::make_unique<StepSet>();
     for (int k = 0; k < ScanTab::entries(); ++k) SSp->scan.fill(d.huff, k);
+    set_block_sel(SSp->scan, d.huff, make_sel(d));
     const ScanTab& T = SSp->scan;
     const Huff* H = d.huff;
     std::unordered_map<int64_t, int> truth;  // pos -> (b<<8|z)
@@ -309,6 +312,8 @@ extern "C" int emu_step_selftest(const uint8_t* dcc17, const uint8_t* dcs, int n
     d.nc = 1;
     d.c[0].nblk = 1; d.c[0].hs = 1; d.c[0].vs = 1; d.c[0].dc_tab = 0; d.c[0].ac_tab = 2;
     const Sel SL = make_sel(d);
+    set_block_sel(SSp->scan, H, SL);
+    set_block_sel(SSp->write, H, SL);
     const int64_t ulen = nbytes;
     int bad = 0;
     // reference: symbol by symbol
@@ -436,8 +441,9 @@ int emu_write_study(const uint8_t* file, int64_t size, int64_t* out) {
     const int64_t ulen = emu_unstuff(R, d.size - d.scan_off, ustf_align(R), U, errpos, gu, nullptr);
     auto SSp = std::make_unique<StepSet>();
     for (int k = 0; k < WriteTab::entries(); ++k) SSp->write.fill(d.huff, k);
-    const WriteTab& TW = SSp->write;
     const Sel SL = make_sel(d);
+    set_block_sel(SSp->write, d.huff, SL);
+    const WriteTab& TW = SSp->write;
     std::vector<uint8_t> ev;  // per lookup: bit0 SUB, bit1 block completed
     Reader r; r.init(U.data(), ulen, 0);
     int b = 0, z = 0;
@@ -446,7 +452,7 @@ int emu_write_study(const uint8_t* file, int64_t size, int64_t* out) {
     while (blocks < total) {
         const bool dc = z == 0;
         r.refill();  // (write_step refills again: harmless for the peek below)
-        const uint32_t e = TW.look(SL.tab(b, dc), (uint32_t)(r.buf >> 32));
+        const uint32_t e = TW.look_b(b, dc, (uint32_t)(r.buf >> 32));
         (void)write_step(r, TW, d.huff, SL, b, z, false);
         const bool done = z == 0;
         blocks += done;
