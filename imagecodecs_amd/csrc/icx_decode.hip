@@ -1478,8 +1478,11 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     const int tb = 64, nb = (n + tb - 1) / tb;
     B(kStIdct);
     const int64_t maxblk = ws.coef_cap;
-    // ~16K workgroups per launch in total; every kernel grid-strides over its image's work
-    int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 32 * kIdctU - 1) / (32 * kIdctU), 16384 / n));
+    // ~16K workgroups per launch in total; every kernel grid-strides over its image's work. The
+    // kernels for the other samplings get kGenericWG in total (ICX_GENERIC_WG overrides): in a
+    // 4:2:0 batch they are no-ops, and dispatching 16K empty workgroups each cost ~1% per step.
+    static const int gwg = std::getenv("ICX_GENERIC_WG") ? std::max(8, std::atoi(std::getenv("ICX_GENERIC_WG"))) : kGenericWG;
+    int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 32 * kIdctU - 1) / (32 * kIdctU), gwg / n));
     if (gx >= 8) gx &= ~7;  // XCD-aware chunk order in k_idct needs a multiple of 8
     // 4:2:0 images (fused420): mode 2 (default) transforms their planes with the lane-pair IDCT,
     // k_idct420y / k_idct420c, whose stores are whole 128-byte plane rows (k_idct skips them);
@@ -1505,7 +1508,7 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     }
     E(kStIdct);
     B(kStUpsample);
-    const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, 16384 / (3 * n)));
+    const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, gwg / (3 * n)));
 #ifndef ICX_EXP_ONLY420
     for (int p = 0; p < 6; ++p)
         hipLaunchKernelGGL(k_upsample, dim3(ux, n * 3), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
@@ -1513,9 +1516,10 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
 #endif
     E(kStUpsample);
     B(kStConvert);
-    const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, 16384 / n));
-    const int sxg = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)(ws.max_w + 255) / 256) *
-                                                                 ((ws.max_h + kSH - 1) / kSH) / 4 + 1, 16384 / n));
+    const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, gwg / n));
+    const int64_t sxw = ((int64_t)(ws.max_w + 255) / 256) * ((ws.max_h + kSH - 1) / kSH) / 4 + 1;
+    const int sxg = (int)std::max<int64_t>(1, std::min<int64_t>(sxw, 16384 / n));
+    const int sxo = (int)std::max<int64_t>(1, std::min<int64_t>(sxw, gwg / n));  // the other layouts
     hipLaunchKernelGGL(k_convert_stream<3>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
     const int fgx = (int)std::max<int64_t>(1, std::min<int64_t>((((int64_t)(ws.max_w + 255) / 256) *
@@ -1525,21 +1529,23 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
         hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                            ws.plane_cap, d_out, out_stride);
 #ifndef ICX_EXP_ONLY420
-    hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+    hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
-    hipLaunchKernelGGL(k_convert_stream<1>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+    hipLaunchKernelGGL(k_convert_stream<1>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
-    hipLaunchKernelGGL(k_convert_stream<2>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+    hipLaunchKernelGGL(k_convert_stream<2>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
-    hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+    hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
 #endif
     // border lanes of the doubled layouts: ~3 lanes x (H / kSHE) strips per image
-    const int egx = (int)std::max<int64_t>(1, std::min<int64_t>((4 * ((ws.max_h + kSHE - 1) / kSHE) + 255) / 256, 16384 / n));
+    const int64_t egw = (4 * ((ws.max_h + kSHE - 1) / kSHE) + 255) / 256;
+    const int egx = (int)std::max<int64_t>(1, std::min<int64_t>(egw, 16384 / n));
+    const int ego = (int)std::max<int64_t>(1, std::min<int64_t>(egw, gwg / n));
     hipLaunchKernelGGL(k_convert_edge<3>, dim3(egx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
 #ifndef ICX_EXP_ONLY420
-    hipLaunchKernelGGL(k_convert_edge<1>, dim3(egx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+    hipLaunchKernelGGL(k_convert_edge<1>, dim3(ego, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
     hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride);

@@ -14,6 +14,8 @@ namespace icx {
 constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16 B)
 constexpr int kSubBytes = 2048;    // unstuffed bytes per decode lane (subsequence)
 constexpr int kRec = 16;           // block-start states a guess lane records for resync
+constexpr int kGenericWG = 4096;    // workgroups per launch of the other-sampling back-half kernels
+constexpr int kGuessLead = 2048;     // bits a guess lane decodes before its range (k_spec_guess)
 constexpr int kMaxRepair = 1024;   // unsynchronised lanes repaired per image before giving up
 constexpr int kLanes = 256;        // lanes per decode workgroup (lane records are numbered in these)
 constexpr int kWriteLanesBig = 512;  // write-pass workgroup for large images: tables amortised

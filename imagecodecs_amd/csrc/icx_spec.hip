@@ -479,7 +479,7 @@ __global__ __launch_bounds__(NL) void k_spec_guess(int n, const Desc* __restrict
                                                    int tsel, const StepSet* __restrict__ steps,
                                                    const uint8_t* __restrict__ U, int64_t ucap, uint64_t* __restrict__ X,
                                                    RecState* __restrict__ rec, int32_t* __restrict__ nrec,
-                                                   int32_t* __restrict__ gtot) {
+                                                   int32_t* __restrict__ gtot, int lead) {
     __shared__ ScanTab T;
     int cur = -1;
     const int total = totals[tsel];
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(NL) void k_spec_guess(int n, const Desc* __restrict
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
         const int64_t sb = (int64_t)kSubBytes * 8;
         X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j * sb, (j + 1) * sb, 0,
-                          rec + f * kRec, nrec + f, gtot + 4 * f);
+                          rec + f * kRec, nrec + f, gtot + 4 * f, lead);
     }
 }
 
@@ -823,6 +823,9 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     static const int g = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
+    // Guess lanes start kGuessLead bits before their range (ICX_GUESS_LEAD overrides), so they are
+    // resynchronised when they reach it and the count lanes splice at their first MCU start.
+    static const int lead = std::getenv("ICX_GUESS_LEAD") ? std::max(0, std::atoi(std::getenv("ICX_GUESS_LEAD"))) : kGuessLead;
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
                        ws.totals, ws.ucap);
@@ -837,7 +840,7 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     B(kStEntropy);
     // guess / count: 512-lane workgroups (the 41 KB scan tables amortised over more lanes)
     hipLaunchKernelGGL(k_spec_guess<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                       ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt);
+                       ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
     hipLaunchKernelGGL(k_spec_count<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
                        ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.ucap, ws.X, ws.Y,

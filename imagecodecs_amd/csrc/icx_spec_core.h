@@ -431,22 +431,26 @@ ICX_HD WriteOut write_step(Reader& r, const WriteTab& T, const Huff* H, const Se
 }
 
 // ------------------------------------------------------------------------ lane logic
-// Guess lane: decode [start, end) from the block-start guess (b0, z=0). Records the first
-// kRec MCU-start states (b == 0, z == 0) it passes through (rec, *nrec) and its totals tot = {DC codes,
-// DC-diff sums per component} over the whole lane. Returns the exit state: the first lookup
-// boundary at or after `end`.
+// Guess lane: decode [start - lead, end) from the block-start guess (b0, z=0) at start - lead
+// (clamped to 0). Records the first kRec MCU-start states (b == 0, z == 0) it passes through at
+// or after `start` (rec, *nrec; rel = bits past `start`) and its totals tot = {DC codes, DC-diff
+// sums per component} over everything it decoded. Returns the exit state: the first lookup
+// boundary at or after `end`. The lead lets the lane resynchronise before `start`, so its first
+// recorded state is (almost always) on the true path and the count lane splices at once; only
+// differences of the totals are ever used (tot - rec[m]), so the extra prefix cancels.
 ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S, int64_t start,
-                           int64_t end, int b0, RecState* rec, int32_t* nrec, int32_t* tot) {
+                           int64_t end, int b0, RecState* rec, int32_t* nrec, int32_t* tot, int64_t lead = 0) {
+    const int64_t s0 = start - lead > 0 ? start - lead : 0;
     Reader r;
-    r.init(U, ulen, start);
+    r.init(U, ulen, s0);
     int b = b0, z = 0;
     int32_t val, cnt = 0, ds[3] = {0, 0, 0};
     int nr = 0;
-    const uint32_t span = (uint32_t)(end - start);
+    const uint32_t pre = (uint32_t)(start - s0), span = (uint32_t)(end - s0);
     while (r.used < span) {
-        if (z == 0 && b == 0 && nr < kRec) {  // MCU starts: the true path passes one per MCU
+        if (z == 0 && b == 0 && nr < kRec && r.used >= pre) {  // MCU starts: the true path passes one per MCU
             RecState& e = rec[nr++];
-            e.rel = r.used;
+            e.rel = r.used - pre;
             e.b = b;
             e.cnt = cnt;
             e.ds[0] = ds[0];
@@ -475,7 +479,7 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const ScanTab& T, con
 // whole lane is decoded and its own exit returned.
 ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S,
                            uint64_t entry, int64_t start, int64_t end, const RecState* rec, int nrec, const int32_t* tot,
-                           uint64_t guess_exit, SubRec& out, bool& synced) {
+                           uint64_t guess_exit, SubRec& out, bool& synced, uint32_t* bits = nullptr) {
     Reader r;
     r.init(U, ulen, st_pos(entry));
     int b = st_b(entry), z = st_z(entry);
@@ -494,6 +498,7 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const ScanTab& T, con
                 out.ds2 = wadd(ds[2], wsub(tot[3], rec[m].ds[2]));
                 out.mism = 0;
                 synced = true;
+                if (bits) *bits = r.used;
                 return guess_exit;
             }
         }
@@ -506,6 +511,7 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const ScanTab& T, con
         }
     }
     const uint64_t ex = pack_state(r.pos(), b, z);
+    if (bits) *bits = r.used;
     out.cnt = cnt;
     out.ds0 = ds[0];
     out.ds1 = ds[1];

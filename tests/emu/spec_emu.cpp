@@ -4,6 +4,7 @@
 // kernel's bookkeeping, so the algorithm can be checked on a machine without a GPU.
 // Never linked into libicx.so.
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -96,7 +97,13 @@ static int64_t emu_unstuff(const uint8_t* R, int64_t L, int sh, std::vector<uint
     return ulen;
 }
 
+// guess-lane lead in bits: k_spec_guess's kGuessLead, or ICX_GUESS_LEAD as for libicx.so
+static int64_t g_lead = std::getenv("ICX_GUESS_LEAD") ? std::atoll(std::getenv("ICX_GUESS_LEAD")) : kGuessLead;
+static std::vector<uint32_t>* g_count_bits = nullptr;  // emu_count_study: bits each count lane decoded
+
 extern "C" {
+
+void emu_set_lead(int64_t lead) { g_lead = lead; }
 
 // Returns: 0 parallel path finished (status in *status), 1 image would fall back to the
 // sequential kernel, 2 not eligible for the parallel path (status = header result).
@@ -138,7 +145,8 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     std::vector<RecState> rec(nsub * kRec);
     std::vector<int32_t> nrec(nsub, 0), tot(nsub * 4, 0);
     for (int64_t j = 0; j + 1 < nsub; ++j)
-        X[j] = lane_guess(U.data(), ulen, T, H, SL, j * sb, (j + 1) * sb, 0, rec.data() + j * kRec, &nrec[j], &tot[4 * j]);
+        X[j] = lane_guess(U.data(), ulen, T, H, SL, j * sb, (j + 1) * sb, 0, rec.data() + j * kRec, &nrec[j], &tot[4 * j],
+                          g_lead);
     // ---- count (k_spec_count)
     std::vector<SubRec> sub(nsub, SubRec{0, 0, 0, 0, 0});
     std::vector<int32_t> queue;
@@ -146,8 +154,10 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     for (int64_t j = 0; j + 1 < nsub; ++j) {
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[j - 1];
         bool synced;
+        uint32_t cbits = 0;
         Y[j] = lane_count(U.data(), ulen, T, H, SL, entry, j * sb, (j + 1) * sb, rec.data() + j * kRec, nrec[j],
-                          &tot[4 * j], X[j], sub[j], synced);
+                          &tot[4 * j], X[j], sub[j], synced, &cbits);
+        if (g_count_bits) g_count_bits->push_back(cbits);
         synced_lanes += synced;
         if (sub[j].mism) queue.push_back((int32_t)j);
     }
@@ -217,6 +227,24 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
 
 #include <unordered_map>
 extern "C" {
+// Count-pass study (tuning aid): run emu_spec_decode with guess lead `lead` and report the bits
+// each count lane decoded before it spliced (or its whole lane); returns the number of lanes
+// (at most cap written to out).
+int64_t emu_count_study(const uint8_t* file, int64_t size, int64_t lead, int16_t* coef, int32_t* dc, int64_t cap_blocks,
+                        uint32_t* out, int64_t cap) {
+    std::vector<uint32_t> bits;
+    g_count_bits = &bits;
+    const int64_t old = g_lead;
+    g_lead = lead;
+    int64_t nb = 0, st[4] = {0, 0, 0, 0};
+    int32_t status = 0;
+    emu_spec_decode(file, size, kSubBytes, coef, dc, cap_blocks, &nb, &status, st);
+    g_lead = old;
+    g_count_bits = nullptr;
+    for (int64_t k = 0; k < (int64_t)bits.size() && k < cap; ++k) out[k] = bits[k];
+    return (int64_t)bits.size();
+}
+
 // Sync-distance study: for `nstarts` evenly spaced start bits, decode from a guessed state
 // (b = guess_b, z = 0) and report the bits consumed until the lane's state equals the true
 // decoder's state at the same position (-1 if not within `maxbits`).
