@@ -405,7 +405,8 @@ struct WriteOut {
     bool w1, w2;  // write v1 at c1 / v2 at c2
     bool err;
 };
-ICX_HD WriteOut write_step(Reader& r, const WriteTab& T, const Huff* H, const Sel& S, int& b, int& z, bool near_err) {
+template <class Tab>
+ICX_HD WriteOut write_step(Reader& r, const Tab& T, const Huff* H, const Sel& S, int& b, int& z, bool near_err) {
     const bool dc = z == 0;
     uint32_t x;
     const uint32_t e = step_lookup(r, T, H, S, b, dc, x);

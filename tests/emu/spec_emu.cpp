@@ -502,3 +502,39 @@ int emu_write_study(const uint8_t* file, int64_t size, int64_t* out) {
     return 0;
 }
 }
+
+// Write-table width study (tuning aid): lookups per block of a sequential write_step decode with
+// AC windows of 10 / 11 / 12 bits (pairs fit more often in wider windows). out[k] = lookups
+// with AC window 10 + k, out[3] = blocks.
+template <int AB>
+static int64_t write_lookups(const Desc& d, const std::vector<uint8_t>& U, int64_t ulen, int64_t total) {
+    using Tab = StepTab<8, AB, 1280, false>;
+    auto T = std::make_unique<Tab>();
+    for (int k = 0; k < Tab::entries(); ++k) T->fill(d.huff, k);
+    const Sel SL = make_sel(d);
+    set_block_sel(*T, d.huff, SL);
+    Reader r; r.init(U.data(), ulen, 0);
+    int b = 0, z = 0;
+    int64_t blocks = 0, n = 0;
+    while (blocks < total) {
+        (void)write_step(r, *T, d.huff, SL, b, z, false);
+        ++n;
+        blocks += z == 0;
+    }
+    return n;
+}
+extern "C" int emu_write_width_study(const uint8_t* file, int64_t size, int64_t* out) {
+    auto dp = std::make_unique<Desc>();
+    Desc& d = *dp;
+    if (parse_headers(file, size, d) != kPending || d.restart || d.bpm > kSpecMaxBpm) return -1;
+    const uint8_t* R = file + d.scan_off;
+    std::vector<uint8_t> U;
+    int64_t errpos; int32_t gu = 0;
+    const int64_t ulen = emu_unstuff(R, d.size - d.scan_off, ustf_align(R), U, errpos, gu, nullptr);
+    const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
+    out[0] = write_lookups<10>(d, U, ulen, total);
+    out[1] = write_lookups<11>(d, U, ulen, total);
+    out[2] = write_lookups<12>(d, U, ulen, total);
+    out[3] = total;
+    return 0;
+}
