@@ -166,8 +166,9 @@ static int64_t ws_per_slot(GroupWs& ws, int max_w, int max_h) {
     ws.tmp_cap = ws_tmp_cap(max_w, max_h);
     ws.ucap = ((int64_t)max_w * max_h + 4095) / 4096 * 4096;  // 1 B/px of entropy data (q90 ~0.4)
     ws.rst_cap = ((int64_t)max_w / 8 + 1) * ((int64_t)max_h / 8 + 1);  // >= MCUs per image
+    // decode lanes of kSubBytesSmall .. kSubBytes bytes (k_spec_plan picks per image)
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
-    const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
+    const int64_t lanes_per_slot = ((ws.ucap + kSubBytesSmall - 1) / kSubBytesSmall + kLanes - 1) / kLanes * kLanes + kLanes;
     return ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
            (int64_t)sizeof(StepSet) +
            tiles_per_slot * 28 + ws.rst_cap * 8 +
@@ -195,7 +196,7 @@ static bool ws_alloc(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int max_h)
 static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int max_h) {
     (void)ws_per_slot(ws, max_w, max_h);
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
-    const int64_t lanes_per_slot = ((ws.ucap + kSubBytes - 1) / kSubBytes + kLanes - 1) / kLanes * kLanes + kLanes;
+    const int64_t lanes_per_slot = ((ws.ucap + kSubBytesSmall - 1) / kSubBytesSmall + kLanes - 1) / kLanes * kLanes + kLanes;
     ws.slots = group;
     ICX_HIP(ctx, hipMalloc(&ws.desc, sizeof(Desc) * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)ws.coef_cap * 64 * 2 * group), false);

@@ -12,7 +12,9 @@ namespace icx {
 
 // ---- speculative parallel entropy decode (icx_spec.hip) ----
 constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16 B)
-constexpr int kSubBytes = 2048;    // unstuffed bytes per decode lane (subsequence)
+constexpr int kSubBytes = 2048;      // longest decode lane (unstuffed bytes per subsequence)
+constexpr int kSubBytesSmall = 512;  // shortest: k_spec_plan sizes each image's lanes in between so
+                                     // they fill whole 512-lane workgroups (icx_spec.hip)
 constexpr int kRec = 16;           // block-start states a guess lane records for resync
 constexpr int kGenericWG = 4096;    // workgroups per launch of the other-sampling back-half kernels
 constexpr int kGuessLead = 2048;     // bits a guess lane decodes before its range (k_spec_guess)
@@ -31,6 +33,7 @@ struct SpecImg {
     int32_t nwg, wg_base;  // 256-lane decode groups, flat numbering over the batch group
     int32_t nsub, nrepair;   // lanes; unsynchronised lanes queued for repair
     int32_t nint, nrst;      // DRI (mode 3): restart intervals; restart markers found in U
+    int32_t sub_bytes, pad_; // unstuffed bytes per decode lane (mode 1)
     int64_t scan_len;      // raw entropy-coded bytes (file end - scan start)
     int64_t ulen;          // unstuffed data bytes before FF D9 / end of file / bad marker
     int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)

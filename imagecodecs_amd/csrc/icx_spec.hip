@@ -50,7 +50,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     int32_t* __restrict__ tilepre, int32_t* __restrict__ wgpre,
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
-                                                    int64_t ucap) {
+                                                    int64_t ucap, int sub_bytes) {
     __shared__ int sh[1024];
     int carry_t = 0, carry_w = 0, carry_w2 = 0;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
@@ -63,6 +63,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             s.err = 0;
             s.nrepair = 0;
             s.nrst = 0;
+            s.sub_bytes = kSubBytes;
             const int64_t scan_len = d.size - d.scan_off;
             // (U also holds the reader padding: u_pad_end(ulen) <= ulen + 32, ulen <= scan_len)
             const bool ok = d.status == kPending && d.nc >= 1 && d.bpm <= kSpecMaxBpm && scan_len > 0 &&
@@ -72,10 +73,20 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                 s.scan_len = scan_len;
                 s.total_blocks = (int64_t)d.mbw * d.mbh * d.bpm;
                 nt = (int)ustf_ntiles(scan_len, ustf_align(data + off[i] + d.scan_off));
-                // lanes: 2 KiB subsequences, or (DRI) one per restart interval
+                // lanes: subsequences of kSubBytesSmall .. kSubBytes unstuffed bytes, sized so the
+                // image's lanes fill whole 512-lane workgroups (a 1024^2 q90 image: 512 lanes of
+                // 768 B, not 194 lanes of 2 KiB in a workgroup 62% idle); or (DRI) one per
+                // restart interval. sub_bytes > 0 (ICX_SUB_BYTES) fixes the size.
                 const int64_t nmcu = (int64_t)d.mbw * d.mbh;
-                const int64_t nsub = s.mode == 1 ? (scan_len + kSubBytes - 1) / kSubBytes
-                                                 : (nmcu + d.restart - 1) / d.restart;
+                int64_t sb = sub_bytes;
+                if (sb <= 0) {
+                    const int64_t full = (int64_t)kWriteLanesBig * kSubBytes;
+                    const int64_t nwg = (scan_len + full - 1) / full;
+                    sb = (scan_len + nwg * kWriteLanesBig - 1) / (nwg * kWriteLanesBig);
+                    sb = min<int64_t>(kSubBytes, max<int64_t>(kSubBytesSmall, (sb + 15) & ~15));
+                }
+                s.sub_bytes = (int32_t)sb;
+                const int64_t nsub = s.mode == 1 ? (scan_len + sb - 1) / sb : (nmcu + d.restart - 1) / d.restart;
                 s.nint = s.mode == 3 ? (int32_t)nsub : 0;
                 nw = (int)((nsub + kLanes - 1) / kLanes);
                 nw2 = (int)((nsub + kWriteLanesBig - 1) / kWriteLanesBig);
@@ -325,7 +336,7 @@ __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ 
         s.ulen = carry;
         s.nrst = rcarry;
         s.errpos = (fe != INT32_MAX && tiles[s.tile_base + fe].end_err) ? carry : INT64_MAX;
-        const int64_t nsub = carry > 0 ? (carry + kSubBytes - 1) / kSubBytes : 1;
+        const int64_t nsub = carry > 0 ? (carry + s.sub_bytes - 1) / s.sub_bytes : 1;
         s.nsub = s.mode == 3 ? s.nint : (int32_t)nsub;
     }
 }
@@ -490,9 +501,9 @@ __global__ __launch_bounds__(NL) void k_spec_guess(int n, const Desc* __restrict
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         if (j >= s.nsub - 1) continue;  // the last lane's exit is never needed
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
-        const int64_t sb = (int64_t)kSubBytes * 8;
+        const int64_t sb = (int64_t)s.sub_bytes * 8;
         X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j * sb, (j + 1) * sb, 0,
-                          rec + f * kRec, nrec + f, gtot + 4 * f, lead);
+                          rec + f * kRec, nrec + f, gtot + 4 * f, lead >= 0 ? lead : min(kGuessLead, s.sub_bytes * 2));
     }
 }
 
@@ -515,7 +526,7 @@ __global__ __launch_bounds__(NL) void k_spec_count(int n, const Desc* __restrict
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         if (j >= s.nsub - 1) continue;
         const int64_t base = (int64_t)s.wg_base * kLanes, f = base + j;
-        const int64_t sb = (int64_t)kSubBytes * 8;
+        const int64_t sb = (int64_t)s.sub_bytes * 8;
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
         SubRec out;
         bool synced;
@@ -558,7 +569,7 @@ __global__ __launch_bounds__(64) void k_spec_repair(int n, const Desc* __restric
     for (int a = 0; a < nq; ++a) {
         const int64_t j = q[a];
         if (j <= done) continue;  // re-derived by an earlier walk
-        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j, s.nsub, (int64_t)kSubBytes * 8, X + base,
+        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j, s.nsub, (int64_t)s.sub_bytes * 8, X + base,
                            Y + base, rec + base * kRec, nrec + base, gtot + 4 * base, sub + base, 64);
         if (done < 0) { s.mode = 2; return; }  // pathological stream: sequential decode
     }
@@ -825,10 +836,12 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     static const int g = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
     // Guess lanes start kGuessLead bits before their range (ICX_GUESS_LEAD overrides), so they are
     // resynchronised when they reach it and the count lanes splice at their first MCU start.
-    static const int lead = std::getenv("ICX_GUESS_LEAD") ? std::max(0, std::atoi(std::getenv("ICX_GUESS_LEAD"))) : kGuessLead;
+    // (per image: at most a quarter of a short lane, the lead is extra work on every lane)
+    static const int lead = std::getenv("ICX_GUESS_LEAD") ? std::max(0, std::atoi(std::getenv("ICX_GUESS_LEAD"))) : -1;
+    static const int sub_env = std::getenv("ICX_SUB_BYTES") ? std::max(16, std::atoi(std::getenv("ICX_SUB_BYTES"))) & ~15 : 0;
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
-                       ws.totals, ws.ucap);
+                       ws.totals, ws.ucap, sub_env);
     hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
@@ -838,20 +851,29 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
                        ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.ucap, ws.rst, ws.rst_cap);
     E(kStUnstuff);
     B(kStEntropy);
-    // guess / count: 512-lane workgroups (the 41 KB scan tables amortised over more lanes)
-    hipLaunchKernelGGL(k_spec_guess<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                       ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
-    hipLaunchKernelGGL(k_spec_count<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                       ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+    // guess / count / write: 512-lane workgroups (tables amortised over more lanes), which each
+    // image's lanes fill (k_spec_plan); ICX_BIG_WG=0 selects 256-lane ones (experiments)
+    static const bool big = std::getenv("ICX_BIG_WG") ? std::atoi(std::getenv("ICX_BIG_WG")) != 0 : true;
+    if (big) {
+        hipLaunchKernelGGL(k_spec_guess<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                           ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
+        hipLaunchKernelGGL(k_spec_count<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                           ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+    } else {
+        hipLaunchKernelGGL(k_spec_guess<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
+                           ws.totals, 1, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
+        hipLaunchKernelGGL(k_spec_count<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
+                           ws.totals, 1, ws.steps, ws.U, ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+    }
     hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.ucap, ws.X, ws.Y,
                        ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
     E(kStEntropy);
     B(kStWrite);
-    if ((int64_t)ws.max_w * ws.max_h >= (int64_t)2048 * 2048) {  // >= 1 MB of entropy data per image
-        // 2 KiB subsequences: 512-lane workgroups (tables amortised); restart intervals (DRI,
-        // typically one per MCU row, so a few hundred long lanes per image): 256-lane workgroups,
-        // which a 512-lane numbering would leave half idle
+    if (big) {
+        // subsequences: 512-lane workgroups; restart intervals (DRI, typically one per MCU row, so
+        // a few hundred long lanes per image): 256-lane workgroups, which a 512-lane numbering
+        // would leave half idle
         hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, 1, n, ws.desc, ws.spec,
                            ws.wg2pre, ws.totals, ws.steps, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,

@@ -60,7 +60,7 @@ def check(data, sub_bytes, allow_fallback=False):
     return mode
 
 
-@pytest.mark.parametrize("sub_bytes", [64, 256, 2048])
+@pytest.mark.parametrize("sub_bytes", [64, 256, 512, 2048])
 def test_emulated_parallel_decode_goldens(sub_bytes):
     """Every non-DRI golden finishes on the parallel path (repair walks included)."""
     modes = [check(open(os.path.join(GOLDEN, n), "rb").read(), sub_bytes, allow_fallback=False) for n in sorted(MANIFEST)]
