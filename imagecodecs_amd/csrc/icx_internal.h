@@ -12,7 +12,7 @@ namespace icx {
 
 // ---- speculative parallel entropy decode (icx_spec.hip) ----
 constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16 B)
-constexpr int kSubBytes = 2048;      // longest decode lane (unstuffed bytes per subsequence)
+constexpr int kSubBytes = 2560;      // longest decode lane (unstuffed bytes per subsequence)
 constexpr int kSubBytesSmall = 512;  // shortest: k_spec_plan sizes each image's lanes in between so
                                      // they fill whole 512-lane workgroups (icx_spec.hip)
 constexpr int kRec = 16;           // block-start states a guess lane records for resync

@@ -79,11 +79,12 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                 // restart interval. sub_bytes > 0 (ICX_SUB_BYTES) fixes the size.
                 const int64_t nmcu = (int64_t)d.mbw * d.mbh;
                 int64_t sb = sub_bytes;
-                if (sb <= 0) {
-                    const int64_t full = (int64_t)kWriteLanesBig * kSubBytes;
+                if (sb <= 0) {  // (sub_bytes < 0: experiments with another longest lane, -sub_bytes)
+                    const int64_t smax = sub_bytes < 0 ? -(int64_t)sub_bytes : kSubBytes;
+                    const int64_t full = (int64_t)kWriteLanesBig * smax;
                     const int64_t nwg = (scan_len + full - 1) / full;
                     sb = (scan_len + nwg * kWriteLanesBig - 1) / (nwg * kWriteLanesBig);
-                    sb = min<int64_t>(kSubBytes, max<int64_t>(kSubBytesSmall, (sb + 15) & ~15));
+                    sb = min<int64_t>(smax, max<int64_t>(kSubBytesSmall, (sb + 15) & ~15));
                 }
                 s.sub_bytes = (int32_t)sb;
                 const int64_t nsub = s.mode == 1 ? (scan_len + sb - 1) / sb : (nmcu + d.restart - 1) / d.restart;
@@ -838,7 +839,8 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     // resynchronised when they reach it and the count lanes splice at their first MCU start.
     // (per image: at most a quarter of a short lane, the lead is extra work on every lane)
     static const int lead = std::getenv("ICX_GUESS_LEAD") ? std::max(0, std::atoi(std::getenv("ICX_GUESS_LEAD"))) : -1;
-    static const int sub_env = std::getenv("ICX_SUB_BYTES") ? std::max(16, std::atoi(std::getenv("ICX_SUB_BYTES"))) & ~15 : 0;
+    static const int sub_env = std::getenv("ICX_SUB_BYTES") ? std::max(16, std::atoi(std::getenv("ICX_SUB_BYTES"))) & ~15
+                               : std::getenv("ICX_SUB_MAX") ? -(std::max(kSubBytesSmall, std::atoi(std::getenv("ICX_SUB_MAX"))) & ~15) : 0;
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
                        ws.totals, ws.ucap, sub_env);
