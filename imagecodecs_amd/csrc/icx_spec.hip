@@ -246,10 +246,19 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
                                                     const int32_t* __restrict__ totals, TileRec* __restrict__ tiles) {
     const int lane = threadIdx.x & 63;
     const TileRange tr = wave_tiles(tilepre, n, totals[0]);
-    TileImg im;
-    if (tr.t < tr.t1) im.set(tr.i, data, off, desc, spec, tilepre);
+    // Software pipelined over the wave's tiles: tile t + 1 is loaded while tile t is scanned.
+    TileImg im, imn;
+    TileChunks tc, tn;
+    if (tr.t < tr.t1) {
+        im.set(tr.i, data, off, desc, spec, tilepre);
+        tc.load(im.R, im.L, im.t0(tr.t), lane);
+    }
+    imn = im;
     for (int t = tr.t; t < tr.t1; ++t) {
-        while (t >= im.t_end) im.set(im.i + 1, data, off, desc, spec, tilepre);
+        if (t + 1 < tr.t1) {  // wave-uniform
+            while (t + 1 >= imn.t_end) imn.set(imn.i + 1, data, off, desc, spec, tilepre);
+            tn.load(imn.R, imn.L, imn.t0(t + 1), lane);
+        }
         const int i = im.i;
         const uint8_t* R = im.R;
         const int64_t L = im.L;
@@ -257,8 +266,6 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
         int32_t giveup = 0;
         int kept = 0, nrst = 0, err = 0;  // per lane until the end of the tile
         long long tend = LLONG_MAX;
-        TileChunks tc;
-        tc.load(R, L, t0, lane);
         for (int r = 0; r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
             const int64_t a = t0 + r * 1024 + lane * 16;
             RstSink rs{0, 0, nullptr, 0, 0};
@@ -290,6 +297,8 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
             rec.pad_ = 0;
             tiles[t] = rec;
         }
+        tc = tn;
+        im = imn;
     }
 }
 
@@ -355,22 +364,26 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
     uint32_t* sbuf = sbuf_all[threadIdx.x >> 6];
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(sbuf);
     const TileRange tr = wave_tiles(tilepre, n, totals[0]);
-    TileImg im;
+    // Software pipelined like k_ustf_count: tile t + 1 is loaded while tile t is written.
+    TileImg im, imn;
+    TileChunks tc, tn;
     int64_t ulen = 0;
     int32_t obv = 0;  // lane k: tile_obase[tb + k] for the current block of 64 tiles
     if (tr.t < tr.t1) {
         im.set(tr.i, data, off, desc, spec, tilepre);
-        ulen = spec[im.i].ulen;
+        tc.load(im.R, im.L, im.t0(tr.t), lane);
     }
+    imn = im;
     for (int t = tr.t; t < tr.t1; ++t) {
-        while (t >= im.t_end) {
-            im.set(im.i + 1, data, off, desc, spec, tilepre);
-            ulen = spec[im.i].ulen;
+        if (t + 1 < tr.t1) {  // wave-uniform
+            while (t + 1 >= imn.t_end) imn.set(imn.i + 1, data, off, desc, spec, tilepre);
+            tn.load(imn.R, imn.L, imn.t0(t + 1), lane);
         }
+        ulen = spec[im.i].ulen;
         if (t == tr.t || ((t - tr.t) & 63) == 0) obv = tr.t + ((t - tr.t) & ~63) + lane < tr.t1 ? tile_obase[t + lane] : 0;
         const int i = im.i;
         const int64_t obase = __shfl(obv, (t - tr.t) & 63);  // == ulen for every tile past the first end event
-        if (obase >= ulen) continue;                          // wave-uniform
+        if (obase < ulen) {                                    // wave-uniform
         const uint8_t* R = im.R;
         const int64_t L = im.L;
         const int64_t t0 = im.t0(t);
@@ -378,14 +391,14 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
         __builtin_amdgcn_wave_barrier();
         int32_t giveup = 0;
         int kept = 0, nrst = 0;
-        TileChunks tc;
-        tc.load(R, L, t0, lane);
         for (int r = 0; r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
             const int64_t a = t0 + r * 1024 + lane * 16;
             RstSink rs0{0, 0, nullptr, 0, 0};
             const ChunkIn c = tc.next(a, lane);
             const Ustf16 u = ustf16<true>(R, L, a, c.D, c.nx, c.prun, &giveup, &rs0);
-            const long long e = wave_min_ll(u.end_at >= 0 ? (long long)u.end_at : LLONG_MAX);
+            // (the data's end is rare: the 64-bit wave minimum only runs in a round that has it)
+            const long long e = __any(u.end_at >= 0) ? wave_min_ll(u.end_at >= 0 ? (long long)u.end_at : LLONG_MAX)
+                                                     : LLONG_MAX;
             const bool before = u.end_at >= 0 ? u.end_at <= e : a < e;
             const int k = before ? u.kept : 0;
             const int incl = wave_incl_scan(k);
@@ -402,7 +415,9 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
             if (k) {  // the kept bytes at byte offset ob of the tile buffer (ORed into zeroed dwords)
                 const int ob = kept + incl - k, q = ob >> 2, sft = ob & 3;
                 const uint32_t* d = u.out;
-                if (sft == 0) {
+                if (k == 16 && (ob & 15) == 0) {  // the common case: a whole aligned 16-byte unit of its own
+                    reinterpret_cast<uint4*>(sbuf)[q >> 2] = make_uint4(d[0], d[1], d[2], d[3]);
+                } else if (sft == 0) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) atomicOr(&sbuf[q + j], d[j]);
                 } else {
@@ -434,6 +449,9 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
             *reinterpret_cast<uint4*>(dst + b0) = make_uint4(v[0], v[1], v[2], v[3]);
         }
         __builtin_amdgcn_wave_barrier();
+        }
+        tc = tn;
+        im = imn;
     }
 }
 
