@@ -448,22 +448,18 @@ __global__ __launch_bounds__(256) void k_hdr_unpack(const uint8_t* __restrict__ 
     }
 }
 
-// grid (x: row chunks, y: image); 256 lanes across a row, one pixel (16 bytes out) each.
-__global__ __launch_bounds__(256) void k_hdr_convert(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
-                                                     const HdrDesc* __restrict__ desc, const int64_t* __restrict__ start,
-                                                     const uint8_t* __restrict__ kind, const uint8_t* __restrict__ planes,
-                                                     float* __restrict__ out, uint64_t out_stride, int max_w, int max_h) {
-    const int i = blockIdx.y;
-    const HdrDesc& dd = desc[i];
-    if (dd.mode == 0) return;
-    const uint8_t* d = data + off[i];
+// The rows of one image, one pixel (16 bytes out) per lane. VEC: the image base is 16-byte
+// aligned and each pixel leaves as one float4 store; otherwise four float stores (out_stride is
+// any number of floats). Two instantiations, chosen once per image: a per-store branch on the
+// alignment halved the kernel's rate (2.1 -> 4.1 ms per 32 images).
+template <bool VEC>
+__device__ __forceinline__ void hdr_convert_rows(const HdrDesc& dd, const uint8_t* d, int i, const int64_t* start,
+                                                 const uint8_t* kind, const uint8_t* planes, float* fo, int max_w,
+                                                 int max_h) {
     const int w = dd.w;
-    float* const fo = out + (int64_t)i * out_stride;
-    // 16-byte stores need a 16-byte aligned image base (out_stride is any number of floats)
-    const bool vec = (reinterpret_cast<uintptr_t>(fo) & 15) == 0;
     float4* o = reinterpret_cast<float4*>(fo);
     auto put = [&](float4* p, const float4& v) {
-        if (vec) {
+        if (VEC) {
             *p = v;
         } else {
             float* q = reinterpret_cast<float*>(p);
@@ -506,6 +502,21 @@ __global__ __launch_bounds__(256) void k_hdr_convert(const uint8_t* __restrict__
             put(orow + x, make_float4(ldexpf((float)r, ex), ldexpf((float)g, ex), ldexpf((float)b, ex), (float)e));
         }
     }
+}
+
+// grid (x: row chunks, y: image); 256 lanes across a row, one pixel (16 bytes out) each.
+__global__ __launch_bounds__(256) void k_hdr_convert(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                     const HdrDesc* __restrict__ desc, const int64_t* __restrict__ start,
+                                                     const uint8_t* __restrict__ kind, const uint8_t* __restrict__ planes,
+                                                     float* __restrict__ out, uint64_t out_stride, int max_w, int max_h) {
+    const int i = blockIdx.y;
+    const HdrDesc& dd = desc[i];
+    if (dd.mode == 0) return;
+    float* const fo = out + (int64_t)i * out_stride;
+    if ((reinterpret_cast<uintptr_t>(fo) & 15) == 0)  // uniform per workgroup
+        hdr_convert_rows<true>(dd, data + off[i], i, start, kind, planes, fo, max_w, max_h);
+    else
+        hdr_convert_rows<false>(dd, data + off[i], i, start, kind, planes, fo, max_w, max_h);
 }
 
 __global__ void k_hdr_finish(int n, HdrDesc* __restrict__ desc, int32_t* __restrict__ status, int32_t* __restrict__ dims) {

@@ -268,3 +268,19 @@ def test_420_plane_modes_bit_exact(ctx, monkeypatch, mode):
     for data, (code, w, h, c, pix) in zip(imgs, b2.decode_host(imgs)):
         ocode, ow, oh, on, opix = O.decode(data)
         assert (code, w, h) == (ocode, ow, oh) and pix.tobytes() == opix
+
+
+def test_batch_create_failure_frees_partial_workspaces(ctx):
+    """A batch whose second pipeline's workspace cannot be allocated (two pipes of 600 4096^2 slots,
+    ~175 GB each, against 288 GB of HBM) fails cleanly and frees what it had already allocated:
+    device free memory is unchanged after repeated failures (icx_batch_create leaked
+    the first pipe's buffers on a partial failure)."""
+    import torch
+
+    torch.cuda.mem_get_info(0)  # (torch's own context first, so it is not counted below)
+    free0, _ = torch.cuda.mem_get_info(0)
+    for _ in range(2):
+        with pytest.raises(icx.ICXError):
+            icx.Batch(ctx, 1200, 4096, 4096, group=1200)
+    free1, _ = torch.cuda.mem_get_info(0)
+    assert abs(free1 - free0) < (256 << 20), (free0, free1)
