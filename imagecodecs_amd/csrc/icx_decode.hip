@@ -1237,10 +1237,20 @@ __device__ __forceinline__ void load_qw(const uint8_t* qz, uint32_t (&qw)[16]) {
         qw[4 * k] = w.x; qw[4 * k + 1] = w.y; qw[4 * k + 2] = w.z; qw[4 * k + 3] = w.w;
     }
 }
-__device__ __forceinline__ void load_block(const int16_t* A, int64_t n, int4 (&c)[8]) {
+// The block's 16-byte zig-zag chunks that lane h of a pair uses: natural rows 0-3 (h = 0) lie in
+// chunks {0,1,2,3,5,6}, rows 4-7 (h = 1) in {1,2,4,5,6,7}. So a lane loads six chunks, and its
+// chunk 0 / 3 slots hold chunks 4 / 7 for h = 1 (pair_idct selects between the halves' values,
+// and a half never reads the other half's private chunks): 6 loads per lane instead of 8.
+__device__ __forceinline__ void load_block(const int16_t* A, int64_t n, int h, int4 (&c)[8]) {
     const int4* src = reinterpret_cast<const int4*>(A + n * 64);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = src[k];
+    c[0] = src[h ? 4 : 0];
+    c[1] = src[1];
+    c[2] = src[2];
+    c[3] = src[h ? 7 : 3];
+    c[5] = src[5];
+    c[6] = src[6];
+    c[4] = c[0];
+    c[7] = c[3];
 }
 
 // A wave's units wid, wid + nw, ... (wave-uniform loop): unit u's coefficient block is blk(u),
@@ -1250,19 +1260,19 @@ __device__ __forceinline__ void load_block(const int16_t* A, int64_t n, int4 (&c
 #define ICX_IDCT_PF 0
 #endif
 template <class BlkF, class UnitF>
-__device__ __forceinline__ void idct_units(const int16_t* A, uint32_t wid, uint32_t nw, uint32_t nunits, BlkF blk,
+__device__ __forceinline__ void idct_units(const int16_t* A, int h, uint32_t wid, uint32_t nw, uint32_t nunits, BlkF blk,
                                            UnitF unit) {
 #if ICX_IDCT_PF
     if (wid >= nunits) return;
     const uint32_t ulast = nunits - 1;
     int4 c0[8], c1[8];
-    load_block(A, blk(wid), c0);
+    load_block(A, blk(wid), h, c0);
     for (uint32_t u = wid;;) {
-        load_block(A, blk(min(u + nw, ulast)), c1);  // (past the end: a harmless reload)
+        load_block(A, blk(min(u + nw, ulast)), h, c1);  // (past the end: a harmless reload)
         unit(u, c0);
         u += nw;
         if (u >= nunits) break;
-        load_block(A, blk(min(u + nw, ulast)), c0);
+        load_block(A, blk(min(u + nw, ulast)), h, c0);
         unit(u, c1);
         u += nw;
         if (u >= nunits) break;
@@ -1270,7 +1280,7 @@ __device__ __forceinline__ void idct_units(const int16_t* A, uint32_t wid, uint3
 #else
     for (uint32_t u = wid; u < nunits; u += nw) {
         int4 c[8];
-        load_block(A, blk(u), c);
+        load_block(A, blk(u), h, c);
         unit(u, c);
     }
 #endif
@@ -1315,7 +1325,7 @@ __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc,
             for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
         }
     };
-    idct_units(A, wid, nw, nunits, blk, unit);
+    idct_units(A, h, wid, nw, nunits, blk, unit);
 }
 
 // Luma planes of fused420 images when the conversion reads them from HBM (ICX_FUSE420 = 2): a
@@ -1357,7 +1367,7 @@ __global__ __launch_bounds__(256) void k_idct420y(const Desc* __restrict__ desc,
             for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
         }
     };
-    idct_units(A, wid, nw, nunits, blk, unit);
+    idct_units(A, h, wid, nw, nunits, blk, unit);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
@@ -1414,7 +1424,7 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
                 const bool live = mx < mbw;
                 const int64_t n = ((int64_t)mby * mbw + (live ? mx : mbw - 1)) * 6 + k;
                 int4 c[8];
-                load_block(A, n, c);
+                load_block(A, n, h, c);
                 uint32_t rowd[8];
                 pair_idct(c, qw, h, D, n, rowd);
                 if (live) {
