@@ -707,6 +707,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         const uint32_t kFar = 1u << 30;
         const uint32_t err_rel = errbits == INT64_MAX ? kFar : (uint32_t)min<int64_t>(kFar, max<int64_t>(0, errbits - e0));
         uint32_t lim_rel = kFar;
+        // the loop's error-byte tests as one compare each: u0 + 16 > err_rel, u0 + 16 + kAcBits > err_rel
+        const int32_t err_peek = (int32_t)err_rel - 16, err_pair = err_peek - WriteTab::kAcBits;
         int64_t bend = total_blocks;  // block index the lane stops at
         uint32_t used_end = 0;        // bits consumed when the lane's last block completed
         if (act && dri) {
@@ -752,10 +754,10 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             // symbol is only paired when its own peek stays clear of the error byte
             const uint32_t u0 = r.used;
             const int z0 = z;
-            const WriteOut o = write_step(r, T, H, S, b, z, u0 + 16 + WriteTab::kAcBits > err_rel);
+            const WriteOut o = write_step(r, T, H, S, b, z, (int32_t)u0 > err_pair);
             // Bookkeeping by selects, not per-lane branches (each divergent `if` cost its exec-mask
             // save / restore and a branch in every iteration).
-            const bool fail = u0 + 16 > err_rel || o.err || r.used > err_rel;
+            const bool fail = (int32_t)u0 > err_peek || o.err || r.used > err_rel;
             bad = bad || (act && fail);
             const bool ok = act && !fail;
             const bool okdc = ok && dc;
