@@ -50,7 +50,8 @@ struct icx_batch {
     bool stagger = false;                // group g's front waits for group g-1's front (ICX_STAGGER=1; measured slower)
     uint8_t* d_hin = nullptr;  // staging for icx_jpeg_batch_decode_host
     size_t d_hin_cap = 0;
-    hipStream_t last_st = nullptr;  // the stream the last decode was ordered on
+    hipEvent_t done = nullptr;      // recorded after the last decode call's work (path_stats waits on it)
+    bool decoded = false;
     std::unique_ptr<EventHook> hook;
 };
 
@@ -198,13 +199,17 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytesSmall - 1) / kSubBytesSmall + kLanes - 1) / kLanes * kLanes + kLanes;
     ws.slots = group;
+    // the U pool and the flat tile / lane records it bounds: two slots' worth beyond the group, so
+    // even a one-image group takes a 3 B/px scan (k_spec_plan sends images past the pool to
+    // the sequential kernel)
+    ws.upool = (int64_t)(group + 2) * ws.ucap;
     ICX_HIP(ctx, hipMalloc(&ws.desc, sizeof(Desc) * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)ws.coef_cap * 64 * 2 * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)ws.coef_cap * 4 * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.planes, (size_t)ws.plane_cap * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), false);
-    ws.tiles_cap = tiles_per_slot * group;
-    ws.lanes_cap = lanes_per_slot * group;
+    ws.tiles_cap = tiles_per_slot * (group + 2);
+    ws.lanes_cap = lanes_per_slot * (group + 2);
     ICX_HIP(ctx, hipMalloc(&ws.spec, sizeof(SpecImg) * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.tilepre, sizeof(int32_t) * (group + 1)), false);
     ICX_HIP(ctx, hipMalloc(&ws.wgpre, sizeof(int32_t) * (group + 1)), false);
@@ -213,7 +218,7 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ICX_HIP(ctx, hipMalloc(&ws.tiles, sizeof(TileRec) * ws.tiles_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.tile_obase, sizeof(int32_t) * ws.tiles_cap), false);
     // + slack: the entropy readers load whole 16-byte chunks (icx_spec_core.h Reader)
-    ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.ucap * group + 256), false);
+    ICX_HIP(ctx, hipMalloc(&ws.U, (size_t)ws.upool + 256), false);
     ICX_HIP(ctx, hipMalloc(&ws.X, sizeof(uint64_t) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.sub, sizeof(SubRec) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.rst, sizeof(int64_t) * ws.rst_cap * group), false);
@@ -265,6 +270,7 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
         ICX_HIP(ctx, hipEventCreateWithFlags(&b->join[p], hipEventDisableTiming), nullptr);
     }
     ICX_HIP(ctx, hipEventCreateWithFlags(&b->fork, hipEventDisableTiming), nullptr);
+    ICX_HIP(ctx, hipEventCreateWithFlags(&b->done, hipEventDisableTiming), nullptr);
     b->hook = std::make_unique<EventHook>();
     return b.release();
 }
@@ -278,6 +284,7 @@ void icx_batch_destroy(icx_batch* b) {
         if (b->join[p]) (void)hipEventDestroy(b->join[p]);
     }
     if (b->fork) (void)hipEventDestroy(b->fork);
+    if (b->done) (void)hipEventDestroy(b->done);
     for (auto e : b->front_done) (void)hipEventDestroy(e);
     if (b->d_hin) (void)hipFree(b->d_hin);
     delete b;
@@ -292,7 +299,6 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     if (!d_data || !d_off || !d_size || !d_out || !d_status || !d_dims) { ctx->err = "null pointer"; return ICX_INTERNAL_ERR; }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-    b->last_st = st;
     b->hook->reset();
     for (int p = 0; p < b->pipes; ++p)
         ICX_HIP(ctx, hipMemsetAsync(b->ws[p].stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
@@ -332,6 +338,10 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
         ICX_HIP(ctx, hipEventRecord(b->join[p], b->pst[p]), ICX_INTERNAL_ERR);
         ICX_HIP(ctx, hipStreamWaitEvent(st, b->join[p], 0), ICX_INTERNAL_ERR);
     }
+    // owned by the batch: path_stats waits on this event, never on the caller's stream (which
+    // the caller may destroy after the call)
+    ICX_HIP(ctx, hipEventRecord(b->done, st), ICX_INTERNAL_ERR);
+    b->decoded = true;
     ICX_HIP(ctx, hipGetLastError(), ICX_INTERNAL_ERR);
     return ICX_OK;
 }
@@ -340,11 +350,9 @@ int icx_batch_path_stats(const icx_batch* b, int32_t* parallel, int32_t* fallbac
     if (!b) return ICX_INTERNAL_ERR;
     int32_t h[4] = {0, 0, 0, 0};
     // The decode ran on non-blocking streams, which the null stream does not order against:
-    // wait for them (every pipe joins into last_st) before reading the counters.
+    // wait for the batch's own event recorded after every pipe joined.
     ICX_HIP(b->ctx, hipSetDevice(b->ctx->device), ICX_INTERNAL_ERR);
-    if (b->last_st) ICX_HIP(b->ctx, hipStreamSynchronize(b->last_st), ICX_INTERNAL_ERR);
-    for (int p = 1; p < b->pipes; ++p)
-        if (b->pst[p]) ICX_HIP(b->ctx, hipStreamSynchronize(b->pst[p]), ICX_INTERNAL_ERR);
+    if (b->decoded) ICX_HIP(b->ctx, hipEventSynchronize(b->done), ICX_INTERNAL_ERR);
     for (int p = 0; p < b->pipes; ++p) {
         int32_t q[4];
         ICX_HIP(b->ctx, hipMemcpy(q, b->ws[p].stats, sizeof q, hipMemcpyDeviceToHost), ICX_INTERNAL_ERR);

@@ -252,7 +252,9 @@ constexpr uint8_t kZigOfNatC[64] = {
     9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
     21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 }
-// Full row / column formulas (no shortcuts) with 24-bit multiplies: exact on the fast path.
+// Full row / column formulas (no shortcuts): 24-bit multiplies of the inputs and their pairwise
+// sums (below 2^23 on the fast path), 32-bit multiplies for the last butterfly's 181 products,
+// whose operands x4 +- x5 are not (a dequantized AC of 2500 puts 8.5M there).
 __device__ __forceinline__ void idct_row_full(int32_t (&r)[8]) {
     int32_t x0 = (r[0] << 11) + 128, x1 = r[4] << 11, x2 = r[6], x3 = r[2];
     int32_t x4 = r[1], x5 = r[7], x6 = r[5], x7 = r[3], x8;
@@ -275,8 +277,9 @@ __device__ __forceinline__ void idct_row_full(int32_t (&r)[8]) {
     x8 -= x3;
     x3 = x0 + x2;
     x0 -= x2;
-    x2 = (m24(181, x4 + x5) + 128) >> 8;
-    x4 = (m24(181, x4 - x5) + 128) >> 8;
+    // (x4 +- x5 reaches ~2^27 here: the 181 products stay 32-bit, as in idct_row)
+    x2 = (wmul(181, x4 + x5) + 128) >> 8;
+    x4 = (wmul(181, x4 - x5) + 128) >> 8;
     r[0] = (x7 + x1) >> 8;
     r[1] = (x3 + x2) >> 8;
     r[2] = (x0 + x4) >> 8;
@@ -308,8 +311,8 @@ __device__ __forceinline__ void idct_col_full(const int32_t (&v)[8], int32_t (&o
     x8 -= x3;
     x3 = x0 + x2;
     x0 -= x2;
-    x2 = (m24(181, x4 + x5) + 128) >> 8;
-    x4 = (m24(181, x4 - x5) + 128) >> 8;
+    x2 = (wmul(181, x4 + x5) + 128) >> 8;  // (32-bit: as in idct_col)
+    x4 = (wmul(181, x4 - x5) + 128) >> 8;
     auto cl = [](int32_t x) { return min(max((x >> 14) + 128, 0), 255); };
     o[0] = cl(x7 + x1);
     o[1] = cl(x3 + x2);
@@ -1499,7 +1502,11 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     // mode 1 takes k_idct420c + k_fused420 (the luma IDCT inside the conversion; bit-exact, but
     // slower beside the second pipeline: DESIGN.md §4); mode 0 leaves them to k_idct. ICX_FUSE420
     // overrides the mode (tests, experiments).
-    const int fuse = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 2;
+    // (any value other than 0, 1, 2 is the default: an unknown mode would leave 4:2:0 luma untransformed)
+    const int fuse = [] {  // (read per launch: tests switch modes within one process)
+        const int v = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 2;
+        return (v >= 0 && v <= 2) ? v : 2;
+    }();
 #ifndef ICX_EXP_ONLY420  // timing experiment only: the 4:2:0 kernels alone (other samplings undecoded)
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
                        ws.plane_cap, fuse);

@@ -38,6 +38,7 @@ struct SpecImg {
     int64_t ulen;          // unstuffed data bytes before FF D9 / end of file / bad marker
     int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)
     int64_t total_blocks;
+    int64_t uoff;          // byte offset of the image's unstuffed stream in GroupWs::U (4 KiB aligned)
 };
 struct TileRec { int32_t kept, end_err; int64_t end_at; int32_t nrst, pad_; };
 struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };
@@ -68,7 +69,10 @@ struct GroupWs {
     uint8_t* planes = nullptr;  // [slots][plane_cap]
     uint8_t* tmp = nullptr;     // [slots][3 comps][2 buffers][tmp_cap]
     // parallel entropy decode
-    int64_t ucap = 0;           // unstuffed bytes per slot
+    int64_t ucap = 0;           // unstuffed bytes per slot on average: U is one pool of (slots + 2) * ucap
+                                // bytes, each image's stream at SpecImg::uoff (k_spec_plan), so one
+                                // image may take several slots' worth (a noisy q100 4:4:4 scan ~2 B/px)
+    int64_t upool = 0;          // bytes of the U pool: (slots + 2) * ucap
     int64_t tiles_cap = 0;      // flat tile records for the whole group
     int64_t lanes_cap = 0;      // flat lane records for the whole group
     SpecImg* spec = nullptr;    // [slots]

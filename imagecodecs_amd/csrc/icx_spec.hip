@@ -50,48 +50,61 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     int32_t* __restrict__ tilepre, int32_t* __restrict__ wgpre,
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
-                                                    int64_t ucap, int sub_bytes) {
+                                                    int64_t upool, int64_t lanes_cap, int sub_bytes) {
     __shared__ int sh[1024];
-    int carry_t = 0, carry_w = 0, carry_w2 = 0;
+    __shared__ int last[5];
+    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0;
+    const int64_t pool_units = upool >> 12, wg_cap = lanes_cap / kLanes;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
         const int i = i0 + threadIdx.x;
-        int nt = 0, nw = 0, nw2 = 0;
+        // Candidates, with the work they would take: U pool units (whole 4 KiB, + the reader
+        // padding: u_pad_end(ulen) <= ulen + 32, ulen <= scan_len), tiles and lanes.
+        const int64_t scan_len = i < n ? desc[i].size - desc[i].scan_off : 0;
+        const bool cand = i < n && desc[i].status == kPending && desc[i].nc >= 1 && desc[i].bpm <= kSpecMaxBpm &&
+                          scan_len > 0 && scan_len < ((int64_t)1 << 40);
+        int nt = 0, nw = 0, nw2 = 0, nu = 0;
+        int64_t sb = kSubBytes, nsub = 0;
+        if (cand) {
+            const Desc& d = desc[i];
+            nu = (int)min<int64_t>((scan_len + 64 + 4095) >> 12, INT32_MAX / 4);
+            nt = (int)ustf_ntiles(scan_len, ustf_align(data + off[i] + d.scan_off));
+            // lanes: subsequences of kSubBytesSmall .. kSubBytes unstuffed bytes, sized so the
+            // image's lanes fill whole 512-lane workgroups (a 1024^2 q90 image: 512 lanes of
+            // 768 B, not 194 lanes of 2 KiB in a workgroup 62% idle); or (DRI) one per
+            // restart interval. sub_bytes > 0 (ICX_SUB_BYTES) fixes the size.
+            const int64_t nmcu = (int64_t)d.mbw * d.mbh;
+            sb = sub_bytes;
+            if (sb <= 0) {  // (sub_bytes < 0: experiments with another longest lane, -sub_bytes)
+                const int64_t smax = sub_bytes < 0 ? -(int64_t)sub_bytes : kSubBytes;
+                const int64_t full = (int64_t)kWriteLanesBig * smax;
+                const int64_t nwg = (scan_len + full - 1) / full;
+                sb = (scan_len + nwg * kWriteLanesBig - 1) / (nwg * kWriteLanesBig);
+                sb = min<int64_t>(smax, max<int64_t>(kSubBytesSmall, (sb + 15) & ~15));
+            }
+            nsub = d.restart == 0 ? (scan_len + sb - 1) / sb : (nmcu + d.restart - 1) / d.restart;
+            nw = (int)min<int64_t>((nsub + kLanes - 1) / kLanes, INT32_MAX / 4);
+            nw2 = (int)((nsub + kWriteLanesBig - 1) / kWriteLanesBig);
+        }
+        // Capacity: an image whose U units or lane records (DRI with tiny intervals) would pass
+        // the workspace's goes to the sequential kernel. The prefixes count every candidate, so
+        // they bound what the images taken below use.
+        const int eu = block_exclusive_scan(nu, sh);
+        const int ec = block_exclusive_scan(nw, sh);
+        const bool ok = cand && (int64_t)carry_u + eu + nu <= pool_units && (int64_t)carry_c + ec + nw <= wg_cap;
+        if (threadIdx.x == blockDim.x - 1) { last[3] = eu + nu; last[4] = ec + nw; }
+        if (!ok) nt = nw = nw2 = 0;
         if (i < n) {
             const Desc& d = desc[i];
             SpecImg& s = spec[i];
-            s.mode = 0;
+            s.mode = ok ? (d.restart == 0 ? 1 : 3) : 0;
             s.err = 0;
             s.nrepair = 0;
             s.nrst = 0;
-            s.sub_bytes = kSubBytes;
-            const int64_t scan_len = d.size - d.scan_off;
-            // (U also holds the reader padding: u_pad_end(ulen) <= ulen + 32, ulen <= scan_len)
-            const bool ok = d.status == kPending && d.nc >= 1 && d.bpm <= kSpecMaxBpm && scan_len > 0 &&
-                            scan_len + 64 <= ucap;
-            if (ok) {
-                s.mode = d.restart == 0 ? 1 : 3;
-                s.scan_len = scan_len;
-                s.total_blocks = (int64_t)d.mbw * d.mbh * d.bpm;
-                nt = (int)ustf_ntiles(scan_len, ustf_align(data + off[i] + d.scan_off));
-                // lanes: subsequences of kSubBytesSmall .. kSubBytes unstuffed bytes, sized so the
-                // image's lanes fill whole 512-lane workgroups (a 1024^2 q90 image: 512 lanes of
-                // 768 B, not 194 lanes of 2 KiB in a workgroup 62% idle); or (DRI) one per
-                // restart interval. sub_bytes > 0 (ICX_SUB_BYTES) fixes the size.
-                const int64_t nmcu = (int64_t)d.mbw * d.mbh;
-                int64_t sb = sub_bytes;
-                if (sb <= 0) {  // (sub_bytes < 0: experiments with another longest lane, -sub_bytes)
-                    const int64_t smax = sub_bytes < 0 ? -(int64_t)sub_bytes : kSubBytes;
-                    const int64_t full = (int64_t)kWriteLanesBig * smax;
-                    const int64_t nwg = (scan_len + full - 1) / full;
-                    sb = (scan_len + nwg * kWriteLanesBig - 1) / (nwg * kWriteLanesBig);
-                    sb = min<int64_t>(smax, max<int64_t>(kSubBytesSmall, (sb + 15) & ~15));
-                }
-                s.sub_bytes = (int32_t)sb;
-                const int64_t nsub = s.mode == 1 ? (scan_len + sb - 1) / sb : (nmcu + d.restart - 1) / d.restart;
-                s.nint = s.mode == 3 ? (int32_t)nsub : 0;
-                nw = (int)((nsub + kLanes - 1) / kLanes);
-                nw2 = (int)((nsub + kWriteLanesBig - 1) / kWriteLanesBig);
-            }
+            s.sub_bytes = ok ? (int32_t)sb : kSubBytes;
+            s.uoff = ((int64_t)carry_u + eu) << 12;
+            s.scan_len = ok ? scan_len : 0;
+            s.total_blocks = ok ? (int64_t)d.mbw * d.mbh * d.bpm : 0;
+            s.nint = ok && s.mode == 3 ? (int32_t)nsub : 0;
             s.ntiles = nt;
             s.nwg = nw;
         }
@@ -105,12 +118,13 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             spec[i].tile_base = carry_t + et;
             spec[i].wg_base = carry_w + ew;
         }
-        __shared__ int last_t, last_w, last_w2;
-        if (threadIdx.x == blockDim.x - 1) { last_t = et + nt; last_w = ew + nw; last_w2 = ew2 + nw2; }
+        if (threadIdx.x == blockDim.x - 1) { last[0] = et + nt; last[1] = ew + nw; last[2] = ew2 + nw2; }
         __syncthreads();
-        carry_t += last_t;
-        carry_w += last_w;
-        carry_w2 += last_w2;
+        carry_t += last[0];
+        carry_w += last[1];
+        carry_w2 += last[2];
+        carry_u = min(carry_u + last[3], INT32_MAX / 4);
+        carry_c = min(carry_c + last[4], INT32_MAX / 4);
         __syncthreads();
     }
     if (threadIdx.x == 0) {
@@ -305,7 +319,7 @@ __global__ __launch_bounds__(256) void k_ustf_count(int n, const uint8_t* __rest
 // Per image: exclusive prefix of kept bytes over tiles, data length, error position.
 __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ spec, TileRec* __restrict__ tiles,
                                                    int32_t* __restrict__ tile_obase, int32_t* __restrict__ tile_rbase,
-                                                   uint8_t* __restrict__ U, int64_t ucap) {
+                                                   uint8_t* __restrict__ U) {
     __shared__ int sh[256];
     __shared__ int s_first_end;
     const int i = blockIdx.x;
@@ -339,7 +353,7 @@ __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ 
         __syncthreads();
     }
     {  // 0xFF padding behind the data for the lane readers (icx_spec_core.h, u_pad_end)
-        uint8_t* u = U + (int64_t)i * ucap;
+        uint8_t* u = U + s.uoff;
         for (int64_t p = carry + threadIdx.x; p < u_pad_end(carry); p += blockDim.x) u[p] = 0xFF;
     }
     if (threadIdx.x == 0) {
@@ -357,7 +371,7 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
                                                     const int32_t* __restrict__ totals, const TileRec* __restrict__ tiles,
                                                     const int32_t* __restrict__ tile_obase,
                                                     const int32_t* __restrict__ tile_rbase, uint8_t* __restrict__ U,
-                                                    int64_t ucap, int64_t* __restrict__ rst, int64_t rst_cap) {
+                                                    int64_t* __restrict__ rst, int64_t rst_cap) {
     constexpr int kBufW = kTileBytes / 4 + 8;           // per wave: the tile's kept bytes (+ slack)
     __shared__ uint32_t sbuf_all[4][kBufW];
     const int lane = threadIdx.x & 63;
@@ -434,7 +448,7 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
         // copy out: bytes up to the first 16-byte boundary and after the last one byte-wise
         // (they may share a 16-byte unit with the neighbouring tiles), the rest as 16-byte units
         const int64_t nout = min<int64_t>(kept, ulen - obase);
-        uint8_t* dst = U + (int64_t)i * ucap + obase;  // U + i*ucap is 4 KiB aligned
+        uint8_t* dst = U + spec[i].uoff + obase;  // (uoff is 4 KiB aligned)
         const int head = (int)min<int64_t>(nout, (16 - (obase & 15)) & 15);
         const int nunit = (int)((nout - head) >> 4);
         const int tail0 = head + nunit * 16;
@@ -507,7 +521,7 @@ template <int NL>
 __global__ __launch_bounds__(NL) void k_spec_guess(int n, const Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
                                                    const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                    int tsel, const StepSet* __restrict__ steps,
-                                                   const uint8_t* __restrict__ U, int64_t ucap, uint64_t* __restrict__ X,
+                                                   const uint8_t* __restrict__ U, uint64_t* __restrict__ X,
                                                    RecState* __restrict__ rec, int32_t* __restrict__ nrec,
                                                    int32_t* __restrict__ gtot, int lead) {
     __shared__ ScanTab T;
@@ -521,7 +535,7 @@ __global__ __launch_bounds__(NL) void k_spec_guess(int n, const Desc* __restrict
         if (j >= s.nsub - 1) continue;  // the last lane's exit is never needed
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
         const int64_t sb = (int64_t)s.sub_bytes * 8;
-        X[f] = lane_guess(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j * sb, (j + 1) * sb, 0,
+        X[f] = lane_guess(U + s.uoff, s.ulen, T, desc[i].huff, make_sel(desc[i]), j * sb, (j + 1) * sb, 0,
                           rec + f * kRec, nrec + f, gtot + 4 * f, lead >= 0 ? lead : min(kGuessLead, s.sub_bytes * 2));
     }
 }
@@ -530,7 +544,7 @@ template <int NL>
 __global__ __launch_bounds__(NL) void k_spec_count(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                    const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                    int tsel, const StepSet* __restrict__ steps,
-                                                   const uint8_t* __restrict__ U, int64_t ucap,
+                                                   const uint8_t* __restrict__ U,
                                                    const uint64_t* __restrict__ X, uint64_t* __restrict__ Y,
                                                    const RecState* __restrict__ rec, const int32_t* __restrict__ nrec,
                                                    const int32_t* __restrict__ gtot, SubRec* __restrict__ sub,
@@ -549,7 +563,7 @@ __global__ __launch_bounds__(NL) void k_spec_count(int n, const Desc* __restrict
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
         SubRec out;
         bool synced;
-        Y[f] = lane_count(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), entry, j * sb, (j + 1) * sb,
+        Y[f] = lane_count(U + s.uoff, s.ulen, T, desc[i].huff, make_sel(desc[i]), entry, j * sb, (j + 1) * sb,
                           rec + f * kRec, nrec[f], gtot + 4 * f, X[f], out, synced);
         sub[f] = out;
         if (out.mism) {  // queue for the serial repair walk
@@ -563,7 +577,7 @@ __global__ __launch_bounds__(NL) void k_spec_count(int n, const Desc* __restrict
 // a guess lane that never resynchronised inside its 2 KiB).
 __global__ __launch_bounds__(64) void k_spec_repair(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     const StepSet* __restrict__ steps,
-                                                    const uint8_t* __restrict__ U, int64_t ucap, uint64_t* __restrict__ X,
+                                                    const uint8_t* __restrict__ U, uint64_t* __restrict__ X,
                                                     const uint64_t* __restrict__ Y, const RecState* __restrict__ rec,
                                                     const int32_t* __restrict__ nrec, const int32_t* __restrict__ gtot,
                                                     SubRec* __restrict__ sub, int32_t* __restrict__ repair) {
@@ -588,7 +602,7 @@ __global__ __launch_bounds__(64) void k_spec_repair(int n, const Desc* __restric
     for (int a = 0; a < nq; ++a) {
         const int64_t j = q[a];
         if (j <= done) continue;  // re-derived by an earlier walk
-        done = repair_walk(U + (int64_t)i * ucap, s.ulen, T, desc[i].huff, make_sel(desc[i]), j, s.nsub, (int64_t)s.sub_bytes * 8, X + base,
+        done = repair_walk(U + s.uoff, s.ulen, T, desc[i].huff, make_sel(desc[i]), j, s.nsub, (int64_t)s.sub_bytes * 8, X + base,
                            Y + base, rec + base * kRec, nrec + base, gtot + 4 * base, sub + base, 64);
         if (done < 0) { s.mode = 2; return; }  // pathological stream: sequential decode
     }
@@ -653,7 +667,7 @@ template <int NL>
 __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                     const StepSet* __restrict__ steps,
-                                                    const uint8_t* __restrict__ U, int64_t ucap,
+                                                    const uint8_t* __restrict__ U,
                                                     const uint64_t* __restrict__ X, const LaneEntry* __restrict__ ent,
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                     int64_t coef_cap, const int64_t* __restrict__ rst, int64_t rst_cap) {
@@ -695,7 +709,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         const uint64_t entry = dri ? pack_state(start_byte * 8, 0, 0)
                                    : ((!act || j == 0) ? pack_state(0, 0, 0) : X[base + j - 1]);
         Reader r;
-        r.init(U + (int64_t)i * ucap, s.ulen, st_pos(entry));
+        r.init(U + s.uoff, s.ulen, st_pos(entry));
         int b = st_b(entry), z = st_z(entry), ci = 0;
         int32_t pred[3] = {0, 0, 0};
         int64_t bi = 0, limit = 0;
@@ -859,18 +873,19 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     // resynchronised when they reach it and the count lanes splice at their first MCU start.
     // (per image: at most a quarter of a short lane, the lead is extra work on every lane)
     static const int lead = std::getenv("ICX_GUESS_LEAD") ? std::max(0, std::atoi(std::getenv("ICX_GUESS_LEAD"))) : -1;
-    static const int sub_env = std::getenv("ICX_SUB_BYTES") ? std::max(16, std::atoi(std::getenv("ICX_SUB_BYTES"))) & ~15
+    // (at least kSubBytesSmall: the lane records are sized for lanes of that length, ws_per_slot)
+    static const int sub_env = std::getenv("ICX_SUB_BYTES") ? std::max(kSubBytesSmall, std::atoi(std::getenv("ICX_SUB_BYTES"))) & ~15
                                : std::getenv("ICX_SUB_MAX") ? -(std::max(kSubBytesSmall, std::atoi(std::getenv("ICX_SUB_MAX"))) & ~15) : 0;
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
-                       ws.totals, ws.ucap, sub_env);
+                       ws.totals, ws.upool, ws.lanes_cap, sub_env);
     hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
     hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,
-                       ws.U, ws.ucap);
+                       ws.U);
     hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
-                       ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.ucap, ws.rst, ws.rst_cap);
+                       ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.rst, ws.rst_cap);
     E(kStUnstuff);
     B(kStEntropy);
     // guess / count / write: 512-lane workgroups (tables amortised over more lanes), which each
@@ -878,16 +893,16 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     static const bool big = std::getenv("ICX_BIG_WG") ? std::atoi(std::getenv("ICX_BIG_WG")) != 0 : true;
     if (big) {
         hipLaunchKernelGGL(k_spec_guess<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                           ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
+                           ws.totals, 2, ws.steps, ws.U, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
         hipLaunchKernelGGL(k_spec_count<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                           ws.totals, 2, ws.steps, ws.U, ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+                           ws.totals, 2, ws.steps, ws.U, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     } else {
         hipLaunchKernelGGL(k_spec_guess<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, 1, ws.steps, ws.U, ws.ucap, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
+                           ws.totals, 1, ws.steps, ws.U, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
         hipLaunchKernelGGL(k_spec_count<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, 1, ws.steps, ws.U, ws.ucap, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+                           ws.totals, 1, ws.steps, ws.U, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     }
-    hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.ucap, ws.X, ws.Y,
+    hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y,
                        ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
     hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
     E(kStEntropy);
@@ -897,12 +912,12 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
         // a few hundred long lanes per image): 256-lane workgroups, which a 512-lane numbering
         // would leave half idle
         hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, 1, n, ws.desc, ws.spec,
-                           ws.wg2pre, ws.totals, ws.steps, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.wg2pre, ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.steps, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
     } else {
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 0, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.steps, ws.U, ws.ucap, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
     }
     E(kStWrite);
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);

@@ -121,3 +121,14 @@ def test_png_device_api(ctx):
 def test_png_rejects(ctx):
     assert ctx.png_encode(4, 4, 2, bytes(32)) is None
     assert ctx.png_encode(0, 4, 4, b"") is None
+
+
+def test_png_c5_8192_rgba(ctx):
+    """C5 at full size: one 8192^2 RGBA alpha-gradient image (tests/pngutil.synth_rgba, the
+    bench's input): exact colour type and filtered stream (the oracle's MINSUM filters), IDAT
+    inflating to it, and a size within 5% of zlib -6 on the same filtered stream."""
+    w = h = 8192
+    px = P.synth_rgba(8192, w, h)
+    png = check(ctx, px, decode=False)
+    ref = O.png_encode_zlib(px.tobytes(), w, h, 4, 6)
+    assert len(png) <= 1.05 * len(ref), (len(png), len(ref))

@@ -286,3 +286,19 @@ def test_emulated_unstuff_every_alignment():
             assert (u, e, rst) == ref, sh
         checked += 1
     assert checked >= 140
+
+
+FOREIGN = json.load(open(os.path.join(GOLDEN, "foreign_manifest.json")))
+
+
+@pytest.mark.parametrize("sub_bytes", [256, 2048])
+def test_emulated_parallel_decode_foreign(sub_bytes):
+    """Foreign-encoder tables (libjpeg-turbo optimised Huffman, other quant scalings) and the
+    crafted corner streams (long codes on common symbols, tables beyond the pool): the lane code
+    verifies its chains and writes the oracle's coefficients block for block."""
+    modes = []
+    for n in sorted(FOREIGN):
+        if FOREIGN[n]["code"] != 0:
+            continue
+        modes.append(check(open(os.path.join(GOLDEN, n), "rb").read(), sub_bytes, allow_fallback=False))
+    assert modes.count(1) == 0 and modes.count(0) >= 40, modes
