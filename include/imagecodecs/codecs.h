@@ -17,10 +17,20 @@
  * reference's unknown-extension branch (codecs.cpp:80-83), so a build that needs those codecs
  * keeps the reference's codecs.cpp for them.
  *
+ *   flip() / swapBR() / idx<T>() -- the reference's public pixel utilities (codecs.h:80, 82-88,
+ *                  98; bodies codecs.cpp:162-251) on the host buffer: rows reversed; channels 0 and
+ *                  2 exchanged; a row-major element read.
  * Deliberate deviations (DESIGN.md "Boundary"): a grayscale JPEG yields channels() == 1 (the
  * reference reports 3 and over-reads the 1-channel buffer, codecs.cpp:840-844); errors throw
  * std::runtime_error (the reference's std::exception(const char*) is MSVC-only, :836). There is
- * no CPU fallback: without a usable GPU, read()/write() of a JPEG throw.
+ * no CPU fallback: without a usable GPU, read()/write() of a JPEG throw. The pixel utilities
+ * follow the reference's evident intent where its code is broken: idx<T> copies into its result
+ * (the reference's memcpy(&T, ...) does not compile, codecs.h:86); flip / swapBR move whole
+ * elements of byteSize() bytes (the reference copies one byte per USHORT element and leaves the
+ * other uninitialised, codecs.cpp:180-185, and swaps FLOAT bytes at offsets 0 and 2,
+ * :213-224); swapBR of an image with fewer than 3 channels is a no-op (the reference reads
+ * past the end of the buffer there). For UBYTE images with 3 or 4 channels -- every JPEG --
+ * the results equal the reference's byte for byte.
  *
  * Header-only; link with -L<repo>/imagecodecs_amd/lib -licx. One icx context per process
  * (device ICX_DEVICE, default 0), created on first use and serialised by a mutex -- the
@@ -172,6 +182,39 @@ public:
     int totalBytes() const { return w_ * h_ * d_ * byteSize(); }
     Type type() const { return type_; }
     bool lastWriteOk() const { return last_write_ok_; }  // extension: tje's result of the last write()
+    // flip (codecs.h:80, codecs.cpp:162-196): reverse the row order in place.
+    void flip() {
+        if (empty()) return;
+        const size_t row = (size_t)w_ * d_ * byteSize();
+        std::vector<unsigned char> tmp(row);
+        for (int i = 0, j = h_ - 1; i < j; ++i, --j) {
+            unsigned char* a = pixels_ + (size_t)i * row;
+            unsigned char* b = pixels_ + (size_t)j * row;
+            std::memcpy(tmp.data(), a, row);
+            std::memcpy(a, b, row);
+            std::memcpy(b, tmp.data(), row);
+        }
+    }
+    // swapBR (codecs.h:98, codecs.cpp:198-251): exchange channels 0 and 2 of every pixel.
+    void swapBR() {
+        if (empty() || d_ < 3) return;
+        const int bs = byteSize();
+        const size_t px = (size_t)w_ * h_, step = (size_t)d_ * bs;
+        unsigned char t[4];
+        for (size_t p = 0; p < px; ++p) {
+            unsigned char* q = pixels_ + p * step;
+            std::memcpy(t, q, bs);
+            std::memmove(q, q + 2 * bs, bs);
+            std::memcpy(q + 2 * bs, t, bs);
+        }
+    }
+    // idx (codecs.h:82-88): element (row i, column j, channel k) of a row-major T array.
+    template <typename T>
+    T idx(int i, int j, int k) const {
+        T ret;
+        std::memcpy(&ret, pixels_ + ((size_t)i * w_ * d_ + (size_t)j * d_ + (size_t)k) * sizeof(T), sizeof(T));
+        return ret;
+    }
     void load(unsigned char* pixels, int w, int h, int channels) {
         d_ = channels;
         w_ = w;

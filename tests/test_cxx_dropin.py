@@ -79,3 +79,60 @@ def test_dropin_read_hdr(demo, tmp_path):
     code, _, _, rows, arr = pyoracle.hdr_decode(open(src, "rb").read())
     assert code == 0 and rows == 289
     assert raw[12:] == arr.tobytes()
+
+
+def _utils_expect(px: np.ndarray):
+    """numpy restatement of the reference's flip (codecs.cpp:162-196), then swapBR (:198-251),
+    then idx at (0,0,0), (h-1,w-1,d-1), (h/2,1,1) on the swapped image."""
+    f = px[::-1].copy()
+    s = f.copy()
+    if s.shape[2] >= 3:
+        s[..., [0, 2]] = s[..., [2, 0]]
+    h, w, d = s.shape
+    pts = [s[0, 0, 0], s[h - 1, w - 1, d - 1], s[h // 2, 1, 1]]
+    return f, s, pts
+
+
+def _utils_read(path, dtype):
+    raw = open(path, "rb").read()
+    w, h, d, bs = np.frombuffer(raw[:16], np.int32)
+    n = w * h * d * bs
+    f = np.frombuffer(raw[16:16 + n], dtype).reshape(h, w, d)
+    s = np.frombuffer(raw[16 + n:16 + 2 * n], dtype).reshape(h, w, d)
+    pts = np.frombuffer(raw[16 + 2 * n:], dtype)
+    return f, s, list(pts)
+
+
+def test_dropin_utils_on_loaded_buffer(demo, tmp_path):
+    """flip / swapBR / idx<T> (codecs.h:80, 82-88, 98) on an adopted UBYTE buffer (no GPU)."""
+    out = str(tmp_path / "u.bin")
+    r = run(demo, "loadutils", out)
+    assert r.returncode == 0, r.stderr
+    px = ((np.arange(60) * 7 + 3) & 255).astype(np.uint8).reshape(3, 5, 4)
+    f, s, pts = _utils_read(out, np.uint8)
+    ef, es, epts = _utils_expect(px)
+    np.testing.assert_array_equal(f, ef)
+    np.testing.assert_array_equal(s, es)
+    assert pts == epts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src", ["test.jpg", "test.hdr"])
+def test_dropin_utils_after_gpu_read(demo, tmp_path, src):
+    """The pixel utilities after a GPU read(): UBYTE (JPEG) and FLOAT (HDR) images."""
+    from oracle import pyoracle
+    out = str(tmp_path / "u.bin")
+    r = run(demo, "utils", os.path.join(GOLDEN, src), out)
+    assert r.returncode == 0, r.stderr
+    data = open(os.path.join(GOLDEN, src), "rb").read()
+    if src.endswith(".jpg"):
+        code, w, h, n, pix = pyoracle.decode(data)
+        px, dt = np.frombuffer(pix, np.uint8).reshape(h, w, n), np.uint8
+    else:
+        code, w, h, rows, arr = pyoracle.hdr_decode(data)
+        px, dt = np.asarray(arr, np.float32).reshape(h, w, 4), np.float32
+    f, s, pts = _utils_read(out, dt)
+    ef, es, epts = _utils_expect(px)
+    np.testing.assert_array_equal(f, ef)
+    np.testing.assert_array_equal(s, es)
+    assert [float(a) for a in pts] == [float(b) for b in epts]
