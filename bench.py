@@ -84,7 +84,9 @@ def _oracle_decode(data):
 
 def cpu_baseline(pool, target_s, cores):
     """Time the oracle (bit-exact CPU restatement of NanoJPEG; the reference is not on the GPU
-    box) on a bounded sample of the same pool: one image per worker process."""
+    box) on a bounded sample of the same pool: one image per worker thread on `cores` cores, then
+    one core alone. The restatement's speed relative to the reference NanoJPEG build is measured
+    in the container (tools/cpu_calibrate.py -> profiles/cpu_calibration.json) and reported."""
     probe_t, _, _, px = _oracle_decode(pool[0])
     per_core = max(1, int(target_s / max(probe_t, 1e-3)))
     sample = [pool[i % len(pool)] for i in range(per_core * cores)]
@@ -99,9 +101,22 @@ def cpu_baseline(pool, target_s, cores):
     hashes = {}
     for s, r in zip(sample, res):
         hashes[hashlib.sha256(s).hexdigest()] = r[2]
-    return {"value": round(mpx / wall, 2), "unit": "megapixels/s", "cores": cores, "kind": "port",
-            "sample": f"{len(sample)} images of the same pool ({len(sample) // cores} per core), oracle/ "
-                      f"NanoJPEG restatement, {wall:.1f} s wall"}, hashes
+    # one core: a third of the budget, whole images in sequence
+    n1 = max(1, int(target_s / 3 / max(probe_t, 1e-3)))
+    t1 = time.perf_counter()
+    res1 = [_oracle_decode(pool[i % len(pool)]) for i in range(n1)]
+    wall1 = time.perf_counter() - t1
+    out = {"value": round(mpx / wall, 2), "unit": "megapixels/s", "cores": cores, "kind": "port",
+           "sample": f"{len(sample)} images of the same pool ({len(sample) // cores} per core), oracle/ "
+                     f"NanoJPEG restatement, {wall:.1f} s wall",
+           "value_1core": round(sum(r[3] for r in res1) / 1e6 / wall1, 2),
+           "sample_1core": f"{n1} images on one core, {wall1:.1f} s"}
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if os.path.exists(cal):
+        c = json.load(open(cal))
+        out["port_over_reference"] = c.get("ratio_4096")
+        out["calibration"] = "profiles/cpu_calibration.json (restatement vs oracle/_ref NanoJPEG, same images, container)"
+    return out, hashes
 
 
 def _oracle_encode(args):
@@ -516,7 +531,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--images", type=int, default=0, help="override images per GPU")
-    ap.add_argument("--pool", type=int, default=16, help="distinct images per rank")
+    ap.add_argument("--pool", type=int, default=64, help="distinct images per rank (SURVEY §8(d): 64)")
     ap.add_argument("--group", type=int, default=0, help="images per workspace group (0=auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0)")
     ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1),
@@ -524,6 +539,25 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive sub-batch (decode workloads)")
     args = ap.parse_args()
+
+    # --gpus N: one rank per GPU. Without a launcher (WORLD_SIZE unset) the bench starts
+    # torch.distributed.run itself -- as a child, before anything touches the GPU -- and exits
+    # with its status; a launcher whose world size differs from --gpus is an error, never a
+    # silent single-rank run.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        import socket
+        import subprocess
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+        sys.exit(subprocess.run(cmd).returncode)
+    if env_world is not None and int(env_world) != args.gpus and "--gpus" in " ".join(sys.argv):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -606,6 +640,27 @@ def main():
     stages = batch.stage_times()  # HIP events on this stream, last step
     paths = batch.path_stats()
 
+    # Final gather: every rank's per-image records {status, w, h, ncomp,
+    # checksum64}, computed on its device (icx_jpeg_records) from the last step's outputs,
+    # gathered over RCCL with padding to the largest shard. Outside the timed region.
+    d_rec = torch.empty(n * 24, dtype=torch.uint8, device=dev)
+    icx.records_device(ctx, n, d_out.data_ptr(), stride, d_st.data_ptr(), d_dims.data_ptr(), W, H, d_rec.data_ptr(),
+                       stream.cuda_stream)
+    r32 = d_rec.view(torch.int32).reshape(n, 6).to(torch.int64)
+    rec = torch.cat([r32[:, :4], ((r32[:, 5] << 32) | (r32[:, 4] & 0xFFFFFFFF))[:, None]], dim=1)
+    allrec, counts = shard.gather_records(rec, dist) if world > 1 else (rec, [n])
+    allrec = allrec.cpu().numpy()
+    # the pool is cycled: every repeat of an image must carry the same checksum (per rank)
+    consistent = True
+    o = 0
+    for r, c in enumerate(counts):
+        cs = allrec[o: o + c, 4]
+        p = min(args.pool, c)
+        consistent &= bool(all((cs[k::p] == cs[k]).all() for k in range(p)))
+        o += c
+    records = {"gathered": int(allrec.shape[0]), "per_rank": counts, "status_ok": bool((allrec[:, 0] == 0).all()),
+               "repeats_consistent": consistent}
+
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -621,9 +676,12 @@ def main():
         for i in range(min(len(pool), n)):
             key = hashlib.sha256(pool[i]).hexdigest()
             if key in cpu_hashes:
-                got = hashlib.sha256(d_out[i * stride: i * stride + W * H * 3].cpu().numpy().tobytes()).hexdigest()
+                img = d_out[i * stride: i * stride + W * H * 3].cpu().numpy()
+                got = hashlib.sha256(img.tobytes()).hexdigest()
                 checked += 1
                 mismatches += got != cpu_hashes[key]
+                # and the gathered record's checksum is that of the oracle-identical pixels
+                mismatches += int(int(allrec[i:i + 1, 4].view(np.uint64)[0]) != shard.checksum64(img))
 
     # PCIe-inclusive rate (rank 0, reported beside `value`, never as it): a bounded sub-batch goes
     # host (pinned) -> HBM, is decoded, and its RGB comes back to pinned host memory, serially
@@ -692,6 +750,7 @@ def main():
         "cpu_baseline": cpu,
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
         "entropy_paths": paths,
+        "records": records,
         "pcie_inclusive": pcie,
         "gen_seconds": round(gen_s, 1),
     }

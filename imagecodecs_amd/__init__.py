@@ -27,7 +27,8 @@ import numpy as np
 __all__ = ["ICXError", "Context", "Batch", "HdrBatch", "Image", "lib", "build", "LIB_PATH",
            "OK", "NO_JPEG", "UNSUPPORTED", "OUT_OF_MEM", "INTERNAL_ERR", "SYNTAX_ERROR",
            "HDR_OK", "HDR_NOT_RADIANCE", "HDR_BAD_HEADER", "HDR_MALFORMED", "HDR_TRUNCATED",
-           "HDR_TOO_LARGE", "HDR_INTERNAL_ERR", "hdr_probe"]
+           "HDR_TOO_LARGE", "HDR_INTERNAL_ERR", "hdr_probe", "Multi", "RECORD_DTYPE", "records_device",
+           "checksum64", "multi_shard"]
 
 OK, NO_JPEG, UNSUPPORTED, OUT_OF_MEM, INTERNAL_ERR, SYNTAX_ERROR = range(6)  # nj_result_t
 RESULT_NAMES = ["NJ_OK", "NJ_NO_JPEG", "NJ_UNSUPPORTED", "NJ_OUT_OF_MEM", "NJ_INTERNAL_ERR", "NJ_SYNTAX_ERROR"]
@@ -94,7 +95,20 @@ _SIGS = {
     "icx_hdr_batch_destroy": (None, [_vp]),
     "icx_hdr_batch_decode": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "icx_hdr_batch_stage_times": (_i32, [_vp, _vp, _vp, _i32]),
+    "icx_jpeg_records": (_i32, [_vp, _i32, _vp, _u64, _vp, _vp, _i32, _i32, _vp, _vp]),
+    "icx_checksum64": (_u64, [_vp, _sz]),
+    "icx_ctx_device": (_i32, [_vp]),
+    "icx_ctx_stream": (_vp, [_vp]),
+    "icx_multi_create": (_vp, [_vp, _i32, _i32, _i32]),
+    "icx_multi_destroy": (None, [_vp]),
+    "icx_multi_decode_host": (_i32, [_vp, _i32, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "icx_multi_last_error": (C.c_char_p, [_vp]),
+    "icx_multi_shard": (_i32, [_vp, _i32, _i32, _vp]),
 }
+
+# icx_record (include/icx.h): per-image result record gathered across devices / ranks
+RECORD_DTYPE = np.dtype([("status", "<i4"), ("width", "<i4"), ("height", "<i4"), ("ncomp", "<i4"),
+                         ("checksum", "<u8")])
 
 # icx_hdr_result (include/icx.h): Image::readHdr outcomes
 HDR_OK, HDR_NOT_RADIANCE, HDR_BAD_HEADER, HDR_MALFORMED, HDR_TRUNCATED, HDR_TOO_LARGE = range(6)
@@ -350,6 +364,77 @@ def probe(jpeg: bytes):
     buf = C.create_string_buffer(bytes(jpeg), max(1, len(jpeg)))
     code = lib().icx_jpeg_probe(buf, len(jpeg), C.byref(w), C.byref(h), C.byref(n))
     return code, w.value, h.value, n.value
+
+
+def records_device(ctx: "Context", n, d_out, out_stride, d_status, d_dims, max_width, max_height, d_records,
+                   stream=0):
+    """icx_jpeg_records: per-image {status, w, h, ncomp, checksum64} of a batch call's outputs,
+    computed on the device into d_records (n x 24 bytes, RECORD_DTYPE)."""
+    rc = lib().icx_jpeg_records(ctx.ptr, n, d_out, out_stride, d_status, d_dims, max_width, max_height, d_records,
+                                stream or None)
+    if rc != OK:
+        raise ICXError(f"icx_jpeg_records -> {rc}: {_err(ctx.ptr)}")
+
+
+def checksum64(data: bytes) -> int:
+    """icx_checksum64 on the host (the records' checksum of a decoded image's bytes)."""
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    return int(lib().icx_checksum64(buf, len(data)))
+
+
+def multi_shard(sizes, ndev: int) -> np.ndarray:
+    """icx_multi_shard: the device index each image goes to (greedy longest-first by size)."""
+    n = len(sizes)
+    sz = (C.c_size_t * max(1, n))(*[int(x) for x in sizes])
+    out = np.zeros(max(1, n), np.int32)
+    if lib().icx_multi_shard(sz, n, ndev, out.ctypes.data) != OK:
+        raise ICXError("icx_multi_shard failed")
+    return out[:n]
+
+
+class Multi:
+    """Multi-GPU decode in one process (icx_multi_*): the batch is split over `devices` by
+    compressed size, one host thread per device, records and pixels gathered to host memory."""
+
+    def __init__(self, devices, max_width: int, max_height: int):
+        devs = (C.c_int * len(devices))(*devices)
+        self._p = lib().icx_multi_create(devs, len(devices), max_width, max_height)
+        if not self._p:
+            raise ICXError("icx_multi_create failed: " + _err(None))
+        self.devices = list(devices)
+        self.max_width, self.max_height = max_width, max_height
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().icx_multi_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+    def decode_host(self, jpegs, want_pixels: bool = True):
+        """-> (records (RECORD_DTYPE array), shard_of (int32 array), pixels list or None)."""
+        n = len(jpegs)
+        stride = self.max_width * self.max_height * 3
+        bufs = [C.create_string_buffer(bytes(j), max(1, len(j))) for j in jpegs]
+        ptrs = (C.c_void_p * max(1, n))(*[C.cast(b, C.c_void_p) for b in bufs])
+        sizes = (C.c_size_t * max(1, n))(*[len(j) for j in jpegs])
+        outs_np = [np.empty(stride, np.uint8) for _ in range(n)] if want_pixels else None
+        outs = (C.c_void_p * max(1, n))(*[o.ctypes.data for o in outs_np]) if want_pixels else None
+        rec = np.zeros(max(1, n), RECORD_DTYPE)
+        shard_of = np.zeros(max(1, n), np.int32)
+        rc = lib().icx_multi_decode_host(self._p, n, ptrs, sizes, outs, stride, rec.ctypes.data, shard_of.ctypes.data)
+        if rc != OK:
+            msg = lib().icx_multi_last_error(self._p)
+            raise ICXError(f"icx_multi_decode_host -> {rc}: {msg.decode() if msg else ''}")
+        pix = None
+        if want_pixels:
+            pix = []
+            for i in range(n):
+                r = rec[i]
+                nb = int(r["width"]) * int(r["height"]) * int(r["ncomp"])
+                pix.append(outs_np[i][:nb] if r["status"] == OK else None)
+        return rec[:n], shard_of[:n], pix
 
 
 class Batch:

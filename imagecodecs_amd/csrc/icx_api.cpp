@@ -142,6 +142,8 @@ void icx_destroy(icx_ctx* c) {
 }
 
 void icx_free(void* p) { std::free(p); }
+int icx_ctx_device(const icx_ctx* c) { return c ? c->device : -1; }
+void* icx_ctx_stream(const icx_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int icx_jpeg_probe(const uint8_t* jpeg, size_t size, int* w, int* h, int* ncomp) {
     if (w) *w = 0;

@@ -126,6 +126,16 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
                          StageHook* hook);
 
+// Per-image result record (icx_records.hip; include/icx.h icx_record): status, dims and the
+// 64-bit weighted word sum of the decoded bytes.
+struct Record {
+    int32_t status, w, h, c;
+    uint64_t checksum;
+};
+static_assert(sizeof(Record) == 24, "icx_record layout");
+void launch_records(int n, const uint8_t* d_out, uint64_t out_stride, const int32_t* d_status, const int32_t* d_dims,
+                    Record* d_rec, int max_w, int max_h, hipStream_t st);
+
 // tiny_jpeg-exact encode on the GPU (icx_encode.hip); `out` receives the whole file.
 bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const uint8_t* src,
                     std::vector<uint8_t>& out);

@@ -113,6 +113,40 @@ int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int
  * Synchronizes with the device. */
 int icx_batch_path_stats(const icx_batch* b, int32_t* parallel, int32_t* fallback, int32_t* sequential);
 
+/* ---- per-image result records and multi-GPU decode ------------- */
+/* The record each device computes for every image it decoded; ranks (or devices) exchange
+ * these 24 bytes per image instead of pixels. checksum = sum of the decoded bytes' little-
+ * endian 32-bit words w_k (last one zero-padded) times (2k + 1), mod 2^64 (icx_checksum64). */
+typedef struct icx_record {
+    int32_t status, width, height, ncomp; /* icx_result; dims as d_dims (0s on error) */
+    uint64_t checksum;                    /* 0 for a failed image */
+} icx_record;
+
+/* Records of a batch call's outputs (device pointers, enqueued on `stream`, NULL = the
+ * context's stream): d_status / d_dims / d_out as icx_jpeg_batch_decode wrote them. */
+int icx_jpeg_records(icx_ctx* ctx, int n, const uint8_t* d_out, uint64_t out_stride, const int32_t* d_status,
+                     const int32_t* d_dims, int max_width, int max_height, icx_record* d_records, void* stream);
+/* The same checksum on the host (a reference for tests and callers). */
+uint64_t icx_checksum64(const uint8_t* data, size_t size);
+int icx_ctx_device(const icx_ctx* ctx);   /* the context's HIP device ordinal */
+void* icx_ctx_stream(const icx_ctx* ctx); /* the context's hipStream_t */
+
+/* Multi-GPU batch decode in one process: the batch is split over `ndev` devices by
+ * compressed size (greedy longest-first, icx_multi_shard), one host thread per device decodes
+ * its shard with its own context, workspace and stream, and the records and pixels are
+ * gathered into host memory. Every image of every device may be up to max_width x max_height. */
+typedef struct icx_multi icx_multi;
+icx_multi* icx_multi_create(const int* devices, int ndev, int max_width, int max_height);
+void icx_multi_destroy(icx_multi* m);
+/* outs[i] (may be NULL, or outs itself NULL: records only) receives image i's packed pixels,
+ * at most out_stride bytes; records[i] its record; shard_of[i] (optional) the index into
+ * `devices` that decoded it. Returns ICX_OK or the first device's call-level error. */
+int icx_multi_decode_host(icx_multi* m, int n, const uint8_t* const* jpegs, const size_t* sizes,
+                          uint8_t* const* outs, uint64_t out_stride, icx_record* records, int32_t* shard_of);
+const char* icx_multi_last_error(const icx_multi* m);
+/* The split: shard_of[i] in [0, ndev) for n images of the given compressed sizes. */
+int icx_multi_shard(const size_t* sizes, int n, int ndev, int32_t* shard_of);
+
 /* ---- encode (tiny_jpeg, jpeg_enc.h:114-160) --------------------------------------- */
 typedef void icx_write_func(void* context, void* data, int size); /* = tje_write_func */
 
