@@ -30,7 +30,8 @@ struct SpecImg {
                            // 3 restart intervals (DRI): one write lane per interval
     int32_t err;           // kSpecSyntax | kSpecGiveUp (atomicOr)
     int32_t ntiles, tile_base;
-    int32_t nwg, wg_base;  // 256-lane decode groups, flat numbering over the batch group
+    int32_t nwg, wg_base;  // 256-lane decode groups; the image's first lane record / 256 (subsequence
+                           // images only: a flat numbering over the batch group's lane records)
     int32_t nsub, nrepair;   // lanes; unsynchronised lanes queued for repair
     int32_t nint, nrst;      // DRI (mode 3): restart intervals; restart markers found in U
     int32_t sub_bytes, pad_; // unstuffed bytes per decode lane (mode 1)

@@ -52,8 +52,8 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
                                                     int64_t upool, int64_t lanes_cap, int sub_bytes) {
     __shared__ int sh[1024];
-    __shared__ int last[5];
-    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0;
+    __shared__ int last[6];
+    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0;
     const int64_t pool_units = upool >> 12, wg_cap = lanes_cap / kLanes;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
         const int i = i0 + threadIdx.x;
@@ -85,14 +85,19 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             nw = (int)min<int64_t>((nsub + kLanes - 1) / kLanes, INT32_MAX / 4);
             nw2 = (int)((nsub + kWriteLanesBig - 1) / kWriteLanesBig);
         }
-        // Capacity: an image whose U units or lane records (DRI with tiny intervals) would pass
-        // the workspace's goes to the sequential kernel. The prefixes count every candidate, so
-        // they bound what the images taken below use.
+        // Capacity: an image whose U units or lane records would pass the workspace's goes to
+        // the sequential kernel. Only subsequence lanes have records (X, rec, sub, ent: a DRI
+        // interval lane needs none), numbered apart from the workgroups. The prefixes count
+        // every candidate, so they bound what the images taken below use.
+        const int nwc = cand && desc[i].restart == 0 ? nw : 0;
         const int eu = block_exclusive_scan(nu, sh);
-        const int ec = block_exclusive_scan(nw, sh);
-        const bool ok = cand && (int64_t)carry_u + eu + nu <= pool_units && (int64_t)carry_c + ec + nw <= wg_cap;
-        if (threadIdx.x == blockDim.x - 1) { last[3] = eu + nu; last[4] = ec + nw; }
+        const int ec = block_exclusive_scan(nwc, sh);
+        const bool ok = cand && (int64_t)carry_u + eu + nu <= pool_units && (int64_t)carry_c + ec + nwc <= wg_cap;
+        if (threadIdx.x == blockDim.x - 1) { last[3] = eu + nu; last[4] = ec + nwc; }
         if (!ok) nt = nw = nw2 = 0;
+        const int nwr = ok ? nwc : 0;
+        const int er = block_exclusive_scan(nwr, sh);
+        if (threadIdx.x == blockDim.x - 1) last[5] = er + nwr;
         if (i < n) {
             const Desc& d = desc[i];
             SpecImg& s = spec[i];
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             wgpre[i] = carry_w + ew;
             wg2pre[i] = carry_w2 + ew2;
             spec[i].tile_base = carry_t + et;
-            spec[i].wg_base = carry_w + ew;
+            spec[i].wg_base = carry_r + er;  // lane records, in 256-lane units
         }
         if (threadIdx.x == blockDim.x - 1) { last[0] = et + nt; last[1] = ew + nw; last[2] = ew2 + nw2; }
         __syncthreads();
@@ -125,6 +130,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         carry_w2 += last[2];
         carry_u = min(carry_u + last[3], INT32_MAX / 4);
         carry_c = min(carry_c + last[4], INT32_MAX / 4);
+        carry_r += last[5];
         __syncthreads();
     }
     if (threadIdx.x == 0) {
