@@ -172,10 +172,12 @@ static int64_t ws_per_slot(GroupWs& ws, int max_w, int max_h) {
     // decode lanes of kSubBytesSmall .. kSubBytes bytes (k_spec_plan picks per image)
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytesSmall - 1) / kSubBytesSmall + kLanes - 1) / kLanes * kLanes + kLanes;
-    return ws.coef_cap * (64 * 2 + 4) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
+    // coefficient pool: 1.25 x coef_cap blocks per slot (int16 block + int32 DC escape + map entry)
+    return ws.coef_cap * 5 / 4 * (64 * 2 + 4 + 8) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
            (int64_t)sizeof(StepSet) +
            tiles_per_slot * 28 + ws.rst_cap * 8 +
-           lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec) + kMaxRepair * 4;
+           lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec + (int64_t)sizeof(GwOut) +
+                             (int64_t)sizeof(GcRec) + 8) + kMaxRepair * 4;
 }
 
 static void ws_free(GroupWs& ws) {
@@ -183,7 +185,8 @@ static void ws_free(GroupWs& ws) {
                     (void*)ws.tilepre, (void*)ws.wgpre, (void*)ws.wg2pre, (void*)ws.totals, (void*)ws.tiles,
                     (void*)ws.tile_obase, (void*)ws.U, (void*)ws.X, (void*)ws.sub, (void*)ws.rst, (void*)ws.tile_rbase,
                     (void*)ws.ent, (void*)ws.stats, (void*)ws.Y, (void*)ws.rec, (void*)ws.nrec, (void*)ws.guess_cnt,
-                    (void*)ws.repair, (void*)ws.steps})
+                    (void*)ws.repair, (void*)ws.steps, (void*)ws.map, (void*)ws.chunk_next, (void*)ws.pool_next,
+                    (void*)ws.gw, (void*)ws.crec, (void*)ws.clist, (void*)ws.clist_n})
         if (p) (void)hipFree(p);
     ws = GroupWs{};
 }
@@ -206,8 +209,14 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     // the sequential kernel)
     ws.upool = (int64_t)(group + 2) * ws.ucap;
     ICX_HIP(ctx, hipMalloc(&ws.desc, sizeof(Desc) * group), false);
-    ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)ws.coef_cap * 64 * 2 * group), false);
-    ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)ws.coef_cap * 4 * group), false);
+    // the coefficient pool (k_spec_plan places each image in it; the guess-write lanes' overflow
+    // chunks and count blocks take its tail), + kGwChunk scratch blocks past pool_cap
+    ws.pool_cap = (int64_t)(group + 2) * ws.coef_cap * 5 / 4;
+    ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)(ws.pool_cap + kGwChunk) * 64 * 2), false);
+    ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)(ws.pool_cap + kGwChunk) * 4), false);
+    ICX_HIP(ctx, hipMalloc(&ws.map, (size_t)ws.pool_cap * sizeof(uint2)), false);
+    ICX_HIP(ctx, hipMalloc(&ws.chunk_next, (size_t)(ws.pool_cap / kGwChunk + 2) * 4), false);
+    ICX_HIP(ctx, hipMalloc(&ws.pool_next, sizeof(unsigned long long)), false);
     ICX_HIP(ctx, hipMalloc(&ws.planes, (size_t)ws.plane_cap * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), false);
     ws.tiles_cap = tiles_per_slot * (group + 2);
@@ -233,6 +242,10 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ICX_HIP(ctx, hipMalloc(&ws.guess_cnt, sizeof(int32_t) * 4 * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.repair, sizeof(int32_t) * kMaxRepair * group), false);
     ICX_HIP(ctx, hipMalloc(&ws.steps, sizeof(StepSet) * group), false);
+    ICX_HIP(ctx, hipMalloc(&ws.gw, sizeof(GwOut) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.crec, sizeof(GcRec) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.clist, sizeof(int2) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipMalloc(&ws.clist_n, sizeof(int32_t)), false);
     return true;
 }
 

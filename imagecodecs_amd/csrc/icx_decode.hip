@@ -55,15 +55,14 @@ __global__ __launch_bounds__(64) void k_parse(int n, const uint8_t* __restrict__
 // every image the parallel path (icx_spec.hip) does not finish: restart-interval streams,
 // exotic sampling, oversized scans, and chains that failed verification.
 __global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
-                              Desc* __restrict__ desc, int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
-                              int64_t coef_cap) {
+                              Desc* __restrict__ desc, int16_t* __restrict__ ac, int32_t* __restrict__ dcv) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Desc& d = desc[i];
     if (d.status != kPending) return;
     RawBits b{data + off[i] + d.scan_off, d.size - d.scan_off, 0u, 0, 0};
-    int16_t* A = ac + (int64_t)i * coef_cap * 64;
-    int32_t* D = dcv + (int64_t)i * coef_cap;
+    int16_t* A = ac + d.acbase * 64;  // (in place: the pool region k_spec_plan gave the image)
+    int32_t* D = dcv + d.acbase;
     int32_t pred[3] = {0, 0, 0};
     int left = d.restart, expect = 0;
     const int64_t nmcu = (int64_t)d.mbw * d.mbh;
@@ -145,8 +144,8 @@ struct IdctGeo {
 constexpr int kIdctU = 4;
 constexpr int kIdctUnitBlocks = 64;
 __global__ __launch_bounds__(256) void k_idct_any(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
-                                              const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
-                                              int64_t coef_cap, int64_t plane_cap) {
+                                              const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                              uint8_t* __restrict__ planes, int64_t plane_cap) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     if (d.status != kOk || d.bpm <= kIdctUnitBlocks) return;  // k_idct takes those
@@ -176,8 +175,6 @@ __global__ __launch_bounds__(256) void k_idct_any(const Desc* __restrict__ desc,
 #pragma unroll
     for (int j = 0; j < 8; ++j) zo[j] = 2u * kZigOfNat[r * 8 + j];
     const uint8_t* zrow = reinterpret_cast<const uint8_t*>(&zzb[wave][lb][0]);
-    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
-    const int32_t* D = dcv + (int64_t)img * coef_cap;
     uint8_t* P = planes + (int64_t)img * plane_cap;
     const bool small_mcu = bpm <= kSpecMaxBpm;
     // XCD-aware order: workgroups dispatched to one XCD (linear id % 8, gridDim.x a multiple of
@@ -186,10 +183,12 @@ __global__ __launch_bounds__(256) void k_idct_any(const Desc* __restrict__ desc,
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
     for (uint32_t o0 = wid * kIdctU; o0 < noct; o0 += nw * kIdctU) {
         int4 c[kIdctU];
+        BlkLoc loc[kIdctU];
 #pragma unroll
         for (int u = 0; u < kIdctU; ++u) {
             const uint32_t n = (o0 + u) * 8 + lb;
-            c[u] = n < nblocks ? *reinterpret_cast<const int4*>(A + (int64_t)n * 64 + r * 8) : make_int4(0, 0, 0, 0);
+            loc[u] = blk_loc(d, map, n < nblocks ? n : 0);
+            c[u] = n < nblocks ? *reinterpret_cast<const int4*>(ac + loc[u].blk * 64 + r * 8) : make_int4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int u = 0; u < kIdctU; ++u) {
@@ -214,7 +213,7 @@ __global__ __launch_bounds__(256) void k_idct_any(const Desc* __restrict__ desc,
             int32_t v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = m24(s[j], qn[g.ci][r * 8 + j]);  // int16 x 8-bit: exact
-            if (r == 0 && s[0] == kDcEscape && live) v[0] = wmul(D[n], qn[g.ci][0]);  // DC outside int16
+            if (r == 0 && live) v[0] = wmul(blk_dc(s[0], dcv, loc[u]), qn[g.ci][0]);  // absolute DC (pool cell + offset)
             if (idct_fast_ok(v)) idct_row<true>(v);
             else idct_row<false>(v);
 #pragma unroll
@@ -340,8 +339,8 @@ struct IdctComp {
     int32_t stride, mx, my, cpr;  // plane stride, MCU pitch (px), 8-byte chunks per unit row
 };
 __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
-                                              const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
-                                              int64_t coef_cap, int64_t plane_cap, int fuse) {
+                                              const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                              uint8_t* __restrict__ planes, int64_t plane_cap, int fuse) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     // (bpm is 0 for a descriptor without a frame header: nothing to transform)
@@ -393,8 +392,6 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
     int4* zzw = reinterpret_cast<int4*>(&rows[wave][0][0][0]);  // this wave's [8][8] stage
     const uint8_t* zrow = reinterpret_cast<const uint8_t*>(zzw + lb * 8);
     uint8_t* pb = reinterpret_cast<uint8_t*>(&pixu[wave][0]);
-    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
-    const int32_t* D = dcv + (int64_t)img * coef_cap;
     uint8_t* P = planes + (int64_t)img * plane_cap;
     const uint32_t ucols = (uint32_t)((mbw + kum - 1) / kum), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
@@ -406,10 +403,12 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
         const uint32_t b0 = ((uint32_t)mby * (uint32_t)mbw + mbx0) * (uint32_t)bpm;  // first block
         for (int o0 = 0; o0 < noct; o0 += kIdctU) {
             int4 c[kIdctU];
+            BlkLoc loc[kIdctU];
 #pragma unroll
             for (int k = 0; k < kIdctU; ++k) {
                 const int q = (o0 + k) * 8 + lb;
-                c[k] = q < nb ? *reinterpret_cast<const int4*>(A + (int64_t)(b0 + q) * 64 + r * 8) : make_int4(0, 0, 0, 0);
+                loc[k] = blk_loc(d, map, b0 + (q < nb ? q : 0));
+                c[k] = q < nb ? *reinterpret_cast<const int4*>(ac + loc[k].blk * 64 + r * 8) : make_int4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int k = 0; k < kIdctU; ++k) {
@@ -426,7 +425,7 @@ __global__ __launch_bounds__(256) void k_idct(const Desc* __restrict__ desc, con
                 int32_t v[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v[j] = m24(s[j], qn[ci][r * 8 + j]);  // int16 x 8-bit: exact
-                if (r == 0 && s[0] == kDcEscape && live) v[0] = wmul(D[b0 + q], qn[ci][0]);  // DC outside int16
+                if (r == 0 && live) v[0] = wmul(blk_dc(s[0], dcv, loc[k]), qn[ci][0]);  // absolute DC (pool cell + offset)
                 if (idct_fast_ok(v)) idct_row<true>(v);
                 else idct_row<false>(v);
 #pragma unroll
@@ -1157,8 +1156,8 @@ __device__ __forceinline__ bool fused420(const Desc& d) {
 // dequant table (zig-zag, 4 bytes per register), h = the lane's half; rowd[r] = pixels 4h..4h+3
 // of row r. D / n: the int32 DC of a block whose cell 0 holds kDcEscape. Wave-level (the fast
 // path is a wave vote): every lane of the wave calls it.
-__device__ __forceinline__ void pair_idct(const int4 (&c)[8], const uint32_t (&qw)[16], int h, const int32_t* D, int64_t n,
-                                          uint32_t (&rowd)[8]) {
+__device__ __forceinline__ void pair_idct(const int4 (&c)[8], const uint32_t (&qw)[16], int h, const int32_t* dcv,
+                                          const BlkLoc& loc, uint32_t (&rowd)[8]) {
     auto qt = [&](int z) { return (int32_t)((qw[z >> 2] >> (8 * (z & 3))) & 0xFFu); };
     auto coef = [&](int z) {
         const int4& w = c[z >> 3];
@@ -1176,14 +1175,16 @@ __device__ __forceinline__ void pair_idct(const int4 (&c)[8], const uint32_t (&q
             const int z0 = kZigOfNatC[8 * i + j], z1 = kZigOfNatC[8 * (4 + i) + j];
             const int32_t v0 = m24(coef(z0), qt(z0)), v1 = m24(coef(z1), qt(z1));  // int16 x 8-bit: exact
             R[i][j] = h ? v1 : v0;
-            hi = max(hi, R[i][j]);
-            lo = min(lo, R[i][j]);
+            if (i != 0 || j != 0) {
+                hi = max(hi, R[i][j]);
+                lo = min(lo, R[i][j]);
+            }
         }
     }
-    if (h == 0 && (int16_t)c[0].x == kDcEscape) {  // DC outside int16 (corrupt streams only)
-        R[0][0] = wmul(D[n], qt(0));
-        hi = INT32_MAX;
-    }
+    // the absolute DC: the pool cell (or its int32 escape) plus the block's offset
+    if (h == 0) R[0][0] = wmul(blk_dc((int16_t)c[0].x, dcv, loc), qt(0));
+    hi = max(hi, R[0][0]);
+    lo = min(lo, R[0][0]);
     const bool fast = __all(hi < (1 << 14) && lo > -(1 << 14));
     if (fast) {
 #pragma unroll
@@ -1244,8 +1245,8 @@ __device__ __forceinline__ void load_qw(const uint8_t* qz, uint32_t (&qw)[16]) {
 // chunks {0,1,2,3,5,6}, rows 4-7 (h = 1) in {1,2,4,5,6,7}. So a lane loads six chunks, and its
 // chunk 0 / 3 slots hold chunks 4 / 7 for h = 1 (pair_idct selects between the halves' values,
 // and a half never reads the other half's private chunks): 6 loads per lane instead of 8.
-__device__ __forceinline__ void load_block(const int16_t* A, int64_t n, int h, int4 (&c)[8]) {
-    const int4* src = reinterpret_cast<const int4*>(A + n * 64);
+__device__ __forceinline__ void load_block(const int16_t* ac, int64_t blk, int h, int4 (&c)[8]) {
+    const int4* src = reinterpret_cast<const int4*>(ac + blk * 64);
     c[0] = src[h ? 4 : 0];
     c[1] = src[1];
     c[2] = src[2];
@@ -1256,35 +1257,40 @@ __device__ __forceinline__ void load_block(const int16_t* A, int64_t n, int h, i
     c[7] = c[3];
 }
 
-// A wave's units wid, wid + nw, ... (wave-uniform loop): unit u's coefficient block is blk(u),
-// transformed and stored by unit(u, c). ICX_IDCT_PF: the next unit's block is loaded while the
-// current one is transformed (two register sets, the loop unrolled by two so neither is copied).
+// A wave's units wid, wid + nw, ... (wave-uniform loop): unit u's coefficient block is at loc(u)
+// (blk_loc: its pool block and DC offset), transformed and stored by unit(u, c, loc).
+// ICX_IDCT_PF: the next unit's block is loaded while the current one is transformed (two
+// register sets, the loop unrolled by two so neither is copied).
 #ifndef ICX_IDCT_PF  // measured: no gain (4:2:0 luma 6.12 -> 6.26 ms; 125 VGPRs, 4 waves/SIMD)
 #define ICX_IDCT_PF 0
 #endif
-template <class BlkF, class UnitF>
-__device__ __forceinline__ void idct_units(const int16_t* A, int h, uint32_t wid, uint32_t nw, uint32_t nunits, BlkF blk,
+template <class LocF, class UnitF>
+__device__ __forceinline__ void idct_units(const int16_t* ac, int h, uint32_t wid, uint32_t nw, uint32_t nunits, LocF locf,
                                            UnitF unit) {
 #if ICX_IDCT_PF
     if (wid >= nunits) return;
     const uint32_t ulast = nunits - 1;
     int4 c0[8], c1[8];
-    load_block(A, blk(wid), h, c0);
+    BlkLoc l0 = locf(wid), l1;
+    load_block(ac, l0.blk, h, c0);
     for (uint32_t u = wid;;) {
-        load_block(A, blk(min(u + nw, ulast)), h, c1);  // (past the end: a harmless reload)
-        unit(u, c0);
+        l1 = locf(min(u + nw, ulast));
+        load_block(ac, l1.blk, h, c1);  // (past the end: a harmless reload)
+        unit(u, c0, l0);
         u += nw;
         if (u >= nunits) break;
-        load_block(A, blk(min(u + nw, ulast)), h, c0);
-        unit(u, c1);
+        l0 = locf(min(u + nw, ulast));
+        load_block(ac, l0.blk, h, c0);
+        unit(u, c1, l1);
         u += nw;
         if (u >= nunits) break;
     }
 #else
     for (uint32_t u = wid; u < nunits; u += nw) {
         int4 c[8];
-        load_block(A, blk(u), h, c);
-        unit(u, c);
+        const BlkLoc l = locf(u);
+        load_block(ac, l.blk, h, c);
+        unit(u, c, l);
     }
 #endif
 }
@@ -1293,8 +1299,8 @@ __device__ __forceinline__ void idct_units(const int16_t* A, int h, uint32_t wid
 // takes Cb of MCU mx0 + q, q >= 16 Cr of MCU mx0 + q - 16, so each plane row of the unit is
 // 128 contiguous bytes written by one store instruction.
 __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
-                                                  const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
-                                                  int64_t coef_cap, int64_t plane_cap) {
+                                                  const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                                  uint8_t* __restrict__ planes, int64_t plane_cap) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     if (!fused420(d)) return;
@@ -1306,29 +1312,27 @@ __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc,
 #pragma unroll
     for (int k = 0; k < 16; ++k) qw[k] = cc ? qb[k] : qw[k];
     const int mbw = d.mbw, stride = d.c[1].stride;
-    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
-    const int32_t* D = dcv + (int64_t)img * coef_cap;
     uint8_t* Pc = planes + (int64_t)img * plane_cap + comp_plane_off(d, 1 + cc);
     const uint32_t ucols = (uint32_t)((mbw + 15) >> 4), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
-    auto blk = [&](uint32_t u) {
+    auto locf = [&](uint32_t u) {
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 4) + mq;
-        return ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + 4 + cc;
+        return blk_loc(d, map, ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + 4 + cc);
     };
-    auto unit = [&](uint32_t u, const int4 (&c)[8]) {
+    auto unit = [&](uint32_t u, const int4 (&c)[8], const BlkLoc& l) {
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 4) + mq;
         uint32_t rowd[8];
-        pair_idct(c, qw, h, D, blk(u), rowd);
+        pair_idct(c, qw, h, dcv, l, rowd);
         if (mx < mbw) {
             uint8_t* dst = Pc + (int64_t)mby * 8 * stride + mx * 8 + 4 * h;
 #pragma unroll
             for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
         }
     };
-    idct_units(A, h, wid, nw, nunits, blk, unit);
+    idct_units(ac, h, wid, nw, nunits, locf, unit);
 }
 
 // Luma planes of fused420 images when the conversion reads them from HBM (ICX_FUSE420 = 2): a
@@ -1336,8 +1340,8 @@ __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc,
 // so each store instruction writes two whole 128-byte plane rows (the unit's upper and lower
 // block rows).
 __global__ __launch_bounds__(256) void k_idct420y(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
-                                                  const int32_t* __restrict__ dcv, uint8_t* __restrict__ planes,
-                                                  int64_t coef_cap, int64_t plane_cap) {
+                                                  const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                                  uint8_t* __restrict__ planes, int64_t plane_cap) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     if (!fused420(d)) return;
@@ -1348,29 +1352,27 @@ __global__ __launch_bounds__(256) void k_idct420y(const Desc* __restrict__ desc,
     uint32_t qw[16];
     load_qw_g(d.q[d.c[0].tq], qw);
     const int mbw = d.mbw, stride = d.c[0].stride;
-    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
-    const int32_t* D = dcv + (int64_t)img * coef_cap;
     uint8_t* Py = planes + (int64_t)img * plane_cap;  // component 0 is first in the slot
     const uint32_t ucols = (uint32_t)((mbw + 7) >> 3), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
-    auto blk = [&](uint32_t u) {
+    auto locf = [&](uint32_t u) {
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 3) + mq;
-        return ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + k;
+        return blk_loc(d, map, ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + k);
     };
-    auto unit = [&](uint32_t u, const int4 (&c)[8]) {
+    auto unit = [&](uint32_t u, const int4 (&c)[8], const BlkLoc& l) {
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 3) + mq;
         uint32_t rowd[8];
-        pair_idct(c, qw, h, D, blk(u), rowd);
+        pair_idct(c, qw, h, dcv, l, rowd);
         if (mx < mbw) {
             uint8_t* dst = Py + ((int64_t)mby * 16 + sby * 8) * stride + mx * 16 + sbx * 8 + 4 * h;
 #pragma unroll
             for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
         }
     };
-    idct_units(A, h, wid, nw, nunits, blk, unit);
+    idct_units(ac, h, wid, nw, nunits, locf, unit);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
@@ -1384,8 +1386,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // from the planes k_idct420c wrote, luma from LDS). No workgroup barriers.
 constexpr int kFB = 4;
 __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
-                                                  const int32_t* __restrict__ dcv, const uint8_t* __restrict__ planes,
-                                                  int64_t coef_cap, int64_t plane_cap, uint8_t* __restrict__ out,
+                                                  const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                                  const uint8_t* __restrict__ planes, int64_t plane_cap, uint8_t* __restrict__ out,
                                                   uint64_t out_stride) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
@@ -1402,8 +1404,6 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
     uint32_t qw[16];
     load_qw(qz, qw);
     const int W = d.W, H = d.H, mbw = d.mbw, mbh = d.mbh;
-    const int16_t* A = ac + (int64_t)img * coef_cap * 64;
-    const int32_t* D = dcv + (int64_t)img * coef_cap;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     const CPl c1{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
     const CPl c2{pslot + comp_plane_off(d, 2), d.c[2].w, d.c[2].h, d.c[2].stride};
@@ -1427,9 +1427,10 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
                 const bool live = mx < mbw;
                 const int64_t n = ((int64_t)mby * mbw + (live ? mx : mbw - 1)) * 6 + k;
                 int4 c[8];
-                load_block(A, n, h, c);
+                const BlkLoc l = blk_loc(d, map, n);
+                load_block(ac, l.blk, h, c);
                 uint32_t rowd[8];
-                pair_idct(c, qw, h, D, n, rowd);
+                pair_idct(c, qw, h, dcv, l, rowd);
                 if (live) {
                     const int lc = mq * 4 + sbx * 2 + h;
 #pragma unroll
@@ -1478,8 +1479,7 @@ void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const 
     E(kStParse);
     launch_spec_entropy(ws, n, d_data, d_off, st, hook);
     B(kStEntropy);
-    hipLaunchKernelGGL(k_entropy_seq, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc,
-                       ws.coef_cap);
+    hipLaunchKernelGGL(k_entropy_seq, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc);
     E(kStEntropy);
 }
 
@@ -1508,19 +1508,19 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
         return (v >= 0 && v <= 2) ? v : 2;
     }();
 #ifndef ICX_EXP_ONLY420  // timing experiment only: the 4:2:0 kernels alone (other samplings undecoded)
-    hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
-                       ws.plane_cap, fuse);
-    hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
+    hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes, ws.plane_cap,
+                       fuse);
+    hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                        ws.plane_cap);
 #endif
     if (fuse) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
         const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;
-        hipLaunchKernelGGL(k_idct420c, dim3(std::max(cgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes,
-                           ws.coef_cap, ws.plane_cap);
+        hipLaunchKernelGGL(k_idct420c, dim3(std::max(cgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map,
+                           ws.planes, ws.plane_cap);
         if (fuse == 2) {
             const int ygx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 8 + 31) / 32, 16384 / n)) & ~7;
-            hipLaunchKernelGGL(k_idct420y, dim3(std::max(ygx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc,
-                               ws.planes, ws.coef_cap, ws.plane_cap);
+            hipLaunchKernelGGL(k_idct420y, dim3(std::max(ygx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map,
+                               ws.planes, ws.plane_cap);
         }
     }
     E(kStIdct);
@@ -1543,7 +1543,7 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
                                                                   ((ws.max_h + 16 * kFB - 1) / (16 * kFB)) + 3) / 4,
                                                                  16384 / n));
     if (fuse == 1)
-        hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.planes, ws.coef_cap,
+        hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap, d_out, out_stride);
 #ifndef ICX_EXP_ONLY420
     hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,

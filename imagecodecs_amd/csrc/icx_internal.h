@@ -34,7 +34,8 @@ struct SpecImg {
                            // images only: a flat numbering over the batch group's lane records)
     int32_t nsub, nrepair;   // lanes; unsynchronised lanes queued for repair
     int32_t nint, nrst;      // DRI (mode 3): restart intervals; restart markers found in U
-    int32_t sub_bytes, pad_; // unstuffed bytes per decode lane (mode 1)
+    int32_t sub_bytes;       // unstuffed bytes per decode lane (mode 1)
+    int32_t gw_S;            // guess-write static pool slots per lane (mode 1)
     int64_t scan_len;      // raw entropy-coded bytes (file end - scan start)
     int64_t ulen;          // unstuffed data bytes before FF D9 / end of file / bad marker
     int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)
@@ -47,6 +48,33 @@ struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };
 // DC codes decoded before it, and the per-component DC-diff sums before it.
 struct RecState { uint32_t rel; int32_t b, cnt; int32_t ds[3]; };
 struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
+
+// ---- guess-write path (icx_spec.hip k_gw_*; icx_spec_core.h gw_*) ----
+// A guess lane decodes with the write tables and stores the blocks that start in its range
+// itself; only lanes not synchronised at their start are decoded again (from the true entry, up
+// to the first state they share with the guess). Blocks go to the group's coefficient pool:
+// kGwStaticSlack x the image's average blocks per lane in a static region per lane, then chunks
+// of kGwChunk blocks taken from the pool's tail by atomic add (flat areas hold thousands of
+// blocks per lane), chained through GroupWs::chunk_next.
+constexpr int kGwChunk = 32;
+constexpr int kGwMaxWalk = 64;  // lanes a repair walk may re-derive before the image goes sequential
+struct GwOut {
+    uint64_t g0;     // first block start at or after the lane's start: pack_state(pos, b, 0)
+    int32_t k;       // blocks the lane stored (slots 0 .. k-1)
+    int32_t ds[3];   // lane-local DC sums over them (predictors relative to g0)
+    int32_t err;     // slot of the first block whose decode failed (INT32_MAX: none)
+    int32_t chunk0;  // first overflow chunk (pool block / kGwChunk), -1: none
+    int32_t nrec;    // block-start records (RecState, b = 0: MCU starts) taken after g0
+    int32_t over;    // the pool ran out: the image goes sequential
+};
+struct GcRec {
+    int64_t rep;     // pool block of the first block the count lane stored
+    int32_t c;       // blocks it stored: the true path from the previous lane's exit to the splice
+    int32_t m;       // guess record it spliced at; -1: none (the c blocks are the whole lane); -2: the
+                     // lane was synchronised at its start (no count decode)
+    int32_t cds[3];  // DC sums over the c blocks
+    int32_t err;     // first of the c blocks whose decode failed (INT32_MAX: none)
+};
 
 // Device workspace for one group of images processed together (slot i = image i of the
 // group). Capacities are per slot and cover any sampling NanoJPEG accepts at max_w x max_h.
@@ -65,8 +93,8 @@ struct GroupWs {
     int64_t plane_cap = 0;   // bytes per slot (all components' IDCT planes)
     int64_t tmp_cap = 0;     // bytes per ping-pong buffer per component per slot
     Desc* desc = nullptr;    // [slots]
-    int16_t* ac = nullptr;   // [slots][coef_cap][64] quantized coefficients, zig-zag order
-    int32_t* dc = nullptr;   // [slots][coef_cap] int32 DC of blocks whose cell holds kDcEscape
+    int16_t* ac = nullptr;   // [pool_cap + kGwChunk][64] coefficient pool: quantized blocks, zig-zag order
+    int32_t* dc = nullptr;   // [pool_cap + kGwChunk] int32 DC of pool blocks whose cell holds kDcEscape
     uint8_t* planes = nullptr;  // [slots][plane_cap]
     uint8_t* tmp = nullptr;     // [slots][3 comps][2 buffers][tmp_cap]
     // parallel entropy decode
@@ -97,7 +125,32 @@ struct GroupWs {
     LaneEntry* ent = nullptr;   // [lanes_cap]
     struct StepSet* steps = nullptr;  // [slots] step tables (icx_step.h), built per group
     int32_t* stats = nullptr;   // [4] path counters, accumulated over a batch call
+    // coefficient pool (Desc::acbase / mapped) and the guess-write path's records
+    int64_t pool_cap = 0;              // pool blocks (+ kGwChunk scratch blocks allocated past it)
+    uint2* map = nullptr;              // [pool_cap] block n of a mapped image: {pool block, DC offset} at acbase + n
+    int32_t* chunk_next = nullptr;     // [pool_cap / kGwChunk + 1] overflow chunk chains
+    unsigned long long* pool_next = nullptr;  // [1] next free pool block (k_spec_plan sets it past the static regions)
+    GwOut* gw = nullptr;               // [lanes_cap]
+    GcRec* crec = nullptr;             // [lanes_cap]
+    int2* clist = nullptr;             // [lanes_cap] (image, lane) of lanes to count-decode
+    int32_t* clist_n = nullptr;        // [1]
 };
+
+// Where block n of an image lives in its group's coefficient pool: the pool block and the offset
+// to add to its DC cell (Desc::acbase / mapped).
+struct BlkLoc {
+    int64_t blk;
+    int32_t dcoff;
+};
+__device__ __forceinline__ BlkLoc blk_loc(const Desc& d, const uint2* map, int64_t n) {
+    if (!d.mapped) return BlkLoc{d.acbase + n, 0};
+    const uint2 e = map[d.acbase + n];
+    return BlkLoc{(int64_t)e.x, (int32_t)e.y};
+}
+// A block's absolute quantized DC: its cell (or the int32 escape) plus the location's offset.
+__device__ __forceinline__ int32_t blk_dc(int16_t cell, const int32_t* dcv, const BlkLoc& l) {
+    return wadd(cell == kDcEscape ? dcv[l.blk] : (int32_t)cell, l.dcoff);
+}
 
 
 int64_t ws_coef_cap(int w, int h);

@@ -147,6 +147,11 @@ struct Desc {
     Comp c[3];
     uint8_t q[4][64];        // DQT tables in zig-zag order (jpeg_dec.h:618-633)
     Huff huff[4];            // 0,1: DC tables; 2,3: AC tables ((Tc|Th>>3)&3, :587)
+    // Where the image's coefficient blocks live in the group's pool (set by k_spec_plan):
+    // block n at pool block acbase + n (mapped == 0), or at the pool block map[acbase + n]
+    // names, with that entry's DC offset (mapped == 1: the guess-write path, icx_spec.hip)
+    int64_t acbase;
+    int32_t mapped, pad_;
 };
 
 // ---------------------------------------------------------------------------------------

@@ -50,10 +50,11 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                     int32_t* __restrict__ tilepre, int32_t* __restrict__ wgpre,
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
-                                                    int64_t upool, int64_t lanes_cap, int sub_bytes) {
+                                                    int64_t upool, int64_t lanes_cap, int sub_bytes, int64_t pool_cap,
+                                                    unsigned long long* __restrict__ pool_next, int gw) {
     __shared__ int sh[1024];
-    __shared__ int last[6];
-    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0;
+    __shared__ int last[7];
+    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0, carry_a = 0;
     const int64_t pool_units = upool >> 12, wg_cap = lanes_cap / kLanes;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
         const int i = i0 + threadIdx.x;
@@ -98,6 +99,16 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         const int nwr = ok ? nwc : 0;
         const int er = block_exclusive_scan(nwr, sh);
         if (threadIdx.x == blockDim.x - 1) last[5] = er + nwr;
+        // Coefficient pool region, whole kGwChunk units: a guess-write image gets nsub lanes x
+        // gw_S static slots (1.1 x its blocks, so a sequential fallback fits too), every other
+        // decodable image its blocks (written in place: k_entropy_seq, the DRI lanes).
+        const int64_t tb = i < n && desc[i].status == kPending ? (int64_t)desc[i].mbw * desc[i].mbh * desc[i].bpm : 0;
+        const bool gwi = gw && ok && desc[i].restart == 0;
+        const int32_t gS = gwi ? (int32_t)((tb * 11 / 10 + nsub - 1) / nsub + 1) : 0;
+        const int64_t region = gwi ? nsub * gS : tb;
+        const int na = (int)min<int64_t>((region + kGwChunk - 1) / kGwChunk, INT32_MAX / 4);
+        const int ea = block_exclusive_scan(na, sh);
+        if (threadIdx.x == blockDim.x - 1) last[6] = ea + na;
         if (i < n) {
             const Desc& d = desc[i];
             SpecImg& s = spec[i];
@@ -107,11 +118,22 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             s.nrst = 0;
             s.sub_bytes = ok ? (int32_t)sb : kSubBytes;
             s.uoff = ((int64_t)carry_u + eu) << 12;
+            s.ulen = 0;
             s.scan_len = ok ? scan_len : 0;
             s.total_blocks = ok ? (int64_t)d.mbw * d.mbh * d.bpm : 0;
             s.nint = ok && s.mode == 3 ? (int32_t)nsub : 0;
             s.ntiles = nt;
             s.nwg = nw;
+            s.gw_S = gS;
+            Desc& dd = desc[i];
+            dd.acbase = ((int64_t)carry_a + ea) * kGwChunk;
+            dd.mapped = gwi;
+            // (cannot happen with the workspace's pool of 1.25 x coef_cap per slot: reported, not written)
+            if (dd.acbase + region > pool_cap && dd.status == kPending) {
+                dd.status = kOutOfMem;
+                s.mode = 0;
+                dd.mapped = 0;
+            }
         }
         const int et = block_exclusive_scan(nt, sh);
         const int ew = block_exclusive_scan(nw, sh);
@@ -131,6 +153,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         carry_u = min(carry_u + last[3], INT32_MAX / 4);
         carry_c = min(carry_c + last[4], INT32_MAX / 4);
         carry_r += last[5];
+        carry_a = min(carry_a + last[6], INT32_MAX / 4);
         __syncthreads();
     }
     if (threadIdx.x == 0) {
@@ -140,6 +163,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         totals[0] = carry_t;
         totals[1] = carry_w;
         totals[2] = carry_w2;
+        *pool_next = (unsigned long long)carry_a * kGwChunk;  // overflow chunks and count blocks from here
     }
 }
 
@@ -399,11 +423,12 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
             while (t + 1 >= imn.t_end) imn.set(imn.i + 1, data, off, desc, spec, tilepre);
             tn.load(imn.R, imn.L, imn.t0(t + 1), lane);
         }
-        ulen = spec[im.i].ulen;
+        ulen = spec[im.i].ulen;  // (0 for an image the plan took off the path: its tiles write nothing)
+        if (spec[im.i].mode != 1 && spec[im.i].mode != 3) ulen = 0;
         if (t == tr.t || ((t - tr.t) & 63) == 0) obv = tr.t + ((t - tr.t) & ~63) + lane < tr.t1 ? tile_obase[t + lane] : 0;
         const int i = im.i;
         const int64_t obase = __shfl(obv, (t - tr.t) & 63);  // == ulen for every tile past the first end event
-        if (obase < ulen) {                                    // wave-uniform
+        if (obase >= 0 && obase < ulen) {                    // wave-uniform
         const uint8_t* R = im.R;
         const int64_t L = im.L;
         const int64_t t0 = im.t0(t);
@@ -676,7 +701,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
                                                     const uint8_t* __restrict__ U,
                                                     const uint64_t* __restrict__ X, const LaneEntry* __restrict__ ent,
                                                     int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
-                                                    int64_t coef_cap, const int64_t* __restrict__ rst, int64_t rst_cap) {
+                                                    const int64_t* __restrict__ rst, int64_t rst_cap) {
     __shared__ WriteTab T;
     __shared__ int4 slots[NL][8];
     __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
@@ -707,8 +732,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         }
         const int64_t base = (int64_t)s.wg_base * kLanes;
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
-        int4* A = reinterpret_cast<int4*>(ac + (int64_t)i * coef_cap * 64);
-        int32_t* D = dcv + (int64_t)i * coef_cap;
+        int4* A = reinterpret_cast<int4*>(ac + desc[i].acbase * 64);  // (in place: the image's pool region)
+        int32_t* D = dcv + desc[i].acbase;
         const int64_t total_blocks = s.total_blocks;
         bool act = j < s.nsub && lane_ok;
         // every lane runs a reader (lanes past the image's last lane idle at position 0)
@@ -856,12 +881,449 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
     }
 }
 
+// ======================================================================= guess-write path
+// The default for images without restart markers (ICX_GW=0 selects the guess / count / write
+// passes above). Each lane decodes once, with the write tables, from `lead` bits before its range
+// and stores the blocks that start in its range itself (k_gw_lane); a lane whose first block start
+// is not its predecessor's exit (not synchronised at its start) is decoded again from that exit
+// up to the first MCU start it shares with the guess (k_gw_check / k_gw_count), and only those
+// blocks are stored twice. The blocks land in the group's coefficient pool in lane order; a map
+// gives the IDCT each block's pool block and DC offset (k_gw_scan, k_gw_map). The per-lane logic
+// is icx_spec_core.h's gw_* / gc_*, which tests/emu/spec_emu.cpp runs lane by lane on the CPU.
+
+// NL lanes per workgroup (the wg2pre numbering: kWriteLanesBig). The loop is k_spec_write's --
+// one lookup per lane per iteration, completed blocks assembled in LDS slots and flushed by the
+// whole wave -- with the guess lane's phases: 0 before the lane's first block start at or after
+// its start (decoded, not stored), 1 storing, 2 done (at the first block start at or after end).
+template <int NL>
+__global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
+                                                const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
+                                                int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
+                                                int32_t* __restrict__ chunk_next, unsigned long long* __restrict__ pool_next,
+                                                int64_t pool_cap, uint64_t* __restrict__ X, GwOut* __restrict__ gwo,
+                                                RecState* __restrict__ rec, int lead) {
+    __shared__ WriteTab T;
+    __shared__ int4 slots[NL][8];
+    __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
+    int cur = -1;
+    const int total = totals[2];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    int4* slot = &slots[threadIdx.x][0];
+    int16_t* sv = reinterpret_cast<int16_t*>(slot);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
+    int4* A = reinterpret_cast<int4*>(ac);
+    const int32_t scratch = (int32_t)pool_cap;  // (a lane the pool could not hold writes here)
+    for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        const int i = wg_image_setup(wpre, n, wg, cur, T, steps);
+        SpecImg& s = spec[i];
+        if (s.mode != 1) continue;  // uniform per workgroup
+        const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
+        const Sel S = make_sel(desc[i]);
+        const Huff* H = desc[i].huff;
+        const bool act = j < s.nsub;
+        const int64_t f = (int64_t)s.wg_base * kLanes + (act ? j : 0);
+        const int64_t sb = (int64_t)s.sub_bytes * 8;
+        const int64_t start = j * sb, end = j == s.nsub - 1 ? s.ulen * 8 : (j + 1) * sb;
+        const int64_t ld = j == 0 ? 0 : (lead >= 0 ? lead : min(kGuessLead, s.sub_bytes * 2));
+        const int64_t s0 = act && start - ld > 0 ? start - ld : 0;
+        const uint32_t kFar = 1u << 30;
+        const uint32_t pre = act ? (uint32_t)(start - s0) : kFar, span = act ? (uint32_t)(end - s0) : kFar;
+        Reader r;
+        r.init(U + s.uoff, s.ulen, s0);
+        ErrBounds eb;
+        eb.set(s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, s0);
+        const int32_t Sst = s.gw_S;
+        const int32_t sbase = (int32_t)(desc[i].acbase + j * Sst);
+        RecState* R = rec + f * kRec;
+        int b = 0, z = 0, ci = 0, phase = 0, nrec = 0;
+        int32_t k = 0, err = INT32_MAX, chunk = -1, chunk0 = -1, over = 0, addr = 0;
+        int32_t ds0 = 0, ds1 = 0, ds2 = 0;
+        uint64_t g0 = 0, xs = 0;
+        while (__any(act && phase < 2)) {
+            // ---- block-start bookkeeping (z == 0): phase changes, MCU-start records, the pool slot
+            const bool bs = z == 0;
+            const uint32_t u = r.used;
+            const bool enter = act && bs && phase == 0 && u >= pre;
+            g0 = enter ? pack_state(s0 + u, b, 0) : g0;
+            phase = enter ? 1 : phase;
+            const bool leave = bs && phase == 1 && u >= span;
+            xs = leave ? pack_state(s0 + u, b, 0) : xs;
+            phase = leave ? 2 : phase;
+            const bool own_bs = bs && phase == 1;
+            if (wave_any(own_bs && b == 0 && nrec < kRec)) {  // MCU start: a splice point for the count lane
+                if (own_bs && b == 0 && nrec < kRec) {
+                    RecState e;
+                    e.rel = u - pre;
+                    e.b = 0;
+                    e.cnt = k;
+                    e.ds[0] = ds0;
+                    e.ds[1] = ds1;
+                    e.ds[2] = ds2;
+                    R[nrec] = e;
+                    ++nrec;
+                }
+            }
+            const bool need = own_bs && k >= Sst && (k - Sst) % kGwChunk == 0;
+            if (wave_any(need)) {  // an overflow chunk from the pool's tail (flat regions)
+                if (need) {
+                    const unsigned long long nb = atomicAdd(pool_next, (unsigned long long)kGwChunk);
+                    if (nb + kGwChunk <= (unsigned long long)pool_cap) {
+                        const int32_t c = (int32_t)(nb / kGwChunk);
+                        if (chunk < 0) chunk0 = c;
+                        else chunk_next[chunk] = c;
+                        chunk = c;
+                    } else {
+                        over = 1;
+                    }
+                }
+            }
+            addr = own_bs ? (k < Sst ? sbase + k : (over ? scratch : chunk * kGwChunk + (k - Sst) % kGwChunk)) : addr;
+            if (wave_any(enter)) {  // the slot holds the decode before the lane's range: clear it
+                if (enter) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
+                }
+            }
+            ci = bs ? S.comp(b) : ci;
+            // ---- one lookup (every lane: the reader moves on idle lanes too, see k_spec_write)
+            const uint32_t u0 = r.used;
+            const int z0 = z;
+            const WriteOut o = write_step(r, T, H, S, b, z, eb.near(u0));
+            const bool own = phase == 1;
+            const bool fail = eb.fail(u0, o.err, r.used);
+            err = own && fail && err == INT32_MAX ? k : err;
+            const bool owndc = own && bs;
+            const int32_t pc = wadd(ci == 0 ? ds0 : (ci == 1 ? ds1 : ds2), o.v1);
+            ds0 = owndc && ci == 0 ? pc : ds0;
+            ds1 = owndc && ci == 1 ? pc : ds1;
+            ds2 = owndc && ci == 2 ? pc : ds2;
+            const int32_t cell = dc_cell(pc);
+            if (owndc && cell == kDcEscape) dcv[addr] = pc;  // lane-local DC outside int16 (rare)
+            const int n1 = o.w1 ? (o.c1 & 63) : min(z0, 63);
+            const int n2 = o.w2 ? (o.c2 & 63) : (o.w1 ? min(o.c1 + 1, 63) : min(z0, 63));
+            sv[slot_elem(threadIdx.x, n2)] = (int16_t)(o.w2 ? o.v2 : 0);
+            sv[slot_elem(threadIdx.x, n1)] = (int16_t)(o.w1 ? (bs ? cell : o.v1) : 0);
+            const bool done = own && z == 0;
+            k += done ? 1 : 0;
+            const uint64_t m = __ballot(done);
+            if (m) {  // wave-uniform: flush the completed blocks, 8 per round
+                if (done) {
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    done_lane[wave][rank] = (uint8_t)lane;
+                }
+                __builtin_amdgcn_wave_barrier();
+                const int cnt = __popcll(m);
+                for (int k0 = 0; k0 < cnt; k0 += 8) {
+                    const int e = k0 + (lane >> 3), q = lane & 7;
+                    const int src = done_lane[wave][min(e, cnt - 1)];
+                    const int bsrc = __shfl(addr, src);
+                    if (e < cnt) {
+                        const int sl = (wave << 6) | src;
+                        int4* sp = &slots[sl][0];
+                        const int sq = q ^ (sl & 7);
+                        typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+                        const int4 v = sp[sq];
+                        const i32x4 vv = {v.x, v.y, v.z, v.w};
+                        __builtin_nontemporal_store(vv, reinterpret_cast<i32x4*>(A) + (int64_t)bsrc * 8 + q);
+                        sp[sq] = make_int4(0, 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
+        if (act) {
+            X[f] = xs;
+            GwOut g;
+            g.g0 = g0;
+            g.k = k;
+            g.ds[0] = ds0;
+            g.ds[1] = ds1;
+            g.ds[2] = ds2;
+            g.err = err;
+            g.chunk0 = chunk0;
+            g.nrec = nrec;
+            g.over = over;
+            gwo[f] = g;
+            if (over) atomicOr(&s.err, kSpecGiveUp);
+        }
+    }
+}
+
+// Lanes whose first block start is not their predecessor's exit: queued for the count decode
+// (one entry per lane, any image); the others are synchronised at their start.
+__global__ __launch_bounds__(256) void k_gw_check(int n, const SpecImg* __restrict__ spec, const int32_t* __restrict__ wpre,
+                                                  const int32_t* __restrict__ totals, const uint64_t* __restrict__ X,
+                                                  const GwOut* __restrict__ gwo, GcRec* __restrict__ crec,
+                                                  int2* __restrict__ clist, int32_t* __restrict__ clist_n) {
+    const int total = totals[1];
+    for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        const int i = find_image(wpre, n, wg);
+        const SpecImg& s = spec[i];
+        if (s.mode != 1) continue;
+        const int64_t j = (int64_t)(wg - wpre[i]) * kLanes + threadIdx.x;
+        if (j >= s.nsub) continue;
+        const int64_t f = (int64_t)s.wg_base * kLanes + j;
+        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
+        GcRec c;
+        c.rep = 0;
+        c.c = 0;
+        c.m = -2;
+        c.cds[0] = c.cds[1] = c.cds[2] = 0;
+        c.err = INT32_MAX;
+        crec[f] = c;
+        if (gwo[f].g0 != entry) {
+            const int q = atomicAdd(clist_n, 1);
+            clist[q] = make_int2(i, (int)j);
+        }
+    }
+}
+
+// Global-memory block sink for the count lanes (gc_write): whole 128-byte blocks zeroed, then
+// the decoded cells.
+struct PoolSink {
+    int16_t* ac;
+    int32_t* dcv;
+    int64_t base;
+    __device__ void begin(int32_t t) {
+        int4* p = reinterpret_cast<int4*>(ac + (base + t) * 64);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) p[q] = make_int4(0, 0, 0, 0);
+    }
+    __device__ void cell(int32_t t, int zz, int32_t v) { ac[(base + t) * 64 + zz] = (int16_t)v; }
+    __device__ void dc(int32_t t, int32_t v) {
+        const int16_t c = dc_cell(v);
+        ac[(base + t) * 64] = c;
+        if (c == kDcEscape) dcv[base + t] = v;
+    }
+};
+
+// One count lane (k_gw_count, k_gw_repair): from the true entry to the splice with the guess lane
+// (or its whole range), storing those blocks; *exit = its own exit when it did not splice.
+__device__ void gw_count_lane(const Desc& d, const SpecImg& s, const StepSet& SS, const uint8_t* U, int64_t j, int64_t f,
+                              uint64_t entry, const GwOut& g, const RecState* rec, int16_t* ac, int32_t* dcv,
+                              unsigned long long* pool_next, int64_t pool_cap, GcRec* crec, uint64_t* exit, int32_t* give_up) {
+    const Sel S = make_sel(d);
+    const int64_t sb = (int64_t)s.sub_bytes * 8;
+    const int64_t start = j * sb, end = j == s.nsub - 1 ? s.ulen * 8 : (j + 1) * sb;
+    GcRec c;
+    c.err = INT32_MAX;
+    c.c = gc_find(U + s.uoff, s.ulen, SS.scan, d.huff, S, entry, start, end, rec, g.nrec, c.cds, &c.m, exit);
+    const unsigned long long nb = c.c ? atomicAdd(pool_next, (unsigned long long)c.c) : 0ull;
+    if (nb + (unsigned long long)c.c > (unsigned long long)pool_cap) {
+        *give_up = 1;
+        c.rep = 0;
+        c.c = 0;
+    } else {
+        c.rep = (int64_t)nb;
+        PoolSink sink{ac, dcv, c.rep};
+        c.err = gc_write(U + s.uoff, s.ulen, SS.write, d.huff, S, entry, c.c,
+                         s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, sink);
+    }
+    crec[f] = c;
+}
+
+// The queued lanes, one per thread (a few percent of all lanes; tables read from global memory).
+__global__ __launch_bounds__(64) void k_gw_count(const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                 const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
+                                                 const uint64_t* __restrict__ X, const GwOut* __restrict__ gwo,
+                                                 const RecState* __restrict__ rec, int16_t* __restrict__ ac,
+                                                 int32_t* __restrict__ dcv, unsigned long long* __restrict__ pool_next,
+                                                 int64_t pool_cap, GcRec* __restrict__ crec, uint64_t* __restrict__ Y,
+                                                 const int2* __restrict__ clist, const int32_t* __restrict__ clist_n,
+                                                 int32_t* __restrict__ repair) {
+    const int nq = *clist_n;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        const int i = clist[q].x;
+        const int64_t j = clist[q].y;
+        SpecImg& s = spec[i];
+        const int64_t f = (int64_t)s.wg_base * kLanes + j;
+        uint64_t ex = 0;
+        int32_t give_up = 0;
+        gw_count_lane(desc[i], s, steps[i], U, j, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, pool_next, pool_cap,
+                      crec, &ex, &give_up);
+        if (give_up) atomicOr(&s.err, kSpecGiveUp);
+        Y[f] = ex;
+        if (crec[f].m < 0 && j + 1 < s.nsub && ex != X[f]) {  // no splice, another exit: repair walk
+            const int r = atomicAdd(&s.nrepair, 1);
+            if (r < kMaxRepair) repair[(int64_t)i * kMaxRepair + r] = (int32_t)j;
+        }
+    }
+}
+
+// Serial repair walks (one thread per image with queued lanes): adopt the count lane's exit and
+// re-derive the following lanes until one is synchronised at its start or splices.
+__global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                  const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
+                                                  uint64_t* __restrict__ X, const uint64_t* __restrict__ Y,
+                                                  const GwOut* __restrict__ gwo, const RecState* __restrict__ rec,
+                                                  int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
+                                                  unsigned long long* __restrict__ pool_next, int64_t pool_cap,
+                                                  GcRec* __restrict__ crec, int32_t* __restrict__ repair) {
+    const int i = blockIdx.x;
+    if (i >= n || threadIdx.x != 0) return;
+    SpecImg& s = spec[i];
+    if (s.mode != 1 || s.nrepair == 0) return;
+    if (s.nrepair > kMaxRepair) { s.mode = 2; return; }
+    int32_t* q = repair + (int64_t)i * kMaxRepair;
+    const int nq = s.nrepair;
+    for (int a = 1; a < nq; ++a) {  // insertion sort (short list)
+        const int32_t v = q[a];
+        int c = a - 1;
+        while (c >= 0 && q[c] > v) { q[c + 1] = q[c]; --c; }
+        q[c + 1] = v;
+    }
+    const int64_t base = (int64_t)s.wg_base * kLanes;
+    int64_t done = -1;
+    for (int a = 0; a < nq; ++a) {
+        const int64_t j = q[a];
+        if (j <= done) continue;
+        X[base + j] = Y[base + j];
+        int64_t k = j + 1;
+        for (int steps_ = 0; k < s.nsub; ++k, ++steps_) {
+            if (steps_ >= kGwMaxWalk) { s.mode = 2; return; }
+            const int64_t f = base + k;
+            if (gwo[f].g0 == X[f - 1]) {
+                GcRec c;
+                c.rep = 0; c.c = 0; c.m = -2; c.cds[0] = c.cds[1] = c.cds[2] = 0; c.err = INT32_MAX;
+                crec[f] = c;
+                break;
+            }
+            uint64_t ex = 0;
+            int32_t give_up = 0;
+            gw_count_lane(desc[i], s, steps[i], U, k, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, pool_next, pool_cap,
+                          crec, &ex, &give_up);
+            if (give_up) { s.mode = 2; return; }
+            if (crec[f].m >= 0 || k + 1 == s.nsub || ex == X[f]) break;
+            X[f] = ex;
+        }
+        done = k;
+    }
+}
+
+// Per image: each lane's first block index and DC predictors (exclusive scans of the lane
+// totals), and the status: a decode failure on the true path before the image's last block is
+// NanoJPEG's syntax error; blocks that run out before the last one (data ends early) or an
+// exhausted pool send the image to the sequential kernel.
+__global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                 const GwOut* __restrict__ gwo, const GcRec* __restrict__ crec,
+                                                 const RecState* __restrict__ rec, LaneEntry* __restrict__ ent) {
+    __shared__ int sh[256];
+    __shared__ int s_cnt, s_d0, s_d1, s_d2;
+    __shared__ int s_bad;
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    SpecImg& s = spec[i];
+    if (s.mode != 1) return;
+    if (s.err & kSpecGiveUp) {
+        if (threadIdx.x == 0) { s.mode = 2; desc[i].mapped = 0; }
+        return;
+    }
+    if (threadIdx.x == 0) s_bad = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)s.wg_base * kLanes;
+    int64_t G = 0;
+    int32_t P0 = 0, P1 = 0, P2 = 0;
+    for (int64_t j0 = 0; j0 < s.nsub; j0 += blockDim.x) {
+        const int64_t j = j0 + threadIdx.x;
+        const bool live = j < s.nsub;
+        int32_t cnt = 0, d[3] = {0, 0, 0}, e = INT32_MAX;
+        if (live) {
+            const GwOut g = gwo[base + j];
+            const GcRec c = crec[base + j];
+            cnt = gw_lane_total(g, c, rec + (base + j) * kRec, d);
+            e = gw_lane_err(g, c, rec + (base + j) * kRec);
+        }
+        // int32 prefix sums (wrap-around adds commute, matching dcpred += diff)
+        const int ec = block_exclusive_scan(cnt, sh);
+        const int e0 = block_exclusive_scan(d[0], sh);
+        const int e1 = block_exclusive_scan(d[1], sh);
+        const int e2 = block_exclusive_scan(d[2], sh);
+        if (live) {
+            LaneEntry le;
+            le.G = G + ec;
+            le.p0 = wadd(P0, e0);
+            le.p1 = wadd(P1, e1);
+            le.p2 = wadd(P2, e2);
+            le.pad = cnt;
+            ent[base + j] = le;
+            if (e != INT32_MAX && le.G + e < s.total_blocks) atomicOr(&s_bad, 1);
+        }
+        if (threadIdx.x == blockDim.x - 1) {
+            s_cnt = ec + cnt;
+            s_d0 = wadd(e0, d[0]);
+            s_d1 = wadd(e1, d[1]);
+            s_d2 = wadd(e2, d[2]);
+        }
+        __syncthreads();
+        G += s_cnt;
+        P0 = wadd(P0, s_d0);
+        P1 = wadd(P1, s_d1);
+        P2 = wadd(P2, s_d2);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (s_bad) s.err |= kSpecSyntax;
+        else if (G < s.total_blocks) { s.mode = 2; desc[i].mapped = 0; }  // NanoJPEG reads on into the padding
+    }
+}
+
+// Per lane: the map entries {pool block, DC offset} of the blocks it owns.
+__global__ __launch_bounds__(256) void k_gw_map(int n, const Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
+                                                const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
+                                                const GwOut* __restrict__ gwo, const GcRec* __restrict__ crec,
+                                                const RecState* __restrict__ rec, const LaneEntry* __restrict__ ent,
+                                                const int32_t* __restrict__ chunk_next, uint2* __restrict__ map) {
+    const int total = totals[1];
+    for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        const int i = find_image(wpre, n, wg);
+        const SpecImg& s = spec[i];
+        if (s.mode != 1 || (s.err & kSpecSyntax)) continue;  // (an image in error shows no pixels)
+        const int64_t j = (int64_t)(wg - wpre[i]) * kLanes + threadIdx.x;
+        if (j >= s.nsub) continue;
+        const Desc& d = desc[i];
+        const Sel S = make_sel(d);
+        const int64_t f = (int64_t)s.wg_base * kLanes + j;
+        const GwOut g = gwo[f];
+        const GcRec c = crec[f];
+        const LaneEntry le = ent[f];
+        const int32_t P[3] = {le.p0, le.p1, le.p2};
+        int32_t Q[3] = {P[0], P[1], P[2]};  // the guess blocks' offsets
+        int32_t m0 = 0, cc = 0;
+        if (c.m >= 0) {
+            const RecState e = rec[f * kRec + c.m];
+            m0 = e.cnt;
+            for (int q = 0; q < 3; ++q) Q[q] = wadd(P[q], wsub(c.cds[q], e.ds[q]));
+        }
+        if (c.m != -2) cc = c.c;
+        GwSlots sl{d.acbase + j * s.gw_S, s.gw_S, -1, 0};
+        const int64_t n1 = min<int64_t>(le.G + le.pad, s.total_blocks);
+        int bm = (int)(le.G % d.bpm);
+        for (int64_t nb = le.G; nb < n1; ++nb) {
+            const int32_t t = (int32_t)(nb - le.G);
+            const int ci = S.comp(bm);
+            bm = bm + 1 == d.bpm ? 0 : bm + 1;
+            uint2 e;
+            if (t < cc) {
+                e = make_uint2((uint32_t)(c.rep + t), (uint32_t)P[ci]);
+            } else {
+                e = make_uint2((uint32_t)sl.addr(t - cc + m0, g.chunk0, chunk_next), (uint32_t)Q[ci]);
+            }
+            map[d.acbase + nb] = e;
+        }
+    }
+}
+
 __global__ void k_spec_finish(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                               int32_t* __restrict__ stats) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SpecImg& s = spec[i];
     if (s.mode == 3 && (s.err & kSpecGiveUp)) s.mode = 2;  // DRI markers not where NanoJPEG reads them
+    if (s.mode != 1) desc[i].mapped = 0;  // the sequential kernel writes in place
     if (s.mode == 1 || s.mode == 3) desc[i].status = (s.err & kSpecSyntax) ? kSyntaxError : kOk;
     // path statistics: [0] parallel path (incl. DRI intervals), [1] parallel -> sequential
     // fallback, [2] sequential only
@@ -882,9 +1344,10 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     // (at least kSubBytesSmall: the lane records are sized for lanes of that length, ws_per_slot)
     static const int sub_env = std::getenv("ICX_SUB_BYTES") ? std::max(kSubBytesSmall, std::atoi(std::getenv("ICX_SUB_BYTES"))) & ~15
                                : std::getenv("ICX_SUB_MAX") ? -(std::max(kSubBytesSmall, std::atoi(std::getenv("ICX_SUB_MAX"))) & ~15) : 0;
+    static const int gw = std::getenv("ICX_GW") ? std::atoi(std::getenv("ICX_GW")) != 0 : 1;
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
-                       ws.totals, ws.upool, ws.lanes_cap, sub_env);
+                       ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw);
     hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
@@ -893,6 +1356,31 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.rst, ws.rst_cap);
     E(kStUnstuff);
+    // Guess-write path (default; ICX_GW=0: guess, count, write)
+    if (gw) {
+        B(kStWrite);
+        hipLaunchKernelGGL(k_gw_lane<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                           ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.X, ws.gw,
+                           ws.rec, lead);
+        E(kStWrite);
+        B(kStEntropy);
+        (void)hipMemsetAsync(ws.clist_n, 0, sizeof(int32_t), st);
+        hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,
+                           ws.clist, ws.clist_n);
+        hipLaunchKernelGGL(k_gw_count, dim3(1024), dim3(64), 0, st, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
+                           ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.clist_n, ws.repair);
+        hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
+                           ws.rec, ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
+        hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent);
+        hipLaunchKernelGGL(k_gw_map, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.gw, ws.crec,
+                           ws.rec, ws.ent, ws.chunk_next, ws.map);
+        E(kStEntropy);
+        B(kStWrite);
+        // restart intervals (DRI): one write lane per interval, 256-lane workgroups
+        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
+                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
+        E(kStWrite);
+    } else {
     B(kStEntropy);
     // guess / count / write: 512-lane workgroups (tables amortised over more lanes), which each
     // image's lanes fill (k_spec_plan); ICX_BIG_WG=0 selects 256-lane ones (experiments)
@@ -918,14 +1406,15 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
         // a few hundred long lanes per image): 256-lane workgroups, which a 512-lane numbering
         // would leave half idle
         hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, 1, n, ws.desc, ws.spec,
-                           ws.wg2pre, ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.wg2pre, ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
     } else {
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 0, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.coef_cap, ws.rst, ws.rst_cap);
+                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
     }
     E(kStWrite);
+    }
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
 }
 

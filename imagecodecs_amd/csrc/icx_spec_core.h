@@ -542,4 +542,130 @@ ICX_HD int64_t repair_walk(const uint8_t* U, int64_t ulen, const ScanTab& T, con
     return k;
 }
 
+// ------------------------------------------------------------------ guess-write path
+// (icx_spec.hip k_gw*; tests/emu/spec_emu.cpp emu_gw_decode runs the same functions lane by lane)
+
+// Error-byte bounds of a lane reading from bit `e0`, as k_spec_write tests them: NanoJPEG fetches
+// bytes to cover a 16-bit peek before each code (jpeg_dec.h:644), so a lookup starting past
+// err_peek fails, a second symbol is only paired while its own peek stays clear (err_pair), and
+// a lookup ending past err_rel fails. Relative to e0, clamped to 2^30 (no error byte).
+struct ErrBounds {
+    uint32_t err_rel;
+    int32_t err_peek, err_pair;
+    ICX_HD void set(int64_t errbits, int64_t e0) {
+        const uint32_t kFar = 1u << 30;
+        const int64_t rel = errbits == INT64_MAX ? (int64_t)kFar : errbits - e0;
+        err_rel = (uint32_t)(rel < 0 ? 0 : (rel > (int64_t)kFar ? (int64_t)kFar : rel));
+        err_peek = (int32_t)err_rel - 16;
+        err_pair = err_peek - WriteTab::kAcBits;
+    }
+    ICX_HD bool near(uint32_t u0) const { return (int32_t)u0 > err_pair; }
+    ICX_HD bool fail(uint32_t u0, bool step_err, uint32_t u1) const {
+        return (int32_t)u0 > err_peek || step_err || u1 > err_rel;
+    }
+};
+
+// Count lane, pass 1 (scan tables): from the true entry (a block start) to the first MCU start
+// the guess lane recorded (splice: *m = its index; the guess lane's blocks from there on are the
+// true ones), or -- no such state -- to the first block start at or after `end` (*m = -1,
+// *exit = that state). Returns the blocks decoded on the way, *cds their DC sums per component.
+ICX_HD int32_t gc_find(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S, uint64_t entry,
+                       int64_t start, int64_t end, const RecState* rec, int nrec, int32_t* cds, int* m,
+                       uint64_t* exit) {
+    Reader r;
+    r.init(U, ulen, st_pos(entry));
+    int b = st_b(entry), z = 0, mi = 0;
+    int32_t cnt = 0, val;
+    cds[0] = cds[1] = cds[2] = 0;
+    for (;;) {
+        if (z == 0) {
+            const int64_t p = r.pos();
+            if (b == 0 && mi < nrec) {
+                while (mi < nrec && (int64_t)rec[mi].rel < p - start) ++mi;
+                if (mi < nrec && (int64_t)rec[mi].rel == p - start) { *m = mi; return cnt; }
+            }
+            if (p >= end) { *m = -1; *exit = pack_state(p, b, 0); return cnt; }
+        }
+        const int ci = S.comp(b);
+        const bool dc = z == 0;
+        scan_step(r, T, H, S, b, z, val);
+        if (dc) {
+            ++cnt;
+            cds[ci] = wadd(cds[ci], val);
+        }
+    }
+}
+
+// Count lane, pass 2 (write tables): the c blocks from `entry` again, stored through `sink`
+// (begin(t): zero block t; cell(t, zz, v): coefficient; dc(t, v): the block's lane-local DC,
+// cumulative from entry). Returns the first block whose decode failed (INT32_MAX: none).
+template <class Sink>
+ICX_HD int32_t gc_write(const uint8_t* U, int64_t ulen, const WriteTab& TW, const Huff* H, const Sel& S, uint64_t entry,
+                        int32_t c, int64_t errbits, Sink& sink) {
+    Reader r;
+    r.init(U, ulen, st_pos(entry));
+    ErrBounds eb;
+    eb.set(errbits, st_pos(entry));
+    int b = st_b(entry), z = 0, ci = 0;
+    int32_t ds[3] = {0, 0, 0}, err = INT32_MAX;
+    for (int32_t t = 0; t < c;) {
+        const bool dc = z == 0;
+        if (dc) {
+            ci = S.comp(b);
+            sink.begin(t);
+        }
+        const uint32_t u0 = r.used;
+        const WriteOut o = write_step(r, TW, H, S, b, z, eb.near(u0));
+        if (eb.fail(u0, o.err, r.used) && err == INT32_MAX) err = t;
+        if (dc) {
+            ds[ci] = wadd(ds[ci], o.v1);
+            sink.dc(t, ds[ci]);
+        } else if (o.w1) {
+            sink.cell(t, o.c1 & 63, o.v1);
+        }
+        if (o.w2) sink.cell(t, o.c2 & 63, o.v2);
+        if (z == 0) ++t;
+    }
+    return err;
+}
+
+// A lane's true totals (blocks it owns, DC sums) from its guess and count records.
+ICX_HD int32_t gw_lane_total(const GwOut& g, const GcRec& c, const RecState* rec, int32_t* ds) {
+    if (c.m == -2) {
+        ds[0] = g.ds[0]; ds[1] = g.ds[1]; ds[2] = g.ds[2];
+        return g.k;
+    }
+    if (c.m < 0) {
+        ds[0] = c.cds[0]; ds[1] = c.cds[1]; ds[2] = c.cds[2];
+        return c.c;
+    }
+    const RecState& e = rec[c.m];
+    for (int q = 0; q < 3; ++q) ds[q] = wadd(c.cds[q], wsub(g.ds[q], e.ds[q]));
+    return c.c + g.k - e.cnt;
+}
+// Block index (lane-relative) of the first true-path decode failure, INT32_MAX if none: the
+// count lane's blocks, then the guess lane's after the splice (its blocks before are not on the
+// true path).
+ICX_HD int32_t gw_lane_err(const GwOut& g, const GcRec& c, const RecState* rec) {
+    if (c.m == -2) return g.err;
+    if (c.err != INT32_MAX) return c.err;
+    if (c.m < 0 || g.err == INT32_MAX) return INT32_MAX;
+    const int32_t m0 = rec[c.m].cnt;
+    return g.err >= m0 ? c.c + (g.err - m0) : INT32_MAX;
+}
+// Pool block of guess slot s of a lane: the static region, then the chained overflow chunks.
+struct GwSlots {
+    int64_t sbase;      // pool block of slot 0
+    int32_t S;          // static slots
+    int32_t chunk;      // current chunk while walking (-1 before the first)
+    int32_t chunk_idx;  // its index in the lane's chain
+    ICX_HD int64_t addr(int32_t s, int32_t chunk0, const int32_t* chunk_next) {
+        if (s < S) return sbase + s;
+        const int32_t q = (s - S) / kGwChunk;
+        if (chunk < 0 || q < chunk_idx) { chunk = chunk0; chunk_idx = 0; }
+        while (chunk_idx < q && chunk >= 0) { chunk = chunk_next[chunk]; ++chunk_idx; }
+        return (int64_t)chunk * kGwChunk + (s - S) % kGwChunk;
+    }
+};
+
 }  // namespace icx

@@ -225,6 +225,256 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
 }
 }
 
+// ---- guess-write path (k_gw_lane / k_gw_check / k_gw_count / k_gw_repair / k_gw_scan / k_gw_map) ----
+// The group's coefficient pool as the kernels address it: zig-zag int16 blocks, int32 DC escapes,
+// overflow chunks chained through chunk_next, taken from `next` upwards.
+struct EmuPool {
+    std::vector<int16_t> coef;
+    std::vector<int32_t> dc;
+    std::vector<int32_t> chunk_next;
+    int64_t next = 0, cap = 0;
+    void init(int64_t blocks, int64_t static_end) {
+        cap = blocks;
+        coef.assign((size_t)blocks * 64, 0x5A5A);  // garbage: every stored block must be written whole
+        dc.assign((size_t)blocks, 0);
+        chunk_next.assign((size_t)(blocks / kGwChunk + 1), -1);
+        next = (static_end + kGwChunk - 1) / kGwChunk * kGwChunk;
+    }
+    int64_t take(int64_t n) {  // the kernels' atomicAdd on the pool counter; -1 when exhausted
+        if (next + n > cap) return -1;
+        const int64_t b = next;
+        next += n;
+        return b;
+    }
+};
+struct EmuSink {
+    EmuPool* P;
+    int64_t base;
+    void begin(int32_t t) { std::memset(&P->coef[(size_t)(base + t) * 64], 0, 128); }
+    void cell(int32_t t, int zz, int32_t v) { P->coef[(size_t)(base + t) * 64 + zz] = (int16_t)v; }
+    void dc(int32_t t, int32_t v) {
+        const int16_t c = dc_cell(v);
+        P->coef[(size_t)(base + t) * 64] = c;
+        if (c == kDcEscape) P->dc[(size_t)(base + t)] = v;
+    }
+};
+
+// One guess-write lane (k_gw_lane's per-lane logic, scalar): decode [start - lead, end) from a
+// guessed block start; from the first block start at or after `start` (g0) store every block
+// started before the first block start at or after `end` (the exit), recording MCU starts.
+static uint64_t emu_gw_lane(const uint8_t* U, int64_t ulen, const WriteTab& TW, const Huff* H, const Sel& S, int64_t start,
+                            int64_t end, int64_t lead, int64_t errbits, int64_t sbase, int32_t Sst, EmuPool& P,
+                            RecState* rec, GwOut& out) {
+    const int64_t s0 = start - lead > 0 ? start - lead : 0;
+    Reader r;
+    r.init(U, ulen, s0);
+    ErrBounds eb;
+    eb.set(errbits, s0);
+    const uint32_t pre = (uint32_t)(start - s0), span = (uint32_t)(end - s0);
+    int b = 0, z = 0, ci = 0, phase = 0;
+    out.k = 0;
+    out.ds[0] = out.ds[1] = out.ds[2] = 0;
+    out.err = INT32_MAX;
+    out.chunk0 = -1;
+    out.nrec = 0;
+    out.over = 0;
+    int32_t chunk = -1;  // current overflow chunk
+    int64_t addr = 0;    // pool block of the block in progress
+    for (;;) {
+        if (z == 0) {
+            const uint32_t u = r.used;
+            if (phase == 0 && u >= pre) {
+                phase = 1;
+                out.g0 = pack_state(s0 + u, b, 0);
+            }
+            if (phase == 1 && u >= span) return pack_state(s0 + u, b, 0);
+            if (phase == 1 && b == 0 && out.nrec < kRec) {
+                RecState& e = rec[out.nrec++];
+                e.rel = u - pre;
+                e.b = 0;
+                e.cnt = out.k;
+                e.ds[0] = out.ds[0]; e.ds[1] = out.ds[1]; e.ds[2] = out.ds[2];
+            }
+            ci = S.comp(b);
+            if (phase == 1) {  // the block's pool slot
+                const int32_t k = out.k;
+                if (k < Sst) {
+                    addr = sbase + k;
+                } else {
+                    if ((k - Sst) % kGwChunk == 0) {
+                        const int64_t nb = P.take(kGwChunk);
+                        if (nb < 0) { out.over = 1; addr = P.cap - 1; }  // (the kernels write a scratch block)
+                        else {
+                            const int32_t c = (int32_t)(nb / kGwChunk);
+                            if (chunk < 0) out.chunk0 = c;
+                            else P.chunk_next[chunk] = c;
+                            chunk = c;
+                        }
+                    }
+                    if (!out.over) addr = (int64_t)chunk * kGwChunk + (k - Sst) % kGwChunk;
+                }
+                std::memset(&P.coef[(size_t)addr * 64], 0, 128);
+            }
+        }
+        const bool dc = z == 0;
+        const uint32_t u0 = r.used;
+        const WriteOut o = write_step(r, TW, H, S, b, z, eb.near(u0));
+        if (phase == 1) {
+            if (eb.fail(u0, o.err, r.used) && out.err == INT32_MAX) out.err = out.k;
+            int16_t* blk = &P.coef[(size_t)addr * 64];
+            if (dc) {
+                out.ds[ci] = wadd(out.ds[ci], o.v1);
+                blk[0] = dc_cell(out.ds[ci]);
+                if (blk[0] == kDcEscape) P.dc[(size_t)addr] = out.ds[ci];
+            } else if (o.w1) {
+                blk[o.c1 & 63] = (int16_t)o.v1;
+            }
+            if (o.w2) blk[o.c2 & 63] = (int16_t)o.v2;
+            if (z == 0) ++out.k;
+        }
+    }
+}
+
+static int64_t g_gw_stats[8];  // lanes, synced at start, count lanes, spliced, repaired, overflow chunks, pool used
+
+extern "C" {
+
+// The guess-write path end to end on the CPU. Returns like emu_spec_decode; static_frac scales
+// the static slots per lane (k_spec_plan's kGwStaticSlack; small values force overflow chunks).
+int emu_gw_decode(const uint8_t* file, int64_t size, int sub_bytes, int64_t lead, double static_frac, int16_t* coef,
+                  int32_t* dcout, int64_t cap_blocks, int64_t* nblocks, int32_t* status, int64_t* stats /*[8]*/) {
+    auto dp = std::make_unique<Desc>();
+    Desc& d = *dp;
+    *status = parse_headers(file, size, d);
+    *nblocks = 0;
+    const int64_t scan_len = d.size - d.scan_off;
+    if (!(d.status == kPending && d.restart == 0 && d.nc >= 1 && d.bpm <= kSpecMaxBpm && scan_len > 0)) return 2;
+    const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
+    *nblocks = total;
+    if (total > cap_blocks) return 2;
+    const uint8_t* R = file + d.scan_off;
+    std::vector<uint8_t> U;
+    int64_t errpos;
+    int32_t giveup = 0;
+    const int64_t ulen = emu_unstuff(R, scan_len, ustf_align(R), U, errpos, giveup, nullptr);
+    if (giveup) return 1;
+    const int64_t errbits = errpos == INT64_MAX ? INT64_MAX : errpos * 8;
+    auto SSp = std::make_unique<StepSet>();
+    StepSet& SS = *SSp;
+    for (int k = 0; k < ScanTab::entries(); ++k) SS.scan.fill(d.huff, k);
+    for (int k = 0; k < WriteTab::entries(); ++k) SS.write.fill(d.huff, k);
+    const Sel SL = make_sel(d);
+    set_block_sel(SS.scan, d.huff, SL);
+    set_block_sel(SS.write, d.huff, SL);
+    const Huff* H = d.huff;
+    const int64_t sb = (int64_t)sub_bytes * 8;
+    const int64_t nsub = ulen > 0 ? (ulen + sub_bytes - 1) / sub_bytes : 1;
+    auto lane_end = [&](int64_t j) { return j == nsub - 1 ? ulen * 8 : (j + 1) * sb; };
+    const int32_t Sst = (int32_t)std::max<double>(1.0, static_frac * (double)total / (double)nsub + 1.0);
+    EmuPool P;
+    P.init(nsub * Sst + 4 * total + 64 * nsub + 1024, nsub * Sst);
+    // ---- k_gw_lane
+    std::vector<uint64_t> X(nsub);
+    std::vector<GwOut> g(nsub);
+    std::vector<RecState> rec(nsub * kRec);
+    for (int64_t j = 0; j < nsub; ++j) {
+        X[j] = emu_gw_lane(U.data(), ulen, SS.write, H, SL, j * sb, lane_end(j), j ? lead : 0, errbits, j * Sst, Sst, P,
+                           &rec[j * kRec], g[j]);
+        if (g[j].over) return 1;
+    }
+    // ---- k_gw_check + k_gw_count: lanes not synchronised at their start
+    std::vector<GcRec> c(nsub);
+    std::vector<uint64_t> Y(nsub, 0);
+    std::vector<int64_t> queue;
+    auto count_lane = [&](int64_t j, uint64_t entry) -> bool {  // false: pool exhausted
+        GcRec& q = c[j];
+        uint64_t ex = 0;
+        q.c = gc_find(U.data(), ulen, SS.scan, H, SL, entry, j * sb, lane_end(j), &rec[j * kRec], g[j].nrec, q.cds, &q.m, &ex);
+        Y[j] = ex;
+        q.rep = P.take(q.c);
+        if (q.rep < 0) return false;
+        EmuSink sk{&P, q.rep};
+        q.err = gc_write(U.data(), ulen, SS.write, H, SL, entry, q.c, errbits, sk);
+        return true;
+    };
+    int64_t counted = 0, spliced = 0;
+    for (int64_t j = 0; j < nsub; ++j) {
+        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[j - 1];
+        c[j] = GcRec{0, 0, -2, {0, 0, 0}, INT32_MAX};
+        if (g[j].g0 == entry) continue;
+        ++counted;
+        if (!count_lane(j, entry)) return 1;
+        spliced += c[j].m >= 0;
+        if (c[j].m < 0 && j + 1 < nsub && Y[j] != X[j]) queue.push_back(j);
+    }
+    // ---- k_gw_repair: an unspliced count lane whose exit differs re-derives the next lanes
+    int64_t repaired = 0, done = -1;
+    for (int64_t j : queue) {
+        if (j <= done) continue;
+        X[j] = Y[j];
+        int64_t k = j + 1, steps = 0;
+        for (; k < nsub; ++k, ++steps) {
+            if (steps >= kGwMaxWalk) return 1;
+            ++repaired;
+            if (g[k].g0 == X[k - 1]) { c[k] = GcRec{0, 0, -2, {0, 0, 0}, INT32_MAX}; break; }
+            if (!count_lane(k, X[k - 1])) return 1;
+            if (c[k].m >= 0 || k + 1 == nsub || Y[k] == X[k]) break;
+            X[k] = Y[k];
+        }
+        done = k;
+    }
+    // ---- k_gw_scan: lane totals -> first block index and DC predictors; true-path errors
+    std::vector<int64_t> G(nsub + 1, 0);
+    std::vector<int32_t> Pd(3 * nsub, 0);
+    int32_t Pc[3] = {0, 0, 0};
+    bool bad = false;
+    for (int64_t j = 0; j < nsub; ++j) {
+        int32_t ds[3];
+        const int32_t n = gw_lane_total(g[j], c[j], &rec[j * kRec], ds);
+        for (int q = 0; q < 3; ++q) { Pd[3 * j + q] = Pc[q]; Pc[q] = wadd(Pc[q], ds[q]); }
+        const int32_t e = gw_lane_err(g[j], c[j], &rec[j * kRec]);
+        if (e != INT32_MAX && G[j] + e < total) bad = true;
+        G[j + 1] = G[j] + n;
+    }
+    // the blocks run past the data: unless a true-path error already decided the status, the
+    // sequential kernel continues into the 0xFF padding as NanoJPEG does
+    if (G[nsub] < total && !bad) return 1;
+    // ---- k_gw_map + IDCT-side assembly
+    std::vector<int64_t> maddr(total, 0);
+    std::vector<int32_t> moff(total, 0);
+    for (int64_t j = 0; j < nsub; ++j) {
+        GwSlots sl{j * Sst, Sst, -1, 0};
+        const int32_t m0 = c[j].m >= 0 ? rec[j * kRec + c[j].m].cnt : 0;
+        for (int64_t n = G[j]; n < G[j + 1] && n < total; ++n) {
+            const int32_t t = (int32_t)(n - G[j]);
+            const int ci = SL.comp((int)(n % d.bpm));
+            if (t < c[j].c && c[j].m != -2) {
+                maddr[n] = c[j].rep + t;
+                moff[n] = Pd[3 * j + ci];
+            } else {
+                maddr[n] = sl.addr(t - (c[j].m == -2 ? 0 : c[j].c) + m0, g[j].chunk0, P.chunk_next.data());
+                moff[n] = c[j].m >= 0 ? wadd(Pd[3 * j + ci], wsub(c[j].cds[ci], rec[j * kRec + c[j].m].ds[ci]))
+                                      : Pd[3 * j + ci];
+            }
+        }
+    }
+    std::memset(coef, 0, sizeof(int16_t) * 64 * total);
+    for (int64_t n = 0; n < total && !bad; ++n) {
+        const int16_t* blk = &P.coef[(size_t)maddr[n] * 64];
+        const int32_t dl = blk[0] == kDcEscape ? P.dc[(size_t)maddr[n]] : blk[0];
+        dcout[n] = wadd(dl, moff[n]);
+        for (int zz = 1; zz < 64; ++zz) coef[n * 64 + nat_of_zig(zz)] = blk[zz];
+    }
+    *status = bad ? kSyntaxError : kOk;
+    int64_t synced = 0;
+    for (int64_t j = 0; j < nsub; ++j) synced += c[j].m == -2;
+    stats[0] += nsub; stats[1] += synced; stats[2] += counted; stats[3] += spliced; stats[4] += repaired;
+    stats[5] += (P.next - (nsub * Sst + kGwChunk - 1) / kGwChunk * kGwChunk) / kGwChunk;
+    stats[6] += P.next;
+    return 0;
+}
+}
+
 #include <unordered_map>
 extern "C" {
 // Count-pass study (tuning aid): run emu_spec_decode with guess lead `lead` and report the bits

@@ -302,3 +302,73 @@ def test_emulated_parallel_decode_foreign(sub_bytes):
             continue
         modes.append(check(open(os.path.join(GOLDEN, n), "rb").read(), sub_bytes, allow_fallback=False))
     assert modes.count(1) == 0 and modes.count(0) >= 40, modes
+
+
+# ---- guess-write path (icx_spec.hip k_gw_*): the emulator's emu_gw_decode runs the same lane
+# functions (icx_spec_core.h gc_find / gc_write / gw_lane_total / gw_lane_err / GwSlots) ----
+def gw_lib():
+    L = emu_lib()
+    if not hasattr(L, "_gw"):
+        L.emu_gw_decode.restype = C.c_int
+        L.emu_gw_decode.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_double, C.c_void_p, C.c_void_p,
+                                    C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.c_void_p]
+        L._gw = True
+    return L
+
+
+def gw_check(data, sub=256, lead=2048, frac=1.1, cap=1 << 18):
+    coef = np.zeros((cap, 64), np.int16)
+    dc = np.zeros(cap, np.int32)
+    nb, st = C.c_int64(), C.c_int32()
+    stats = np.zeros(8, np.int64)
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    mode = gw_lib().emu_gw_decode(buf, len(data), sub, lead, frac, coef.ctypes.data, dc.ctypes.data, cap, C.byref(nb),
+                                  C.byref(st), stats.ctypes.data)
+    if mode != 0:
+        return mode, stats
+    oc, ocoef, odc = O.decode_trace(data)
+    assert st.value == (0 if oc == 0 else 5), (st.value, oc)
+    if oc == 0:
+        n = nb.value
+        assert np.array_equal(dc[:n], odc) and np.array_equal(coef[:n], ocoef)
+    return mode, stats
+
+
+@pytest.mark.parametrize("sub,lead", [(64, 0), (256, 512), (2048, 2048)])
+def test_gw_goldens(sub, lead):
+    """Every non-DRI golden decodes bit-exact on the guess-write path; only streams whose data
+    ends before the last block without an error (NanoJPEG reads on into the 0xFF padding) go
+    sequential."""
+    modes = {}
+    for n in sorted(MANIFEST):
+        m, _ = gw_check(open(os.path.join(GOLDEN, n), "rb").read(), sub, lead)
+        modes.setdefault(m, []).append(n)
+    assert len(modes.get(0, [])) >= 40
+    assert all("truncated" in n for n in modes.get(1, [])), modes.get(1)
+
+
+@pytest.mark.parametrize("sub,frac", [(256, 1.1), (2048, 1.1), (512, 0.05)])
+def test_gw_foreign_and_overflow_chunks(sub, frac):
+    """Foreign-encoder and crafted streams, with the static slots per lane cut to 5% so most
+    blocks go through chained overflow chunks (GwSlots)."""
+    tot = np.zeros(8, np.int64)
+    for n in sorted(FOREIGN):
+        if FOREIGN[n]["code"] != 0:
+            continue
+        m, st = gw_check(open(os.path.join(GOLDEN, n), "rb").read(), sub, 2048, frac)
+        assert m == 0 or (m == 2 and "rst" in n), n  # (restart-marker streams take the DRI lanes)
+        tot += st
+    assert tot[2] > 0 and tot[3] > 0  # some lanes were count-decoded and spliced
+    if frac < 1:
+        assert tot[5] > 100  # overflow chunks in use
+
+
+@pytest.mark.parametrize("sampling", ["420", "444", "422", "gray", "440", "411"])
+def test_gw_synthetic_random_leads(sampling):
+    rng = np.random.default_rng(abs(hash("gw" + sampling)) % 1000)
+    for k in range(2):
+        w, h = int(rng.integers(40, 500)), int(rng.integers(40, 500))
+        data = S.synth_jpeg(5000 + k, w, h, sampling, int(rng.integers(10, 100)))
+        for sub in (64, 512):
+            m, _ = gw_check(data, sub, int(rng.integers(0, 3000)), float(rng.choice([0.02, 1.1])))
+            assert m == 0
