@@ -33,9 +33,12 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # stage (icx_batch_stage_times) -> the kernel it times
-STAGE_KERNEL = {"write": "k_spec_write", "idct": "k_idct", "convert": "k_convert_stream",
-                "unstuff": "k_ustf_count+k_ustf_scan+k_ustf_write", "entropy": "k_spec_guess+k_spec_count+k_spec_scan",
+STAGE_KERNEL = {"write": "k_gw_lane", "idct": "k_idct420y+k_idct420c", "convert": "k_convert_stream",
+                "unstuff": "k_ustf_count+k_ustf_scan+k_ustf_write",
+                "entropy": "k_gw_check+k_gw_count+k_gw_repair+k_gw_scan+k_gw_map",
                 "parse": "k_parse", "upsample": "k_upsample"}
+if os.environ.get("ICX_GW", "1") == "0":  # the guess / count / write passes (experiments)
+    STAGE_KERNEL.update(write="k_spec_write", entropy="k_spec_guess+k_spec_count+k_spec_scan")
 
 WORKLOADS = {
     "c3": dict(n=512, w=4096, h=4096, sampling="420", quality=90,

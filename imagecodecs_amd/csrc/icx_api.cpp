@@ -186,7 +186,7 @@ static void ws_free(GroupWs& ws) {
                     (void*)ws.tile_obase, (void*)ws.U, (void*)ws.X, (void*)ws.sub, (void*)ws.rst, (void*)ws.tile_rbase,
                     (void*)ws.ent, (void*)ws.stats, (void*)ws.Y, (void*)ws.rec, (void*)ws.nrec, (void*)ws.guess_cnt,
                     (void*)ws.repair, (void*)ws.steps, (void*)ws.map, (void*)ws.chunk_next, (void*)ws.pool_next,
-                    (void*)ws.gw, (void*)ws.crec, (void*)ws.clist, (void*)ws.clist_n})
+                    (void*)ws.gw, (void*)ws.crec, (void*)ws.clist})
         if (p) (void)hipFree(p);
     ws = GroupWs{};
 }
@@ -245,7 +245,6 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ICX_HIP(ctx, hipMalloc(&ws.gw, sizeof(GwOut) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.crec, sizeof(GcRec) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.clist, sizeof(int2) * ws.lanes_cap), false);
-    ICX_HIP(ctx, hipMalloc(&ws.clist_n, sizeof(int32_t)), false);
     return true;
 }
 

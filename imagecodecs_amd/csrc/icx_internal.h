@@ -41,6 +41,7 @@ struct SpecImg {
     int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)
     int64_t total_blocks;
     int64_t uoff;          // byte offset of the image's unstuffed stream in GroupWs::U (4 KiB aligned)
+    int32_t ncount, pad2_; // guess-write lanes queued for the count decode (k_gw_check)
 };
 struct TileRec { int32_t kept, end_err; int64_t end_at; int32_t nrst, pad_; };
 struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };
@@ -132,8 +133,7 @@ struct GroupWs {
     unsigned long long* pool_next = nullptr;  // [1] next free pool block (k_spec_plan sets it past the static regions)
     GwOut* gw = nullptr;               // [lanes_cap]
     GcRec* crec = nullptr;             // [lanes_cap]
-    int2* clist = nullptr;             // [lanes_cap] (image, lane) of lanes to count-decode
-    int32_t* clist_n = nullptr;        // [1]
+    int2* clist = nullptr;             // [lanes_cap] per image, in its lane-record range: (image, lane) to count-decode
 };
 
 // Where block n of an image lives in its group's coefficient pool: the pool block and the offset

@@ -115,6 +115,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             s.mode = ok ? (d.restart == 0 ? 1 : 3) : 0;
             s.err = 0;
             s.nrepair = 0;
+            s.ncount = 0;
             s.nrst = 0;
             s.sub_bytes = ok ? (int32_t)sb : kSubBytes;
             s.uoff = ((int64_t)carry_u + eu) << 12;
@@ -1055,10 +1056,10 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
 
 // Lanes whose first block start is not their predecessor's exit: queued for the count decode
 // (one entry per lane, any image); the others are synchronised at their start.
-__global__ __launch_bounds__(256) void k_gw_check(int n, const SpecImg* __restrict__ spec, const int32_t* __restrict__ wpre,
+__global__ __launch_bounds__(256) void k_gw_check(int n, SpecImg* __restrict__ spec, const int32_t* __restrict__ wpre,
                                                   const int32_t* __restrict__ totals, const uint64_t* __restrict__ X,
                                                   const GwOut* __restrict__ gwo, GcRec* __restrict__ crec,
-                                                  int2* __restrict__ clist, int32_t* __restrict__ clist_n) {
+                                                  int2* __restrict__ clist) {
     const int total = totals[1];
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = find_image(wpre, n, wg);
@@ -1075,9 +1076,9 @@ __global__ __launch_bounds__(256) void k_gw_check(int n, const SpecImg* __restri
         c.cds[0] = c.cds[1] = c.cds[2] = 0;
         c.err = INT32_MAX;
         crec[f] = c;
-        if (gwo[f].g0 != entry) {
-            const int q = atomicAdd(clist_n, 1);
-            clist[q] = make_int2(i, (int)j);
+        if (gwo[f].g0 != entry) {  // the image's list, in its own lane-record range
+            const int q = atomicAdd(&spec[i].ncount, 1);
+            clist[(int64_t)s.wg_base * kLanes + q] = make_int2(i, (int)j);
         }
     }
 }
@@ -1126,25 +1127,31 @@ __device__ void gw_count_lane(const Desc& d, const SpecImg& s, const StepSet& SS
     crec[f] = c;
 }
 
-// The queued lanes, one per thread (a few percent of all lanes; tables read from global memory).
-__global__ __launch_bounds__(64) void k_gw_count(const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
-                                                 const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
-                                                 const uint64_t* __restrict__ X, const GwOut* __restrict__ gwo,
-                                                 const RecState* __restrict__ rec, int16_t* __restrict__ ac,
-                                                 int32_t* __restrict__ dcv, unsigned long long* __restrict__ pool_next,
-                                                 int64_t pool_cap, GcRec* __restrict__ crec, uint64_t* __restrict__ Y,
-                                                 const int2* __restrict__ clist, const int32_t* __restrict__ clist_n,
-                                                 int32_t* __restrict__ repair) {
-    const int nq = *clist_n;
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
-        const int i = clist[q].x;
-        const int64_t j = clist[q].y;
-        SpecImg& s = spec[i];
-        const int64_t f = (int64_t)s.wg_base * kLanes + j;
+// One workgroup per image: its queued lanes (a few percent of all), one per thread, with the
+// image's scan and write tables staged in LDS.
+__global__ __launch_bounds__(256) void k_gw_count(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                  const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
+                                                  const uint64_t* __restrict__ X, const GwOut* __restrict__ gwo,
+                                                  const RecState* __restrict__ rec, int16_t* __restrict__ ac,
+                                                  int32_t* __restrict__ dcv, unsigned long long* __restrict__ pool_next,
+                                                  int64_t pool_cap, GcRec* __restrict__ crec, uint64_t* __restrict__ Y,
+                                                  const int2* __restrict__ clist, int32_t* __restrict__ repair) {
+    __shared__ StepSet SS;
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    SpecImg& s = spec[i];
+    if (s.mode != 1 || s.ncount == 0) return;
+    stage_tab(SS.scan, steps[i].scan);
+    stage_tab(SS.write, steps[i].write);
+    __syncthreads();
+    const int64_t base = (int64_t)s.wg_base * kLanes;
+    for (int q = threadIdx.x; q < s.ncount; q += blockDim.x) {
+        const int64_t j = clist[base + q].y;
+        const int64_t f = base + j;
         uint64_t ex = 0;
         int32_t give_up = 0;
-        gw_count_lane(desc[i], s, steps[i], U, j, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, pool_next, pool_cap,
-                      crec, &ex, &give_up);
+        gw_count_lane(desc[i], s, SS, U, j, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, pool_next, pool_cap, crec, &ex,
+                      &give_up);
         if (give_up) atomicOr(&s.err, kSpecGiveUp);
         Y[f] = ex;
         if (crec[f].m < 0 && j + 1 < s.nsub && ex != X[f]) {  // no splice, another exit: repair walk
@@ -1364,11 +1371,10 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
                            ws.rec, lead);
         E(kStWrite);
         B(kStEntropy);
-        (void)hipMemsetAsync(ws.clist_n, 0, sizeof(int32_t), st);
         hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,
-                           ws.clist, ws.clist_n);
-        hipLaunchKernelGGL(k_gw_count, dim3(1024), dim3(64), 0, st, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
-                           ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.clist_n, ws.repair);
+                           ws.clist);
+        hipLaunchKernelGGL(k_gw_count, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
+                           ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair);
         hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
                            ws.rec, ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
         hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent);

@@ -6,7 +6,7 @@ R="$GRAFT_REPO_ROOT"; [ -n "$R" ] || R=$(pwd)
 cd "$R"
 L="${LABEL:-t}"
 mkdir -p gpurun_out
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > "gpurun_out/${L}_gpu_tests.log" 2>&1 || { tail -40 "gpurun_out/${L}_gpu_tests.log"; exit 1; }
+timeout -k 10 900 python3 -u -m pytest ${PYTEST_ARGS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > "gpurun_out/${L}_gpu_tests.log" 2>&1 || { tail -40 "gpurun_out/${L}_gpu_tests.log"; exit 1; }
 tail -3 "gpurun_out/${L}_gpu_tests.log"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "gpurun_out/${L}_smoke.log" 2>&1
 tail -2 "gpurun_out/${L}_smoke.log"
