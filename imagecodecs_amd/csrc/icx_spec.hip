@@ -892,10 +892,14 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 // gives the IDCT each block's pool block and DC offset (k_gw_scan, k_gw_map). The per-lane logic
 // is icx_spec_core.h's gw_* / gc_*, which tests/emu/spec_emu.cpp runs lane by lane on the CPU.
 
-// NL lanes per workgroup (the wg2pre numbering: kWriteLanesBig). The loop is k_spec_write's --
-// one lookup per lane per iteration, completed blocks assembled in LDS slots and flushed by the
-// whole wave -- with the guess lane's phases: 0 before the lane's first block start at or after
-// its start (decoded, not stored), 1 storing, 2 done (at the first block start at or after end).
+// NL lanes per workgroup (the wg2pre numbering: kWriteLanesBig). Two loops per lane:
+//  1. the lead: from `lead` bits before the lane's start to its first block start at or after
+//     the start (g0), with the scan tables (runs of symbols per lookup; nothing is stored). The
+//     scan tables sit in the LDS the slots use later, so they cost no occupancy.
+//  2. k_spec_write's loop from g0 -- one lookup per lane per iteration, completed blocks
+//     assembled in LDS slots and flushed by the whole wave -- storing every block until the
+//     first block start at or after the lane's end (the exit), recording MCU starts for the
+//     count lanes' splice.
 template <int NL>
 __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                 const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
@@ -905,21 +909,27 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
                                                 int64_t pool_cap, uint64_t* __restrict__ X, GwOut* __restrict__ gwo,
                                                 RecState* __restrict__ rec, int lead) {
     __shared__ WriteTab T;
-    __shared__ int4 slots[NL][8];
+    union SlotsOrScan {  // the lead loop's scan tables, then the write loop's slots
+        ScanTab st;
+        int4 slots[NL][8];
+    };
+    static_assert(sizeof(ScanTab) <= sizeof(int4) * NL * 8, "scan tables fit the slots' LDS");
+    __shared__ SlotsOrScan L;
     __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
     int cur = -1;
     const int total = totals[2];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    int4* slot = &slots[threadIdx.x][0];
+    int4* slot = &L.slots[threadIdx.x][0];
     int16_t* sv = reinterpret_cast<int16_t*>(slot);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
     int4* A = reinterpret_cast<int4*>(ac);
     const int32_t scratch = (int32_t)pool_cap;  // (a lane the pool could not hold writes here)
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = wg_image_setup(wpre, n, wg, cur, T, steps);
         SpecImg& s = spec[i];
         if (s.mode != 1) continue;  // uniform per workgroup
+        __syncthreads();  // (the previous item's slots are done with)
+        stage_tab(L.st, steps[i].scan);
+        __syncthreads();
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         const Sel S = make_sel(desc[i]);
         const Huff* H = desc[i].huff;
@@ -930,29 +940,39 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
         const int64_t ld = j == 0 ? 0 : (lead >= 0 ? lead : min(kGuessLead, s.sub_bytes * 2));
         const int64_t s0 = act && start - ld > 0 ? start - ld : 0;
         const uint32_t kFar = 1u << 30;
-        const uint32_t pre = act ? (uint32_t)(start - s0) : kFar, span = act ? (uint32_t)(end - s0) : kFar;
+        const uint32_t pre = act ? (uint32_t)(start - s0) : 0u, span = act ? (uint32_t)(end - s0) : 0u;
         Reader r;
         r.init(U + s.uoff, s.ulen, s0);
+        int b = 0, z = 0;
+        {  // 1. the lead
+            int32_t v;
+            while (!(z == 0 && r.used >= pre)) scan_step(r, L.st, H, S, b, z, v);
+        }
+        const uint64_t g0 = pack_state(s0 + r.used, b, 0);
+        __syncthreads();  // every wave is done with the scan tables: the slots take their LDS
+#pragma unroll
+        for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
+        __builtin_amdgcn_wave_barrier();
+        r.phase();  // the lead ran a lane-dependent number of lookups
         ErrBounds eb;
         eb.set(s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, s0);
         const int32_t Sst = s.gw_S;
         const int32_t sbase = (int32_t)(desc[i].acbase + j * Sst);
         RecState* R = rec + f * kRec;
-        int b = 0, z = 0, ci = 0, phase = 0, nrec = 0;
+        int ci = 0, nrec = 0;
+        bool live = act;  // storing; false from the exit on (and for lanes past the image's last)
         int32_t k = 0, err = INT32_MAX, chunk = -1, chunk0 = -1, over = 0, addr = 0;
         int32_t ds0 = 0, ds1 = 0, ds2 = 0;
-        uint64_t g0 = 0, xs = 0;
-        while (__any(act && phase < 2)) {
-            // ---- block-start bookkeeping (z == 0): phase changes, MCU-start records, the pool slot
+        uint64_t xs = 0;
+        (void)kFar;
+        // 2. store every block from g0 on
+        while (__any(live)) {
             const bool bs = z == 0;
             const uint32_t u = r.used;
-            const bool enter = act && bs && phase == 0 && u >= pre;
-            g0 = enter ? pack_state(s0 + u, b, 0) : g0;
-            phase = enter ? 1 : phase;
-            const bool leave = bs && phase == 1 && u >= span;
+            const bool leave = live && bs && u >= span;
             xs = leave ? pack_state(s0 + u, b, 0) : xs;
-            phase = leave ? 2 : phase;
-            const bool own_bs = bs && phase == 1;
+            live = live && !leave;
+            const bool own_bs = live && bs;
             if (wave_any(own_bs && b == 0 && nrec < kRec)) {  // MCU start: a splice point for the count lane
                 if (own_bs && b == 0 && nrec < kRec) {
                     RecState e;
@@ -981,21 +1001,14 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
                 }
             }
             addr = own_bs ? (k < Sst ? sbase + k : (over ? scratch : chunk * kGwChunk + (k - Sst) % kGwChunk)) : addr;
-            if (wave_any(enter)) {  // the slot holds the decode before the lane's range: clear it
-                if (enter) {
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
-                }
-            }
             ci = bs ? S.comp(b) : ci;
-            // ---- one lookup (every lane: the reader moves on idle lanes too, see k_spec_write)
+            // one lookup (every lane: the reader moves on idle lanes too, see k_spec_write)
             const uint32_t u0 = r.used;
             const int z0 = z;
             const WriteOut o = write_step(r, T, H, S, b, z, eb.near(u0));
-            const bool own = phase == 1;
             const bool fail = eb.fail(u0, o.err, r.used);
-            err = own && fail && err == INT32_MAX ? k : err;
-            const bool owndc = own && bs;
+            err = live && fail && err == INT32_MAX ? k : err;
+            const bool owndc = own_bs;
             const int32_t pc = wadd(ci == 0 ? ds0 : (ci == 1 ? ds1 : ds2), o.v1);
             ds0 = owndc && ci == 0 ? pc : ds0;
             ds1 = owndc && ci == 1 ? pc : ds1;
@@ -1006,7 +1019,7 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
             const int n2 = o.w2 ? (o.c2 & 63) : (o.w1 ? min(o.c1 + 1, 63) : min(z0, 63));
             sv[slot_elem(threadIdx.x, n2)] = (int16_t)(o.w2 ? o.v2 : 0);
             sv[slot_elem(threadIdx.x, n1)] = (int16_t)(o.w1 ? (bs ? cell : o.v1) : 0);
-            const bool done = own && z == 0;
+            const bool done = live && z == 0;
             k += done ? 1 : 0;
             const uint64_t m = __ballot(done);
             if (m) {  // wave-uniform: flush the completed blocks, 8 per round
@@ -1022,7 +1035,7 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
                     const int bsrc = __shfl(addr, src);
                     if (e < cnt) {
                         const int sl = (wave << 6) | src;
-                        int4* sp = &slots[sl][0];
+                        int4* sp = &L.slots[sl][0];
                         const int sq = q ^ (sl & 7);
                         typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
                         const int4 v = sp[sq];
@@ -1034,8 +1047,6 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
                 __builtin_amdgcn_wave_barrier();
             }
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
         if (act) {
             X[f] = xs;
             GwOut g;
@@ -1129,7 +1140,7 @@ __device__ void gw_count_lane(const Desc& d, const SpecImg& s, const StepSet& SS
 
 // One workgroup per image: its queued lanes (a few percent of all), one per thread, with the
 // image's scan and write tables staged in LDS.
-__global__ __launch_bounds__(256) void k_gw_count(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+__global__ __launch_bounds__(512) void k_gw_count(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                   const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
                                                   const uint64_t* __restrict__ X, const GwOut* __restrict__ gwo,
                                                   const RecState* __restrict__ rec, int16_t* __restrict__ ac,
@@ -1373,7 +1384,7 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
         B(kStEntropy);
         hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,
                            ws.clist);
-        hipLaunchKernelGGL(k_gw_count, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
+        hipLaunchKernelGGL(k_gw_count, dim3(n), dim3(512), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
                            ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair);
         hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
                            ws.rec, ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
