@@ -58,6 +58,8 @@ struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
 // of kGwChunk blocks taken from the pool's tail by atomic add (flat areas hold thousands of
 // blocks per lane), chained through GroupWs::chunk_next.
 constexpr int kGwChunk = 32;
+constexpr int kRecGw = 8;       // MCU starts a guess-write lane records (the count lanes splice at the first
+                                // they reach; the lead synchronises most guess lanes before their first)
 constexpr int kGwMaxWalk = 64;  // lanes a repair walk may re-derive before the image goes sequential
 struct GwOut {
     uint64_t g0;     // first block start at or after the lane's start: pack_state(pos, b, 0)
@@ -69,7 +71,8 @@ struct GwOut {
     int32_t over;    // the pool ran out: the image goes sequential
 };
 struct GcRec {
-    int64_t rep;     // pool block of the first block the count lane stored
+    int32_t chunk0;  // the count lane's blocks: a chain of pool chunks (-1: none)
+    int32_t pad_;
     int32_t c;       // blocks it stored: the true path from the previous lane's exit to the splice
     int32_t m;       // guess record it spliced at; -1: none (the c blocks are the whole lane); -2: the
                      // lane was synchronised at its start (no count decode)

@@ -963,18 +963,21 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
         bool live = act;  // storing; false from the exit on (and for lanes past the image's last)
         int32_t k = 0, err = INT32_MAX, chunk = -1, chunk0 = -1, over = 0, addr = 0;
         int32_t ds0 = 0, ds1 = 0, ds2 = 0;
-        uint64_t xs = 0;
+        uint32_t ul = 0;  // exit: bits read and block-in-MCU there
+        int bl = 0;
+        int32_t left = Sst, nxt = sbase;  // slots left in the current run (static, then chunks), the next one
         (void)kFar;
         // 2. store every block from g0 on
         while (__any(live)) {
             const bool bs = z == 0;
             const uint32_t u = r.used;
             const bool leave = live && bs && u >= span;
-            xs = leave ? pack_state(s0 + u, b, 0) : xs;
+            ul = leave ? u : ul;
+            bl = leave ? b : bl;
             live = live && !leave;
             const bool own_bs = live && bs;
-            if (wave_any(own_bs && b == 0 && nrec < kRec)) {  // MCU start: a splice point for the count lane
-                if (own_bs && b == 0 && nrec < kRec) {
+            if (wave_any(own_bs && b == 0 && nrec < kRecGw)) {  // MCU start: a splice point for the count lane
+                if (own_bs && b == 0 && nrec < kRecGw) {
                     RecState e;
                     e.rel = u - pre;
                     e.b = 0;
@@ -986,7 +989,7 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
                     ++nrec;
                 }
             }
-            const bool need = own_bs && k >= Sst && (k - Sst) % kGwChunk == 0;
+            const bool need = own_bs && left == 0;
             if (wave_any(need)) {  // an overflow chunk from the pool's tail (flat regions)
                 if (need) {
                     const unsigned long long nb = atomicAdd(pool_next, (unsigned long long)kGwChunk);
@@ -995,12 +998,17 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
                         if (chunk < 0) chunk0 = c;
                         else chunk_next[chunk] = c;
                         chunk = c;
+                        nxt = c * kGwChunk;
                     } else {
                         over = 1;
+                        nxt = scratch;
                     }
+                    left = over ? INT32_MAX : kGwChunk;
                 }
             }
-            addr = own_bs ? (k < Sst ? sbase + k : (over ? scratch : chunk * kGwChunk + (k - Sst) % kGwChunk)) : addr;
+            addr = own_bs ? nxt : addr;
+            nxt += own_bs && !over ? 1 : 0;
+            left -= own_bs ? 1 : 0;
             ci = bs ? S.comp(b) : ci;
             // one lookup (every lane: the reader moves on idle lanes too, see k_spec_write)
             const uint32_t u0 = r.used;
@@ -1048,7 +1056,7 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
             }
         }
         if (act) {
-            X[f] = xs;
+            X[f] = pack_state(s0 + ul, bl, 0);
             GwOut g;
             g.g0 = g0;
             g.k = k;
@@ -1081,7 +1089,8 @@ __global__ __launch_bounds__(256) void k_gw_check(int n, SpecImg* __restrict__ s
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
         GcRec c;
-        c.rep = 0;
+        c.chunk0 = -1;
+        c.pad_ = 0;
         c.c = 0;
         c.m = -2;
         c.cds[0] = c.cds[1] = c.cds[2] = 0;
@@ -1094,22 +1103,36 @@ __global__ __launch_bounds__(256) void k_gw_check(int n, SpecImg* __restrict__ s
     }
 }
 
-// Global-memory block sink for the count lanes (gc_write): whole 128-byte blocks zeroed, then
-// the decoded cells.
-struct PoolSink {
+// Global-memory block sink of a count lane (gc_walk): a chain of pool chunks taken by atomic add
+// as the walk goes; whole 128-byte blocks zeroed, then the decoded cells.
+struct ChainSink {
     int16_t* ac;
     int32_t* dcv;
-    int64_t base;
-    __device__ void begin(int32_t t) {
-        int4* p = reinterpret_cast<int4*>(ac + (base + t) * 64);
+    int32_t* chunk_next;
+    unsigned long long* pool_next;
+    int64_t pool_cap;
+    int32_t chunk0, chunk;
+    int64_t cur;
+    __device__ bool begin(int32_t t) {
+        if (t % kGwChunk == 0) {
+            const unsigned long long nb = atomicAdd(pool_next, (unsigned long long)kGwChunk);
+            if (nb + kGwChunk > (unsigned long long)pool_cap) return false;
+            const int32_t c = (int32_t)(nb / kGwChunk);
+            if (chunk < 0) chunk0 = c;
+            else chunk_next[chunk] = c;
+            chunk = c;
+        }
+        cur = (int64_t)chunk * kGwChunk + t % kGwChunk;
+        int4* p = reinterpret_cast<int4*>(ac + cur * 64);
 #pragma unroll
         for (int q = 0; q < 8; ++q) p[q] = make_int4(0, 0, 0, 0);
+        return true;
     }
-    __device__ void cell(int32_t t, int zz, int32_t v) { ac[(base + t) * 64 + zz] = (int16_t)v; }
-    __device__ void dc(int32_t t, int32_t v) {
+    __device__ void cell(int32_t, int zz, int32_t v) { ac[cur * 64 + zz] = (int16_t)v; }
+    __device__ void dc(int32_t, int32_t v) {
         const int16_t c = dc_cell(v);
-        ac[(base + t) * 64] = c;
-        if (c == kDcEscape) dcv[base + t] = v;
+        ac[cur * 64] = c;
+        if (c == kDcEscape) dcv[cur] = v;
     }
 };
 
@@ -1117,24 +1140,18 @@ struct PoolSink {
 // (or its whole range), storing those blocks; *exit = its own exit when it did not splice.
 __device__ void gw_count_lane(const Desc& d, const SpecImg& s, const StepSet& SS, const uint8_t* U, int64_t j, int64_t f,
                               uint64_t entry, const GwOut& g, const RecState* rec, int16_t* ac, int32_t* dcv,
-                              unsigned long long* pool_next, int64_t pool_cap, GcRec* crec, uint64_t* exit, int32_t* give_up) {
+                              int32_t* chunk_next, unsigned long long* pool_next, int64_t pool_cap, GcRec* crec,
+                              uint64_t* exit, int32_t* give_up) {
     const Sel S = make_sel(d);
     const int64_t sb = (int64_t)s.sub_bytes * 8;
     const int64_t start = j * sb, end = j == s.nsub - 1 ? s.ulen * 8 : (j + 1) * sb;
+    ChainSink sink{ac, dcv, chunk_next, pool_next, pool_cap, -1, -1, 0};
     GcRec c;
-    c.err = INT32_MAX;
-    c.c = gc_find(U + s.uoff, s.ulen, SS.scan, d.huff, S, entry, start, end, rec, g.nrec, c.cds, &c.m, exit);
-    const unsigned long long nb = c.c ? atomicAdd(pool_next, (unsigned long long)c.c) : 0ull;
-    if (nb + (unsigned long long)c.c > (unsigned long long)pool_cap) {
-        *give_up = 1;
-        c.rep = 0;
-        c.c = 0;
-    } else {
-        c.rep = (int64_t)nb;
-        PoolSink sink{ac, dcv, c.rep};
-        c.err = gc_write(U + s.uoff, s.ulen, SS.write, d.huff, S, entry, c.c,
-                         s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, sink);
-    }
+    c.pad_ = 0;
+    c.c = gc_walk(U + s.uoff, s.ulen, SS.write, d.huff, S, entry, start, end, rec, g.nrec,
+                  s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, sink, c.cds, &c.m, exit, &c.err);
+    c.chunk0 = sink.chunk0;
+    if (c.m == -3) *give_up = 1;  // the pool ran out
     crec[f] = c;
 }
 
@@ -1144,8 +1161,9 @@ __global__ __launch_bounds__(512) void k_gw_count(int n, const Desc* __restrict_
                                                   const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
                                                   const uint64_t* __restrict__ X, const GwOut* __restrict__ gwo,
                                                   const RecState* __restrict__ rec, int16_t* __restrict__ ac,
-                                                  int32_t* __restrict__ dcv, unsigned long long* __restrict__ pool_next,
-                                                  int64_t pool_cap, GcRec* __restrict__ crec, uint64_t* __restrict__ Y,
+                                                  int32_t* __restrict__ dcv, int32_t* __restrict__ chunk_next,
+                                                  unsigned long long* __restrict__ pool_next, int64_t pool_cap,
+                                                  GcRec* __restrict__ crec, uint64_t* __restrict__ Y,
                                                   const int2* __restrict__ clist, int32_t* __restrict__ repair) {
     __shared__ StepSet SS;
     const int i = blockIdx.x;
@@ -1161,8 +1179,8 @@ __global__ __launch_bounds__(512) void k_gw_count(int n, const Desc* __restrict_
         const int64_t f = base + j;
         uint64_t ex = 0;
         int32_t give_up = 0;
-        gw_count_lane(desc[i], s, SS, U, j, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, pool_next, pool_cap, crec, &ex,
-                      &give_up);
+        gw_count_lane(desc[i], s, SS, U, j, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, chunk_next, pool_next, pool_cap,
+                      crec, &ex, &give_up);
         if (give_up) atomicOr(&s.err, kSpecGiveUp);
         Y[f] = ex;
         if (crec[f].m < 0 && j + 1 < s.nsub && ex != X[f]) {  // no splice, another exit: repair walk
@@ -1179,8 +1197,8 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
                                                   uint64_t* __restrict__ X, const uint64_t* __restrict__ Y,
                                                   const GwOut* __restrict__ gwo, const RecState* __restrict__ rec,
                                                   int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
-                                                  unsigned long long* __restrict__ pool_next, int64_t pool_cap,
-                                                  GcRec* __restrict__ crec, int32_t* __restrict__ repair) {
+                                                  int32_t* __restrict__ chunk_next, unsigned long long* __restrict__ pool_next,
+                                                  int64_t pool_cap, GcRec* __restrict__ crec, int32_t* __restrict__ repair) {
     const int i = blockIdx.x;
     if (i >= n || threadIdx.x != 0) return;
     SpecImg& s = spec[i];
@@ -1206,14 +1224,14 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
             const int64_t f = base + k;
             if (gwo[f].g0 == X[f - 1]) {
                 GcRec c;
-                c.rep = 0; c.c = 0; c.m = -2; c.cds[0] = c.cds[1] = c.cds[2] = 0; c.err = INT32_MAX;
+                c.chunk0 = -1; c.pad_ = 0; c.c = 0; c.m = -2; c.cds[0] = c.cds[1] = c.cds[2] = 0; c.err = INT32_MAX;
                 crec[f] = c;
                 break;
             }
             uint64_t ex = 0;
             int32_t give_up = 0;
-            gw_count_lane(desc[i], s, steps[i], U, k, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, pool_next, pool_cap,
-                          crec, &ex, &give_up);
+            gw_count_lane(desc[i], s, steps[i], U, k, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, chunk_next, pool_next,
+                          pool_cap, crec, &ex, &give_up);
             if (give_up) { s.mode = 2; return; }
             if (crec[f].m >= 0 || k + 1 == s.nsub || ex == X[f]) break;
             X[f] = ex;
@@ -1222,6 +1240,7 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
     }
 }
 
+constexpr int kMapChain = 384;  // chunks per chain k_gw_map stages: a lane of 2560 B holds at most ~10K blocks
 // Per image: each lane's first block index and DC predictors (exclusive scans of the lane
 // totals), and the status: a decode failure on the true path before the image's last block is
 // NanoJPEG's syntax error; blocks that run out before the last one (data ends early) or an
@@ -1231,7 +1250,7 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
                                                  const RecState* __restrict__ rec, LaneEntry* __restrict__ ent) {
     __shared__ int sh[256];
     __shared__ int s_cnt, s_d0, s_d1, s_d2;
-    __shared__ int s_bad;
+    __shared__ int s_bad, s_long;
     const int i = blockIdx.x;
     if (i >= n) return;
     SpecImg& s = spec[i];
@@ -1240,7 +1259,7 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
         if (threadIdx.x == 0) { s.mode = 2; desc[i].mapped = 0; }
         return;
     }
-    if (threadIdx.x == 0) s_bad = 0;
+    if (threadIdx.x == 0) s_bad = s_long = 0;
     __syncthreads();
     const int64_t base = (int64_t)s.wg_base * kLanes;
     int64_t G = 0;
@@ -1254,6 +1273,8 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
             const GcRec c = crec[base + j];
             cnt = gw_lane_total(g, c, rec + (base + j) * kRec, d);
             e = gw_lane_err(g, c, rec + (base + j) * kRec);
+            // (chains longer than k_gw_map's LDS holds: only with lanes far beyond kSubBytes)
+            if (g.k - s.gw_S > kMapChain * kGwChunk || (c.m != -2 && c.c > kMapChain * kGwChunk)) atomicOr(&s_long, 1);
         }
         // int32 prefix sums (wrap-around adds commute, matching dcpred += diff)
         const int ec = block_exclusive_scan(cnt, sh);
@@ -1285,31 +1306,34 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
     }
     if (threadIdx.x == 0) {
         if (s_bad) s.err |= kSpecSyntax;
-        else if (G < s.total_blocks) { s.mode = 2; desc[i].mapped = 0; }  // NanoJPEG reads on into the padding
+        else if (G < s.total_blocks || s_long) { s.mode = 2; desc[i].mapped = 0; }  // (G short: NanoJPEG reads on into the padding)
     }
 }
 
-// Per lane: the map entries {pool block, DC offset} of the blocks it owns.
+// The map entries {pool block, DC offset} of every lane's blocks: one wave per lane, one entry per
+// thread per round, so each store instruction writes 512 contiguous bytes. The lane's overflow
+// chains (guess and count) are walked once into LDS by the wave's first thread.
 __global__ __launch_bounds__(256) void k_gw_map(int n, const Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
                                                 const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                 const GwOut* __restrict__ gwo, const GcRec* __restrict__ crec,
                                                 const RecState* __restrict__ rec, const LaneEntry* __restrict__ ent,
                                                 const int32_t* __restrict__ chunk_next, uint2* __restrict__ map) {
-    const int total = totals[1];
-    for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
-        const int i = find_image(wpre, n, wg);
+    __shared__ int32_t chain[4][2][kMapChain];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t nlanes = (int64_t)totals[1] * kLanes;
+    for (int64_t L = (int64_t)blockIdx.x * 4 + wave; L < nlanes; L += (int64_t)gridDim.x * 4) {
+        const int grp = (int)(L / kLanes);
+        const int i = find_image(wpre, n, grp);
         const SpecImg& s = spec[i];
-        if (s.mode != 1 || (s.err & kSpecSyntax)) continue;  // (an image in error shows no pixels)
-        const int64_t j = (int64_t)(wg - wpre[i]) * kLanes + threadIdx.x;
-        if (j >= s.nsub) continue;
+        const int64_t j = (int64_t)(grp - wpre[i]) * kLanes + (L % kLanes);
+        if (s.mode != 1 || (s.err & kSpecSyntax) || j >= s.nsub) continue;  // (wave-uniform)
         const Desc& d = desc[i];
         const Sel S = make_sel(d);
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
         const GwOut g = gwo[f];
         const GcRec c = crec[f];
         const LaneEntry le = ent[f];
-        const int32_t P[3] = {le.p0, le.p1, le.p2};
-        int32_t Q[3] = {P[0], P[1], P[2]};  // the guess blocks' offsets
+        int32_t P[3] = {le.p0, le.p1, le.p2}, Q[3] = {le.p0, le.p1, le.p2};  // count / guess blocks' offsets
         int32_t m0 = 0, cc = 0;
         if (c.m >= 0) {
             const RecState e = rec[f * kRec + c.m];
@@ -1317,21 +1341,38 @@ __global__ __launch_bounds__(256) void k_gw_map(int n, const Desc* __restrict__ 
             for (int q = 0; q < 3; ++q) Q[q] = wadd(P[q], wsub(c.cds[q], e.ds[q]));
         }
         if (c.m != -2) cc = c.c;
-        GwSlots sl{d.acbase + j * s.gw_S, s.gw_S, -1, 0};
-        const int64_t n1 = min<int64_t>(le.G + le.pad, s.total_blocks);
-        int bm = (int)(le.G % d.bpm);
-        for (int64_t nb = le.G; nb < n1; ++nb) {
-            const int32_t t = (int32_t)(nb - le.G);
-            const int ci = S.comp(bm);
-            bm = bm + 1 == d.bpm ? 0 : bm + 1;
+        const int64_t nb = min<int64_t>(le.pad, s.total_blocks - le.G);  // blocks to map
+        const int32_t Sst = s.gw_S;
+        const int32_t gmax = (int32_t)nb - cc + m0;  // guess slots used: [m0, gmax)
+        if (lane == 0) {
+            int32_t q = 0;
+            for (int32_t ch = gmax > Sst ? g.chunk0 : -1; ch >= 0 && q < kMapChain && q * kGwChunk < gmax - Sst; ++q) {
+                chain[wave][0][q] = ch;
+                ch = chunk_next[ch];
+            }
+            q = 0;
+            for (int32_t ch = cc > 0 ? c.chunk0 : -1; ch >= 0 && q < kMapChain && q * kGwChunk < cc; ++q) {
+                chain[wave][1][q] = ch;
+                ch = chunk_next[ch];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int64_t sbase = d.acbase + j * Sst;
+        for (int64_t t = lane; t < nb; t += 64) {
+            const int ci = S.comp((int)((le.G + t) % d.bpm));
             uint2 e;
             if (t < cc) {
-                e = make_uint2((uint32_t)(c.rep + t), (uint32_t)P[ci]);
+                e.x = (uint32_t)chain[wave][1][t / kGwChunk] * kGwChunk + (uint32_t)(t % kGwChunk);
+                e.y = (uint32_t)P[ci];
             } else {
-                e = make_uint2((uint32_t)sl.addr(t - cc + m0, g.chunk0, chunk_next), (uint32_t)Q[ci]);
+                const int64_t sl = t - cc + m0;
+                e.x = sl < Sst ? (uint32_t)(sbase + sl)
+                               : (uint32_t)chain[wave][0][(sl - Sst) / kGwChunk] * kGwChunk + (uint32_t)((sl - Sst) % kGwChunk);
+                e.y = (uint32_t)Q[ci];
             }
-            map[d.acbase + nb] = e;
+            map[d.acbase + le.G + t] = e;
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1385,9 +1426,9 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
         hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,
                            ws.clist);
         hipLaunchKernelGGL(k_gw_count, dim3(n), dim3(512), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
-                           ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair);
+                           ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair);
         hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
-                           ws.rec, ws.ac, ws.dc, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
+                           ws.rec, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
         hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent);
         hipLaunchKernelGGL(k_gw_map, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.gw, ws.crec,
                            ws.rec, ws.ent, ws.chunk_next, ws.map);

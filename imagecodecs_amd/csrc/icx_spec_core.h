@@ -565,68 +565,49 @@ struct ErrBounds {
     }
 };
 
-// Count lane, pass 1 (scan tables): from the true entry (a block start) to the first MCU start
-// the guess lane recorded (splice: *m = its index; the guess lane's blocks from there on are the
-// true ones), or -- no such state -- to the first block start at or after `end` (*m = -1,
-// *exit = that state). Returns the blocks decoded on the way, *cds their DC sums per component.
-ICX_HD int32_t gc_find(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S, uint64_t entry,
-                       int64_t start, int64_t end, const RecState* rec, int nrec, int32_t* cds, int* m,
-                       uint64_t* exit) {
-    Reader r;
-    r.init(U, ulen, st_pos(entry));
-    int b = st_b(entry), z = 0, mi = 0;
-    int32_t cnt = 0, val;
-    cds[0] = cds[1] = cds[2] = 0;
-    for (;;) {
-        if (z == 0) {
-            const int64_t p = r.pos();
-            if (b == 0 && mi < nrec) {
-                while (mi < nrec && (int64_t)rec[mi].rel < p - start) ++mi;
-                if (mi < nrec && (int64_t)rec[mi].rel == p - start) { *m = mi; return cnt; }
-            }
-            if (p >= end) { *m = -1; *exit = pack_state(p, b, 0); return cnt; }
-        }
-        const int ci = S.comp(b);
-        const bool dc = z == 0;
-        scan_step(r, T, H, S, b, z, val);
-        if (dc) {
-            ++cnt;
-            cds[ci] = wadd(cds[ci], val);
-        }
-    }
-}
-
-// Count lane, pass 2 (write tables): the c blocks from `entry` again, stored through `sink`
-// (begin(t): zero block t; cell(t, zz, v): coefficient; dc(t, v): the block's lane-local DC,
-// cumulative from entry). Returns the first block whose decode failed (INT32_MAX: none).
+// Count lane (write tables): from the true entry (a block start), store every block through
+// `sink` until the first MCU start the guess lane recorded (*m = its index: from there on the guess
+// lane's blocks are the true ones) or -- no such state -- the first block start at or after `end`
+// (*m = -1, *exit = that state). sink.begin(t) readies block t (false: no pool left, the walk
+// stops with *m = -3), sink.cell(t, zz, v) stores a coefficient, sink.dc(t, v) the block's
+// lane-local DC, cumulative from the entry. Returns the blocks stored, *cds their DC sums, *err
+// the first block whose decode failed (INT32_MAX: none; error semantics as k_spec_write's).
 template <class Sink>
-ICX_HD int32_t gc_write(const uint8_t* U, int64_t ulen, const WriteTab& TW, const Huff* H, const Sel& S, uint64_t entry,
-                        int32_t c, int64_t errbits, Sink& sink) {
+ICX_HD int32_t gc_walk(const uint8_t* U, int64_t ulen, const WriteTab& TW, const Huff* H, const Sel& S, uint64_t entry,
+                       int64_t start, int64_t end, const RecState* rec, int nrec, int64_t errbits, Sink& sink,
+                       int32_t* cds, int* m, uint64_t* exit, int32_t* err) {
     Reader r;
     r.init(U, ulen, st_pos(entry));
     ErrBounds eb;
     eb.set(errbits, st_pos(entry));
-    int b = st_b(entry), z = 0, ci = 0;
-    int32_t ds[3] = {0, 0, 0}, err = INT32_MAX;
-    for (int32_t t = 0; t < c;) {
+    int b = st_b(entry), z = 0, ci = 0, mi = 0;
+    int32_t t = 0;
+    cds[0] = cds[1] = cds[2] = 0;
+    *err = INT32_MAX;
+    for (;;) {
         const bool dc = z == 0;
         if (dc) {
+            const int64_t p = r.pos();
+            if (b == 0 && mi < nrec) {
+                while (mi < nrec && (int64_t)rec[mi].rel < p - start) ++mi;
+                if (mi < nrec && (int64_t)rec[mi].rel == p - start) { *m = mi; return t; }
+            }
+            if (p >= end) { *m = -1; *exit = pack_state(p, b, 0); return t; }
             ci = S.comp(b);
-            sink.begin(t);
+            if (!sink.begin(t)) { *m = -3; return t; }
         }
         const uint32_t u0 = r.used;
         const WriteOut o = write_step(r, TW, H, S, b, z, eb.near(u0));
-        if (eb.fail(u0, o.err, r.used) && err == INT32_MAX) err = t;
+        if (eb.fail(u0, o.err, r.used) && *err == INT32_MAX) *err = t;
         if (dc) {
-            ds[ci] = wadd(ds[ci], o.v1);
-            sink.dc(t, ds[ci]);
+            cds[ci] = wadd(cds[ci], o.v1);
+            sink.dc(t, cds[ci]);
         } else if (o.w1) {
             sink.cell(t, o.c1 & 63, o.v1);
         }
         if (o.w2) sink.cell(t, o.c2 & 63, o.v2);
         if (z == 0) ++t;
     }
-    return err;
 }
 
 // A lane's true totals (blocks it owns, DC sums) from its guess and count records.

@@ -247,15 +247,29 @@ struct EmuPool {
         return b;
     }
 };
+// Count lanes' blocks: a chain of pool chunks taken as the walk goes (k_gw_count's ChainSink).
 struct EmuSink {
     EmuPool* P;
-    int64_t base;
-    void begin(int32_t t) { std::memset(&P->coef[(size_t)(base + t) * 64], 0, 128); }
-    void cell(int32_t t, int zz, int32_t v) { P->coef[(size_t)(base + t) * 64 + zz] = (int16_t)v; }
-    void dc(int32_t t, int32_t v) {
+    int32_t chunk0 = -1, chunk = -1;
+    int64_t cur = 0;  // pool block of the block in progress
+    bool begin(int32_t t) {
+        if (t % kGwChunk == 0) {
+            const int64_t nb = P->take(kGwChunk);
+            if (nb < 0) return false;
+            const int32_t c = (int32_t)(nb / kGwChunk);
+            if (chunk < 0) chunk0 = c;
+            else P->chunk_next[chunk] = c;
+            chunk = c;
+        }
+        cur = (int64_t)chunk * kGwChunk + t % kGwChunk;
+        std::memset(&P->coef[(size_t)cur * 64], 0, 128);
+        return true;
+    }
+    void cell(int32_t, int zz, int32_t v) { P->coef[(size_t)cur * 64 + zz] = (int16_t)v; }
+    void dc(int32_t, int32_t v) {
         const int16_t c = dc_cell(v);
-        P->coef[(size_t)(base + t) * 64] = c;
-        if (c == kDcEscape) P->dc[(size_t)(base + t)] = v;
+        P->coef[(size_t)cur * 64] = c;
+        if (c == kDcEscape) P->dc[(size_t)cur] = v;
     }
 };
 
@@ -288,7 +302,7 @@ static uint64_t emu_gw_lane(const uint8_t* U, int64_t ulen, const WriteTab& TW, 
                 out.g0 = pack_state(s0 + u, b, 0);
             }
             if (phase == 1 && u >= span) return pack_state(s0 + u, b, 0);
-            if (phase == 1 && b == 0 && out.nrec < kRec) {
+            if (phase == 1 && b == 0 && out.nrec < kRecGw) {
                 RecState& e = rec[out.nrec++];
                 e.rel = u - pre;
                 e.b = 0;
@@ -389,18 +403,17 @@ int emu_gw_decode(const uint8_t* file, int64_t size, int sub_bytes, int64_t lead
     auto count_lane = [&](int64_t j, uint64_t entry) -> bool {  // false: pool exhausted
         GcRec& q = c[j];
         uint64_t ex = 0;
-        q.c = gc_find(U.data(), ulen, SS.scan, H, SL, entry, j * sb, lane_end(j), &rec[j * kRec], g[j].nrec, q.cds, &q.m, &ex);
+        EmuSink sk{&P};
+        q.c = gc_walk(U.data(), ulen, SS.write, H, SL, entry, j * sb, lane_end(j), &rec[j * kRec], g[j].nrec, errbits, sk,
+                      q.cds, &q.m, &ex, &q.err);
+        q.chunk0 = sk.chunk0;
         Y[j] = ex;
-        q.rep = P.take(q.c);
-        if (q.rep < 0) return false;
-        EmuSink sk{&P, q.rep};
-        q.err = gc_write(U.data(), ulen, SS.write, H, SL, entry, q.c, errbits, sk);
-        return true;
+        return q.m != -3;
     };
     int64_t counted = 0, spliced = 0;
     for (int64_t j = 0; j < nsub; ++j) {
         const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[j - 1];
-        c[j] = GcRec{0, 0, -2, {0, 0, 0}, INT32_MAX};
+        c[j] = GcRec{-1, 0, 0, -2, {0, 0, 0}, INT32_MAX};
         if (g[j].g0 == entry) continue;
         ++counted;
         if (!count_lane(j, entry)) return 1;
@@ -416,7 +429,7 @@ int emu_gw_decode(const uint8_t* file, int64_t size, int sub_bytes, int64_t lead
         for (; k < nsub; ++k, ++steps) {
             if (steps >= kGwMaxWalk) return 1;
             ++repaired;
-            if (g[k].g0 == X[k - 1]) { c[k] = GcRec{0, 0, -2, {0, 0, 0}, INT32_MAX}; break; }
+            if (g[k].g0 == X[k - 1]) { c[k] = GcRec{-1, 0, 0, -2, {0, 0, 0}, INT32_MAX}; break; }
             if (!count_lane(k, X[k - 1])) return 1;
             if (c[k].m >= 0 || k + 1 == nsub || Y[k] == X[k]) break;
             X[k] = Y[k];
@@ -449,7 +462,8 @@ int emu_gw_decode(const uint8_t* file, int64_t size, int sub_bytes, int64_t lead
             const int32_t t = (int32_t)(n - G[j]);
             const int ci = SL.comp((int)(n % d.bpm));
             if (t < c[j].c && c[j].m != -2) {
-                maddr[n] = c[j].rep + t;
+                GwSlots cs{0, 0, -1, 0};
+                maddr[n] = cs.addr(t, c[j].chunk0, P.chunk_next.data());
                 moff[n] = Pd[3 * j + ci];
             } else {
                 maddr[n] = sl.addr(t - (c[j].m == -2 ? 0 : c[j].c) + m0, g[j].chunk0, P.chunk_next.data());
