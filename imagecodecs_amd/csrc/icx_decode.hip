@@ -1286,11 +1286,16 @@ __device__ __forceinline__ void idct_units(const int16_t* ac, int h, uint32_t wi
         if (u >= nunits) break;
     }
 #else
+    // the next unit's location (a map load for guess-write images) is fetched while this unit is
+    // transformed, so its block loads do not wait for it
+    if (wid >= nunits) return;
+    BlkLoc l = locf(wid);
     for (uint32_t u = wid; u < nunits; u += nw) {
         int4 c[8];
-        const BlkLoc l = locf(u);
         load_block(ac, l.blk, h, c);
+        const BlkLoc ln = locf(min(u + nw, nunits - 1));
         unit(u, c, l);
+        l = ln;
     }
 #endif
 }

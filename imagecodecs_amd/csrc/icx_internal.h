@@ -58,8 +58,8 @@ struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
 // of kGwChunk blocks taken from the pool's tail by atomic add (flat areas hold thousands of
 // blocks per lane), chained through GroupWs::chunk_next.
 constexpr int kGwChunk = 32;
-constexpr int kRecGw = 8;       // MCU starts a guess-write lane records (the count lanes splice at the first
-                                // they reach; the lead synchronises most guess lanes before their first)
+constexpr int kRecGw = kRec;    // MCU starts a guess-write lane records (the count lanes splice at the first
+                                // they reach; a lane that cannot splice is count-decoded whole)
 constexpr int kGwMaxWalk = 64;  // lanes a repair walk may re-derive before the image goes sequential
 struct GwOut {
     uint64_t g0;     // first block start at or after the lane's start: pack_state(pos, b, 0)

@@ -1240,7 +1240,6 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
     }
 }
 
-constexpr int kMapChain = 384;  // chunks per chain k_gw_map stages: a lane of 2560 B holds at most ~10K blocks
 // Per image: each lane's first block index and DC predictors (exclusive scans of the lane
 // totals), and the status: a decode failure on the true path before the image's last block is
 // NanoJPEG's syntax error; blocks that run out before the last one (data ends early) or an
@@ -1250,7 +1249,7 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
                                                  const RecState* __restrict__ rec, LaneEntry* __restrict__ ent) {
     __shared__ int sh[256];
     __shared__ int s_cnt, s_d0, s_d1, s_d2;
-    __shared__ int s_bad, s_long;
+    __shared__ int s_bad;
     const int i = blockIdx.x;
     if (i >= n) return;
     SpecImg& s = spec[i];
@@ -1259,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
         if (threadIdx.x == 0) { s.mode = 2; desc[i].mapped = 0; }
         return;
     }
-    if (threadIdx.x == 0) s_bad = s_long = 0;
+    if (threadIdx.x == 0) s_bad = 0;
     __syncthreads();
     const int64_t base = (int64_t)s.wg_base * kLanes;
     int64_t G = 0;
@@ -1273,8 +1272,6 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
             const GcRec c = crec[base + j];
             cnt = gw_lane_total(g, c, rec + (base + j) * kRec, d);
             e = gw_lane_err(g, c, rec + (base + j) * kRec);
-            // (chains longer than k_gw_map's LDS holds: only with lanes far beyond kSubBytes)
-            if (g.k - s.gw_S > kMapChain * kGwChunk || (c.m != -2 && c.c > kMapChain * kGwChunk)) atomicOr(&s_long, 1);
         }
         // int32 prefix sums (wrap-around adds commute, matching dcpred += diff)
         const int ec = block_exclusive_scan(cnt, sh);
@@ -1306,73 +1303,69 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
     }
     if (threadIdx.x == 0) {
         if (s_bad) s.err |= kSpecSyntax;
-        else if (G < s.total_blocks || s_long) { s.mode = 2; desc[i].mapped = 0; }  // (G short: NanoJPEG reads on into the padding)
+        else if (G < s.total_blocks) { s.mode = 2; desc[i].mapped = 0; }  // NanoJPEG reads on into the padding
     }
 }
 
-// The map entries {pool block, DC offset} of every lane's blocks: one wave per lane, one entry per
-// thread per round, so each store instruction writes 512 contiguous bytes. The lane's overflow
-// chains (guess and count) are walked once into LDS by the wave's first thread.
+// The map entries {pool block, DC offset} of every lane's blocks. A wave takes 64 consecutive lanes:
+// each thread loads one lane's records, then the wave writes the lanes' entries one lane after
+// the other, one entry per thread per round (512 contiguous bytes per store instruction). Blocks
+// in overflow chunks find their chunk by walking the lane's chain (short: flat regions only).
 __global__ __launch_bounds__(256) void k_gw_map(int n, const Desc* __restrict__ desc, const SpecImg* __restrict__ spec,
                                                 const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                 const GwOut* __restrict__ gwo, const GcRec* __restrict__ crec,
                                                 const RecState* __restrict__ rec, const LaneEntry* __restrict__ ent,
                                                 const int32_t* __restrict__ chunk_next, uint2* __restrict__ map) {
-    __shared__ int32_t chain[4][2][kMapChain];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t nlanes = (int64_t)totals[1] * kLanes;
-    for (int64_t L = (int64_t)blockIdx.x * 4 + wave; L < nlanes; L += (int64_t)gridDim.x * 4) {
-        const int grp = (int)(L / kLanes);
+    const int64_t nchunks = (int64_t)totals[1] * (kLanes / 64);
+    for (int64_t C = (int64_t)blockIdx.x * 4 + wave; C < nchunks; C += (int64_t)gridDim.x * 4) {
+        const int grp = (int)(C / (kLanes / 64));
         const int i = find_image(wpre, n, grp);
         const SpecImg& s = spec[i];
-        const int64_t j = (int64_t)(grp - wpre[i]) * kLanes + (L % kLanes);
-        if (s.mode != 1 || (s.err & kSpecSyntax) || j >= s.nsub) continue;  // (wave-uniform)
+        if (s.mode != 1 || (s.err & kSpecSyntax)) continue;  // (wave-uniform)
+        const int64_t j0 = (int64_t)(grp - wpre[i]) * kLanes + (C % (kLanes / 64)) * 64;
+        if (j0 >= s.nsub) continue;
         const Desc& d = desc[i];
         const Sel S = make_sel(d);
-        const int64_t f = (int64_t)s.wg_base * kLanes + j;
+        const int32_t Sst = s.gw_S;
+        // this thread's lane: its first block, count, offsets and block sources
+        const int64_t j = j0 + lane;
+        const bool live = j < s.nsub;
+        const int64_t f = (int64_t)s.wg_base * kLanes + (live ? j : j0);
         const GwOut g = gwo[f];
         const GcRec c = crec[f];
         const LaneEntry le = ent[f];
-        int32_t P[3] = {le.p0, le.p1, le.p2}, Q[3] = {le.p0, le.p1, le.p2};  // count / guess blocks' offsets
-        int32_t m0 = 0, cc = 0;
+        int32_t P0 = le.p0, P1 = le.p1, P2 = le.p2, Q0 = P0, Q1 = P1, Q2 = P2, m0 = 0;
         if (c.m >= 0) {
             const RecState e = rec[f * kRec + c.m];
             m0 = e.cnt;
-            for (int q = 0; q < 3; ++q) Q[q] = wadd(P[q], wsub(c.cds[q], e.ds[q]));
+            Q0 = wadd(P0, wsub(c.cds[0], e.ds[0]));
+            Q1 = wadd(P1, wsub(c.cds[1], e.ds[1]));
+            Q2 = wadd(P2, wsub(c.cds[2], e.ds[2]));
         }
-        if (c.m != -2) cc = c.c;
-        const int64_t nb = min<int64_t>(le.pad, s.total_blocks - le.G);  // blocks to map
-        const int32_t Sst = s.gw_S;
-        const int32_t gmax = (int32_t)nb - cc + m0;  // guess slots used: [m0, gmax)
-        if (lane == 0) {
-            int32_t q = 0;
-            for (int32_t ch = gmax > Sst ? g.chunk0 : -1; ch >= 0 && q < kMapChain && q * kGwChunk < gmax - Sst; ++q) {
-                chain[wave][0][q] = ch;
-                ch = chunk_next[ch];
-            }
-            q = 0;
-            for (int32_t ch = cc > 0 ? c.chunk0 : -1; ch >= 0 && q < kMapChain && q * kGwChunk < cc; ++q) {
-                chain[wave][1][q] = ch;
-                ch = chunk_next[ch];
+        const int32_t cc = c.m != -2 ? c.c : 0;
+        const int64_t nb = live ? min<int64_t>(le.pad, s.total_blocks - le.G) : 0;
+        const int nl = (int)min<int64_t>(64, s.nsub - j0);
+        for (int q = 0; q < nl; ++q) {  // wave-uniform: lane q's entries
+            const int64_t G = __shfl(le.G, q), nbq = __shfl(nb, q);
+            const int32_t ccq = __shfl(cc, q), m0q = __shfl(m0, q), c0q = __shfl(c.chunk0, q), g0q = __shfl(g.chunk0, q);
+            const int32_t p0 = __shfl(P0, q), p1 = __shfl(P1, q), p2 = __shfl(P2, q);
+            const int32_t q0 = __shfl(Q0, q), q1 = __shfl(Q1, q), q2 = __shfl(Q2, q);
+            const int64_t sbase = d.acbase + (j0 + q) * Sst;
+            GwSlots gs{sbase, Sst, -1, 0}, cs{0, 0, -1, 0};
+            for (int64_t t = lane; t < nbq; t += 64) {
+                const int ci = S.comp((int)((G + t) % d.bpm));
+                uint2 e;
+                if (t < ccq) {
+                    e.x = (uint32_t)cs.addr((int32_t)t, c0q, chunk_next);
+                    e.y = (uint32_t)(ci == 0 ? p0 : (ci == 1 ? p1 : p2));
+                } else {
+                    e.x = (uint32_t)gs.addr((int32_t)(t - ccq + m0q), g0q, chunk_next);
+                    e.y = (uint32_t)(ci == 0 ? q0 : (ci == 1 ? q1 : q2));
+                }
+                map[d.acbase + G + t] = e;
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        const int64_t sbase = d.acbase + j * Sst;
-        for (int64_t t = lane; t < nb; t += 64) {
-            const int ci = S.comp((int)((le.G + t) % d.bpm));
-            uint2 e;
-            if (t < cc) {
-                e.x = (uint32_t)chain[wave][1][t / kGwChunk] * kGwChunk + (uint32_t)(t % kGwChunk);
-                e.y = (uint32_t)P[ci];
-            } else {
-                const int64_t sl = t - cc + m0;
-                e.x = sl < Sst ? (uint32_t)(sbase + sl)
-                               : (uint32_t)chain[wave][0][(sl - Sst) / kGwChunk] * kGwChunk + (uint32_t)((sl - Sst) % kGwChunk);
-                e.y = (uint32_t)Q[ci];
-            }
-            map[d.acbase + le.G + t] = e;
-        }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
