@@ -17,7 +17,8 @@ constexpr int kSubBytesSmall = 512;  // shortest: k_spec_plan sizes each image's
                                      // they fill whole 512-lane workgroups (icx_spec.hip)
 constexpr int kRec = 16;           // block-start states a guess lane records for resync
 constexpr int kGenericWG = 4096;    // workgroups per launch of the other-sampling back-half kernels
-constexpr int kGuessLead = 2048;     // bits a guess lane decodes before its range (k_spec_guess)
+constexpr int kGuessLead = 4096;     // bits a guess lane decodes before its range (k_gw_lane, k_spec_guess):
+                                     // at most a quarter of the lane (min(kGuessLead, 2 x lane bytes))
 constexpr int kMaxRepair = 1024;   // unsynchronised lanes repaired per image before giving up
 constexpr int kLanes = 256;        // lanes per decode workgroup (lane records are numbered in these)
 constexpr int kWriteLanesBig = 512;  // write-pass workgroup for large images: tables amortised
