@@ -43,6 +43,8 @@ struct SpecImg {
     int64_t total_blocks;
     int64_t uoff;          // byte offset of the image's unstuffed stream in GroupWs::U (4 KiB aligned)
     int32_t ncount, pad2_; // guess-write lanes queued for the count decode (k_gw_check)
+    int64_t tail_G, tail_n;  // guess-write: the lanes' blocks end at block tail_G, tail_n before the
+    int32_t tail_p[3], pad3_;// frame's last (k_gw_tail reads on into the padding; DC predictors there)
 };
 struct TileRec { int32_t kept, end_err; int64_t end_at; int32_t nrst, pad_; };
 struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };

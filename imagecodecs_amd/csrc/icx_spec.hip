@@ -1302,8 +1302,47 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        if (s_bad) s.err |= kSpecSyntax;
-        else if (G < s.total_blocks) { s.mode = 2; desc[i].mapped = 0; }  // NanoJPEG reads on into the padding
+        s.tail_n = 0;
+        if (s_bad) {
+            s.err |= kSpecSyntax;
+        } else if (G < s.total_blocks) {  // the data ends early: NanoJPEG reads on into the padding (k_gw_tail)
+            s.tail_G = G;
+            s.tail_n = s.total_blocks - G;
+            s.tail_p[0] = P0;
+            s.tail_p[1] = P1;
+            s.tail_p[2] = P2;
+        }
+    }
+}
+
+// The blocks past the lanes' when the data ends before the frame's last MCU (rare; one thread per
+// such image): gw_tail from the last lane's exit, stored in a chunk chain, mapped here.
+__global__ __launch_bounds__(64) void k_gw_tail(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
+                                                const uint64_t* __restrict__ X, const uint64_t* __restrict__ Y,
+                                                const GcRec* __restrict__ crec, int16_t* __restrict__ ac,
+                                                int32_t* __restrict__ dcv, int32_t* __restrict__ chunk_next,
+                                                unsigned long long* __restrict__ pool_next, int64_t pool_cap,
+                                                uint2* __restrict__ map) {
+    const int i = blockIdx.x;
+    if (i >= n || threadIdx.x != 0) return;
+    SpecImg& s = spec[i];
+    if (s.mode != 1 || s.tail_n == 0 || (s.err & kSpecSyntax)) return;
+    Desc& d = desc[i];
+    const int64_t last = (int64_t)s.wg_base * kLanes + s.nsub - 1;
+    const uint64_t entry = crec[last].m == -1 ? Y[last] : X[last];
+    const Sel S = make_sel(d);
+    ChainSink sink{ac, dcv, chunk_next, pool_next, pool_cap, -1, -1, 0};
+    int32_t ds[3], err;
+    const int32_t got = gw_tail(U + s.uoff, s.ulen, steps[i].write, d.huff, S, entry, s.tail_n,
+                                s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, sink, ds, &err);
+    if (got < 0) { s.mode = 2; d.mapped = 0; return; }  // the pool ran out: the sequential kernel
+    if (err != INT32_MAX) { s.err |= kSpecSyntax; return; }
+    GwSlots ts{0, 0, -1, 0};
+    for (int32_t t = 0; t < got; ++t) {
+        const int64_t nb = s.tail_G + t;
+        const int ci = S.comp((int)(nb % d.bpm));
+        map[d.acbase + nb] = make_uint2((uint32_t)ts.addr(t, sink.chunk0, chunk_next), (uint32_t)s.tail_p[ci]);
     }
 }
 
@@ -1423,6 +1462,8 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
         hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
                            ws.rec, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
         hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent);
+        hipLaunchKernelGGL(k_gw_tail, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.crec,
+                           ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.map);
         hipLaunchKernelGGL(k_gw_map, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.gw, ws.crec,
                            ws.rec, ws.ent, ws.chunk_next, ws.map);
         E(kStEntropy);

@@ -610,6 +610,43 @@ ICX_HD int32_t gc_walk(const uint8_t* U, int64_t ulen, const WriteTab& TW, const
     }
 }
 
+// The image's last blocks when the lanes' blocks end before the frame's (the data stops early,
+// no error decided the status): NanoJPEG reads on into the 0xFF padding (jpeg_dec.h:451-455), and
+// so does this walk, from the last lane's exit, `need` blocks or up to the first failure. Blocks
+// go through `sink` as in gc_walk; *ds their DC sums from the entry; returns the blocks stored and
+// *err the first failed one (INT32_MAX: none).
+template <class Sink>
+ICX_HD int32_t gw_tail(const uint8_t* U, int64_t ulen, const WriteTab& TW, const Huff* H, const Sel& S, uint64_t entry,
+                       int64_t need, int64_t errbits, Sink& sink, int32_t* ds, int32_t* err) {
+    Reader r;
+    r.init(U, ulen, st_pos(entry));
+    ErrBounds eb;
+    eb.set(errbits, st_pos(entry));
+    int b = st_b(entry), z = 0, ci = 0;
+    int32_t t = 0;
+    ds[0] = ds[1] = ds[2] = 0;
+    *err = INT32_MAX;
+    while (t < need && *err == INT32_MAX) {
+        const bool dc = z == 0;
+        if (dc) {
+            ci = S.comp(b);
+            if (!sink.begin(t)) return -1;
+        }
+        const uint32_t u0 = r.used;
+        const WriteOut o = write_step(r, TW, H, S, b, z, eb.near(u0));
+        if (eb.fail(u0, o.err, r.used)) *err = t;
+        if (dc) {
+            ds[ci] = wadd(ds[ci], o.v1);
+            sink.dc(t, ds[ci]);
+        } else if (o.w1) {
+            sink.cell(t, o.c1 & 63, o.v1);
+        }
+        if (o.w2) sink.cell(t, o.c2 & 63, o.v2);
+        if (z == 0) ++t;
+    }
+    return t;
+}
+
 // A lane's true totals (blocks it owns, DC sums) from its guess and count records.
 ICX_HD int32_t gw_lane_total(const GwOut& g, const GcRec& c, const RecState* rec, int32_t* ds) {
     if (c.m == -2) {

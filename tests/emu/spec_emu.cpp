@@ -449,13 +449,26 @@ int emu_gw_decode(const uint8_t* file, int64_t size, int sub_bytes, int64_t lead
         if (e != INT32_MAX && G[j] + e < total) bad = true;
         G[j + 1] = G[j] + n;
     }
-    // the blocks run past the data: unless a true-path error already decided the status, the
-    // sequential kernel continues into the 0xFF padding as NanoJPEG does
-    if (G[nsub] < total && !bad) return 1;
-    // ---- k_gw_map + IDCT-side assembly
+    // ---- k_gw_tail: the blocks run past the data (no error decided the status): read on into
+    // the 0xFF padding from the last lane's exit, as NanoJPEG does
     std::vector<int64_t> maddr(total, 0);
     std::vector<int32_t> moff(total, 0);
-    for (int64_t j = 0; j < nsub; ++j) {
+    if (G[nsub] < total && !bad) {
+        const uint64_t entry = c[nsub - 1].m == -1 ? Y[nsub - 1] : X[nsub - 1];
+        EmuSink sk{&P};
+        int32_t tds[3], terr;
+        const int32_t got = gw_tail(U.data(), ulen, SS.write, H, SL, entry, total - G[nsub], errbits, sk, tds, &terr);
+        if (got < 0) return 1;
+        if (terr != INT32_MAX) bad = true;
+        GwSlots ts{0, 0, -1, 0};
+        for (int32_t t = 0; t < got && !bad; ++t) {
+            const int64_t n = G[nsub] + t;
+            maddr[n] = ts.addr(t, sk.chunk0, P.chunk_next.data());
+            moff[n] = Pc[SL.comp((int)(n % d.bpm))];
+        }
+        stats[7] += 1;
+    }
+    for (int64_t j = 0; j < nsub && !bad; ++j) {
         GwSlots sl{j * Sst, Sst, -1, 0};
         const int32_t m0 = c[j].m >= 0 ? rec[j * kRec + c[j].m].cnt : 0;
         for (int64_t n = G[j]; n < G[j + 1] && n < total; ++n) {
