@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of one kernel from two rocprofv3 PMC passes (GPU box).
 
-    python3 tools/pmc_traffic.py run  [--workload c3] [--kernel k_spec_write] [--out profiles/traffic.json]
+    python3 tools/pmc_traffic.py run  [--workload c3] [--kernel k_gw_lane] [--out profiles/traffic.json]
     python3 tools/pmc_traffic.py parse FETCH_DIR WRITE_DIR [...]
 
 `run` profiles `bench.py --steps 1 --warmup 0 --no-cpu --no-pcie` twice, once with --pmc FETCH_SIZE and once
@@ -98,7 +98,7 @@ def main():
     ap.add_argument("dirs", nargs="*")
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--images", type=int, default=0)
-    ap.add_argument("--kernel", default="k_spec_write")
+    ap.add_argument("--kernel", default="k_gw_lane")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
     if args.mode == "run":
