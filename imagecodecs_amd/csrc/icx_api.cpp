@@ -4,6 +4,7 @@
 // device workspace of one image group. No CPU decode path exists: every decode runs the
 // HIP kernels in icx_decode.hip, and a missing/unusable GPU is reported as an error.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -70,7 +71,10 @@ static thread_local char g_msg[512];
         }                                                                                   \
     } while (0)
 
-// Brackets every pipeline stage with HIP events on the launch stream.
+// Brackets every pipeline stage with HIP events on the launch stream, and with a roctx range on
+// the host (the launch side: `rocprofv3 --marker-trace` shows which stage enqueued which kernels).
+static const char* const kRangeNames[kStCount] = {"icx:parse", "icx:unstuff", "icx:entropy", "icx:write",
+                                                  "icx:idct", "icx:upsample", "icx:convert"};
 struct EventHook : StageHook {
     struct Rec { Stage s; hipEvent_t a, b; };
     std::vector<Rec> recs;
@@ -86,12 +90,14 @@ struct EventHook : StageHook {
     }
     void reset() { recs.clear(); used = 0; }
     void begin(Stage s, hipStream_t st) override {
+        (void)roctxRangePushA(kRangeNames[s]);
         hipEvent_t a = get(), b = get();
         if (!a || !b) return;
         (void)hipEventRecord(a, st);
         recs.push_back({s, a, b});
     }
     void end(Stage s, hipStream_t st) override {
+        (void)roctxRangePop();
         for (auto it = recs.rbegin(); it != recs.rend(); ++it)
             if (it->s == s) { (void)hipEventRecord(it->b, st); return; }
     }
@@ -313,6 +319,10 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     if (!d_data || !d_off || !d_size || !d_out || !d_status || !d_dims) { ctx->err = "null pointer"; return ICX_INTERNAL_ERR; }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    struct Range {  // one roctx range per call, around every stage's range
+        explicit Range(const char* m) { (void)roctxRangePushA(m); }
+        ~Range() { (void)roctxRangePop(); }
+    } range("icx_jpeg_batch_decode");
     b->hook->reset();
     for (int p = 0; p < b->pipes; ++p)
         ICX_HIP(ctx, hipMemsetAsync(b->ws[p].stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
@@ -778,6 +788,10 @@ int icx_hdr_batch_decode(icx_hdr_batch* b, int n, const uint8_t* d_data, const u
     if (out_stride < 4ull * b->ws.max_w * b->ws.max_h) { ctx->err = "icx_hdr_batch_decode: out_stride too small"; return ICX_HDR_INTERNAL_ERR; }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_HDR_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    struct Range {  // one roctx range per call, around every stage's range
+        explicit Range(const char* m) { (void)roctxRangePushA(m); }
+        ~Range() { (void)roctxRangePop(); }
+    } range("icx_jpeg_batch_decode");
     b->hook->reset();
     launch_hdr_decode(b->ws, n, d_data, d_off, d_size, d_out, out_stride, d_status, d_dims, st, b->hook.get());
     ICX_HIP(ctx, hipGetLastError(), ICX_HDR_INTERNAL_ERR);

@@ -42,7 +42,9 @@ struct SpecImg {
     int64_t errpos;        // unstuffed index whose fetch is a syntax error (INT64_MAX: none)
     int64_t total_blocks;
     int64_t uoff;          // byte offset of the image's unstuffed stream in GroupWs::U (4 KiB aligned)
-    int32_t ncount, pad2_; // guess-write lanes queued for the count decode (k_gw_check)
+    int32_t ncount;        // guess-write lanes queued for the count decode (k_gw_check)
+    int32_t dri_first;     // DRI: 2 j + (kind == kDriElsewhere) of the first interval j not ending
+                           // at its marker (dri_end_kind; atomicMin, INT32_MAX: none)
     int64_t tail_G, tail_n;  // guess-write: the lanes' blocks end at block tail_G, tail_n before the
     int32_t tail_p[3], pad3_;// frame's last (k_gw_tail reads on into the padding; DC predictors there)
 };

@@ -116,6 +116,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             s.err = 0;
             s.nrepair = 0;
             s.ncount = 0;
+            s.dri_first = INT32_MAX;
             s.nrst = 0;
             s.sub_bytes = ok ? (int32_t)sb : kSubBytes;
             s.uoff = ((int64_t)carry_u + eu) << 12;
@@ -868,16 +869,20 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         // stopped lanes scribbled in their slots: zero them for the next workgroup item
 #pragma unroll
         for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
-        if (dri && j < s.nsub) {
+        if (dri && j < s.nsub && lane_ok) {
             // NanoJPEG after R MCUs: byte-align, read 16 bits = FF D0+(j&7) (jpeg_dec.h:707-715).
-            // The parallel result stands only if that is exactly marker j at the aligned end of
-            // the interval and no error byte was in the data; else the sequential decoder runs.
-            bool exact = lane_ok && s.errpos == INT64_MAX;
-            if (exact && !bad && j + 1 < s.nsub) {
+            // The first interval that does not end at its own marker decides the image
+            // (k_spec_finish): a decode error or a wrong marker there is NanoJPEG's syntax error
+            // (no sequential decode needed); FF D0+(j&7) read somewhere else than marker j
+            // (data bytes that look like it) resumes NanoJPEG where no lane started: sequential.
+            // (A lane whose start marker is missing always follows such an interval.)
+            int kind = bad ? kDriError : kDriExact;
+            if (!bad && j + 1 < s.nsub) {
                 const int64_t endbyte = (start_byte * 8 + used_end + 7) >> 3;
-                exact = j < s.nrst && j < rst_cap && (RS[j] >> 3) == endbyte && (int)(RS[j] & 7) == (int)(j & 7);
+                const int64_t rsj = j < s.nrst && j < rst_cap ? RS[j] : -1;
+                kind = dri_end_kind(U + s.uoff, s.ulen, s.errpos, endbyte, j, rsj);
             }
-            if (!exact) atomicOr(&s.err, kSpecGiveUp);
+            if (kind != kDriExact) atomicMin(&s.dri_first, (int32_t)(2 * j + (kind == kDriElsewhere)));
         }
     }
 }
@@ -1413,7 +1418,9 @@ __global__ void k_spec_finish(int n, Desc* __restrict__ desc, SpecImg* __restric
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SpecImg& s = spec[i];
-    if (s.mode == 3 && (s.err & kSpecGiveUp)) s.mode = 2;  // DRI markers not where NanoJPEG reads them
+    if (s.mode == 3 && s.dri_first != INT32_MAX)  // the first interval not ending at its marker
+        s.err |= (s.dri_first & 1) ? kSpecGiveUp : kSpecSyntax;
+    if (s.mode == 3 && (s.err & kSpecGiveUp)) s.mode = 2;  // NanoJPEG resumes where no lane started
     if (s.mode != 1) desc[i].mapped = 0;  // the sequential kernel writes in place
     if (s.mode == 1 || s.mode == 3) desc[i].status = (s.err & kSpecSyntax) ? kSyntaxError : kOk;
     // path statistics: [0] parallel path (incl. DRI intervals), [1] parallel -> sequential

@@ -216,6 +216,23 @@ ICX_HD Sel make_sel(const Desc& d) {
 ICX_HD uint32_t u_pad_chunk(int64_t ulen) { return (uint32_t)(ulen >> 4) + 1u; }
 ICX_HD int64_t u_pad_end(int64_t ulen) { return ((ulen >> 4) + 2) << 4; }
 
+// Restart intervals (DRI): how interval j ends for NanoJPEG, when it started where lane j did and
+// its R MCUs decoded without error ending at byte `endbyte` (bits consumed, rounded up: the
+// njByteAlign). It then reads 16 bits there and wants FF D0+(j&7) (jpeg_dec.h:707-715): bytes
+// past ulen read 0xFF, and a read that fetches the error byte (errpos) is a syntax error whatever
+// it returns. Exact: marker j (rs = its record, pos << 3 | number, or -1) is at endbyte, so lane
+// j+1 starts where NanoJPEG continues. Error: anything but FF D0+(j&7) -- NanoJPEG stops with a
+// syntax error. Elsewhere: FF D0+(j&7) that is not marker j's position (data bytes that look like
+// it, or another marker of that number) -- NanoJPEG continues where no lane started.
+enum : int { kDriExact = 0, kDriError = 1, kDriElsewhere = 2 };
+ICX_HD int dri_end_kind(const uint8_t* U, int64_t ulen, int64_t errpos, int64_t endbyte, int64_t j, int64_t rs) {
+    if (errpos <= endbyte + 1) return kDriError;
+    const int b0 = endbyte < ulen ? U[endbyte] : 0xFF;
+    const int b1 = endbyte + 1 < ulen ? U[endbyte + 1] : 0xFF;
+    if (b0 != 0xFF || b1 != (0xD0 | (int)(j & 7))) return kDriError;
+    return rs >= 0 && (rs >> 3) == endbyte ? kDriExact : kDriElsewhere;
+}
+
 // Wave-wide helpers that are the identity on the host (the CPU emulator runs one lane).
 ICX_HD bool wave_any(bool p) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -223,6 +223,77 @@ int emu_spec_decode(const uint8_t* file, int64_t size, int sub_bytes, int16_t* c
     stats[0]++;
     return 0;
 }
+
+// Restart-interval streams (k_spec_write mode 3 + k_spec_finish): lane j decodes interval j from
+// the byte after the (j-1)-th restart marker in U, R MCUs with zero DC predictors; the first
+// interval that does not end at its own marker (dri_end_kind) decides the image. Returns 0
+// parallel result (status in *status; coef / dc as emu_spec_decode), 1 the image would go to the
+// sequential kernel, 2 not eligible. *first = SpecImg::dri_first.
+int emu_dri_decode(const uint8_t* file, int64_t size, int16_t* coef, int32_t* dc, int64_t cap_blocks, int64_t* nblocks,
+                   int32_t* status, int32_t* first) {
+    auto dp = std::make_unique<Desc>();
+    Desc& d = *dp;
+    *status = parse_headers(file, size, d);
+    *nblocks = 0;
+    *first = INT32_MAX;
+    const int64_t scan_len = d.size - d.scan_off;
+    if (!(d.status == kPending && d.restart > 0 && d.nc >= 1 && d.bpm <= kSpecMaxBpm && scan_len > 0)) return 2;
+    const int64_t total = (int64_t)d.mbw * d.mbh * d.bpm;
+    *nblocks = total;
+    if (total > cap_blocks) return 2;
+    const uint8_t* R = file + d.scan_off;
+    std::vector<uint8_t> U;
+    std::vector<int64_t> rst;
+    int64_t errpos;
+    int32_t giveup = 0;
+    const int64_t ulen = emu_unstuff(R, scan_len, ustf_align(R), U, errpos, giveup, &rst);
+    if (giveup) return 1;
+    auto SSp = std::make_unique<StepSet>();
+    for (int k = 0; k < WriteTab::entries(); ++k) SSp->write.fill(d.huff, k);
+    set_block_sel(SSp->write, d.huff, make_sel(d));
+    const WriteTab& TW = SSp->write;
+    const Sel SL = make_sel(d);
+    const int64_t nint = ((int64_t)d.mbw * d.mbh + d.restart - 1) / d.restart;
+    const int64_t iblocks = (int64_t)d.restart * d.bpm;
+    const int64_t errbits = errpos == INT64_MAX ? INT64_MAX : errpos * 8;
+    std::memset(coef, 0, sizeof(int16_t) * 64 * total);
+    int32_t key = INT32_MAX;
+    for (int64_t j = 0; j < nint; ++j) {
+        int64_t start_byte = 0;
+        if (j > 0) {
+            if (j - 1 >= (int64_t)rst.size()) continue;  // marker missing: an earlier interval decides
+            start_byte = (rst[j - 1] >> 3) + 2;
+        }
+        Reader r;
+        r.init(U.data(), ulen, start_byte * 8);
+        int b = 0, z = 0, ci = 0;
+        int32_t pred[3] = {0, 0, 0};
+        int64_t bi = j * iblocks, used_end = start_byte * 8;
+        const int64_t bend = std::min(total, bi + iblocks);
+        bool bad = false;
+        while (bi < bend) {  // k_spec_write's loop, one lane
+            const bool dcl = z == 0;
+            if (dcl) ci = SL.comp(b);
+            const int64_t p0 = r.pos();
+            if (p0 + 16 > errbits) bad = true;
+            const WriteOut o = write_step(r, TW, d.huff, SL, b, z, p0 + 16 + WriteTab::kAcBits > errbits);
+            if (o.err || r.pos() > errbits) bad = true;
+            if (bad) break;
+            if (dcl) { pred[ci] = wadd(pred[ci], o.v1); dc[bi] = pred[ci]; }
+            else if (o.w1) coef[bi * 64 + nat_of_zig(o.c1 & 63)] = (int16_t)o.v1;
+            if (o.w2) coef[bi * 64 + nat_of_zig(o.c2 & 63)] = (int16_t)o.v2;
+            if (z == 0) { ++bi; used_end = r.pos(); }
+        }
+        int kind = bad ? kDriError : kDriExact;
+        if (!bad && j + 1 < nint)
+            kind = dri_end_kind(U.data(), ulen, errpos, (used_end + 7) >> 3, j, j < (int64_t)rst.size() ? rst[j] : -1);
+        if (kind != kDriExact) key = std::min(key, (int32_t)(2 * j + (kind == kDriElsewhere)));
+    }
+    *first = key;
+    if (key != INT32_MAX && (key & 1)) return 1;
+    *status = key == INT32_MAX ? kOk : kSyntaxError;
+    return 0;
+}
 }
 
 // ---- guess-write path (k_gw_lane / k_gw_check / k_gw_count / k_gw_repair / k_gw_scan / k_gw_map) ----

@@ -11,6 +11,7 @@ from conftest import GOLDEN
 import imagecodecs_amd as icx
 from oracle import pyoracle as O
 from tools import synthpy as S
+from driutil import dri_corruptions, elsewhere_case, rst_markers
 
 pytestmark = pytest.mark.gpu
 
@@ -226,21 +227,78 @@ def test_dri_parallel_bit_exact(ctx, restart, sampling):
     b.close()
 
 
-def test_dri_corrupt_marker_falls_back_exactly(ctx):
-    """A restart marker with the wrong number / a shifted marker: the parallel result is not
-    used; the sequential kernel reproduces NanoJPEG's status and pixels."""
-    good = S.synth_jpeg(4100, 320, 240, "420", 80, 5)
+def test_dri_corrupt_markers_decided_in_parallel(ctx):
+    """Corrupt restart markers (wrong number, shifted, missing, doubled, swapped), flipped data
+    and truncation: the first interval not ending at its marker decides the image on the parallel
+    path (k_spec_write mode 3, dri_end_kind) -- NanoJPEG's status, no sequential decode -- and
+    the images that stay OK match the oracle byte for byte."""
+    rng = np.random.default_rng(41)
     cases = []
-    i = good.index(b"\xff\xd2")  # third marker
-    cases.append(good[:i + 1] + b"\xd5" + good[i + 2:])          # wrong marker number
-    cases.append(good[:i] + b"\x00" + good[i:])                   # extra byte before a marker
+    for restart, smp in [(1, "420"), (5, "420"), (3, "gray"), (16, "444")]:
+        cases += dri_corruptions(S.synth_jpeg(4100 + restart, 320, 240, smp, 80, restart), rng, 16)
     b = icx.Batch(ctx, len(cases), 320, 240)
     res = b.decode_host(cases)
+    stats = b.path_stats()
+    assert stats["fallback"] == 0 and stats["sequential"] == 0, stats
     for j, (code, w, h, n, pix) in zip(cases, res):
         ocode, _, _, _, opix = O.decode(j)
         assert code == ocode
         if code == 0:
             assert pix.tobytes() == opix
+    b.close()
+
+
+def test_dri_marker_read_elsewhere_falls_back_exactly(ctx):
+    """FF D0+(j&7) at interval j's end that is stuffed data, not marker j: NanoJPEG resumes there,
+    where no lane started, so that image alone goes to the sequential kernel -- with NanoJPEG's
+    status and pixels."""
+    v, _ = elsewhere_case()
+    good = S.synth_jpeg(4200, 512, 512, "420", 90, 1)
+    b = icx.Batch(ctx, 2, 512, 512)
+    res = b.decode_host([v, good])
+    assert b.path_stats() == {"parallel": 1, "fallback": 1, "sequential": 0}
+    for j, (code, w, h, n, pix) in zip([v, good], res):
+        ocode, _, _, _, opix = O.decode(j)
+        assert code == ocode
+        if code == 0:
+            assert pix.tobytes() == opix
+    b.close()
+
+
+def test_corrupt_dri_images_cost_no_sequential_time(ctx):
+    """A 64-image batch of 2048^2 DRI images (one interval per MCU row) with 8 corrupt ones
+    (wrong marker numbers, a byte lost): all are decided on the parallel path, and the batch takes
+    less than twice the clean batch's time (a sequential decode of one 2048^2 image alone takes
+    longer than the whole clean batch)."""
+    import time
+    pool = [S.synth_jpeg(4300 + k, 2048, 2048, "420", 90, 128) for k in range(8)]
+    clean = [pool[k % 8] for k in range(64)]
+    bad = list(clean)
+    for k in range(0, 64, 8):
+        d = bytearray(pool[k // 8 % 8])
+        mk = rst_markers(d)
+        q = mk[len(mk) // 2 + k]
+        if k % 16 == 0:
+            d[q + 1] = 0xD0 + ((d[q + 1] + 3) & 7)
+        else:
+            del d[q - 1]
+        bad[k] = bytes(d)
+    b = icx.Batch(ctx, 64, 2048, 2048)
+
+    def run(batch):
+        b.decode_host(batch)  # (warm)
+        t0 = time.perf_counter()
+        res = b.decode_host(batch)
+        return time.perf_counter() - t0, res
+
+    t_clean, _ = run(clean)
+    t_bad, res = run(bad)
+    stats = b.path_stats()
+    assert stats == {"parallel": 64, "fallback": 0, "sequential": 0}, stats
+    for k in range(0, 64, 8):
+        assert res[k][0] == O.decode(bad[k])[0] != 0
+    assert res[1][0] == 0 and res[1][4].tobytes() == O.decode(clean[1])[4]
+    assert t_bad < 2 * t_clean, (t_bad, t_clean)
     b.close()
 
 

@@ -15,6 +15,7 @@ import pytest
 from conftest import GOLDEN, ROOT
 from oracle import pyoracle as O
 from tools import synthpy as S
+from driutil import dri_corruptions, elsewhere_case
 
 EMU_DIR = os.path.join(ROOT, "tests", "emu")
 MANIFEST = json.load(open(os.path.join(GOLDEN, "decode_manifest.json")))
@@ -372,3 +373,59 @@ def test_gw_synthetic_random_leads(sampling):
         for sub in (64, 512):
             m, _ = gw_check(data, sub, int(rng.integers(0, 3000)), float(rng.choice([0.02, 1.1])))
             assert m == 0
+
+
+# ---- restart intervals (k_spec_write mode 3 + k_spec_finish) ----
+def dri_emu(data, cap=1 << 17):
+    L = emu_lib()
+    L.emu_dri_decode.restype = C.c_int
+    L.emu_dri_decode.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    coef = np.zeros((cap, 64), np.int16)
+    dc = np.zeros(cap, np.int32)
+    nb, st, first = C.c_int64(), C.c_int32(), C.c_int32()
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    mode = L.emu_dri_decode(buf, len(data), coef.ctypes.data, dc.ctypes.data, cap, C.byref(nb), C.byref(st),
+                            C.byref(first))
+    return mode, st.value, first.value, coef[: nb.value], dc[: nb.value]
+
+
+def dri_check(data):
+    """Emulated DRI decode vs the oracle: a parallel result must carry NanoJPEG's status, and its
+    coefficients when that is OK. Returns the mode (0 parallel, 1 sequential, 2 not eligible)."""
+    mode, st, first, coef, dc = dri_emu(data)
+    if mode != 0:
+        return mode
+    oc, ocoef, odc = O.decode_trace(data)
+    assert st == (0 if oc == 0 else 5), (st, oc, first)
+    if oc == 0:
+        assert np.array_equal(coef, ocoef) and np.array_equal(dc, odc)
+    return mode
+
+
+@pytest.mark.parametrize("restart,sampling", [(1, "420"), (3, "gray"), (5, "444"), (16, "422")])
+def test_emulated_dri_clean(restart, sampling):
+    """Clean DRI streams: every interval ends at its marker; coefficients equal the trace."""
+    for k in range(3):
+        data = S.synth_jpeg(8100 + k, 120 + 56 * k, 96 + 40 * k, sampling, 70 + 10 * k, restart)
+        mode, st, first, _, _ = dri_emu(data)
+        assert mode == 0 and st == 0 and first == 2**31 - 1
+        assert dri_check(data) == 0
+
+
+@pytest.mark.parametrize("restart,sampling", [(1, "420"), (2, "gray"), (7, "444"), (40, "420")])
+def test_emulated_dri_corrupt_status(restart, sampling):
+    """Corrupt DRI streams: the parallel status equals NanoJPEG's for every variant the lanes can
+    decide (the first interval not ending at its marker); only FF D0+(j&7) read somewhere other
+    than marker j sends an image to the sequential kernel."""
+    rng = np.random.default_rng(restart * 100 + len(sampling))
+    base = S.synth_jpeg(8200 + restart, 200, 152, sampling, 85, restart)
+    modes = [dri_check(v) for v in dri_corruptions(base, rng, 64)]
+    assert modes.count(2) == 0
+    assert modes.count(1) <= 2, modes  # (these seeds: none)
+
+
+def test_emulated_dri_elsewhere_goes_sequential():
+    v, j = elsewhere_case()
+    mode, st, first, _, _ = dri_emu(v)
+    assert mode == 1 and first == 2 * j + 1, (mode, first, j)
