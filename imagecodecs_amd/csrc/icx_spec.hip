@@ -715,10 +715,13 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 #pragma unroll
     for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        {  // uniform per workgroup; `want` (1 or 3) limits a launch to one mode. Tested before the
+           // tables are staged: the guess-write path's DRI launch spans every image's workgroups.
+            const int m = spec[find_image(wpre, n, wg)].mode;
+            if ((m != 1 && m != 3) || (want && m != want)) continue;
+        }
         const int i = wg_image_setup(wpre, n, wg, cur, T, steps);
         SpecImg& s = spec[i];
-        // uniform per workgroup; `want` (1 or 3) limits a launch to one mode
-        if ((s.mode != 1 && s.mode != 3) || (want && s.mode != want)) continue;
         const bool dri = s.mode == 3;
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         const Sel S = make_sel(desc[i]);
@@ -973,12 +976,15 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
         int32_t left = Sst, nxt = sbase;  // slots left in the current run (static, then chunks), the next one
         (void)kFar;
         // 2. store every block from g0 on
-        while (__any(live)) {
+        if (wave_any(live)) do {
             const bool bs = z == 0;
             const uint32_t u = r.used;
             const bool leave = live && bs && u >= span;
             ul = leave ? u : ul;
             bl = leave ? b : bl;
+            // (here, not sunk to the latch: there they keep the old b / used alive past their
+            // updates, which costs a copy of each per iteration)
+            asm volatile("" : "+v"(ul), "+v"(bl));
             live = live && !leave;
             const bool own_bs = live && bs;
             if (wave_any(own_bs && b == 0 && nrec < kRecGw)) {  // MCU start: a splice point for the count lane
@@ -1050,16 +1056,18 @@ __global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ 
                         const int sl = (wave << 6) | src;
                         int4* sp = &L.slots[sl][0];
                         const int sq = q ^ (sl & 7);
+#ifndef ICX_EXP_NOSTORE  // timing experiment only: drop the coefficient stores
                         typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
                         const int4 v = sp[sq];
                         const i32x4 vv = {v.x, v.y, v.z, v.w};
                         __builtin_nontemporal_store(vv, reinterpret_cast<i32x4*>(A) + (int64_t)bsrc * 8 + q);
+#endif
                         sp[sq] = make_int4(0, 0, 0, 0);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
             }
-        }
+        } while (wave_any(live));
         if (act) {
             X[f] = pack_state(s0 + ul, bl, 0);
             GwOut g;

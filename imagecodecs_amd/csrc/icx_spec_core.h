@@ -353,7 +353,12 @@ ICX_HD uint32_t ubfe(uint32_t x, uint32_t off, uint32_t w) {  // bits [off, off 
 }
 // njGetVLC's sign extension (jpeg_dec.h:653-654) of an nbx-bit magnitude (nbx = 0: 0).
 ICX_HD int32_t extend_mag(uint32_t raw, uint32_t nbx) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t mask;  // (1 << nbx) - 1 in one instruction (the compiler emits a shift and a not)
+    asm("v_bfm_b32 %0, %1, 0" : "=v"(mask) : "v"(nbx));
+#else
     const uint32_t mask = (1u << nbx) - 1u;
+#endif
     return (int32_t)(raw <= (mask >> 1) ? raw - mask : raw);
 }
 
