@@ -11,6 +11,7 @@ callers (tests, bench): it binds the C ABI with ctypes and offers
   * ``Batch``                     -- device-resident batched decode (the throughput path)
   * ``Context.hdr_decode``        -- Image::readHdr's Radiance RGBE -> float decode (codecs.cpp:706-777)
   * ``HdrBatch``                  -- device-resident batched .hdr decode
+  * ``Context.exr_decode``        -- Image::readExr's OpenEXR -> RGBA float (tinyexr LoadEXRFromMemory)
   * ``Image``                     -- ImageCodecs::Image (codecs.h:16-103) for .jpg/.jpeg/.png/.hdr
 
 There is deliberately no CPU fallback: if libicx.so is missing or no GPU is visible every
@@ -27,7 +28,7 @@ import numpy as np
 __all__ = ["ICXError", "Context", "Batch", "HdrBatch", "Image", "lib", "build", "LIB_PATH",
            "OK", "NO_JPEG", "UNSUPPORTED", "OUT_OF_MEM", "INTERNAL_ERR", "SYNTAX_ERROR",
            "HDR_OK", "HDR_NOT_RADIANCE", "HDR_BAD_HEADER", "HDR_MALFORMED", "HDR_TRUNCATED",
-           "HDR_TOO_LARGE", "HDR_INTERNAL_ERR", "hdr_probe", "Multi", "RECORD_DTYPE", "records_device",
+           "HDR_TOO_LARGE", "HDR_INTERNAL_ERR", "hdr_probe", "exr_probe", "EXR_SUCCESS", "EXR_INVALID_DATA", "Multi", "RECORD_DTYPE", "records_device",
            "checksum64", "multi_shard"]
 
 OK, NO_JPEG, UNSUPPORTED, OUT_OF_MEM, INTERNAL_ERR, SYNTAX_ERROR = range(6)  # nj_result_t
@@ -104,6 +105,8 @@ _SIGS = {
     "icx_multi_decode_host": (_i32, [_vp, _i32, _vp, _vp, _vp, _u64, _vp, _vp]),
     "icx_multi_last_error": (C.c_char_p, [_vp]),
     "icx_multi_shard": (_i32, [_vp, _i32, _i32, _vp]),
+    "icx_exr_probe": (_i32, [_vp, _sz, C.POINTER(_i32), C.POINTER(_i32)]),
+    "icx_exr_decode": (_i32, [_vp, _vp, _sz, C.POINTER(_vp), C.POINTER(_i32), C.POINTER(_i32)]),
 }
 
 # icx_record (include/icx.h): per-image result record gathered across devices / ranks
@@ -113,6 +116,10 @@ RECORD_DTYPE = np.dtype([("status", "<i4"), ("width", "<i4"), ("height", "<i4"),
 # icx_hdr_result (include/icx.h): Image::readHdr outcomes
 HDR_OK, HDR_NOT_RADIANCE, HDR_BAD_HEADER, HDR_MALFORMED, HDR_TRUNCATED, HDR_TOO_LARGE = range(6)
 HDR_INTERNAL_ERR = -1
+
+# icx_exr_result (include/icx.h): tinyexr's LoadEXRFromMemory codes
+EXR_SUCCESS, EXR_INVALID_MAGIC_NUMBER, EXR_INVALID_EXR_VERSION, EXR_INVALID_ARGUMENT, EXR_INVALID_DATA = 0, -1, -2, -3, -4
+EXR_UNSUPPORTED_FORMAT, EXR_INVALID_HEADER, EXR_UNSUPPORTED_FEATURE, EXR_INTERNAL_ERR = -8, -9, -10, -100
 
 WRITE_FUNC = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
 
@@ -251,6 +258,22 @@ class Context:
             arr = np.frombuffer(C.string_at(out.value, n * 4), np.float32).reshape(h.value, w.value, 4).copy()
             lib().icx_free(out)
         return code, w.value, h.value, rows.value, arr
+
+    def exr_decode(self, data: bytes):
+        """Image::readExr's LoadEXRFromMemory (tinyexr.h:6645) on the GPU -> (code, w, h, float32
+        (h, w, 4) RGBA or None); code is an icx_exr_result (tinyexr's codes)."""
+        buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+        out = C.c_void_p()
+        w, h = C.c_int(), C.c_int()
+        code = lib().icx_exr_decode(self._p, buf, len(data), C.byref(out), C.byref(w), C.byref(h))
+        if code == EXR_INTERNAL_ERR:
+            raise ICXError("icx_exr_decode: " + _err(self._p))
+        arr = None
+        if out.value:
+            n = w.value * h.value * 4
+            arr = np.frombuffer(C.string_at(out.value, n * 4), np.float32).reshape(h.value, w.value, 4).copy()
+            lib().icx_free(out)
+        return code, w.value, h.value, arr
 
     def png_encode(self, width: int, height: int, d: int, src: bytes):
         """PNG bytes of an RGB8 (d=3) / RGBA8 (d=4) image (png_encoder::saveToFile), or None."""
@@ -513,6 +536,14 @@ def hdr_probe(data: bytes):
     return code, w.value, h.value
 
 
+def exr_probe(data: bytes):
+    """Host header / offset-table / chunk-header walk of LoadEXRFromMemory -> (code, width, height)."""
+    w, h = C.c_int(), C.c_int()
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    code = lib().icx_exr_probe(buf, len(data), C.byref(w), C.byref(h))
+    return code, w.value, h.value
+
+
 class HdrBatch:
     """Device-resident batched Radiance .hdr decode (icx_hdr_batch_*): image i is
     d_data[d_offsets[i] .. + d_sizes[i]); 4 floats per pixel at d_out + i*out_stride floats."""
@@ -572,6 +603,9 @@ class Image:
         if ext == ".hdr":
             self._read_hdr(filepath)
             return
+        if ext == ".exr":
+            self._read_exr(filepath)
+            return
         if ext not in (".jpg", ".jpeg"):
             raise ValueError("Cannot parse filetype")
         data = open(filepath, "rb").read()
@@ -590,6 +624,19 @@ class Image:
         code, w, h, rows, px = self.context().hdr_decode(data)
         if code not in (HDR_OK, HDR_TRUNCATED):
             raise RuntimeError("Invalid file format")
+        self.w_, self.h_, self.d_ = w, h, 4
+        self.pixels_ = px.reshape(-1).view(np.uint8).copy()
+        self.type_ = Image.FLOAT
+
+    def _read_exr(self, filepath: str):
+        """readExr (codecs.cpp:464-493): LoadEXRFromMemory -> d = 4, type FLOAT, the floats' bytes in
+        pixels_; a failure raises RuntimeError("Could not load .exr") (:489). (The reference reads
+        the file with a loop that appends one extra byte, ifile.get()'s EOF, :468-471; tinyexr
+        ignores bytes past the last chunk, so the result is the same.)"""
+        data = open(filepath, "rb").read()
+        code, w, h, px = self.context().exr_decode(data + b"\xff")
+        if code != EXR_SUCCESS:
+            raise RuntimeError("Could not load .exr")
         self.w_, self.h_, self.d_ = w, h, 4
         self.pixels_ = px.reshape(-1).view(np.uint8).copy()
         self.type_ = Image.FLOAT

@@ -73,6 +73,11 @@ static thread_local char g_msg[512];
 
 // Brackets every pipeline stage with HIP events on the launch stream, and with a roctx range on
 // the host (the launch side: `rocprofv3 --marker-trace` shows which stage enqueued which kernels).
+// One roctx range per API call, around every stage's range.
+struct RoctxRange {
+    explicit RoctxRange(const char* m) { (void)roctxRangePushA(m); }
+    ~RoctxRange() { (void)roctxRangePop(); }
+};
 static const char* const kRangeNames[kStCount] = {"icx:parse", "icx:unstuff", "icx:entropy", "icx:write",
                                                   "icx:idct", "icx:upsample", "icx:convert"};
 struct EventHook : StageHook {
@@ -319,10 +324,7 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     if (!d_data || !d_off || !d_size || !d_out || !d_status || !d_dims) { ctx->err = "null pointer"; return ICX_INTERNAL_ERR; }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-    struct Range {  // one roctx range per call, around every stage's range
-        explicit Range(const char* m) { (void)roctxRangePushA(m); }
-        ~Range() { (void)roctxRangePop(); }
-    } range("icx_jpeg_batch_decode");
+    const RoctxRange range("icx_jpeg_batch_decode");
     b->hook->reset();
     for (int p = 0; p < b->pipes; ++p)
         ICX_HIP(ctx, hipMemsetAsync(b->ws[p].stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
@@ -788,10 +790,7 @@ int icx_hdr_batch_decode(icx_hdr_batch* b, int n, const uint8_t* d_data, const u
     if (out_stride < 4ull * b->ws.max_w * b->ws.max_h) { ctx->err = "icx_hdr_batch_decode: out_stride too small"; return ICX_HDR_INTERNAL_ERR; }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_HDR_INTERNAL_ERR);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-    struct Range {  // one roctx range per call, around every stage's range
-        explicit Range(const char* m) { (void)roctxRangePushA(m); }
-        ~Range() { (void)roctxRangePop(); }
-    } range("icx_jpeg_batch_decode");
+    const RoctxRange range("icx_hdr_batch_decode");
     b->hook->reset();
     launch_hdr_decode(b->ws, n, d_data, d_off, d_size, d_out, out_stride, d_status, d_dims, st, b->hook.get());
     ICX_HIP(ctx, hipGetLastError(), ICX_HDR_INTERNAL_ERR);
@@ -861,6 +860,33 @@ int icx_hdr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out, 
     (void)hipFree(d_meta);
     (void)hipFree(d_res);
     icx_hdr_batch_destroy(b);
+    return rc;
+}
+
+// --------------------------------------------------------- OpenEXR (Image::readExr)
+int icx_exr_probe(const uint8_t* data, size_t size, int* w, int* h) {
+    if (w) *w = 0;
+    if (h) *h = 0;
+    if (!data) return ICX_EXR_INVALID_ARGUMENT;
+    return exr_probe(data, size, w, h);
+}
+
+int icx_exr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out, int* w, int* h) {
+    if (out) *out = nullptr;
+    if (w) *w = 0;
+    if (h) *h = 0;
+    if (!ctx) return ICX_EXR_INTERNAL_ERR;
+    if (!data || !out) return ICX_EXR_INVALID_ARGUMENT;  // LoadEXRFromMemory's NULL checks (:6648-6651)
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_EXR_INTERNAL_ERR);
+    const RoctxRange range("icx_exr_decode");
+    int ww = 0, hh = 0;
+    std::string err;
+    const int rc = exr_decode(ctx->stream, data, size, out, &ww, &hh, err);
+    if (rc == ICX_EXR_INTERNAL_ERR) ctx->err = err.empty() ? "icx_exr_decode: HIP failure" : err;
+    if (rc == ICX_EXR_SUCCESS) {
+        if (w) *w = ww;
+        if (h) *h = hh;
+    }
     return rc;
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
 #include <vector>
 
 #include "icx_jpeg.h"
@@ -254,5 +255,11 @@ void hdr_ws_free(HdrWs& ws);
 void launch_hdr_decode(const HdrWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_size,
                        float* d_out, uint64_t out_stride, int32_t* d_status, int32_t* d_dims, hipStream_t st,
                        StageHook* hook);
+
+// ---- OpenEXR read (icx_exr.hip) ----
+// tinyexr's LoadEXRFromMemory; returns its code (-100: HIP failure, err says which).
+int exr_decode(hipStream_t st, const uint8_t* data, size_t size, float** out_rgba, int* width, int* height,
+               std::string& err);
+int exr_probe(const uint8_t* data, size_t size, int* width, int* height);
 
 }  // namespace icx

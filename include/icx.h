@@ -256,6 +256,33 @@ int icx_hdr_batch_decode(icx_hdr_batch* b, int n, const uint8_t* d_data, const u
  * "convert"; synchronises). Returns the number of stages. */
 int icx_hdr_batch_stage_times(const icx_hdr_batch* b, const char** names, float* ms, int cap);
 
+/* ---- OpenEXR read (Image::readExr, codecs.cpp:464-493 -> tinyexr LoadEXRFromMemory, tinyexr.h:6645) ----
+ * Output as LoadEXRFromMemory returns it: width*height*4 floats (R, G, B, A by channel name; a
+ * one-channel image repeats its channel in all four; no A channel -> 1.0), data-window rows in
+ * tinyexr's order. HALF samples are converted bit for bit (half_to_float), FLOAT copied, UINT
+ * sample bits copied unconverted (tinyexr reads them through its float** view).
+ * Scope: single-part scanline or one-level tiled files, NONE / RLE / ZIPS / ZIP compression;
+ * PIZ -> ICX_EXR_UNSUPPORTED_FORMAT (tinyexr built with TINYEXR_USE_PIZ 0), multi-part, deep and
+ * mip- / rip-mapped files -> ICX_EXR_UNSUPPORTED_FEATURE. Pixels no chunk wrote (tinyexr leaves
+ * them uninitialised) are 0. */
+enum icx_exr_result {
+    ICX_EXR_SUCCESS = 0,                /* TINYEXR_SUCCESS                          */
+    ICX_EXR_INVALID_MAGIC_NUMBER = -1,  /* TINYEXR_ERROR_INVALID_MAGIC_NUMBER       */
+    ICX_EXR_INVALID_EXR_VERSION = -2,   /* TINYEXR_ERROR_INVALID_EXR_VERSION        */
+    ICX_EXR_INVALID_ARGUMENT = -3,      /* TINYEXR_ERROR_INVALID_ARGUMENT           */
+    ICX_EXR_INVALID_DATA = -4,          /* TINYEXR_ERROR_INVALID_DATA               */
+    ICX_EXR_UNSUPPORTED_FORMAT = -8,    /* TINYEXR_ERROR_UNSUPPORTED_FORMAT         */
+    ICX_EXR_INVALID_HEADER = -9,        /* TINYEXR_ERROR_INVALID_HEADER             */
+    ICX_EXR_UNSUPPORTED_FEATURE = -10,  /* TINYEXR_ERROR_UNSUPPORTED_FEATURE        */
+    ICX_EXR_INTERNAL_ERR = -100         /* HIP failure (see icx_last_error)         */
+};
+/* Header, offset table and chunk headers only (host): the data window size, or the error code
+ * LoadEXRFromMemory would return before decoding pixels. */
+int icx_exr_probe(const uint8_t* data, size_t size, int* width, int* height);
+/* One image, host in / host out: *out_rgba receives a malloc()'d width*height*4 float buffer
+ * (free with icx_free). Returns an icx_exr_result. */
+int icx_exr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out_rgba, int* width, int* height);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,8 @@
  *                  decode on the GPU (readJpg, codecs.cpp:821-849 -> icx_jpeg_decode).
  *               ".hdr" decodes Radiance RGBE to 4 floats per pixel on the GPU (readHdr,
  *               codecs.cpp:706-777 -> icx_hdr_decode; bit-identical floats).
+ *               ".exr" decodes OpenEXR to RGBA floats on the GPU (readExr, codecs.cpp:464-493 ->
+ *               icx_exr_decode = tinyexr's LoadEXRFromMemory; scope in include/icx.h).
  *   write(path) -- ".jpg"/".jpeg" encode with tiny_jpeg quality 3 semantics (writeJpg,
  *                  codecs.cpp:851-854 -> icx_tje_encode_to_file, byte-identical stream).
  *               ".png" encodes with png_encoder::saveToFile semantics (writePng,
@@ -152,6 +154,41 @@ class Image {
         type_ = Type::FLOAT;
     }
 
+    // readExr (codecs.cpp:464-493): LoadEXRFromMemory -> d = 4, Type::FLOAT. The reference's read
+    // loop stores one byte more than the file holds (ifile.get()'s EOF as 0xFF, :468-471); it is
+    // passed on the same way. A failure throws "Could not load .exr" (:489).
+    void readExr(const std::string& path) {
+        std::FILE* f = std::fopen(path.c_str(), "rb");
+        std::vector<uint8_t> buf;
+        if (f) {
+            uint8_t chunk[1 << 16];
+            size_t k;
+            while ((k = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + k);
+            std::fclose(f);
+        }
+        buf.push_back(0xFF);
+        auto& P = detail::icx_process();
+        std::lock_guard<std::mutex> lock(P.mu);
+        float* out = nullptr;
+        int w = 0, h = 0;
+        const int rc = icx_exr_decode(P.get(), buf.data(), buf.size(), &out, &w, &h);
+        if (rc != ICX_EXR_SUCCESS) {
+            icx_free(out);
+            if (rc == ICX_EXR_INTERNAL_ERR) throw std::runtime_error(std::string("icx_exr_decode: ") + icx_last_error(P.get()));
+            throw std::runtime_error("Could not load .exr");
+        }
+        const size_t n = (size_t)w * h * 4 * sizeof(float);
+        unsigned char* px = new unsigned char[n ? n : 1];
+        if (n) std::memcpy(px, out, n);
+        icx_free(out);
+        delete[] pixels_;
+        pixels_ = px;
+        w_ = w;
+        h_ = h;
+        d_ = 4;
+        type_ = Type::FLOAT;
+    }
+
     void writeJpg(const std::string& path) {
         auto& P = detail::icx_process();
         std::lock_guard<std::mutex> lock(P.mu);
@@ -226,6 +263,7 @@ public:
         const std::string ext = detail::lower_ext(filepath);
         if (ext == ".jpg" || ext == ".jpeg") readJpg(filepath);
         else if (ext == ".hdr") readHdr(filepath);
+        else if (ext == ".exr") readExr(filepath);
         else throw std::invalid_argument("Cannot parse filetype");
         if (pixels_ == nullptr) throw std::runtime_error("Could not read image data");
     }

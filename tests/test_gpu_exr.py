@@ -1,0 +1,91 @@
+"""GPU tests of the OpenEXR read (Image::readExr -> tinyexr LoadEXRFromMemory, tinyexr.h:6645) through
+the C ABI (icx_exr_decode): every fixture's code and RGBA float bits equal the manifest (the
+oracle's result), larger images and random damage equal the oracle live. PARITY UNPINNED (see
+oracle/exr_oracle.py)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+import imagecodecs_amd as icx
+from oracle import exr_oracle as O
+from tools import exrwrite as W
+
+pytestmark = pytest.mark.gpu
+
+MAN = json.load(open(os.path.join(GOLDEN, "exr_manifest.json")))
+EXR = os.path.join(GOLDEN, "exr")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = icx.Context(0)
+    yield c
+    c.close()
+
+
+def sha(img):
+    return hashlib.sha256(np.ascontiguousarray(img).view(np.uint32).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", sorted(MAN))
+def test_exr_fixture(ctx, name):
+    data = open(os.path.join(EXR, name), "rb").read()
+    code, w, h, img = ctx.exr_decode(data)
+    e = MAN[name]
+    assert (code, w, h) == (e["code"], e["w"], e["h"])
+    assert icx.exr_probe(data)[0] == code or code == icx.EXR_INVALID_DATA  # (pixel-data failures: device)
+    if code == 0:
+        assert sha(img) == e["sha256"]
+
+
+@pytest.mark.parametrize("comp,tiles", [(W.ZIP, None), (W.ZIPS, None), (W.RLE, None), (W.NONE, None), (W.ZIP, (64, 64)),
+                                        (W.RLE, (128, 32))])
+def test_exr_large_vs_oracle(ctx, comp, tiles):
+    """A 1000x700 half RGBA image (ZIP chunks of 16 lines = 22 KB of samples each, windows
+    reaching back past 32 KiB of output) decodes to the oracle's bits."""
+    rng = np.random.default_rng(comp * 10 + (tiles is not None))
+    h, w = 700, 1000
+    y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+    chans = [(n, (np.sin(x * (0.01 + 0.003 * k)) * np.cos(y * 0.013) * 50 + rng.normal(0, 0.05, (h, w))).astype(np.float16))
+             for k, n in enumerate("RGBA")]
+    data = W.write_exr(chans, compression=comp, tiles=tiles)
+    oc, ow, oh, oimg = O.decode(data)
+    code, ww, hh, img = ctx.exr_decode(data)
+    assert (code, ww, hh) == (oc, ow, oh) == (0, w, h)
+    assert np.array_equal(img.view(np.uint32), oimg.view(np.uint32))
+
+
+def test_exr_random_damage(ctx):
+    """Random byte damage to fixtures: the GPU's code equals the oracle's, and so do the bits of
+    the files that still decode."""
+    rng = np.random.default_rng(11)
+    names = [n for n in sorted(MAN) if MAN[n]["code"] == 0 and "wide" not in n]
+    for k in range(80):
+        data = bytearray(open(os.path.join(EXR, names[int(rng.integers(0, len(names)))]), "rb").read())
+        for _ in range(1 + k % 3):
+            data[int(rng.integers(0, len(data)))] ^= int(rng.integers(1, 256))
+        data = bytes(data)
+        oc, ow, oh, oimg = O.decode(data)
+        code, w, h, img = ctx.exr_decode(data)
+        assert (code, w, h) == (oc, ow, oh), k
+        if oc == 0:
+            assert np.array_equal(img.view(np.uint32), oimg.view(np.uint32)), k
+
+
+def test_image_read_exr(tmp_path):
+    """Image.read('.exr') = readExr: d = 4, FLOAT, the decoded floats' bytes; a broken file raises."""
+    name = "scan_zip_half.exr"
+    p = tmp_path / "a.exr"
+    p.write_bytes(open(os.path.join(EXR, name), "rb").read())
+    im = icx.Image()
+    im.read(str(p))
+    assert (im.cols(), im.rows(), im.d_, im.type_) == (MAN[name]["w"], MAN[name]["h"], 4, icx.Image.FLOAT)
+    assert hashlib.sha256(im.pixels_.tobytes()).hexdigest() == MAN[name]["sha256"]
+    q = tmp_path / "b.exr"
+    q.write_bytes(open(os.path.join(EXR, "zip_bad_adler.exr"), "rb").read())
+    with pytest.raises(RuntimeError):
+        icx.Image().read(str(q))
