@@ -29,9 +29,14 @@ struct Deflate {  // RFC 1951 §3.2.5-3.2.7 length / distance bases and extra bi
     static constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 };
 
-struct InfTab {  // canonical code: number of codes per length, symbols in code order
+constexpr int kInfFast = 9;  // bits of the direct decoding table
+
+struct InfTab {  // canonical code: number of codes per length, symbols in code order, and a
+                 // direct table of the codes up to kInfFast bits (bit-reversed index: the stream
+                 // is LSB first; entry = symbol << 4 | length, 0: a longer code)
     uint16_t count[16];
     uint16_t sym[288];
+    uint16_t fast[1 << kInfFast];
 };
 
 struct InfState {
@@ -45,13 +50,16 @@ struct BitIn {
     uint64_t buf;       // LSB-first bit buffer
     int cnt;            // bits in buf (past the end of the input: zero bits)
     int64_t over;       // bits loaded past the end of the input
-    ICX_HD void fill(int k) {
-        while (cnt < k) {
-            if (pos < n) buf |= (uint64_t)s[pos] << cnt;
+    ICX_HD void fill(int k) {  // k <= 32: four bytes at a time (independent loads)
+        if (cnt >= k) return;
+        uint32_t w = 0;
+        for (int j = 0; j < 4; ++j) {
+            if (pos + j < n) w |= (uint32_t)s[pos + j] << (8 * j);
             else over += 8;
-            ++pos;
-            cnt += 8;
         }
+        buf |= (uint64_t)w << cnt;
+        pos += 4;
+        cnt += 32;
     }
     ICX_HD uint32_t bits(int k) {  // k <= 24
         fill(k);
@@ -77,17 +85,34 @@ ICX_HD bool inf_build(InfTab& h, const uint8_t* len, int n) {
         if (left < 0) return false;
     }
     if (left > 0 && used > 1) return false;
-    uint16_t offs[16];
+    uint16_t offs[16], next[16];
     offs[1] = 0;
     for (int l = 1; l < 15; ++l) offs[l + 1] = (uint16_t)(offs[l] + h.count[l]);
-    for (int s = 0; s < n; ++s)
-        if (len[s]) h.sym[offs[len[s]]++] = (uint16_t)s;
+    next[1] = 0;
+    for (int l = 1; l < 15; ++l) next[l + 1] = (uint16_t)((next[l] + h.count[l]) << 1);
+    for (int i = 0; i < (1 << kInfFast); ++i) h.fast[i] = 0;
+    for (int s = 0; s < n; ++s) {
+        const int l = len[s];
+        if (!l) continue;
+        h.sym[offs[l]++] = (uint16_t)s;
+        const uint32_t code = next[l]++;
+        if (l > kInfFast) continue;
+        uint32_t rev = 0;
+        for (int b = 0; b < l; ++b) rev |= ((code >> b) & 1u) << (l - 1 - b);
+        for (uint32_t i = rev; i < (1u << kInfFast); i += 1u << l) h.fast[i] = (uint16_t)((s << 4) | l);
+    }
     return true;
 }
 
 ICX_HD int inf_decode(BitIn& in, const InfTab& h) {
     in.fill(16);
-    uint32_t w = (uint32_t)in.buf;
+    const uint32_t e = h.fast[in.buf & ((1u << kInfFast) - 1u)];
+    if (e) {
+        in.buf >>= e & 15u;
+        in.cnt -= (int)(e & 15u);
+        return (int)(e >> 4);
+    }
+    uint32_t w = (uint32_t)in.buf;  // a code longer than kInfFast bits (or none): by length
     int code = 0, first = 0, index = 0;
     for (int l = 1; l <= 15; ++l) {
         code |= (int)(w & 1u);
@@ -115,15 +140,23 @@ ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap
     if ((cmf * 256u + flg) % 31u != 0 || (flg & 32u) || (cmf & 15u) != 8) return false;
     BitIn in{src, n, 2, 0ull, 0, 0};
     int64_t out = 0;
-    uint32_t a1 = 1, a2 = 0;  // Adler-32
+    uint32_t a1 = 1, a2 = 0, nm = 0;  // Adler-32, reduced every 5552 bytes (zlib's NMAX)
+    uint32_t acc = 0;                 // output bytes gathered into 32-bit stores (dst 4-byte aligned)
     auto put = [&](uint8_t b) {
-        dst[out] = b;
         win[out & (kExrWin - 1)] = b;
+        acc |= (uint32_t)b << (8 * (out & 3));
+        if ((out & 3) == 3) {
+            *reinterpret_cast<uint32_t*>(dst + (out & ~(int64_t)3)) = acc;
+            acc = 0;
+        }
         ++out;
         a1 += b;
-        if (a1 >= 65521u) a1 -= 65521u;
         a2 += a1;
-        if (a2 >= 65521u) a2 -= 65521u;
+        if (++nm == 5552) {
+            a1 %= 65521u;
+            a2 %= 65521u;
+            nm = 0;
+        }
     };
     int last = 0;
     while (!last) {
@@ -197,6 +230,11 @@ ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap
             for (int j = 0; j < len; ++j) put(win[(out - dist) & (kExrWin - 1)]);
         }
     }
+    if (out & 3) {  // the last partial word (dst holds cap bytes: write only what is ours)
+        for (int64_t k = out & ~(int64_t)3; k < out; ++k) dst[k] = (uint8_t)(acc >> (8 * (k & 3)));
+    }
+    a1 %= 65521u;
+    a2 %= 65521u;
     in.bits(in.cnt & 7);  // to a byte boundary
     uint32_t adler = 0;
     for (int k = 0; k < 4; ++k) adler = (adler << 8) | in.bits(8);
