@@ -37,14 +37,26 @@ STAGE_KERNEL = {"write": "k_gw_lane", "idct": "k_idct420y+k_idct420c", "convert"
                 "unstuff": "k_ustf_count+k_ustf_scan+k_ustf_write",
                 "entropy": "k_gw_check+k_gw_count+k_gw_repair+k_gw_scan+k_gw_map",
                 "parse": "k_parse", "upsample": "k_upsample"}
-if os.environ.get("ICX_GW", "1") == "0":  # the guess / count / write passes (experiments)
-    STAGE_KERNEL.update(write="k_spec_write", entropy="k_spec_guess+k_spec_count+k_spec_scan")
+GW_MIN_PIXELS = 2048 * 2048  # icx_internal.h kGwMinPixels: larger workspaces take the guess-write path
+
+
+def stage_kernels(w, h):
+    """STAGE_KERNEL for a batch of w x h images: the three-pass entropy path's kernels where the
+    library takes it (ICX_GW=0, or a workspace for images of at most GW_MIN_PIXELS)."""
+    env = os.environ.get("ICX_GW")
+    gw = env != "0" if env is not None else w * h > GW_MIN_PIXELS
+    k = dict(STAGE_KERNEL)
+    if not gw:
+        k.update(write="k_spec_write", entropy="k_spec_guess+k_spec_count+k_spec_scan")
+    return k
 
 WORKLOADS = {
     "c3": dict(n=512, w=4096, h=4096, sampling="420", quality=90,
                desc="C3 per-GPU shard: 512 x 4096x4096 4:2:0 q90 baseline JPEG (C3 = 4096 images / 8 GPUs)"),
     "c2": dict(n=1024, w=1024, h=1024, sampling="420", quality=90,
                desc="C2: 1024 x 1024x1024 4:2:0 q90 baseline JPEG"),
+    "c2048": dict(n=256, w=2048, h=2048, sampling="420", quality=90,
+                  desc="256 x 2048x2048 4:2:0 q90 baseline JPEG (between C2 and C3: entropy path crossover)"),
     "c3dri": dict(n=512, w=4096, h=4096, sampling="420", quality=90, restart=256,
                   desc="C3 shard with restart markers every MCU row (DRI 256): camera-style streams"),
     "c4": dict(n=64, w=4096, h=4096, sampling="420", quality=90,
@@ -726,7 +738,7 @@ def main():
         achieved = alg_bytes / (stages[dom] * 1e-3) / 1e9  # = per-launch alg bytes / avg launch time
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        kname = STAGE_KERNEL.get(dom, dom)
+        kname = stage_kernels(W, H).get(dom, dom)
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             # PMC runs may group images differently (the profiler holds HBM, so fewer images fit a
@@ -741,8 +753,7 @@ def main():
                 "stage_ms": {k: round(v, 3) for k, v in stages.items()},
                 "pipeline_frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
     out = {
-        "metric": "megapixels/s JPEG decode, 4096x4096 RGB batch" if args.workload.startswith("c3")
-        else "megapixels/s JPEG decode, 1024x1024 RGB batch",
+        "metric": f"megapixels/s JPEG decode, {W}x{H} RGB batch",
         "value": round(value, 2), "unit": "megapixels/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (tools/synth.c, seeded)",

@@ -66,6 +66,7 @@ struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
 constexpr int kGwChunk = 32;
 constexpr int kRecGw = kRec;    // MCU starts a guess-write lane records (the count lanes splice at the first
                                 // they reach; a lane that cannot splice is count-decoded whole)
+constexpr int64_t kGwMinPixels = 2048 * 2048;  // workspaces for larger images take the guess-write path
 constexpr int kGwMaxWalk = 64;  // lanes a repair walk may re-derive before the image goes sequential
 struct GwOut {
     uint64_t g0;     // first block start at or after the lane's start: pack_state(pos, b, 0)

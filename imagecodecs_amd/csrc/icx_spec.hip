@@ -1450,7 +1450,13 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     // (at least kSubBytesSmall: the lane records are sized for lanes of that length, ws_per_slot)
     static const int sub_env = std::getenv("ICX_SUB_BYTES") ? std::max(kSubBytesSmall, std::atoi(std::getenv("ICX_SUB_BYTES"))) & ~15
                                : std::getenv("ICX_SUB_MAX") ? -(std::max(kSubBytesSmall, std::atoi(std::getenv("ICX_SUB_MAX"))) & ~15) : 0;
-    static const int gw = std::getenv("ICX_GW") ? std::atoi(std::getenv("ICX_GW")) != 0 : 1;
+    // Guess-write for large images; the three-pass path where lanes are short: a workspace for
+    // images of up to kGwMinPixels pixels has them (a 1024^2 q90 image: 512 lanes of 768 B, where
+    // the lead and splice records weigh more: C2 159 vs 142-150 GP/s; 2048^2, 1.5 KB lanes: 153
+    // vs 148; 4096^2, 2.5 KB lanes: 207 vs 220).
+    // ICX_GW=0 / 1 forces one (read per launch: tests run both paths in one process).
+    const char* gw_env = std::getenv("ICX_GW");
+    const int gw = gw_env ? (std::atoi(gw_env) != 0) : ((int64_t)ws.max_w * ws.max_h > kGwMinPixels ? 1 : 0);
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
                        ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw);

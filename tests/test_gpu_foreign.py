@@ -58,11 +58,18 @@ def _batch_check(ctx, names, max_w, max_h):
     b.close()
 
 
+@pytest.mark.parametrize("gw", ["1", "0", None])
 @pytest.mark.parametrize("mode", ["0", "1", "2"])
-def test_foreign_batch_all_plane_modes(ctx, monkeypatch, mode):
+def test_foreign_batch_all_plane_modes(ctx, monkeypatch, mode, gw):
     """All foreign + crafted streams in one batch, under each 4:2:0 plane mode (the lane-pair IDCT
-    of modes 1 and 2 meets the large-coefficient streams): parallel path for every valid one."""
+    of modes 1 and 2 meets the large-coefficient streams) and each entropy path (ICX_GW 1:
+    guess-write, 0: three passes, unset: the workspace-size choice): parallel path for every
+    valid one."""
     monkeypatch.setenv("ICX_FUSE420", mode)
+    if gw is None:
+        monkeypatch.delenv("ICX_GW", raising=False)
+    else:
+        monkeypatch.setenv("ICX_GW", gw)
     names = sorted(MANIFEST)
     mw = max(MANIFEST[n]["w"] for n in names)
     mh = max(MANIFEST[n]["h"] for n in names)
