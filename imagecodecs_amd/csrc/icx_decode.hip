@@ -1300,10 +1300,19 @@ __device__ __forceinline__ void idct_units(const int16_t* ac, int h, uint32_t wi
 #endif
 }
 
+// Waves per SIMD the 4:2:0 IDCT kernels are compiled for (timing experiments: 5 keeps them at 96
+// VGPRs, so a wave fits beside four k_gw_lane waves on a SIMD).
+#ifndef ICX_IDCT_Y_MINW
+#define ICX_IDCT_Y_MINW 1
+#endif
+#ifndef ICX_IDCT_C_MINW
+#define ICX_IDCT_C_MINW 1
+#endif
+
 // Chroma planes of fused420 images: a wave's unit is 16 MCUs of one MCU row; lane pair q < 16
 // takes Cb of MCU mx0 + q, q >= 16 Cr of MCU mx0 + q - 16, so each plane row of the unit is
 // 128 contiguous bytes written by one store instruction.
-__global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+__global__ __launch_bounds__(256, ICX_IDCT_C_MINW) void k_idct420c(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                                   const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
                                                   uint8_t* __restrict__ planes, int64_t plane_cap) {
     const int img = blockIdx.y;
@@ -1344,7 +1353,7 @@ __global__ __launch_bounds__(256) void k_idct420c(const Desc* __restrict__ desc,
 // wave's unit is 8 MCUs of one MCU row; lane pair q takes luma block q & 3 of MCU mx0 + (q >> 2),
 // so each store instruction writes two whole 128-byte plane rows (the unit's upper and lower
 // block rows).
-__global__ __launch_bounds__(256) void k_idct420y(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+__global__ __launch_bounds__(256, ICX_IDCT_Y_MINW) void k_idct420y(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                                   const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
                                                   uint8_t* __restrict__ planes, int64_t plane_cap) {
     const int img = blockIdx.y;

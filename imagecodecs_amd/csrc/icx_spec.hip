@@ -908,8 +908,11 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 //     assembled in LDS slots and flushed by the whole wave -- storing every block until the
 //     first block start at or after the lane's end (the exit), recording MCU starts for the
 //     count lanes' splice.
+#ifndef ICX_GW_MINW  // (timing experiments: waves per SIMD k_gw_lane is compiled for)
+#define ICX_GW_MINW 1
+#endif
 template <int NL>
-__global__ __launch_bounds__(NL) void k_gw_lane(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+__global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                 const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                 const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
                                                 int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
