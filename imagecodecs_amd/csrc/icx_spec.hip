@@ -569,7 +569,10 @@ __global__ __launch_bounds__(NL) void k_spec_guess(int n, const Desc* __restrict
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
         const int64_t sb = (int64_t)s.sub_bytes * 8;
         X[f] = lane_guess(U + s.uoff, s.ulen, T, desc[i].huff, make_sel(desc[i]), j * sb, (j + 1) * sb, 0,
-                          rec + f * kRec, nrec + f, gtot + 4 * f, lead >= 0 ? lead : min(2048, s.sub_bytes * 2));  // (measured best here)
+                          rec + f * kRec, nrec + f, gtot + 4 * f,
+                          // a quarter of the lane, at most 2048 bits (C2's 768-byte lanes, one box,
+                          // two rounds each: 1536 bits 160.2-160.7 GP/s, 1024 158.4-158.6, 768 154)
+                          lead >= 0 ? lead : min(2048, s.sub_bytes * 2));
     }
 }
 
