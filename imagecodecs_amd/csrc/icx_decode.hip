@@ -1109,7 +1109,7 @@ __global__ __launch_bounds__(256) void k_convert_edge(const Desc* __restrict__ d
     static_assert(K & 1, "horizontally doubled layouts only");
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk || stream_kind(d) != K || (K == 3 && fuse == 1 && fused420(d))) return;
+    if (d.status != kOk || stream_kind(d) != K || (K == 3 && (fuse == 1 || fuse == 3) && fused420(d))) return;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     uint8_t* o = out + (int64_t)img * out_stride;
     const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_convert_stream(const Desc* __restrict__
                                                         int fuse) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk || stream_kind(d) != K || (K == 3 && fuse == 1 && fused420(d))) return;
+    if (d.status != kOk || stream_kind(d) != K || (K == 3 && (fuse == 1 || fuse == 3) && fused420(d))) return;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     uint8_t* o = out + (int64_t)img * out_stride;
     const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
@@ -1467,6 +1467,220 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
     }
 }
 
+// ------------------------------------------------- 4:2:0 back half in one kernel (mode 3)
+// Dequant + IDCT + H/V chroma doubling + YCbCr->RGB of fused420 images without any plane in
+// HBM: the coefficient blocks are read once and the RGB written once (the plane round trip was
+// half of the back half's bytes). A workgroup owns a strip of kBW MCUs (256 output columns) by
+// `seg` MCU rows and walks down it one MCU row per step; the planes of the rows in flight live in
+// LDS rings:
+//   phase A  IDCT of luma MCU row t+1 and chroma MCU row t+2 (+ the chroma blocks of the MCUs
+//            left and right of the strip: the horizontal taps read 2 samples past each side),
+//            the lane-pair IDCT of k_idct420y/c into the luma / raw chroma rings; then the
+//            horizontal doubling (jpeg_dec.h:736-760, the stride-end quirk included) of chroma
+//            row t+1 into the doubled ring
+//   barrier
+//   phase B  vertical doubling (:762-791) from the doubled rows t-1..t+1 and the conversion
+//            (:834-853) of output rows 16t .. 16t+15; 12-byte streaming stores.
+// Ring slots are chosen so that phase A of step t+1 never writes what phase B of step t reads
+// (one LDS-only barrier per step). The vertical taps read the rows two above and below, so a
+// segment also transforms the chroma of the MCU rows above and below it.
+#ifndef ICX_BACK_PP  // two register sets for the prefetched blocks (see the loop)
+#define ICX_BACK_PP 0
+#endif
+#ifndef ICX_BACK_MINW  // waves per SIMD k_back420 is compiled for
+#define ICX_BACK_MINW 4
+#endif
+constexpr int kBW = 16;     // strip width in MCUs: 64 lanes x 4 columns
+constexpr int kBRaw = 36;   // raw chroma row (dwords): 8 halo + 128 + 8 halo samples
+struct BackLds {
+    uint32_t y[3][16][64];         // luma rows of MCU rows t-1, t, t+1 (ring of 3)
+    uint32_t raw[2][2][8][kBRaw];  // raw Cb / Cr rows of 2 MCU rows, strip + halo columns
+    uint32_t dbl[4][2][8][64];     // horizontally doubled Cb / Cr rows of 4 MCU rows
+    uint32_t q[3][16];             // dequant tables (zig-zag, bytes) of Y, Cb, Cr
+};
+__global__ __launch_bounds__(256, ICX_BACK_MINW) void k_back420(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                                 const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                                 uint8_t* __restrict__ out, uint64_t out_stride, int seg) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (!fused420(d)) return;
+    __shared__ __attribute__((aligned(16))) BackLds L;
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, p = t >> 1, h = t & 1;
+    const int W = d.W, H = d.H, mbw = d.mbw, mbh = d.mbh;
+    const int cw = d.c[1].w, chh = d.c[1].h, cs = d.c[1].stride;  // Cb and Cr: same geometry (1x1)
+    if (t < 48) L.q[t >> 4][t & 15] = reinterpret_cast<const uint32_t*>(d.q[d.c[t >> 4].tq])[t & 15];
+    // pair p's block in an MCU: 0..63 luma block p & 3 of strip MCU p >> 2; 64..95 Cb / Cr of
+    // strip MCU p & 15; 96..99 Cb / Cr of the MCU left (96, 97) / right (98, 99) of the strip
+    const int kb = p < 64 ? (p & 3) : (p < 96 ? 4 + ((p - 64) >> 4) : 4 + (p & 1));
+    const int dmx = p < 64 ? (p >> 2) : (p < 96 ? (p & 15) : (p < 98 ? -1 : kBW));
+    int sbx = 0, sby = 0;
+    if (kb < 4) (void)mcu_block_comp(d, kb, sbx, sby);
+    const uint8_t* qz = reinterpret_cast<const uint8_t*>(L.q[kb < 4 ? 0 : kb - 3]);
+    uint8_t* o = out + (int64_t)img * out_stride;
+    const StreamOut so{o, W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (W & 3) == 0};
+    const int nsx = (mbw + kBW - 1) / kBW, nseg = (mbh + seg - 1) / seg, items = nsx * nseg;
+    for (int it = blockIdx.x; it < items; it += gridDim.x) {
+        const int sg = it / nsx, sx = it - sg * nsx;
+        const int mx0 = sx * kBW, r0 = sg * seg, r1 = min(mbh, r0 + seg);
+        const int lo = max(r0 - 1, 0), hi = min(r1, mbh - 1);  // chroma MCU rows the segment needs
+        const int M = 64 * sx + lane, x0 = 4 * M;             // the lane's output columns x0 .. x0+3
+#ifdef ICX_EXP_BACK_NOSTORE
+        uint32_t sink = 0;
+#endif
+        // step tr transforms luma MCU row tr+1 and chroma MCU row tr+2: whether the pair has a
+        // block then, and where it is (clamped into the image where it has none)
+        auto live_at = [&](int tr) {
+            const int row = kb < 4 ? tr + 1 : tr + 2, mx = mx0 + dmx;
+            return (kb < 4 ? row >= r0 && row < r1 : row >= lo && row <= hi) && p < 100 && mx >= 0 && mx < mbw;
+        };
+        auto pend_at = [&](int tr) {
+            const int row = kb < 4 ? tr + 1 : tr + 2;
+            const int mxc = min(max(mx0 + dmx, 0), mbw - 1), rowc = min(max(row, 0), mbh - 1);
+#ifdef ICX_EXP_BACK_NOMAP  // timing experiment only: blocks as if written in place (wrong pixels)
+            return BlkPend{make_uint2(0, 0), d.acbase + ((int64_t)rowc * mbw + mxc) * 6 + kb};
+#else
+            return blk_pend(d, map, ((int64_t)rowc * mbw + mxc) * 6 + kb);
+#endif
+        };
+        // One step. Software pipeline: D (this step's block) was loaded during the previous step,
+        // issued before that step's RGB stores, and its map entry one step before that; this step
+        // resolves Pn (the next step's entry), loads the next step's block into Dn and the entry
+        // after it into Pa. The loop below alternates two register sets, so no register with a
+        // load in flight is ever copied (a copy waits for it: s_waitcnt vmcnt(0)).
+        auto step = [&](int tr, const int4 (&D)[8], const BlkLoc& lD, int4 (&Dn)[8], BlkLoc& lDn, const BlkPend& Pn,
+                        BlkPend& Pa) {
+            // ---- phase A: transforms
+            const int ry = tr + 1, rc = tr + 2;
+            const bool live = live_at(tr);
+            if (__any(live)) {  // wave-uniform
+                uint32_t qw[16];
+                load_qw(qz, qw);
+                uint32_t rowd[8];
+                pair_idct(D, qw, h, dcv, lD, rowd);
+                if (live) {
+                    if (kb < 4) {
+                        uint32_t* dst = &L.y[ry % 3][sby * 8][dmx * 4 + sbx * 2 + h];
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) dst[r * 64] = rowd[r];
+                    } else {
+                        uint32_t* dst = &L.raw[rc & 1][kb - 4][0][(dmx + 1) * 2 + h];
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) dst[r * kBRaw] = rowd[r];
+                    }
+                }
+            }
+            lDn = blk_resolve(d, Pn);
+            load_block(ac, lDn.blk, h, Dn);  // (past the last step: a harmless reload)
+            Pa = pend_at(tr + 2);
+            const int rd = tr + 1;  // horizontal doubling of chroma MCU row rd (written last step)
+            if (rd >= lo && rd <= hi) {
+                const bool interior = M >= 1 && x0 + 3 <= 2 * cw - 4;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int task = wave * 4 + j, cc = task >> 3, r = task & 7;
+                    const uint32_t* rw = L.raw[rd & 1][cc][r];
+                    uint32_t v;
+                    if (interior) {  // samples 2M-2 .. 2M+3 at raw bytes 2 lane + 6 ..
+                        const int b0 = ((2 * lane + 6) >> 2);
+                        const uint64_t w = ((uint64_t)rw[b0] | ((uint64_t)rw[b0 + 1] << 32)) ^ 0x8080808080808080ull;
+                        const uint64_t b = w >> ((lane & 1) ? 0 : 16);
+                        const uint32_t w0 = (uint32_t)b, w1 = (uint32_t)(b >> 8), w2 = (uint32_t)(b >> 16);
+                        v = pack4(dtap(w0, kTapRev), dtap(w1, kTapFwd), dtap(w1, kTapRev), dtap(w2, kTapFwd));
+                    } else {  // image edges: the generic taps (the right edge reads from the stride end)
+                        const uint8_t* rb = reinterpret_cast<const uint8_t*>(rw);
+                        const int sh = 8 * mx0 - 8;  // chroma column of raw byte 0
+                        auto at = [&](int g) { return (int)rb[min(max(g - sh, 0), 4 * kBRaw - 1)]; };
+                        v = pmap([&](int i) {
+                            const int x = x0 + i;
+                            if (x >= 2 * cw) return 0;
+                            return (int)double_tap(x, cw, at, [&](int jj) { return at(cs - jj); });
+                        });
+                    }
+                    L.dbl[rd & 3][cc][r][lane] = v;
+                }
+            }
+            lds_barrier();
+            // ---- phase B: vertical doubling + conversion of output rows 16 tr + 4 wave .. + 3
+            const int y0 = 16 * tr + 4 * wave;
+            if (tr >= r0 && y0 < H) {  // wave-uniform
+                const int k0 = y0 >> 1;
+                const int nb = x0 < W ? min(4, W - x0) * 3 : 0;
+                uint32_t A[2][6];
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        const int r = min(max(k0 - 2 + i, 0), chh - 1);
+                        A[cc][i] = L.dbl[(r >> 3) & 3][cc][r & 7][lane];
+                    }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int k = k0 + u, y = 2 * k;
+                    if (y >= H) break;  // wave-uniform
+                    uint32_t ev[2], od[2];
+#pragma unroll
+                    for (int cc = 0; cc < 2; ++cc) {
+                        const uint32_t w0 = A[cc][u], w1 = A[cc][u + 1], w2 = A[cc][u + 2], w3 = A[cc][u + 3],
+                                       w4 = A[cc][u + 4];
+                        if (k >= 2 && k <= chh - 3) {
+                            uint32_t e[4], f[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                e[i] = dtap(kv_column(w0, w1, w2, w3, i) ^ kBias8, kTapRev);
+                                f[i] = dtap(kv_column(w1, w2, w3, w4, i) ^ kBias8, kTapFwd);
+                            }
+                            ev[cc] = pack4(e[0], e[1], e[2], e[3]);
+                            od[cc] = pack4(f[0], f[1], f[2], f[3]);
+                        } else {
+                            ev[cc] = vtap_even(k, chh, w0, w1, w2, w3);
+                            od[cc] = vtap_odd(k, chh, w1, w2, w3, w4);
+                        }
+                    }
+                    const uint32_t(*Y)[64] = L.y[tr % 3];
+                    uint32_t wv[3];
+                    ycc4_to_rgb(Y[y - 16 * tr][lane], ev[0], ev[1], wv);
+#ifdef ICX_EXP_BACK_NOSTORE  // timing experiment only: no RGB stores (one per item keeps the work)
+                    sink ^= wv[0] ^ wv[1] ^ wv[2];
+#else
+                    so.put3(y, x0, wv, nb);
+#endif
+                    if (y + 1 < H) {
+                        ycc4_to_rgb(Y[y + 1 - 16 * tr][lane], od[0], od[1], wv);
+#ifdef ICX_EXP_BACK_NOSTORE
+                        sink ^= wv[0] ^ wv[1] ^ wv[2];
+#else
+                        so.put3(y + 1, x0, wv, nb);
+#endif
+                    }
+                }
+            }
+        };
+        lds_barrier();  // (the previous item's phase B is done with the rings; the q tables are in)
+#if ICX_BACK_PP
+        int4 ca[8], cb[8];
+        BlkLoc la = blk_resolve(d, pend_at(lo - 2)), lb;
+        BlkPend pa, pb = pend_at(lo - 1);
+        load_block(ac, la.blk, h, ca);
+        for (int tr = lo - 2;;) {
+            step(tr, ca, la, cb, lb, pb, pa);
+            if (++tr >= r1) break;
+            step(tr, cb, lb, ca, la, pa, pb);
+            if (++tr >= r1) break;
+        }
+#else  // one register set (the next step's block overwrites this one's once it is transformed)
+        int4 ca[8];
+        BlkLoc la = blk_resolve(d, pend_at(lo - 2));
+        BlkPend pa = pend_at(lo - 1);
+        load_block(ac, la.blk, h, ca);
+        for (int tr = lo - 2; tr < r1; ++tr) step(tr, ca, la, ca, la, pa, pa);
+#endif
+#ifdef ICX_EXP_BACK_NOSTORE
+        if (sink == 0x12345678u) o[lane] = 1;
+#endif
+    }
+}
+
 // --------------------------------------------------------------------------- finalize
 __global__ void k_finalize(int n, const Desc* __restrict__ desc, int32_t* __restrict__ status,
                            int32_t* __restrict__ dims) {
@@ -1519,7 +1733,7 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     // (any value other than 0, 1, 2 is the default: an unknown mode would leave 4:2:0 luma untransformed)
     const int fuse = [] {  // (read per launch: tests switch modes within one process)
         const int v = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 2;
-        return (v >= 0 && v <= 2) ? v : 2;
+        return (v >= 0 && v <= 3) ? v : 2;
     }();
 #ifndef ICX_EXP_ONLY420  // timing experiment only: the 4:2:0 kernels alone (other samplings undecoded)
     hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes, ws.plane_cap,
@@ -1527,7 +1741,7 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                        ws.plane_cap);
 #endif
-    if (fuse) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
+    if (fuse == 1 || fuse == 2) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
         const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;
         hipLaunchKernelGGL(k_idct420c, dim3(std::max(cgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map,
                            ws.planes, ws.plane_cap);
@@ -1556,6 +1770,14 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     const int fgx = (int)std::max<int64_t>(1, std::min<int64_t>((((int64_t)(ws.max_w + 255) / 256) *
                                                                   ((ws.max_h + 16 * kFB - 1) / (16 * kFB)) + 3) / 4,
                                                                  16384 / n));
+    if (fuse == 3) {  // 4:2:0: the whole back half in k_back420, no planes
+        const int seg = std::getenv("ICX_BSEG")  // (read per launch: tests vary it)
+             ? std::max(1, std::atoi(std::getenv("ICX_BSEG"))) : 32;
+        const int64_t items = (int64_t)((ws.max_w + 16 * kBW - 1) / (16 * kBW)) * (((ws.max_h + 15) / 16 + seg - 1) / seg);
+        const int bgx = (int)std::max<int64_t>(1, std::min<int64_t>(items, 16384 / n));
+        hipLaunchKernelGGL(k_back420, dim3(bgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, d_out, out_stride,
+                           seg);
+    }
     if (fuse == 1)
         hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap, d_out, out_stride);

@@ -158,8 +158,33 @@ __device__ __forceinline__ BlkLoc blk_loc(const Desc& d, const uint2* map, int64
     return BlkLoc{(int64_t)e.x, (int32_t)e.y};
 }
 // A block's absolute quantized DC: its cell (or the int32 escape) plus the location's offset.
+// (The escape load sits in a wave-uniform branch that valid streams never take: as a per-lane
+// select its s_waitcnt vmcnt(0) landed after the join, in every block's path, where it waited
+// for every load and store the wave had in flight.)
 __device__ __forceinline__ int32_t blk_dc(int16_t cell, const int32_t* dcv, const BlkLoc& l) {
-    return wadd(cell == kDcEscape ? dcv[l.blk] : (int32_t)cell, l.dcoff);
+    int32_t v = cell;
+    if (__any(cell == kDcEscape)) {
+        const int32_t e = dcv[l.blk];
+        v = cell == kDcEscape ? e : v;
+    }
+    return wadd(v, l.dcoff);
+}
+// A block location whose map entry is still in flight: the entry is loaded unconditionally (for an
+// image written in place the slot is in bounds and ignored) and resolved where the location is
+// used, so the load's wait lands there and not right after the load (blk_loc's branch did that).
+struct BlkPend {
+    uint2 e;
+    int64_t n;  // acbase + block index
+};
+__device__ __forceinline__ BlkPend blk_pend(const Desc& d, const uint2* map, int64_t n) {
+    return BlkPend{map[d.acbase + n], d.acbase + n};
+}
+__device__ __forceinline__ BlkLoc blk_resolve(const Desc& d, const BlkPend& q) {
+#ifdef ICX_EXP_BACK_NOMAP
+    return BlkLoc{q.n, 0};
+#else
+    return d.mapped ? BlkLoc{(int64_t)q.e.x, (int32_t)q.e.y} : BlkLoc{q.n, 0};
+#endif
 }
 
 
