@@ -1257,53 +1257,42 @@ __device__ __forceinline__ void load_block(const int16_t* ac, int64_t blk, int h
     c[7] = c[3];
 }
 
-// A wave's units wid, wid + nw, ... (wave-uniform loop): unit u's coefficient block is at loc(u)
-// (blk_loc: its pool block and DC offset), transformed and stored by unit(u, c, loc).
-// ICX_IDCT_PF: the next unit's block is loaded while the current one is transformed (two
-// register sets, the loop unrolled by two so neither is copied).
-#ifndef ICX_IDCT_PF  // measured: no gain (4:2:0 luma 6.12 -> 6.26 ms; 125 VGPRs, 4 waves/SIMD)
-#define ICX_IDCT_PF 0
-#endif
-template <class LocF, class UnitF>
-__device__ __forceinline__ void idct_units(const int16_t* ac, int h, uint32_t wid, uint32_t nw, uint32_t nunits, LocF locf,
-                                           UnitF unit) {
-#if ICX_IDCT_PF
+// A wave's units wid, wid + nw, ... (wave-uniform loop): unit u's coefficient block is at
+// pendf(u) (blk_pend: its pool block and DC offset once resolved), transformed and stored by
+// unit(u, c, loc). Software-pipelined: unit u's block is loaded during unit u - nw and its map
+// entry during the unit before that, and the loop alternates two register sets, so a wave waits
+// only for loads issued one unit earlier -- never for its own stores (unit() must issue the same
+// stores on every path, so the compiler can count them) and never for a register copy of a load
+// in flight. (Before, the next unit's map entry was waited for right after it was issued,
+// together with the unit's own block loads: one full memory latency per unit.)
+template <class PendF, class UnitF>
+__device__ __forceinline__ void idct_units(const int16_t* ac, const Desc& d, int h, uint32_t wid, uint32_t nw,
+                                           uint32_t nunits, PendF pendf, UnitF unit) {
     if (wid >= nunits) return;
-    const uint32_t ulast = nunits - 1;
-    int4 c0[8], c1[8];
-    BlkLoc l0 = locf(wid), l1;
-    load_block(ac, l0.blk, h, c0);
+    auto at = [&](uint32_t u) { return pendf(min(u, nunits - 1)); };  // (past the end: harmless reloads)
+    int4 ca[8], cb[8];
+    BlkLoc la = blk_resolve(d, at(wid)), lb;
+    load_block(ac, la.blk, h, ca);
+    BlkPend pa, pb = at(wid + nw);
+    auto step = [&](uint32_t u, const int4 (&D)[8], const BlkLoc& lD, int4 (&Dn)[8], BlkLoc& lDn, const BlkPend& Pn,
+                    BlkPend& Pa) {
+        lDn = blk_resolve(d, Pn);
+        load_block(ac, lDn.blk, h, Dn);
+        Pa = at(u + 2 * nw);
+        unit(u, D, lD);
+    };
     for (uint32_t u = wid;;) {
-        l1 = locf(min(u + nw, ulast));
-        load_block(ac, l1.blk, h, c1);  // (past the end: a harmless reload)
-        unit(u, c0, l0);
-        u += nw;
-        if (u >= nunits) break;
-        l0 = locf(min(u + nw, ulast));
-        load_block(ac, l0.blk, h, c0);
-        unit(u, c1, l1);
-        u += nw;
-        if (u >= nunits) break;
+        step(u, ca, la, cb, lb, pb, pa);
+        if ((u += nw) >= nunits) break;
+        step(u, cb, lb, ca, la, pa, pb);
+        if ((u += nw) >= nunits) break;
     }
-#else
-    // the next unit's location (a map load for guess-write images) is fetched while this unit is
-    // transformed, so its block loads do not wait for it
-    if (wid >= nunits) return;
-    BlkLoc l = locf(wid);
-    for (uint32_t u = wid; u < nunits; u += nw) {
-        int4 c[8];
-        load_block(ac, l.blk, h, c);
-        const BlkLoc ln = locf(min(u + nw, nunits - 1));
-        unit(u, c, l);
-        l = ln;
-    }
-#endif
 }
 
 // Waves per SIMD the 4:2:0 IDCT kernels are compiled for (timing experiments: 5 keeps them at 96
 // VGPRs, so a wave fits beside four k_gw_lane waves on a SIMD).
 #ifndef ICX_IDCT_Y_MINW
-#define ICX_IDCT_Y_MINW 1
+#define ICX_IDCT_Y_MINW 4
 #endif
 #ifndef ICX_IDCT_C_MINW
 #define ICX_IDCT_C_MINW 1
@@ -1330,23 +1319,23 @@ __global__ __launch_bounds__(256, ICX_IDCT_C_MINW) void k_idct420c(const Desc* _
     const uint32_t ucols = (uint32_t)((mbw + 15) >> 4), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
-    auto locf = [&](uint32_t u) {
+    // a lane pair past the row's last MCU transforms that MCU's block again and stores the same
+    // bytes at its place (the pair that owns it is in the same unit): every lane stores
+    auto pendf = [&](uint32_t u) {
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 4) + mq;
-        return blk_loc(d, map, ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + 4 + cc);
+        return blk_pend(d, map, ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + 4 + cc);
     };
     auto unit = [&](uint32_t u, const int4 (&c)[8], const BlkLoc& l) {
         const uint32_t mby = u / ucols;
-        const int mx = (int)((u - mby * ucols) << 4) + mq;
+        const int mx = min((int)((u - mby * ucols) << 4) + mq, mbw - 1);
         uint32_t rowd[8];
         pair_idct(c, qw, h, dcv, l, rowd);
-        if (mx < mbw) {
-            uint8_t* dst = Pc + (int64_t)mby * 8 * stride + mx * 8 + 4 * h;
+        uint8_t* dst = Pc + (int64_t)mby * 8 * stride + mx * 8 + 4 * h;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
-        }
+        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
     };
-    idct_units(ac, h, wid, nw, nunits, locf, unit);
+    idct_units(ac, d, h, wid, nw, nunits, pendf, unit);
 }
 
 // Luma planes of fused420 images when the conversion reads them from HBM (ICX_FUSE420 = 2): a
@@ -1370,23 +1359,21 @@ __global__ __launch_bounds__(256, ICX_IDCT_Y_MINW) void k_idct420y(const Desc* _
     const uint32_t ucols = (uint32_t)((mbw + 7) >> 3), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
-    auto locf = [&](uint32_t u) {
+    auto pendf = [&](uint32_t u) {  // (past the row's last MCU: that MCU again, as in k_idct420c)
         const uint32_t mby = u / ucols;
         const int mx = (int)((u - mby * ucols) << 3) + mq;
-        return blk_loc(d, map, ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + k);
+        return blk_pend(d, map, ((int64_t)mby * mbw + min(mx, mbw - 1)) * 6 + k);
     };
     auto unit = [&](uint32_t u, const int4 (&c)[8], const BlkLoc& l) {
         const uint32_t mby = u / ucols;
-        const int mx = (int)((u - mby * ucols) << 3) + mq;
+        const int mx = min((int)((u - mby * ucols) << 3) + mq, mbw - 1);
         uint32_t rowd[8];
         pair_idct(c, qw, h, dcv, l, rowd);
-        if (mx < mbw) {
-            uint8_t* dst = Py + ((int64_t)mby * 16 + sby * 8) * stride + mx * 16 + sbx * 8 + 4 * h;
+        uint8_t* dst = Py + ((int64_t)mby * 16 + sby * 8) * stride + mx * 16 + sbx * 8 + 4 * h;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
-        }
+        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
     };
-    idct_units(ac, h, wid, nw, nunits, locf, unit);
+    idct_units(ac, d, h, wid, nw, nunits, pendf, unit);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
