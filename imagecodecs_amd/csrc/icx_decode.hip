@@ -51,16 +51,81 @@ __global__ __launch_bounds__(64) void k_parse(int n, const uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------------- entropy (sequential)
-// One lane walks one image's entropy-coded segment exactly like njDecodeScan. It takes
-// every image the parallel path (icx_spec.hip) does not finish: restart-interval streams,
-// exotic sampling, oversized scans, and chains that failed verification.
-__global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
-                              Desc* __restrict__ desc, int16_t* __restrict__ ac, int32_t* __restrict__ dcv) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per image that neither parallel path takes (a stream whose restart markers NanoJPEG
+// reads where no lane starts, more than kSpecMaxBpm blocks per MCU -- beyond the JPEG limit of 10,
+// so non-conforming --, an exhausted workspace, a repair walk that never resynchronises). Lane 0
+// walks the entropy-coded segment exactly like njDecodeScan (jpeg_dec.h:643-718). The wave keeps
+// the image's four Huffman tables in LDS and the stream's next bytes in an LDS ring, refilled a KiB
+// at a time by all 64 lanes with 16-byte loads, so the serial walk runs at LDS latency instead of
+// a dependent global load per byte and per table lookup.
+constexpr int kSeqRing = 4096;  // 4 quarters of 1 KiB; lane 0 always has >= 2 KiB loaded ahead
+struct RingBits {                // rb_fill's byte rules (icx_jpeg.h) over the ring
+    const uint8_t* ring;
+    int64_t pos, end;            // next byte, stream end (relative to the aligned ring origin)
+    uint32_t acc;
+    int32_t nacc, err;
+    __device__ uint32_t byte() { return ring[(pos++) & (kSeqRing - 1)]; }
+    __device__ void fill(int want) {
+        while (nacc < want) {
+            if (pos >= end) { acc = (acc << 8) | 0xFFu; nacc += 8; continue; }
+            const uint32_t x = byte();
+            acc = (acc << 8) | x;
+            nacc += 8;
+            if (x != 0xFF) continue;
+            if (pos >= end) { err = kSyntaxError; continue; }
+            const uint32_t m = byte();
+            if (m == 0x00 || m == 0xFF) continue;
+            if (m == 0xD9) { end = pos; continue; }
+            if ((m & 0xF8) == 0xD0) { acc = (acc << 8) | m; nacc += 8; }
+            else err = kSyntaxError;
+        }
+    }
+    __device__ uint32_t peek(int n) {
+        if (!n) return 0;
+        fill(n);
+        return (acc >> (nacc - n)) & ((1u << n) - 1u);
+    }
+    __device__ void drop(int n) {
+        if (nacc < n) fill(n);
+        nacc -= n;
+    }
+};
+__global__ __launch_bounds__(64) void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                    Desc* __restrict__ desc, int16_t* __restrict__ ac, int32_t* __restrict__ dcv) {
+    const int i = blockIdx.x;
     if (i >= n) return;
     Desc& d = desc[i];
-    if (d.status != kPending) return;
-    RawBits b{data + off[i] + d.scan_off, d.size - d.scan_off, 0u, 0, 0};
+    if (d.status != kPending) return;  // (uniform)
+    __shared__ Huff HT[4];
+    __shared__ uint4 ring4[kSeqRing / 16];
+    const int lane = threadIdx.x;
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(d.huff);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(HT);
+        for (int k = lane; k < (int)(sizeof(HT) / 4); k += 64) dst[k] = src[k];
+    }
+    // the ring holds the stream from a 16-byte aligned origin: quarter q of the ring = stream KiB qi
+    // with qi % 4 == q; quarters qlo .. qlo+3 are loaded
+    const uint8_t* S = data + off[i] + d.scan_off;
+    const int mis = (int)(reinterpret_cast<uintptr_t>(S) & 15);
+    const uint8_t* S0 = S - mis;
+    const int64_t end = (int64_t)(d.size - d.scan_off) + mis;
+    auto fill_quarter = [&](int64_t qi) {  // all lanes (bytes past the end read as FF, never used)
+        const int64_t at = qi * 1024 + lane * 16;
+        uint4 v = make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (at + 16 <= end) {
+            v = *reinterpret_cast<const uint4*>(S0 + at);
+        } else if (at < end) {
+            uint8_t tb[16];
+            for (int k = 0; k < 16; ++k) tb[k] = at + k < end ? S0[at + k] : 0xFF;
+            __builtin_memcpy(&v, tb, 16);
+        }
+        ring4[(qi & 3) * 64 + lane] = v;
+    };
+    int64_t qlo = 0;
+    for (int q = 0; q < 4; ++q) fill_quarter(q);
+    __syncthreads();
+    RingBits b{reinterpret_cast<const uint8_t*>(ring4), mis, end, 0u, 0, 0};
     int16_t* A = ac + d.acbase * 64;  // (in place: the pool region k_spec_plan gave the image)
     int32_t* D = dcv + d.acbase;
     int32_t pred[3] = {0, 0, 0};
@@ -70,51 +135,70 @@ __global__ void k_entropy_seq(int n, const uint8_t* __restrict__ data, const uin
     int err = 0;
     for (int64_t m = 0; m < (nmcu > 0 ? nmcu : 1) && !err; ++m) {
         for (int r = 0; r < d.bpm && !err; ++r, ++blk) {
-            int sbx, sby;
-            const int ci = mcu_block_comp(d, r, sbx, sby);
-            const Comp& c = d.c[ci];
-            int16_t* row = A + blk * 64;
-            __builtin_memset(row, 0, 64 * sizeof(int16_t));
-            // DC (jpeg_dec.h:662-663)
-            int sym = 0;
-            int len = huff_lookup(d.huff[c.dc_tab], rb_peek(b, 16), sym);
-            if (!len) { err = kSyntaxError; break; }
-            rb_drop(b, len);
-            int nb = sym & 15;
-            int32_t v = 0;
-            if (nb) { v = extend((int32_t)rb_peek(b, nb), nb); rb_drop(b, nb); }
-            pred[ci] = wadd(pred[ci], v);
-            row[0] = dc_cell(pred[ci]);
-            if (row[0] == kDcEscape) D[blk] = pred[ci];
-            // AC (jpeg_dec.h:664-671)
-            int k = 0;
-            do {
-                len = huff_lookup(d.huff[c.ac_tab], rb_peek(b, 16), sym);
-                if (!len) { err = kSyntaxError; break; }
-                rb_drop(b, len);
-                if (!sym) break;  // EOB
-                if (!(sym & 0x0F) && sym != 0xF0) { err = kSyntaxError; break; }
-                nb = sym & 15;
-                v = 0;
-                if (nb) { v = extend((int32_t)rb_peek(b, nb), nb); rb_drop(b, nb); }
-                k += (sym >> 4) + 1;
-                if (k > 63) { err = kSyntaxError; break; }
-                row[k] = (int16_t)v;  // blocks are kept in zig-zag order (k_idct reorders)
-            } while (k < 63);
-            if (b.err) err = b.err;
+            // wave-uniform: keep >= 2 KiB loaded past lane 0's position (a block reads < 600 bytes)
+            const int64_t pos = __builtin_amdgcn_readfirstlane((int)b.pos) |
+                                ((int64_t)__builtin_amdgcn_readfirstlane((int)(b.pos >> 32)) << 32);
+            while (pos >= (qlo + 2) * 1024) {
+                fill_quarter(qlo + 4);
+                ++qlo;
+            }
+            __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses stay in order)
+            if (lane == 0) {
+                int sbx, sby;
+                const int ci = mcu_block_comp(d, r, sbx, sby);
+                const Comp& c = d.c[ci];
+                int16_t* row = A + blk * 64;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) reinterpret_cast<int4*>(row)[q] = make_int4(0, 0, 0, 0);
+                // DC (jpeg_dec.h:662-663)
+                int sym = 0;
+                int len = huff_lookup(HT[c.dc_tab], b.peek(16), sym);
+                if (!len) {
+                    err = kSyntaxError;
+                } else {
+                    b.drop(len);
+                    int nb = sym & 15;
+                    int32_t v = 0;
+                    if (nb) { v = extend((int32_t)b.peek(nb), nb); b.drop(nb); }
+                    pred[ci] = wadd(pred[ci], v);
+                    row[0] = dc_cell(pred[ci]);
+                    if (row[0] == kDcEscape) D[blk] = pred[ci];
+                    // AC (jpeg_dec.h:664-671)
+                    int k = 0;
+                    do {
+                        len = huff_lookup(HT[c.ac_tab], b.peek(16), sym);
+                        if (!len) { err = kSyntaxError; break; }
+                        b.drop(len);
+                        if (!sym) break;  // EOB
+                        if (!(sym & 0x0F) && sym != 0xF0) { err = kSyntaxError; break; }
+                        nb = sym & 15;
+                        v = 0;
+                        if (nb) { v = extend((int32_t)b.peek(nb), nb); b.drop(nb); }
+                        k += (sym >> 4) + 1;
+                        if (k > 63) { err = kSyntaxError; break; }
+                        row[k] = (int16_t)v;  // blocks are kept in zig-zag order (k_idct reorders)
+                    } while (k < 63);
+                    if (b.err) err = b.err;
+                }
+            }
+            err = __builtin_amdgcn_readfirstlane(err);
         }
         if (err) break;
-        if (d.restart && m + 1 < nmcu && !(--left)) {  // jpeg_dec.h:707-715
-            b.nacc &= 0xF8;
-            const int mk = (int)rb_peek(b, 16);
-            rb_drop(b, 16);
-            if ((mk & 0xFFF8) != 0xFFD0 || (mk & 7) != expect) { err = kSyntaxError; break; }
+        if (d.restart && m + 1 < nmcu && !(--left)) {  // jpeg_dec.h:707-715 (uniform control)
+            if (lane == 0) {
+                b.nacc &= 0xF8;
+                const int mk = (int)b.peek(16);
+                b.drop(16);
+                if ((mk & 0xFFF8) != 0xFFD0 || (mk & 7) != expect) err = kSyntaxError;
+            }
+            err = __builtin_amdgcn_readfirstlane(err);
+            if (err) break;
             expect = (expect + 1) & 7;
             left = d.restart;
             pred[0] = pred[1] = pred[2] = 0;
         }
     }
-    d.status = err ? kSyntaxError : kOk;
+    if (lane == 0) d.status = err ? kSyntaxError : kOk;
 }
 
 // ----------------------------------------------------------------------- plane layout
@@ -1687,14 +1771,13 @@ void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const 
     if (n <= 0) return;
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
-    const int tb = 64, nb = (n + tb - 1) / tb;
     B(kStParse);
     hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
                        out_stride);
     E(kStParse);
     launch_spec_entropy(ws, n, d_data, d_off, st, hook);
     B(kStEntropy);
-    hipLaunchKernelGGL(k_entropy_seq, dim3(nb), dim3(tb), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc);
+    hipLaunchKernelGGL(k_entropy_seq, dim3(n), dim3(64), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc);
     E(kStEntropy);
 }
 

@@ -29,7 +29,8 @@ enum : int32_t { kSpecSyntax = 1, kSpecGiveUp = 2 };
 
 struct SpecImg {
     int32_t mode;          // 0 not on this path, 1 active, 2 fall back to the sequential kernel,
-                           // 3 restart intervals (DRI): one write lane per interval
+                           // 3 restart intervals (DRI): one write lane per interval, 4 deferred to the
+                           // next round (the pools were full), 5 finished in an earlier round
     int32_t err;           // kSpecSyntax | kSpecGiveUp (atomicOr)
     int32_t ntiles, tile_base;
     int32_t nwg, wg_base;  // 256-lane decode groups; the image's first lane record / 256 (subsequence
@@ -214,6 +215,8 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
                         int32_t* d_dims, hipStream_t st, StageHook* hook);
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
                          StageHook* hook);
+void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
+                       StageHook* hook, int round, int last);
 
 // Per-image result record (icx_records.hip; include/icx.h icx_record): status, dims and the
 // 64-bit weighted word sum of the decoded bytes.

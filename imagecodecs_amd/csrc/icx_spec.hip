@@ -51,7 +51,8 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     int32_t* __restrict__ tilepre, int32_t* __restrict__ wgpre,
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
                                                     int64_t upool, int64_t lanes_cap, int sub_bytes, int64_t pool_cap,
-                                                    unsigned long long* __restrict__ pool_next, int gw) {
+                                                    unsigned long long* __restrict__ pool_next, int gw, int round,
+                                                    int last_round) {
     __shared__ int sh[1024];
     __shared__ int last[7];
     int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0, carry_a = 0;
@@ -60,8 +61,13 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         const int i = i0 + threadIdx.x;
         // Candidates, with the work they would take: U pool units (whole 4 KiB, + the reader
         // padding: u_pad_end(ulen) <= ulen + 32, ulen <= scan_len), tiles and lanes.
+        // Rounds (launch_spec_entropy): round 0 plans every image; a candidate that does not fit
+        // the U pool / lane records is deferred (mode 4) and planned again in the next round, over
+        // the pools the earlier round's images no longer need; in the last round it goes to the
+        // sequential kernel. Images planned in an earlier round are left alone (mode 5).
         const int64_t scan_len = i < n ? desc[i].size - desc[i].scan_off : 0;
-        const bool cand = i < n && desc[i].status == kPending && desc[i].nc >= 1 && desc[i].bpm <= kSpecMaxBpm &&
+        const bool mine = i < n && (round == 0 || spec[i].mode == 4);
+        const bool cand = mine && desc[i].status == kPending && desc[i].nc >= 1 && desc[i].bpm <= kSpecMaxBpm &&
                           scan_len > 0 && scan_len < ((int64_t)1 << 40);
         int nt = 0, nw = 0, nw2 = 0, nu = 0;
         int64_t sb = kSubBytes, nsub = 0;
@@ -102,17 +108,19 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         // Coefficient pool region, whole kGwChunk units: a guess-write image gets nsub lanes x
         // gw_S static slots (1.1 x its blocks, so a sequential fallback fits too), every other
         // decodable image its blocks (written in place: k_entropy_seq, the DRI lanes).
+        // (round 0 reserves every image's region, a deferred candidate's as for the guess-write
+        // path, so the image keeps it in a later round)
         const int64_t tb = i < n && desc[i].status == kPending ? (int64_t)desc[i].mbw * desc[i].mbh * desc[i].bpm : 0;
-        const bool gwi = gw && ok && desc[i].restart == 0;
-        const int32_t gS = gwi ? (int32_t)((tb * 11 / 10 + nsub - 1) / nsub + 1) : 0;
-        const int64_t region = gwi ? nsub * gS : tb;
-        const int na = (int)min<int64_t>((region + kGwChunk - 1) / kGwChunk, INT32_MAX / 4);
+        const bool gwr = gw && cand && desc[i].restart == 0, gwi = gwr && ok;
+        const int32_t gS = gwr ? (int32_t)((tb * 11 / 10 + nsub - 1) / nsub + 1) : 0;
+        const int64_t region = gwr ? nsub * gS : tb;
+        const int na = round ? 0 : (int)min<int64_t>((region + kGwChunk - 1) / kGwChunk, INT32_MAX / 4);
         const int ea = block_exclusive_scan(na, sh);
         if (threadIdx.x == blockDim.x - 1) last[6] = ea + na;
-        if (i < n) {
+        if (mine) {
             const Desc& d = desc[i];
             SpecImg& s = spec[i];
-            s.mode = ok ? (d.restart == 0 ? 1 : 3) : 0;
+            s.mode = ok ? (d.restart == 0 ? 1 : 3) : (cand && !last_round ? 4 : 0);
             s.err = 0;
             s.nrepair = 0;
             s.ncount = 0;
@@ -128,10 +136,10 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             s.nwg = nw;
             s.gw_S = gS;
             Desc& dd = desc[i];
-            dd.acbase = ((int64_t)carry_a + ea) * kGwChunk;
+            if (round == 0) dd.acbase = ((int64_t)carry_a + ea) * kGwChunk;
             dd.mapped = gwi;
             // (cannot happen with the workspace's pool of 1.25 x coef_cap per slot: reported, not written)
-            if (dd.acbase + region > pool_cap && dd.status == kPending) {
+            if (round == 0 && dd.acbase + region > pool_cap && dd.status == kPending) {
                 dd.status = kOutOfMem;
                 s.mode = 0;
                 dd.mapped = 0;
@@ -165,7 +173,9 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         totals[0] = carry_t;
         totals[1] = carry_w;
         totals[2] = carry_w2;
-        *pool_next = (unsigned long long)carry_a * kGwChunk;  // overflow chunks and count blocks from here
+        // overflow chunks and count blocks from here (a later round goes on from where it is: the
+        // earlier rounds' chunks hold their images' blocks)
+        if (round == 0) *pool_next = (unsigned long long)carry_a * kGwChunk;
     }
 }
 
@@ -1432,6 +1442,7 @@ __global__ void k_spec_finish(int n, Desc* __restrict__ desc, SpecImg* __restric
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SpecImg& s = spec[i];
+    if (s.mode == 4 || s.mode == 5) return;  // deferred to the next round / finished in an earlier one
     if (s.mode == 3 && s.dri_first != INT32_MAX)  // the first interval not ending at its marker
         s.err |= (s.dri_first & 1) ? kSpecGiveUp : kSpecSyntax;
     if (s.mode == 3 && (s.err & kSpecGiveUp)) s.mode = 2;  // NanoJPEG resumes where no lane started
@@ -1442,10 +1453,24 @@ __global__ void k_spec_finish(int n, Desc* __restrict__ desc, SpecImg* __restric
     if (s.mode == 1 || s.mode == 3) atomicAdd(&stats[0], 1);
     else if (s.mode == 2) atomicAdd(&stats[1], 1);
     else if (desc[i].status == kPending) atomicAdd(&stats[2], 1);
+    s.mode = 5;
 }
 
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
                          StageHook* hook) {
+    // Rounds over the group (k_spec_plan): an image that does not fit the U pool / lane records
+    // left by the images before it is deferred to the next round instead of the sequential
+    // kernel (a batch of 4:4:4 q100 photos at 1.3 B/px overflows a pool sized for 1 B/px). A round
+    // with no deferred image costs only its launches (every kernel finds no work).
+    const int rounds = [] {  // (read per launch: tests vary it)
+        const char* e = std::getenv("ICX_ROUNDS");
+        return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
+    }();
+    for (int r = 0; r < rounds; ++r) launch_spec_round(ws, n, d_data, d_off, st, hook, r, r + 1 == rounds);
+}
+
+void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
+                       StageHook* hook, int round, int last) {
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     static const int g = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
@@ -1465,7 +1490,7 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     const int gw = gw_env ? (std::atoi(gw_env) != 0) : ((int64_t)ws.max_w * ws.max_h > kGwMinPixels ? 1 : 0);
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
-                       ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw);
+                       ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw, round, last);
     hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);

@@ -13,7 +13,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
-SAMPLING = {"gray": 0, "444": 0x11, "422": 0x21, "420": 0x22, "440": 0x12, "411": 0x41}
+SAMPLING = {"gray": 0, "444": 0x11, "422": 0x21, "420": 0x22, "440": 0x12, "411": 0x41,
+            "y44": 0x44}  # y44: Y 4x4 + Cb + Cr = 18 blocks per MCU (beyond the JPEG limit of 10; NanoJPEG decodes it)
 
 
 def lib():
