@@ -283,7 +283,8 @@ def _oracle_png(args):
 
 def main_png(args, wl, world, rank, local):
     """C5: device-resident PNG encode (png_encoder::saveToFile) of a per-rank batch of RGBA images,
-    one icx_png_encode_device call per image, pixels resident in HBM, files written to HBM."""
+    one icx_png_encode_device_batch call per step (--png-single: one icx_png_encode_device call per
+    image), pixels resident in HBM, files written to HBM."""
     import zlib
     from imagecodecs_amd import shard
     from tests import pngutil
@@ -325,12 +326,19 @@ def main_png(args, wl, world, rank, local):
     enc = icx.PngEncoder(ctx)
     stream = torch.cuda.current_stream(dev)
 
+    srcs = [d_src[i % npool].data_ptr() for i in range(n)]
+
     def step():
-        for i in range(n):
-            rc, sizes[i] = enc.encode_device(W, H, 4, d_src[i % npool].data_ptr(), d_out[i].data_ptr(), cap,
-                                             stream.cuda_stream)
-            if rc != icx.OK:
-                d_st[i] = rc
+        if args.png_single:  # one icx_png_encode_device call per image (round 2's loop)
+            for i in range(n):
+                rc, sizes[i] = enc.encode_device(W, H, 4, srcs[i], d_out[i].data_ptr(), cap, stream.cuda_stream)
+                if rc != icx.OK:
+                    d_st[i] = rc
+        else:  # icx_png_encode_device_batch: two images in flight
+            st, sz = enc.encode_device_batch(W, H, 4, srcs, d_out.data_ptr(), cap, stream.cuda_stream)
+            sizes[:] = sz
+            if (st != icx.OK).any():
+                d_st.copy_(torch.from_numpy(st.astype(np.int32)))
         if world > 1:
             return shard.gather_results(d_st, dist)
         return d_st
@@ -553,6 +561,7 @@ def main():
                     help="CPU-baseline workers (default: the 16-core share of a GPU box)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive sub-batch (decode workloads)")
+    ap.add_argument("--png-single", action="store_true", help="C5: one encode call per image (no batch entry)")
     args = ap.parse_args()
 
     # --gpus N: one rank per GPU. Without a launcher (WORLD_SIZE unset) the bench starts

@@ -87,6 +87,7 @@ _SIGS = {
     "icx_png_encoder_create": (_vp, [_vp]),
     "icx_png_encoder_destroy": (None, [_vp]),
     "icx_png_encode_device": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
+    "icx_png_encode_device_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _u64, _vp, _vp, _vp]),
     "icx_png_encoder_stage_times": (_i32, [_vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), _i32]),
     "icx_jpeg_encode_device": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _u64, C.POINTER(_u64), _vp]),
     "icx_jpeg_encode_device_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _u64, _vp, _vp, _vp]),
@@ -324,6 +325,19 @@ class PngEncoder:
         if rc not in (OK, OUT_OF_MEM):
             raise ICXError(f"icx_png_encode_device -> {rc}: {_err(self.ctx.ptr)}")
         return rc, int(n.value)
+
+    def encode_device_batch(self, width, height, d, d_srcs, d_out, out_stride, stream=0):
+        """n device images (list of device addresses) -> files at d_out + i*out_stride; returns
+        (statuses, sizes) as numpy arrays (icx_png_encode_device_batch)."""
+        n = len(d_srcs)
+        srcs = (C.c_void_p * max(1, n))(*d_srcs)
+        sizes = np.zeros(max(1, n), np.uint64)
+        status = np.zeros(max(1, n), np.int32)
+        rc = lib().icx_png_encode_device_batch(self._p, n, width, height, d, srcs, d_out, out_stride,
+                                               sizes.ctypes.data, status.ctypes.data, stream or None)
+        if rc != OK:
+            raise ICXError(f"icx_png_encode_device_batch -> {rc}: {_err(self.ctx.ptr)}")
+        return status[:n], sizes[:n].astype(np.int64)
 
     def stage_times(self) -> dict:
         """Summed per-stage ms since the previous call (icx_png_encoder_stage_times)."""

@@ -705,6 +705,9 @@ int icx_png_save_to_file(icx_ctx* ctx, const char* path, const unsigned char* pi
 struct icx_png_encoder {
     icx_ctx* ctx = nullptr;
     PngWs* ws = nullptr;
+    PngWs* ws2 = nullptr;         // second workspace + stream of the batch entry (created on use)
+    hipStream_t st2 = nullptr;
+    hipEvent_t fork = nullptr;
 };
 
 icx_png_encoder* icx_png_encoder_create(icx_ctx* ctx) {
@@ -719,6 +722,9 @@ void icx_png_encoder_destroy(icx_png_encoder* enc) {
     if (!enc) return;
     (void)hipSetDevice(enc->ctx->device);
     png_ws_destroy(enc->ws);
+    if (enc->ws2) png_ws_destroy(enc->ws2);
+    if (enc->st2) (void)hipStreamDestroy(enc->st2);
+    if (enc->fork) (void)hipEventDestroy(enc->fork);
     delete enc;
 }
 
@@ -735,9 +741,43 @@ int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, co
     return rc == 0 ? ICX_OK : ICX_OUT_OF_MEM;
 }
 
+int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int height, int d, const uint8_t* const* d_srcs,
+                                uint8_t* d_out, uint64_t out_stride, uint64_t* out_sizes, int32_t* status,
+                                void* hip_stream) {
+    if (!enc || n < 0 || (n > 0 && (!d_srcs || !out_sizes || !status))) return ICX_UNSUPPORTED;
+    icx_ctx* ctx = enc->ctx;
+    if (const char* e = png_args_bad(width, height, d)) { ctx->err = e; return ICX_UNSUPPORTED; }
+    for (int i = 0; i < n; ++i)
+        if (!d_srcs[i]) { ctx->err = "null buffer"; return ICX_UNSUPPORTED; }
+    if (n > 0 && (!d_out || !out_stride)) { ctx->err = "null buffer"; return ICX_UNSUPPORTED; }
+    if (n == 0) return ICX_OK;
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
+    if (!enc->ws2) enc->ws2 = png_ws_create();
+    if (!enc->st2) ICX_HIP(ctx, hipStreamCreateWithFlags(&enc->st2, hipStreamNonBlocking), ICX_INTERNAL_ERR);
+    if (!enc->fork) ICX_HIP(ctx, hipEventCreateWithFlags(&enc->fork, hipEventDisableTiming), ICX_INTERNAL_ERR);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    // the second stream starts after the caller's prior work on `st` (which may produce the inputs)
+    ICX_HIP(ctx, hipEventRecord(enc->fork, st), ICX_INTERNAL_ERR);
+    ICX_HIP(ctx, hipStreamWaitEvent(enc->st2, enc->fork, 0), ICX_INTERNAL_ERR);
+    std::vector<int32_t> rc(n);
+    if (png_encode_device_batch(st, enc->st2, enc->ws, enc->ws2, n, width, height, d, d_srcs, d_out, out_stride,
+                                out_sizes, rc.data()) < 0) {
+        ctx->err = "HIP failure in png_encode_device_batch";
+        return ICX_INTERNAL_ERR;
+    }
+    for (int i = 0; i < n; ++i) status[i] = rc[i] == 0 ? ICX_OK : ICX_OUT_OF_MEM;
+    return ICX_OK;
+}
+
 int icx_png_encoder_stage_times(icx_png_encoder* enc, const char** names, float* ms, int cap) {
     if (!enc || cap <= 0) return 0;
-    return png_ws_stage_times(enc->ws, names, ms, cap);
+    const int k = png_ws_stage_times(enc->ws, names, ms, cap);
+    if (enc->ws2 && ms) {  // the batch entry's second workspace: summed
+        float m2[8] = {};
+        const int k2 = png_ws_stage_times(enc->ws2, nullptr, m2, std::min(cap, 8));
+        for (int i = 0; i < std::min(k, k2); ++i) ms[i] += m2[i];
+    }
+    return k;
 }
 
 // --------------------------------------------------------- Radiance .hdr (Image::readHdr)

@@ -1101,6 +1101,8 @@ struct PngWs {
     size_t seghist_cap = 0, segx_cap = 0;
     void* tmp = nullptr;
     size_t tmp_cap = 0;
+    struct PngHost* host = nullptr;  // pinned read-back buffer (PngJob)
+    hipEvent_t done = nullptr;       // a job's phase event
     // per-stage HIP events (icx_png_encoder_stage_times): stage i spans ev[2i] .. ev[2i+1];
     // ms[] accumulates over calls until read
     static constexpr int kStages = 6;
@@ -1109,6 +1111,8 @@ struct PngWs {
     ~PngWs() {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (done) (void)hipEventDestroy(done);
+        if (host) (void)hipHostFree(host);
         for (void* p : {(void*)st, (void*)set_key, (void*)set_idx, (void*)mode, (void*)conv, (void*)filt, (void*)tok,
                         (void*)ntok, (void*)hist, (void*)adl, (void*)crc, (void*)small, (void*)bc, (void*)bits,
                         (void*)off, (void*)seghist, (void*)segx, tmp})
@@ -1174,15 +1178,51 @@ static void chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data
     o.insert(o.end(), c, c + 4);
 }
 
-// Encode the device image d_src (w*h*d bytes, d = 3 RGB8 / 4 RGBA8) into a whole PNG file at
-// d_out. Returns 0 ok, 1 d_out too small (*size = bytes needed), -1 HIP failure.
-int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
-                      uint64_t cap, uint64_t* size) {
-    const int64_t np = (int64_t)w * h;
-    const bool timed = ws->ev[2 * PngWs::kStages - 1] != nullptr;
-    auto mark = [&](int i) {  // event i: stage i/2 begins (even) or ends (odd)
+// Host-visible results of one encode, read back between its phases (pinned: the copies into it
+// are asynchronous and the host waits on an event, not on the stream).
+struct PngHost {
+    Stats S;
+    unsigned long long last_off, last_bits;
+    uint32_t ad[2];
+    uint32_t crc_sum;
+    uint8_t pre[2048];  // signature + IHDR / PLTE / tRNS + IDAT header + zlib header
+    uint8_t adl[4], tail[16];
+};
+
+// One image's encode as three issue phases with a host read after each (png_encode_device runs
+// them back to back; png_encode_device_batch interleaves two images on two workspaces and
+// streams, so one image's kernels run while the host waits for the other's results):
+//   A  colour statistics                                          -> Stats
+//   B  (host: colour mode, palette, header) convert, filter, LZ77, Huffman, bit offsets, Adler
+//                                                                 -> stream length, Adler sums
+//   C  (host: file layout) emit, header / Adler bytes, CRC-32      -> CRC; the tail is written
+struct PngJob {
+    PngWs* ws = nullptr;
+    PngHost* hb = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;  // recorded after each phase's read-back
+    int w = 0, h = 0, d = 0;
+    const uint8_t* d_src = nullptr;
+    uint8_t* d_out = nullptr;
+    uint64_t cap = 0, size = 0;
+    Mode M{};
+    std::vector<uint8_t> head;
+    int64_t N = 0, nseg = 0, nblk = 0;
+    unsigned gwave = 0;
+    uint64_t zlen = 0, data_at = 0, dstart = 0, dbytes = 0;
+    bool timed = false;
+    void mark(int i) {  // event i: stage i/2 begins (even) or ends (odd)
         if (timed) (void)hipEventRecord(ws->ev[i], st);
-    };
+    }
+    int issue_a();
+    int issue_b();  // after ev of A
+    int issue_c();  // after ev of B; 1: d_out too small (size = bytes needed)
+    int finish();   // after ev of C
+};
+
+int PngJob::issue_a() {
+    const int64_t np = (int64_t)w * h;
+    timed = ws->ev[2 * PngWs::kStages - 1] != nullptr;
     size_t c1 = ws->st ? sizeof(Stats) : 0, c2 = ws->set_key ? kSetSlots * 8 : 0, c3 = c2, c4 = ws->mode ? sizeof(Mode) : 0;
     if (!pgrow(ws->st, sizeof(Stats), c1) || !pgrow(ws->set_key, kSetSlots * 8, c2) ||
         !pgrow(ws->set_idx, kSetSlots * 8, c3) || !pgrow(ws->mode, sizeof(Mode), c4))
@@ -1191,27 +1231,36 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     Stats zero{};
     zero.bits = 1;
     zero.first_a0 = ~0ull;
-    PNG_HIP(hipMemcpyAsync(ws->st, &zero, sizeof zero, hipMemcpyHostToDevice, st));
+    hb->S = zero;
+    PNG_HIP(hipMemcpyAsync(ws->st, &hb->S, sizeof zero, hipMemcpyHostToDevice, st));
     PNG_HIP(hipMemsetAsync(ws->set_key, 0, kSetSlots * 8, st));
     PNG_HIP(hipMemsetAsync(ws->set_idx, 0xFF, kSetSlots * 8, st));
     mark(0);
     const int gs = (int)std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 4096));
     if (np) hipLaunchKernelGGL(k_png_stats, dim3(gs), dim3(256), 0, st, d_src, np, d, ws->st, ws->set_key, ws->set_idx);
     mark(1);
-    Stats S;
-    PNG_HIP(hipMemcpyAsync(&S, ws->st, sizeof S, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipStreamSynchronize(st));
+    PNG_HIP(hipMemcpyAsync(&hb->S, ws->st, sizeof(Stats), hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipEventRecord(ev, st));
+    return 0;
+}
+
+int PngJob::issue_b() {
+    const int64_t np = (int64_t)w * h;
+    const int gs = (int)std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 4096));
+    Stats S = hb->S;
     uint32_t kr = 0, kg = 0, kb = 0;
     bool alpha = S.alpha_mid != 0, key = false;
-    if (d == 4 && !alpha && S.any_a0) {
+    if (d == 4 && !alpha && S.any_a0) {  // (rare: a colour key candidate; read back synchronously)
         uint8_t kp[4];
-        PNG_HIP(hipMemcpy(kp, d_src + S.first_a0 * 4, 4, hipMemcpyDeviceToHost));
+        PNG_HIP(hipMemcpyAsync(kp, d_src + S.first_a0 * 4, 4, hipMemcpyDeviceToHost, st));
+        PNG_HIP(hipStreamSynchronize(st));
         kr = kp[0];
         kg = kp[1];
         kb = kp[2];
         hipLaunchKernelGGL(k_png_keycheck, dim3(gs), dim3(256), 0, st, d_src, np, kr | kg << 8 | kb << 16, ws->st);
-        PNG_HIP(hipMemcpyAsync(&S, ws->st, sizeof S, hipMemcpyDeviceToHost, st));
+        PNG_HIP(hipMemcpyAsync(&hb->S, ws->st, sizeof S, hipMemcpyDeviceToHost, st));
         PNG_HIP(hipStreamSynchronize(st));
+        S = hb->S;
         alpha = S.a2 || S.a3;
         key = !alpha;
     }
@@ -1231,7 +1280,6 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     bool palette_ok = ncol <= 256 && bits <= 8 && ncol != 0;
     if ((uint64_t)np < (uint64_t)ncol * 2) palette_ok = false;
     if (gray_ok && !alpha && bits <= palettebits) palette_ok = false;
-    Mode M;
     std::memset(&M, 0, sizeof M);
     bool key_defined = false;
     uint32_t key16[3] = {kr + (kr << 8), kg + (kg << 8), kb + (kb << 8)};
@@ -1239,8 +1287,9 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
         M.colortype = kPalette;
         M.bitdepth = (int)palettebits;
         std::vector<unsigned long long> keys(kSetSlots), idx(kSetSlots);
-        PNG_HIP(hipMemcpy(keys.data(), ws->set_key, kSetSlots * 8, hipMemcpyDeviceToHost));
-        PNG_HIP(hipMemcpy(idx.data(), ws->set_idx, kSetSlots * 8, hipMemcpyDeviceToHost));
+        PNG_HIP(hipMemcpyAsync(keys.data(), ws->set_key, kSetSlots * 8, hipMemcpyDeviceToHost, st));
+        PNG_HIP(hipMemcpyAsync(idx.data(), ws->set_idx, kSetSlots * 8, hipMemcpyDeviceToHost, st));
+        PNG_HIP(hipStreamSynchronize(st));
         std::vector<std::pair<unsigned long long, uint32_t>> cols;
         for (int i = 0; i < kSetSlots; ++i)
             if (keys[i]) cols.push_back({idx[i], (uint32_t)keys[i]});
@@ -1263,7 +1312,7 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     PNG_HIP(hipMemcpyAsync(ws->mode, &M, sizeof M, hipMemcpyHostToDevice, st));
 
     // ---- header bytes (host; tiny)
-    std::vector<uint8_t> head = {137, 80, 78, 71, 13, 10, 26, 10};
+    head.assign({137, 80, 78, 71, 13, 10, 26, 10});
     uint8_t ihdr[13];
     be32(ihdr, (uint32_t)w);
     be32(ihdr + 4, (uint32_t)h);
@@ -1297,7 +1346,7 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     }
 
     // ---- P2: convert (unless the input already is the chosen mode) and filter
-    const int64_t N = (int64_t)h * (1 + M.lb);
+    N = (int64_t)h * (1 + M.lb);
     const bool identity = (M.colortype == kRGBA && d == 4) || (M.colortype == kRGB && d == 3);
     const uint8_t* img = d_src;
     mark(2);
@@ -1312,8 +1361,9 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     mark(3);
 
     // ---- P3/P4: deflate
-    const int64_t nseg = (N + kSeg - 1) / kSeg, nblk = (nseg + kSegPerBlock - 1) / kSegPerBlock;
-    size_t c5 = ws->seg_cap, c6 = ws->seg_cap, c7 = ws->seg_cap, c8 = ws->seg_cap, c9 = ws->blk_cap, c10 = ws->blk_cap;
+    nseg = (N + kSeg - 1) / kSeg;
+    nblk = (nseg + kSegPerBlock - 1) / kSegPerBlock;
+    size_t c5 = ws->seg_cap, c6 = ws->seg_cap, c7 = ws->seg_cap, c8 = ws->seg_cap;
     if (!pgrow(ws->tok, (size_t)nseg * kSeg * 2, ws->tok_cap)) return -1;  // <= kSeg slots per segment
     if ((size_t)nseg * 8 > ws->seg_cap || !ws->ntok) {
         if (!pgrow(ws->ntok, (size_t)nseg * 8, c5) || !pgrow(ws->adl, (size_t)nseg * 8, c6) ||
@@ -1321,8 +1371,6 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
             return -1;
         ws->seg_cap = (size_t)nseg * 8;
     }
-    (void)c9;
-    (void)c10;
     if (!pgrow(ws->hist, (size_t)nblk * (kNLL + kND) * 4, ws->hist_cap) ||
         !pgrow(ws->bc, (size_t)nblk * sizeof(BlockCodes), ws->blk_cap))
         return -1;
@@ -1337,7 +1385,7 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     mark(5);
     mark(6);
     hipLaunchKernelGGL(k_png_huff, dim3((unsigned)nblk), dim3(64), 0, st, ws->hist, nblk, ws->bc);
-    const unsigned gwave = (unsigned)((nseg + 3) / 4);  // one wave per segment
+    gwave = (unsigned)((nseg + 3) / 4);  // one wave per segment
     hipLaunchKernelGGL(k_png_segbits, dim3(gwave), dim3(256), 0, st, nseg, ws->seghist, ws->segx, ws->bc, ws->bits);
     size_t tb = 0;
     PNG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ws->bits, ws->off, (int)nseg, st));
@@ -1345,22 +1393,24 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     PNG_HIP(hipcub::DeviceScan::ExclusiveSum(ws->tmp, tb, ws->bits, ws->off, (int)nseg, st));
     hipLaunchKernelGGL(k_png_adler, dim3(1), dim3(256), 0, st, ws->adl, nseg, ws->small);
     mark(7);
-    unsigned long long last_off = 0, last_bits = 0;
-    uint32_t ad[2];
-    PNG_HIP(hipMemcpyAsync(&last_off, ws->off + nseg - 1, 8, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipMemcpyAsync(&last_bits, ws->bits + nseg - 1, 8, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipMemcpyAsync(ad, ws->small, 8, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipStreamSynchronize(st));
-    const uint64_t dbytes = (last_off + last_bits + 7) / 8;  // deflate stream, zero-padded
-    const uint64_t zlen = 2 + dbytes + 4;
+    PNG_HIP(hipMemcpyAsync(&hb->last_off, ws->off + nseg - 1, 8, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipMemcpyAsync(&hb->last_bits, ws->bits + nseg - 1, 8, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipMemcpyAsync(hb->ad, ws->small, 8, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipEventRecord(ev, st));
+    return 0;
+}
+
+int PngJob::issue_c() {
+    dbytes = (hb->last_off + hb->last_bits + 7) / 8;  // deflate stream, zero-padded
+    zlen = 2 + dbytes + 4;
     const uint64_t idat_at = head.size();  // IDAT chunk header position
-    const uint64_t data_at = idat_at + 8;   // zlib stream position
+    data_at = idat_at + 8;                 // zlib stream position
     const uint64_t total = data_at + zlen + 4 + 12;
-    *size = total;
+    size = total;
     if (total > cap) return 1;
     // The deflate bits go to a 4-byte aligned word view of d_out starting at data_at + 2
     // rounded down; the few bytes before it (zlib header) are rewritten afterwards.
-    const uint64_t dstart = data_at + 2;
+    dstart = data_at + 2;
     const uint64_t wbase = dstart & ~3ull;
     const unsigned long long base_bits = (dstart - wbase) * 8;
     PNG_HIP(hipMemsetAsync(d_out + wbase, 0, ((dbytes + (dstart - wbase) + 3) & ~3ull) + 4, st));
@@ -1376,11 +1426,12 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     pre.insert(pre.end(), ih, ih + 8);
     pre.push_back(0x78);
     pre.push_back(0x01);
-    PNG_HIP(hipMemcpyAsync(d_out, pre.data(), pre.size(), hipMemcpyHostToDevice, st));
-    uint8_t adl[4];
-    const uint32_t s1 = (1 + ad[0]) % kAdlerMod, s2 = (uint32_t)(((uint64_t)N + ad[1]) % kAdlerMod);
-    be32(adl, s2 << 16 | s1);
-    PNG_HIP(hipMemcpyAsync(d_out + dstart + dbytes, adl, 4, hipMemcpyHostToDevice, st));
+    if (pre.size() > sizeof hb->pre) return -1;
+    std::memcpy(hb->pre, pre.data(), pre.size());
+    PNG_HIP(hipMemcpyAsync(d_out, hb->pre, pre.size(), hipMemcpyHostToDevice, st));
+    const uint32_t s1 = (1 + hb->ad[0]) % kAdlerMod, s2 = (uint32_t)(((uint64_t)N + hb->ad[1]) % kAdlerMod);
+    be32(hb->adl, s2 << 16 | s1);
+    PNG_HIP(hipMemcpyAsync(d_out + dstart + dbytes, hb->adl, 4, hipMemcpyHostToDevice, st));
     // CRC-32 over "IDAT" + zlib stream: segment CRCs, folded 256:1 per pass into ws->crc
     const int64_t ncs = (int64_t)((zlen + kCrcSeg - 1) / kCrcSeg);
     size_t c12 = ws->crc_cap;
@@ -1388,17 +1439,6 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
     if (crc_need > ws->crc_cap || !ws->crc) {
         if (!pgrow(ws->crc, crc_need, c12)) return -1;
         ws->crc_cap = crc_need;
-    }
-    uint32_t init_raw = 0;  // raw CRC of 0xFFFFFFFF-initialised register over "IDAT", as raw state
-    {
-        // standard crc = raw(init=~0) ^ ~0; raw over "IDAT" from register ~0:
-        uint32_t c = 0xFFFFFFFFu;
-        const uint8_t t4[4] = {'I', 'D', 'A', 'T'};
-        for (int i = 0; i < 4; ++i) {
-            c ^= t4[i];
-            for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-        }
-        init_raw = c;
     }
     mark(10);
     hipLaunchKernelGGL(k_png_crc_seg, dim3((unsigned)((ncs + 255) / 256)), dim3(256), 0, st, d_out + data_at,
@@ -1415,23 +1455,112 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
         m = nb;
     }
     mark(11);
-    uint32_t crc_sum = 0;
-    PNG_HIP(hipMemcpyAsync(&crc_sum, cur, 4, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipStreamSynchronize(st));
-    const uint32_t craw = multmodp(init_raw, x8n(zlen)) ^ crc_sum;  // the "IDAT" prefix shifted over the range
-    uint8_t tail[16];
-    be32(tail, ~craw);
-    const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
-    std::memcpy(tail + 4, iend, 12);
-    PNG_HIP(hipMemcpyAsync(d_out + data_at + zlen, tail, 16, hipMemcpyHostToDevice, st));
+    PNG_HIP(hipMemcpyAsync(&hb->crc_sum, cur, 4, hipMemcpyDeviceToHost, st));
     PNG_HIP(hipGetLastError());
-    PNG_HIP(hipStreamSynchronize(st));
+    PNG_HIP(hipEventRecord(ev, st));
+    return 0;
+}
+
+int PngJob::finish() {
+    uint32_t init_raw;  // raw CRC of a 0xFFFFFFFF-initialised register over "IDAT"
+    {
+        uint32_t c = 0xFFFFFFFFu;
+        const uint8_t t4[4] = {'I', 'D', 'A', 'T'};
+        for (int i = 0; i < 4; ++i) {
+            c ^= t4[i];
+            for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        }
+        init_raw = c;
+    }
+    const uint32_t craw = multmodp(init_raw, x8n(zlen)) ^ hb->crc_sum;  // the "IDAT" prefix shifted over the range
+    be32(hb->tail, ~craw);
+    const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+    std::memcpy(hb->tail + 4, iend, 12);
+    PNG_HIP(hipMemcpyAsync(d_out + data_at + zlen, hb->tail, 16, hipMemcpyHostToDevice, st));
+    PNG_HIP(hipGetLastError());
     if (timed)
         for (int i = 0; i < PngWs::kStages; ++i) {
             float t = 0.f;
             if (hipEventElapsedTime(&t, ws->ev[2 * i], ws->ev[2 * i + 1]) == hipSuccess) ws->ms[i] += t;
         }
     return 0;
+}
+
+static bool png_job_init(PngJob& j, PngWs* ws, hipStream_t st, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
+                         uint64_t cap) {
+    if (!ws->host && hipHostMalloc(reinterpret_cast<void**>(&ws->host), sizeof(PngHost)) != hipSuccess) return false;
+    if (!ws->done && hipEventCreateWithFlags(&ws->done, hipEventDisableTiming) != hipSuccess) return false;
+    j.ws = ws;
+    j.hb = ws->host;
+    j.st = st;
+    j.ev = ws->done;
+    j.w = w;
+    j.h = h;
+    j.d = d;
+    j.d_src = d_src;
+    j.d_out = d_out;
+    j.cap = cap;
+    return true;
+}
+
+// Encode the device image d_src (w*h*d bytes, d = 3 RGB8 / 4 RGBA8) into a whole PNG file at
+// d_out. Returns 0 ok, 1 d_out too small (*size = bytes needed), -1 HIP failure.
+int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
+                      uint64_t cap, uint64_t* size) {
+    PngJob j;
+    if (!png_job_init(j, ws, st, w, h, d, d_src, d_out, cap)) return -1;
+    int rc = j.issue_a();
+    if (rc == 0) rc = hipEventSynchronize(j.ev) == hipSuccess ? j.issue_b() : -1;
+    if (rc == 0) rc = hipEventSynchronize(j.ev) == hipSuccess ? j.issue_c() : -1;
+    *size = j.size;
+    if (rc != 0) return rc;
+    if (hipEventSynchronize(j.ev) != hipSuccess || j.finish() != 0) return -1;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+}
+
+// n images of w x h x d at d_srcs[i] into d_out + i * stride (sizes[i], status[i]: 0 ok, 1 the
+// slot is too small, -1 failure). Two jobs in flight on (ws0, st0) / (ws1, st1): each phase of
+// one image is issued while the host waits for the other's read-back, so the two images' kernel
+// chains share the GPU and the host waits overlap GPU work. Returns -1 on a HIP failure.
+int png_encode_device_batch(hipStream_t st0, hipStream_t st1, PngWs* ws0, PngWs* ws1, int n, int w, int h, int d,
+                            const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t stride, uint64_t* sizes,
+                            int32_t* status) {
+    PngJob job[2];
+    int img[2] = {-1, -1}, phase[2] = {0, 0};
+    int next = 0, fail = 0;
+    auto start = [&](int k) {
+        if (next >= n) { img[k] = -1; return; }
+        img[k] = next++;
+        phase[k] = 0;
+        PngJob& j = job[k];
+        j = PngJob{};
+        if (!png_job_init(j, k ? ws1 : ws0, k ? st1 : st0, w, h, d, d_srcs[img[k]], d_out + (uint64_t)img[k] * stride,
+                          stride) ||
+            j.issue_a() != 0) {
+            status[img[k]] = -1;
+            fail = 1;
+            img[k] = -1;
+        }
+    };
+    start(0);
+    start(1);
+    for (int k = 0; img[0] >= 0 || img[1] >= 0; k ^= 1) {  // alternate: wait for one job, advance it
+        if (img[k] < 0) continue;
+        PngJob& j = job[k];
+        int rc = hipEventSynchronize(j.ev) == hipSuccess ? 0 : -1;
+        if (rc == 0) rc = phase[k] == 0 ? j.issue_b() : phase[k] == 1 ? j.issue_c() : j.finish();
+        if (rc != 0 || phase[k] == 2) {
+            sizes[img[k]] = j.size;
+            status[img[k]] = rc;
+            if (rc < 0) fail = 1;
+            start(k);
+        } else {
+            ++phase[k];
+        }
+    }
+    for (hipStream_t s : {st0, st1})
+        if (hipStreamSynchronize(s) != hipSuccess) fail = 1;
+    return fail ? -1 : 0;
 }
 
 bool png_encode_gpu(hipStream_t st, int w, int h, int d, const uint8_t* src, std::vector<uint8_t>& out) {

@@ -214,6 +214,15 @@ void icx_png_encoder_destroy(icx_png_encoder* enc);
  * failure. */
 int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, const uint8_t* d_src,
                           uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* hip_stream);
+/* n images (width x height x d each, at d_srcs[i] on the context's device) into d_out + i *
+ * out_stride; out_sizes[i] = file size (or the bytes needed), status[i] = ICX_OK or ICX_OUT_OF_MEM
+ * (the slot is too small). The batch form of png_encoder::saveToFile for device-resident images:
+ * two images in flight on two workspaces and streams, so one image's kernels run while the host
+ * reads back the other's (colour statistics, stream length, CRC). Returns when every file is
+ * written. */
+int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int height, int d,
+                                const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t out_stride,
+                                uint64_t* out_sizes, int32_t* status, void* hip_stream);
 /* Milliseconds per stage summed over the icx_png_encode_device calls since the previous read
  * ("stats", "filter", "lz77", "huff", "emit", "crc"; HIP events on the launch stream). Returns
  * the number of stages. */

@@ -118,6 +118,36 @@ def test_png_device_api(ctx):
     enc.close()
 
 
+def test_png_device_batch(ctx):
+    """icx_png_encode_device_batch (two images in flight on two workspaces and streams): every
+    file equals the one-image entry's bytes, including a palette image (the colour-mode read-back
+    path), a grey image and an odd size; a slot too small reports ICX_OUT_OF_MEM and the bytes
+    needed without disturbing the other images."""
+    import torch
+    w, h = 333, 211
+    pxs = [P.synth_rgba(10 + k, w, h) for k in range(5)]
+    pxs.append(np.repeat(np.arange(w * h, dtype=np.uint32).reshape(h, w, 1) % 7 * 30, 4, axis=2).astype(np.uint8))
+    pxs.append(np.repeat((np.arange(w * h) % 251).reshape(h, w, 1), 4, axis=2).astype(np.uint8))
+    pxs[-1][..., 3] = 255
+    want = [ctx.png_encode(w, h, 4, p.tobytes()) for p in pxs]
+    stride = max(len(x) for x in want) + 4096
+    enc = icx.PngEncoder(ctx)
+    d_src = [torch.from_numpy(np.ascontiguousarray(p)).cuda() for p in pxs]
+    d_out = torch.zeros(len(pxs) * stride, dtype=torch.uint8, device="cuda")
+    st, sz = enc.encode_device_batch(w, h, 4, [t.data_ptr() for t in d_src], d_out.data_ptr(), stride)
+    assert (st == icx.OK).all(), st
+    out = d_out.cpu().numpy()
+    for i, wb in enumerate(want):
+        assert int(sz[i]) == len(wb)
+        assert out[i * stride: i * stride + sz[i]].tobytes() == wb, i
+    # a slot smaller than the files: every image reports ICX_OUT_OF_MEM with its size
+    small = 1000
+    d_small = torch.zeros(len(pxs) * small, dtype=torch.uint8, device="cuda")
+    st2, sz2 = enc.encode_device_batch(w, h, 4, [t.data_ptr() for t in d_src], d_small.data_ptr(), small)
+    assert (st2 == icx.OUT_OF_MEM).all() and list(sz2) == [len(x) for x in want]
+    enc.close()
+
+
 def test_png_rejects(ctx):
     assert ctx.png_encode(4, 4, 2, bytes(32)) is None
     assert ctx.png_encode(0, 4, 4, b"") is None
