@@ -1409,11 +1409,14 @@ int PngJob::issue_c() {
     size = total;
     if (total > cap) return 1;
     // The deflate bits go to a 4-byte aligned word view of d_out starting at data_at + 2
-    // rounded down; the few bytes before it (zlib header) are rewritten afterwards.
+    // rounded down -- aligned as an address, since a batch slot may start anywhere (k_png_emit's
+    // atomics on the words two segments share need it) -- and the few bytes before it (zlib
+    // header) are rewritten afterwards.
     dstart = data_at + 2;
-    const uint64_t wbase = dstart & ~3ull;
-    const unsigned long long base_bits = (dstart - wbase) * 8;
-    PNG_HIP(hipMemsetAsync(d_out + wbase, 0, ((dbytes + (dstart - wbase) + 3) & ~3ull) + 4, st));
+    const uint64_t mis = (reinterpret_cast<uintptr_t>(d_out) + dstart) & 3u;
+    const uint64_t wbase = dstart - mis;
+    const unsigned long long base_bits = mis * 8;
+    PNG_HIP(hipMemsetAsync(d_out + wbase, 0, ((dbytes + mis + 3) & ~3ull) + 4, st));
     mark(8);
     hipLaunchKernelGGL(k_png_emit, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->off, ws->bits,
                        reinterpret_cast<uint32_t*>(d_out + wbase), base_bits);
