@@ -702,11 +702,14 @@ int icx_png_save_to_file(icx_ctx* ctx, const char* path, const unsigned char* pi
     return closed ? ICX_OK : ICX_INTERNAL_ERR;
 }
 
+// Images the PNG batch entry keeps in flight (each with its own workspace and stream):
+// ICX_PNG_INFLIGHT, 1..8.
+constexpr int kPngInflightMax = 8;
 struct icx_png_encoder {
     icx_ctx* ctx = nullptr;
     PngWs* ws = nullptr;
-    PngWs* ws2 = nullptr;         // second workspace + stream of the batch entry (created on use)
-    hipStream_t st2 = nullptr;
+    PngWs* wsx[kPngInflightMax] = {};      // the batch entry's other workspaces + streams (created on use)
+    hipStream_t stx[kPngInflightMax] = {};
     hipEvent_t fork = nullptr;
 };
 
@@ -722,8 +725,10 @@ void icx_png_encoder_destroy(icx_png_encoder* enc) {
     if (!enc) return;
     (void)hipSetDevice(enc->ctx->device);
     png_ws_destroy(enc->ws);
-    if (enc->ws2) png_ws_destroy(enc->ws2);
-    if (enc->st2) (void)hipStreamDestroy(enc->st2);
+    for (int j = 0; j < kPngInflightMax; ++j) {
+        if (enc->wsx[j]) png_ws_destroy(enc->wsx[j]);
+        if (enc->stx[j]) (void)hipStreamDestroy(enc->stx[j]);
+    }
     if (enc->fork) (void)hipEventDestroy(enc->fork);
     delete enc;
 }
@@ -752,16 +757,27 @@ int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int heig
     if (n > 0 && (!d_out || !out_stride)) { ctx->err = "null buffer"; return ICX_UNSUPPORTED; }
     if (n == 0) return ICX_OK;
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
-    if (!enc->ws2) enc->ws2 = png_ws_create();
-    if (!enc->st2) ICX_HIP(ctx, hipStreamCreateWithFlags(&enc->st2, hipStreamNonBlocking), ICX_INTERNAL_ERR);
+    const int k = [] {  // (read per call)
+        const char* e = std::getenv("ICX_PNG_INFLIGHT");
+        return e ? std::max(1, std::min(kPngInflightMax, std::atoi(e))) : 3;
+    }();
     if (!enc->fork) ICX_HIP(ctx, hipEventCreateWithFlags(&enc->fork, hipEventDisableTiming), ICX_INTERNAL_ERR);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
-    // the second stream starts after the caller's prior work on `st` (which may produce the inputs)
+    // the other streams start after the caller's prior work on `st` (which may produce the inputs)
     ICX_HIP(ctx, hipEventRecord(enc->fork, st), ICX_INTERNAL_ERR);
-    ICX_HIP(ctx, hipStreamWaitEvent(enc->st2, enc->fork, 0), ICX_INTERNAL_ERR);
+    hipStream_t sts[kPngInflightMax];
+    PngWs* wss[kPngInflightMax];
+    sts[0] = st;
+    wss[0] = enc->ws;
+    for (int j = 1; j < k; ++j) {
+        if (!enc->wsx[j]) enc->wsx[j] = png_ws_create();
+        if (!enc->stx[j]) ICX_HIP(ctx, hipStreamCreateWithFlags(&enc->stx[j], hipStreamNonBlocking), ICX_INTERNAL_ERR);
+        ICX_HIP(ctx, hipStreamWaitEvent(enc->stx[j], enc->fork, 0), ICX_INTERNAL_ERR);
+        sts[j] = enc->stx[j];
+        wss[j] = enc->wsx[j];
+    }
     std::vector<int32_t> rc(n);
-    if (png_encode_device_batch(st, enc->st2, enc->ws, enc->ws2, n, width, height, d, d_srcs, d_out, out_stride,
-                                out_sizes, rc.data()) < 0) {
+    if (png_encode_device_batch(k, sts, wss, n, width, height, d, d_srcs, d_out, out_stride, out_sizes, rc.data()) < 0) {
         ctx->err = "HIP failure in png_encode_device_batch";
         return ICX_INTERNAL_ERR;
     }
@@ -772,9 +788,10 @@ int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int heig
 int icx_png_encoder_stage_times(icx_png_encoder* enc, const char** names, float* ms, int cap) {
     if (!enc || cap <= 0) return 0;
     const int k = png_ws_stage_times(enc->ws, names, ms, cap);
-    if (enc->ws2 && ms) {  // the batch entry's second workspace: summed
+    for (int j = 1; j < kPngInflightMax; ++j) {  // the batch entry's other workspaces: summed
+        if (!enc->wsx[j] || !ms) continue;
         float m2[8] = {};
-        const int k2 = png_ws_stage_times(enc->ws2, nullptr, m2, std::min(cap, 8));
+        const int k2 = png_ws_stage_times(enc->wsx[j], nullptr, m2, std::min(cap, 8));
         for (int i = 0; i < std::min(k, k2); ++i) ms[i] += m2[i];
     }
     return k;

@@ -249,7 +249,7 @@ struct PngWs;
 PngWs* png_ws_create();
 void png_ws_destroy(PngWs* ws);
 int png_ws_stage_times(PngWs* ws, const char** names, float* ms, int cap);
-int png_encode_device_batch(hipStream_t st0, hipStream_t st1, PngWs* ws0, PngWs* ws1, int n, int w, int h, int d,
+int png_encode_device_batch(int k, hipStream_t* sts, PngWs** wss, int n, int w, int h, int d,
                             const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t stride, uint64_t* sizes,
                             int32_t* status);
 int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,

@@ -1522,47 +1522,47 @@ int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint
 }
 
 // n images of w x h x d at d_srcs[i] into d_out + i * stride (sizes[i], status[i]: 0 ok, 1 the
-// slot is too small, -1 failure). Two jobs in flight on (ws0, st0) / (ws1, st1): each phase of
-// one image is issued while the host waits for the other's read-back, so the two images' kernel
-// chains share the GPU and the host waits overlap GPU work. Returns -1 on a HIP failure.
-int png_encode_device_batch(hipStream_t st0, hipStream_t st1, PngWs* ws0, PngWs* ws1, int n, int w, int h, int d,
+// slot is too small, -1 failure). k jobs in flight on (ws[j], st[j]): each phase of one image is
+// issued while the host waits for another's read-back, so the images' kernel chains share the GPU
+// and the host waits overlap GPU work. Returns -1 on a HIP failure.
+int png_encode_device_batch(int k, hipStream_t* sts, PngWs** wss, int n, int w, int h, int d,
                             const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t stride, uint64_t* sizes,
                             int32_t* status) {
-    PngJob job[2];
-    int img[2] = {-1, -1}, phase[2] = {0, 0};
-    int next = 0, fail = 0;
-    auto start = [&](int k) {
-        if (next >= n) { img[k] = -1; return; }
-        img[k] = next++;
-        phase[k] = 0;
-        PngJob& j = job[k];
-        j = PngJob{};
-        if (!png_job_init(j, k ? ws1 : ws0, k ? st1 : st0, w, h, d, d_srcs[img[k]], d_out + (uint64_t)img[k] * stride,
-                          stride) ||
-            j.issue_a() != 0) {
-            status[img[k]] = -1;
+    std::vector<PngJob> job(k);
+    std::vector<int> img(k, -1), phase(k, 0);
+    int next = 0, fail = 0, live = 0;
+    auto start = [&](int j) {
+        img[j] = -1;
+        if (next >= n) return;
+        img[j] = next++;
+        phase[j] = 0;
+        job[j] = PngJob{};
+        if (!png_job_init(job[j], wss[j], sts[j], w, h, d, d_srcs[img[j]], d_out + (uint64_t)img[j] * stride, stride) ||
+            job[j].issue_a() != 0) {
+            status[img[j]] = -1;
             fail = 1;
-            img[k] = -1;
+            img[j] = -1;
         }
     };
-    start(0);
-    start(1);
-    for (int k = 0; img[0] >= 0 || img[1] >= 0; k ^= 1) {  // alternate: wait for one job, advance it
-        if (img[k] < 0) continue;
-        PngJob& j = job[k];
-        int rc = hipEventSynchronize(j.ev) == hipSuccess ? 0 : -1;
-        if (rc == 0) rc = phase[k] == 0 ? j.issue_b() : phase[k] == 1 ? j.issue_c() : j.finish();
-        if (rc != 0 || phase[k] == 2) {
-            sizes[img[k]] = j.size;
-            status[img[k]] = rc;
+    for (int j = 0; j < k; ++j) start(j);
+    for (int j = 0; j < k; ++j) live += img[j] >= 0;
+    for (int j = 0; live > 0; j = (j + 1) % k) {  // round robin: wait for one job, advance it
+        if (img[j] < 0) continue;
+        PngJob& J = job[j];
+        int rc = hipEventSynchronize(J.ev) == hipSuccess ? 0 : -1;
+        if (rc == 0) rc = phase[j] == 0 ? J.issue_b() : phase[j] == 1 ? J.issue_c() : J.finish();
+        if (rc != 0 || phase[j] == 2) {
+            sizes[img[j]] = J.size;
+            status[img[j]] = rc;
             if (rc < 0) fail = 1;
-            start(k);
+            start(j);
+            if (img[j] < 0) --live;
         } else {
-            ++phase[k];
+            ++phase[j];
         }
     }
-    for (hipStream_t s : {st0, st1})
-        if (hipStreamSynchronize(s) != hipSuccess) fail = 1;
+    for (int j = 0; j < k; ++j)
+        if (hipStreamSynchronize(sts[j]) != hipSuccess) fail = 1;
     return fail ? -1 : 0;
 }
 

@@ -217,9 +217,9 @@ int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, co
 /* n images (width x height x d each, at d_srcs[i] on the context's device) into d_out + i *
  * out_stride; out_sizes[i] = file size (or the bytes needed), status[i] = ICX_OK or ICX_OUT_OF_MEM
  * (the slot is too small). The batch form of png_encoder::saveToFile for device-resident images:
- * two images in flight on two workspaces and streams, so one image's kernels run while the host
- * reads back the other's (colour statistics, stream length, CRC). Returns when every file is
- * written. */
+ * several images in flight (ICX_PNG_INFLIGHT, default 3), each on its own workspace and stream,
+ * so some images' kernels run while the host reads back another's (colour statistics, stream
+ * length, CRC). Returns when every file is written. */
 int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int height, int d,
                                 const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t out_stride,
                                 uint64_t* out_sizes, int32_t* status, void* hip_stream);

@@ -118,8 +118,10 @@ def test_png_device_api(ctx):
     enc.close()
 
 
-def test_png_device_batch(ctx):
-    """icx_png_encode_device_batch (two images in flight on two workspaces and streams): every
+@pytest.mark.parametrize("inflight", ["1", "2", "3", "8"])
+def test_png_device_batch(ctx, monkeypatch, inflight):
+    """icx_png_encode_device_batch (ICX_PNG_INFLIGHT images in flight, each on its own workspace
+    and stream; 8 is more than the 7 images): every
     file equals the one-image entry's bytes, including a palette image (the colour-mode read-back
     path), a grey image and an odd size; a slot too small reports ICX_OUT_OF_MEM and the bytes
     needed without disturbing the other images."""
@@ -129,6 +131,7 @@ def test_png_device_batch(ctx):
     pxs.append(np.repeat(np.arange(w * h, dtype=np.uint32).reshape(h, w, 1) % 7 * 30, 4, axis=2).astype(np.uint8))
     pxs.append(np.repeat((np.arange(w * h) % 251).reshape(h, w, 1), 4, axis=2).astype(np.uint8))
     pxs[-1][..., 3] = 255
+    monkeypatch.setenv("ICX_PNG_INFLIGHT", inflight)
     want = [ctx.png_encode(w, h, 4, p.tobytes()) for p in pxs]
     stride = max(len(x) for x in want) + 4096
     enc = icx.PngEncoder(ctx)
