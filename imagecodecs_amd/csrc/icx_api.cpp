@@ -759,7 +759,7 @@ int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int heig
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
     const int k = [] {  // (read per call)
         const char* e = std::getenv("ICX_PNG_INFLIGHT");
-        return e ? std::max(1, std::min(kPngInflightMax, std::atoi(e))) : 3;
+        return e ? std::max(1, std::min(kPngInflightMax, std::atoi(e))) : kPngInflightMax;
     }();
     if (!enc->fork) ICX_HIP(ctx, hipEventCreateWithFlags(&enc->fork, hipEventDisableTiming), ICX_INTERNAL_ERR);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;

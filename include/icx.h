@@ -217,7 +217,7 @@ int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, co
 /* n images (width x height x d each, at d_srcs[i] on the context's device) into d_out + i *
  * out_stride; out_sizes[i] = file size (or the bytes needed), status[i] = ICX_OK or ICX_OUT_OF_MEM
  * (the slot is too small). The batch form of png_encoder::saveToFile for device-resident images:
- * several images in flight (ICX_PNG_INFLIGHT, default 3), each on its own workspace and stream,
+ * several images in flight (ICX_PNG_INFLIGHT, default 8), each on its own workspace and stream,
  * so some images' kernels run while the host reads back another's (colour statistics, stream
  * length, CRC). Returns when every file is written. */
 int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int height, int d,
