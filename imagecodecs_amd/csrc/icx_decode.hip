@@ -863,8 +863,23 @@ __device__ __forceinline__ CRaw chroma_fetch(const CPl& c, int r, int M, bool fa
 constexpr uint32_t kBias8 = 0x80808080u;
 constexpr int32_t kTapFwd = (int32_t)((uint32_t)(uint8_t)-9 | (111u << 8) | (29u << 16) | ((uint32_t)(uint8_t)-3 << 24));
 constexpr int32_t kTapRev = (int32_t)((uint32_t)(uint8_t)-3 | (29u << 8) | (111u << 16) | ((uint32_t)(uint8_t)-9 << 24));
+// The VOP3P dot products, whose accumulator is a source operand. The builtins compile to the
+// VOP2 v_dot4c_i32_i8 / v_dot2c_i32_i16, whose accumulator is the destination, so every dot with
+// a constant bias spent a v_mov re-loading it: a quarter of each tap, 3 VALU per converted pixel.
+// (The weights -- wave-uniform constants -- in an SGPR, the one a VOP3 may read; the biases in
+// VGPRs. Both are loop-invariant, so they are set up once.)
+__device__ __forceinline__ int32_t dot4_i8(uint32_t a, int32_t b, int32_t acc) {
+    int32_t r;
+    asm("v_dot4_i32_i8 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ int32_t dot2_i16(uint32_t a, uint32_t b, int32_t acc) {
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(acc));
+    return r;
+}
 __device__ __forceinline__ uint32_t dtap(uint32_t biased, int32_t k) {
-    const int32_t v = __builtin_amdgcn_sdot4((int)biased, k, 128 * 128 + 64, false) >> 7;
+    const int32_t v = dot4_i8(biased, k, 128 * 128 + 64) >> 7;
     return (uint32_t)min(max(v, 0), 255);
 }
 
@@ -914,16 +929,18 @@ __device__ __forceinline__ uint32_t vtap_odd(int k, int h, uint32_t w1, uint32_t
 typedef short icx_short2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ icx_short2 as_s2(uint32_t v) { return __builtin_bit_cast(icx_short2, v); }
 __device__ __forceinline__ void ycc4_to_rgb(uint32_t yv, uint32_t cb, uint32_t cr, uint32_t (&w)[3]) {
-    const icx_short2 kR = {256, 359}, kG1 = {256, -88}, kG2 = {0, -183}, kB = {256, 454};
+    // (Y, c) weight pairs as packed int16: (256, 359), (256, -88), (0, -183), (256, 454)
+    constexpr uint32_t kR = 256u | (359u << 16), kG1 = 256u | ((uint32_t)(uint16_t)-88 << 16),
+                       kG2 = (uint32_t)(uint16_t)-183 << 16, kB = 256u | (454u << 16);
     uint32_t R[4], G[4], B[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t sel = (uint32_t)i | (0x0cu << 8) | ((uint32_t)(4 + i) << 16) | (0x0cu << 24);
-        const icx_short2 yb = as_s2(__builtin_amdgcn_perm(cb, yv, sel));  // (Y_i, cb_i)
-        const icx_short2 yr = as_s2(__builtin_amdgcn_perm(cr, yv, sel));  // (Y_i, cr_i)
-        const int rn = __builtin_amdgcn_sdot2(yr, kR, 128 - 359 * 128, false);
-        const int gn = __builtin_amdgcn_sdot2(yr, kG2, __builtin_amdgcn_sdot2(yb, kG1, 128 + (88 + 183) * 128, false), false);
-        const int bn = __builtin_amdgcn_sdot2(yb, kB, 128 - 454 * 128, false);
+        const uint32_t yb = __builtin_amdgcn_perm(cb, yv, sel);  // (Y_i, cb_i)
+        const uint32_t yr = __builtin_amdgcn_perm(cr, yv, sel);  // (Y_i, cr_i)
+        const int rn = dot2_i16(yr, kR, 128 - 359 * 128);
+        const int gn = dot2_i16(yr, kG2, dot2_i16(yb, kG1, 128 + (88 + 183) * 128));
+        const int bn = dot2_i16(yb, kB, 128 - 454 * 128);
         R[i] = (uint32_t)min(max(rn, 0), 65535);
         G[i] = (uint32_t)min(max(gn, 0), 65535);
         B[i] = (uint32_t)min(max(bn, 0), 65535);
@@ -1212,8 +1229,11 @@ __global__ __launch_bounds__(256) void k_convert_edge(const Desc* __restrict__ d
 
 // One instantiation per layout (K as in stream_kind), so each gets its own register allocation;
 // every instantiation is launched and skips the images of other layouts.
+#ifndef ICX_CONV_MINW  // (timing experiments: waves per SIMD k_convert_stream is compiled for)
+#define ICX_CONV_MINW 1
+#endif
 template <int K>
-__global__ __launch_bounds__(256) void k_convert_stream(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
+__global__ __launch_bounds__(256, ICX_CONV_MINW) void k_convert_stream(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
                                                         int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride,
                                                         int fuse) {
     const int img = blockIdx.y;
@@ -1642,7 +1662,9 @@ __global__ __launch_bounds__(256, ICX_BACK_MINW) void k_back420(const Desc* __re
                 }
             }
             lDn = blk_resolve(d, Pn);
+#ifndef ICX_EXP_BACK_NOLOAD  // timing experiment only: keep transforming the first block (no loads)
             load_block(ac, lDn.blk, h, Dn);  // (past the last step: a harmless reload)
+#endif
             Pa = pend_at(tr + 2);
             const int rd = tr + 1;  // horizontal doubling of chroma MCU row rd (written last step)
             if (rd >= lo && rd <= hi) {
@@ -1671,7 +1693,9 @@ __global__ __launch_bounds__(256, ICX_BACK_MINW) void k_back420(const Desc* __re
                     L.dbl[rd & 3][cc][r][lane] = v;
                 }
             }
+#ifndef ICX_EXP_BACK_NOBAR  // timing experiment only: no barrier (wrong pixels)
             lds_barrier();
+#endif
             // ---- phase B: vertical doubling + conversion of output rows 16 tr + 4 wave .. + 3
             const int y0 = 16 * tr + 4 * wave;
             if (tr >= r0 && y0 < H) {  // wave-uniform
