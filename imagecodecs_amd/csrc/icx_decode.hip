@@ -1419,7 +1419,10 @@ __global__ __launch_bounds__(256, ICX_IDCT_C_MINW) void k_idct420c(const Desc* _
 #pragma unroll
     for (int k = 0; k < 16; ++k) qw[k] = cc ? qb[k] : qw[k];
     const int mbw = d.mbw, stride = d.c[1].stride;
-    uint8_t* Pc = planes + (int64_t)img * plane_cap + comp_plane_off(d, 1 + cc);
+    // Cb plane base (wave-uniform) and the Cr lanes' 32-bit offset from it (a chroma plane is
+    // at most (65535 / 2)^2 bytes)
+    uint8_t* Pc = planes + (int64_t)img * plane_cap + comp_plane_off(d, 1);
+    const uint32_t ccoff = cc ? (uint32_t)(comp_plane_off(d, 2) - comp_plane_off(d, 1)) : 0u;
     const uint32_t ucols = (uint32_t)((mbw + 15) >> 4), nunits = ucols * (uint32_t)d.mbh;
     const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
@@ -1435,9 +1438,12 @@ __global__ __launch_bounds__(256, ICX_IDCT_C_MINW) void k_idct420c(const Desc* _
         const int mx = min((int)((u - mby * ucols) << 4) + mq, mbw - 1);
         uint32_t rowd[8];
         pair_idct(c, qw, h, dcv, l, rowd);
-        uint8_t* dst = Pc + (int64_t)mby * 8 * stride + mx * 8 + 4 * h;
+        // the unit's row base is wave-uniform (scalar); a lane adds a 32-bit offset per row, so
+        // the stores take the SGPR-base + VGPR-offset form with one VALU add each
+        uint8_t* const rowp = Pc + (int64_t)mby * 8 * stride;
+        const uint32_t lo = ccoff + (uint32_t)(mx * 8 + 4 * h);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
+        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(rowp + (lo + (uint32_t)(r * stride))) = rowd[r];
     };
     idct_units(ac, d, h, wid, nw, nunits, pendf, unit);
 }
@@ -1473,9 +1479,10 @@ __global__ __launch_bounds__(256, ICX_IDCT_Y_MINW) void k_idct420y(const Desc* _
         const int mx = min((int)((u - mby * ucols) << 3) + mq, mbw - 1);
         uint32_t rowd[8];
         pair_idct(c, qw, h, dcv, l, rowd);
-        uint8_t* dst = Py + ((int64_t)mby * 16 + sby * 8) * stride + mx * 16 + sbx * 8 + 4 * h;
+        uint8_t* const rowp = Py + (int64_t)mby * 16 * stride;  // (as in k_idct420c)
+        const uint32_t lo = (uint32_t)(sby * 8 * stride + mx * 16 + sbx * 8 + 4 * h);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(dst + (int64_t)r * stride) = rowd[r];
+        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(rowp + (lo + (uint32_t)(r * stride))) = rowd[r];
     };
     idct_units(ac, d, h, wid, nw, nunits, pendf, unit);
 }
