@@ -852,10 +852,10 @@ struct CRaw {
 // per-lane branch gets an s_waitcnt vmcnt(0) at the join, which serialised every row fetch.)
 template <bool KH>
 __device__ __forceinline__ CRaw chroma_fetch(const CPl& c, int r, int M, bool fast) {
-    const uint8_t* row = c.p + (int64_t)r * c.s;
-    if (!KH) return CRaw{ld4(row + 4 * M), 0u};
-    const int base = fast ? (2 * M - 2) & ~3 : 0;  // edge lanes load inside chroma_make
-    return CRaw{ld4(row + base), ld4(row + base + 4)};
+    const uint8_t* row = c.p + (int64_t)r * c.s;  // (uniform row base + 32-bit lane offset, as put3)
+    if (!KH) return CRaw{ld4(row + (uint32_t)(4 * M)), 0u};
+    const uint32_t base = fast ? (uint32_t)((2 * M - 2) & ~3) : 0u;  // edge lanes load inside chroma_make
+    return CRaw{ld4(row + base), ld4(row + (base + 4))};
 }
 // The 4-tap kernel as one v_dot4 on four packed samples: samples are biased to int8 (x ^ 0x80
 // = x - 128) and, since the taps sum to 128, sum(k*x) + 64 = dot(k, x - 128) + 128*128 + 64.
@@ -958,7 +958,9 @@ struct StreamOut {
     int W;
     bool vec;  // rows 4-byte aligned
     __device__ __forceinline__ void put3(int y, int x0, const uint32_t (&w)[3], int nb) const {
-        uint8_t* dst = o + ((int64_t)y * W + x0) * 3;
+        // row base (wave-uniform in k_convert_stream: SGPRs) + the lane's 32-bit offset, so the
+        // store takes the SGPR-base form instead of a 64-bit multiply-add chain per row
+        uint8_t* dst = o + (int64_t)y * W * 3 + (uint32_t)(x0 * 3);
         if (vec && nb == 12) {
             typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
             const u32x3 v = {w[0], w[1], w[2]};
@@ -1113,7 +1115,7 @@ __device__ __forceinline__ void lane_strip(const CPl& c1, const CPl& c2, const u
         ycc4_to_rgb(yv, cb, cr, w);
         so.put3(y, x0, w, nb);
     };
-    auto luma = [&](int y) { return ld4(P0 + (int64_t)y * s0 + x0); };
+    auto luma = [&](int y) { return ld4(P0 + (int64_t)y * s0 + (uint32_t)x0); };
     if (K == 4) {  // gray: stride removal (jpeg_dec.h:854-865)
 #pragma unroll 4
         for (int y = Y0; y < Y1; ++y) {
