@@ -40,6 +40,26 @@ STAGE_KERNEL = {"write": "k_gw_lane", "idct": "k_idct420y+k_idct420c", "convert"
 GW_MIN_PIXELS = 2048 * 2048  # icx_internal.h kGwMinPixels: larger workspaces take the guess-write path
 
 
+def coef_cell_bytes():
+    """Bytes one coefficient block occupies in the pool (icx_internal.h: 64 int16 cells)."""
+    return 128
+
+
+def pipeline_traffic(workload, n, alg_bytes):
+    """Whole-step HBM traffic from the committed PMC profile (tools/pmc_traffic.py pipeline: every
+    kernel's FETCH_SIZE x correction + WRITE_SIZE, per image), scaled to this run's n images, and
+    its ratio to the step's algorithmic bytes. Empty when no profile of this workload exists."""
+    p = os.path.join(ROOT, "profiles", "pipeline_traffic.json")
+    if not os.path.exists(p):
+        return {}
+    tj = json.load(open(p))
+    if tj.get("workload") != workload:
+        return {}
+    moved = tj["moved_MB_per_image"] * 1e6 * n
+    return {"pipeline_traffic": round(moved), "moved_over_alg": round(moved / alg_bytes, 3),
+            "pipeline_traffic_source": "profiles/pipeline_traffic.json (" + tj.get("source", "PMC run") + ")"}
+
+
 def stage_kernels(w, h):
     """STAGE_KERNEL for a batch of w x h images: the three-pass entropy path's kernels where the
     library takes it (ICX_GW=0, or a workspace for images of at most GW_MIN_PIXELS)."""
@@ -198,8 +218,6 @@ def main_encode(args, wl, world, rank, local):
         sizes[:] = sz
         if (st != icx.OK).any():
             d_st.copy_(torch.from_numpy(st.astype(np.int32)))
-        if world > 1:
-            return shard.gather_results(d_st, dist)
         return d_st
 
     for _ in range(args.warmup):
@@ -219,6 +237,8 @@ def main_encode(args, wl, world, rank, local):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     stages = {k: v / args.steps for k, v in enc.stage_times().items()}  # ms per step
+    if world > 1:  # the final gather of every rank's statuses, after the timed steps
+        last = shard.gather_results(last, dist)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -258,7 +278,7 @@ def main_encode(args, wl, world, rank, local):
         "data": "synthetic (tools/synth.c RGB, seeded)",
         "config": {"workload": wl["desc"], "images_per_gpu": n, "pool": npool, "width": W, "height": H,
                    "quality": Q, "subsampling": SUB, "bytes_per_pixel_compressed": round(comp / (n * W * H), 4),
-                   "parallelism": f"dp{world} (images sharded; RCCL gather of statuses)"},
+                   "parallelism": f"dp{world} (images sharded; one RCCL all-gather of statuses after the timed steps)"},
         "roofline": roof, "cpu_baseline": cpu,
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
     }
@@ -334,13 +354,11 @@ def main_png(args, wl, world, rank, local):
                 rc, sizes[i] = enc.encode_device(W, H, 4, srcs[i], d_out[i].data_ptr(), cap, stream.cuda_stream)
                 if rc != icx.OK:
                     d_st[i] = rc
-        else:  # icx_png_encode_device_batch: two images in flight
+        else:  # icx_png_encode_device_batch: ICX_PNG_INFLIGHT (default 8) images in flight
             st, sz = enc.encode_device_batch(W, H, 4, srcs, d_out.data_ptr(), cap, stream.cuda_stream)
             sizes[:] = sz
             if (st != icx.OK).any():
                 d_st.copy_(torch.from_numpy(st.astype(np.int32)))
-        if world > 1:
-            return shard.gather_results(d_st, dist)
         return d_st
 
     for _ in range(args.warmup):
@@ -360,6 +378,8 @@ def main_png(args, wl, world, rank, local):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     stages = {k: v / args.steps for k, v in enc.stage_times().items()}  # ms per step
+    if world > 1:  # the final gather of every rank's statuses, after the timed steps
+        last = shard.gather_results(last, dist)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -405,7 +425,7 @@ def main_png(args, wl, world, rank, local):
         "data": "synthetic (tools/synth.c RGB + alpha gradient, seeded)",
         "config": {"workload": wl["desc"], "images_per_gpu": n, "pool": npool, "width": W, "height": H,
                    "png_bytes_per_pixel": round(out_b / (n * W * H), 4),
-                   "parallelism": f"dp{world} (images sharded; RCCL gather of statuses)"},
+                   "parallelism": f"dp{world} (images sharded; one RCCL all-gather of statuses after the timed steps)"},
         "roofline": roof, "cpu_baseline": cpu,
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
     }
@@ -537,7 +557,7 @@ def main_hdr(args, wl, world, rank, local):
         "dtype": "u8->f32", "data": "synthetic (tools/synth.c synth_rgbe + hdr_encode, seeded)",
         "config": {"workload": wl["desc"], "images_per_gpu": n, "pool": npool, "width": W, "height": H,
                    "file_bytes_per_pixel": round(file_b / (n * W * H), 4),
-                   "parallelism": f"dp{world} (images sharded; RCCL gather of statuses)"},
+                   "parallelism": f"dp{world} (images sharded; one RCCL all-gather of statuses after the timed steps)"},
         "roofline": roof, "cpu_baseline": cpu,
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
     }
@@ -639,11 +659,9 @@ def main():
     batch = icx.Batch(ctx, n, W, H, args.group)
     stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def step():  # no collective inside the timed loop: the records gather after it is the only one
         batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out.data_ptr(), stride,
                             d_st.data_ptr(), d_dims.data_ptr(), stream.cuda_stream)
-        if world > 1:  # final gather of per-image statuses over RCCL/xGMI (the only collective)
-            return shard.gather_results(d_st, dist)
         return d_st
 
     for _ in range(args.warmup):
@@ -690,10 +708,9 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
 
-    # correctness of the measured run: every image of the job OK (gathered statuses); this rank's
-    # pool images bit-exact vs the oracle
-    st = last.cpu().numpy()
-    ok_all = bool((st == 0).all())
+    # correctness of the measured run: every image of the job OK (the gathered records carry every
+    # rank's statuses); this rank's pool images bit-exact vs the oracle
+    ok_all = bool((last.cpu().numpy() == 0).all()) and records["status_ok"]
     checked = 0
     mismatches = 0
     if rank == 0 and cpu_hashes:
@@ -754,13 +771,20 @@ def main():
             # group): the per-image traffic is scaled to this run's images per launch
             if tj.get("workload") == args.workload and tj.get("kernel") == kname and tj.get("images_per_launch"):
                 traffic = round(tj["bytes_per_launch"] / tj["images_per_launch"] * (-(-n // launches)))
+        # the dominant kernel's own necessary bytes (what `traffic` is to be read against): the
+        # entropy decode reads the unstuffed stream (<= the compressed bytes) and writes the
+        # coefficient blocks (128 B each); the other stages' kernels move their own planes
+        blocks = n * sum((-(-W // 8)) * (-(-H // 8)) // d for d in (1, 4, 4))  # 4:2:0: Y + two quarter planes
+        own = {"write": comp_bytes + blocks * coef_cell_bytes(), "unstuff": 2 * comp_bytes}.get(dom)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": kname, "launches_per_step": launches,
                 "alg_bytes_per_launch": round(alg_bytes / launches),
+                "kernel_own_bytes_per_launch": round(own / launches) if own else None,
                 "avg_launch_ms": round(stages[dom] / launches, 3),
                 "stage_ms": {k: round(v, 3) for k, v in stages.items()},
                 "pipeline_frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+        roof.update(pipeline_traffic(args.workload, n, alg_bytes))
     out = {
         "metric": f"megapixels/s JPEG decode, {W}x{H} RGB batch",
         "value": round(value, 2), "unit": "megapixels/s", "n_gpus": world, "steps": args.steps,
@@ -768,7 +792,8 @@ def main():
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (tools/synth.c, seeded)",
         "config": {"workload": wl["desc"], "images_per_gpu": n, "pool": len(pool), "width": W, "height": H,
                    "bytes_per_pixel_compressed": round(comp_bytes / (n * W * H), 4),
-                   "parallelism": f"dp{world} (images sharded; RCCL gather of statuses)"},
+                   "parallelism": f"dp{world} (images sharded; one RCCL all-gather of per-image records after the "
+                                          f"timed steps)"},
         "roofline": roof,
         "cpu_baseline": cpu,
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},

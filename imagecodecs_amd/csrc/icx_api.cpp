@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <string>
 #include <vector>
@@ -178,13 +179,17 @@ static int64_t ws_per_slot(GroupWs& ws, int max_w, int max_h) {
     ws.coef_cap = ws_coef_cap(max_w, max_h);
     ws.plane_cap = ws_plane_cap(max_w, max_h);
     ws.tmp_cap = ws_tmp_cap(max_w, max_h);
-    ws.ucap = ((int64_t)max_w * max_h + 4095) / 4096 * 4096;  // 1 B/px of entropy data (q90 ~0.4)
+    // unstuffed entropy bytes per slot: 2 B/px (ICX_UPOOL_BPP; q90 4:2:0 is ~0.4, a 4:4:4 q100 photo
+    // 1.3-2.5). A group whose scans pass the pool defers the rest to further entropy rounds
+    // (launch_spec_entropy), so this sizes the common case, not a limit.
+    const int bpp = std::getenv("ICX_UPOOL_BPP") ? std::max(1, std::min(16, std::atoi(std::getenv("ICX_UPOOL_BPP")))) : 2;
+    ws.ucap = ((int64_t)max_w * max_h * bpp + 4095) / 4096 * 4096;
     ws.rst_cap = ((int64_t)max_w / 8 + 1) * ((int64_t)max_h / 8 + 1);  // >= MCUs per image
     // decode lanes of kSubBytesSmall .. kSubBytes bytes (k_spec_plan picks per image)
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytesSmall - 1) / kSubBytesSmall + kLanes - 1) / kLanes * kLanes + kLanes;
-    // coefficient pool: 1.25 x coef_cap blocks per slot (int16 block + int32 DC escape + map entry)
-    return ws.coef_cap * 5 / 4 * (64 * 2 + 4 + 8) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
+    // coefficient pool: kPoolPerSlot x coef_cap blocks per slot (int16 block + int32 DC escape + map entry)
+    return ws.coef_cap * kPoolPerSlotX4 / 4 * (64 * 2 + 4 + 8) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
            (int64_t)sizeof(StepSet) +
            tiles_per_slot * 28 + ws.rst_cap * 8 +
            lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec + (int64_t)sizeof(GwOut) +
@@ -221,8 +226,12 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ws.upool = (int64_t)(group + 2) * ws.ucap;
     ICX_HIP(ctx, hipMalloc(&ws.desc, sizeof(Desc) * group), false);
     // the coefficient pool (k_spec_plan places each image in it; the guess-write lanes' overflow
-    // chunks and count blocks take its tail), + kGwChunk scratch blocks past pool_cap
-    ws.pool_cap = (int64_t)(group + 2) * ws.coef_cap * 5 / 4;
+    // chunks and count blocks take its tail), + kGwChunk scratch blocks past pool_cap. The static
+    // regions take 1.1 x each image's blocks; the tail, 2.5 (G + 2) - 1.1 G > 1.4 G image-blocks,
+    // holds every block of every image in overflow chunks (a photo whose flat sky is a few lanes'
+    // worth of bytes stores nearly all its blocks there) plus the count lanes' copies and the
+    // chunks' rounding, so a conforming group never runs out of it.
+    ws.pool_cap = (int64_t)(group + 2) * ws.coef_cap * kPoolPerSlotX4 / 4;
     ICX_HIP(ctx, hipMalloc(&ws.ac, (size_t)(ws.pool_cap + kGwChunk) * 64 * 2), false);
     ICX_HIP(ctx, hipMalloc(&ws.dc, (size_t)(ws.pool_cap + kGwChunk) * 4), false);
     ICX_HIP(ctx, hipMalloc(&ws.map, (size_t)ws.pool_cap * sizeof(uint2)), false);
@@ -776,12 +785,22 @@ int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int heig
         sts[j] = enc->stx[j];
         wss[j] = enc->wsx[j];
     }
-    std::vector<int32_t> rc(n);
-    if (png_encode_device_batch(k, sts, wss, n, width, height, d, d_srcs, d_out, out_stride, out_sizes, rc.data()) < 0) {
+    std::vector<int32_t> rc(n, -1);
+    for (int i = 0; i < n; ++i) out_sizes[i] = 0;
+    const int call = png_encode_device_batch(k, sts, wss, n, width, height, d, d_srcs, d_out, out_stride, out_sizes,
+                                             rc.data());
+    // every image gets its own status, also when another one failed: 0 OK, 1 its file did not fit
+    // out_stride, -1 a HIP or host allocation failure in its own job
+    for (int i = 0; i < n; ++i) {
+        status[i] = rc[i] == 0 ? ICX_OK : rc[i] == 1 ? ICX_OUT_OF_MEM : ICX_INTERNAL_ERR;
+        if (rc[i] < 0) out_sizes[i] = 0;
+    }
+    if (call < 0) {  // a stream failed: the whole call
         ctx->err = "HIP failure in png_encode_device_batch";
         return ICX_INTERNAL_ERR;
     }
-    for (int i = 0; i < n; ++i) status[i] = rc[i] == 0 ? ICX_OK : ICX_OUT_OF_MEM;
+    for (int i = 0; i < n; ++i)
+        if (rc[i] < 0) { ctx->err = "png_encode_device_batch: an image's job failed (see status)"; break; }
     return ICX_OK;
 }
 
@@ -925,7 +944,11 @@ int icx_exr_probe(const uint8_t* data, size_t size, int* w, int* h) {
     if (w) *w = 0;
     if (h) *h = 0;
     if (!data) return ICX_EXR_INVALID_ARGUMENT;
-    return exr_probe(data, size, w, h);
+    try {  // (nothing may cross the C ABI: a host allocation failure is an internal error)
+        return exr_probe(data, size, w, h);
+    } catch (const std::exception&) {
+        return ICX_EXR_INTERNAL_ERR;
+    }
 }
 
 int icx_exr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out, int* w, int* h) {
@@ -938,7 +961,13 @@ int icx_exr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out, 
     const RoctxRange range("icx_exr_decode");
     int ww = 0, hh = 0;
     std::string err;
-    const int rc = exr_decode(ctx->stream, data, size, out, &ww, &hh, err);
+    int rc;
+    try {  // (nothing may cross the C ABI: a host allocation failure is an internal error)
+        rc = exr_decode(ctx->stream, data, size, out, &ww, &hh, err);
+    } catch (const std::exception& e) {
+        err = std::string("icx_exr_decode: ") + e.what();
+        rc = ICX_EXR_INTERNAL_ERR;
+    }
     if (rc == ICX_EXR_INTERNAL_ERR) ctx->err = err.empty() ? "icx_exr_decode: HIP failure" : err;
     if (rc == ICX_EXR_SUCCESS) {
         if (w) *w = ww;

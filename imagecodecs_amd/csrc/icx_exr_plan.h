@@ -176,6 +176,9 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
     std::vector<uint64_t> offsets;
     int64_t ntx = 0, nty = 0;
     auto read_offsets = [&](int64_t n) -> bool {
+        // (a count the file cannot hold fails before any allocation: tinyexr's loop runs off the
+        // buffer with the same kExrInvalidData; a bad_alloc here would cross the C ABI)
+        if (n < 0 || n > (size - marker) / 8) return false;
         offsets.resize((size_t)n);
         for (int64_t k = 0; k < n; ++k) {
             if (marker + 8 >= size) return false;

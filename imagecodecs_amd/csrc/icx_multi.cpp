@@ -152,9 +152,17 @@ static int run_shard(icx_multi* m, Dev& d, const std::vector<int>& idx, const ui
     if (rc == ICX_OK) chk(hipMemcpyAsync(rec.data(), d_rec, sizeof(Record) * n, hipMemcpyDeviceToHost, st), "D2H records");
     if (rc == ICX_OK) chk(hipStreamSynchronize(st), "decode");
     for (int k = 0; k < n && rc == ICX_OK; ++k) {
-        const Record& r = rec[k];
+        Record& r = rec[k];
+        uint64_t bytes = (uint64_t)r.w * r.h * r.c;
+        if (r.status == ICX_OK && bytes > out_stride) {
+            // decoded into the 256-aligned staging stride, but the caller's buffer holds less:
+            // NanoJPEG's allocation failure, as icx_jpeg_batch_decode reports an image past its
+            // out_stride (never a truncated copy under an OK status)
+            r = Record{};
+            r.status = ICX_OUT_OF_MEM;
+            bytes = 0;
+        }
         std::memcpy(&records[idx[k]], &r, sizeof r);
-        const uint64_t bytes = (uint64_t)r.w * r.h * r.c;
         if (outs && outs[idx[k]] && r.status == ICX_OK && bytes)
             chk(hipMemcpyAsync(outs[idx[k]], d_out + (uint64_t)k * stride_al, std::min<uint64_t>(bytes, out_stride),
                                hipMemcpyDeviceToHost, st), "D2H pixels");

@@ -1561,9 +1561,12 @@ int png_encode_device_batch(int k, hipStream_t* sts, PngWs** wss, int n, int w, 
             ++phase[j];
         }
     }
+    // per-image failures are in status[] (-1); the call fails only when a stream itself did
+    bool stream_fail = false;
     for (int j = 0; j < k; ++j)
-        if (hipStreamSynchronize(sts[j]) != hipSuccess) fail = 1;
-    return fail ? -1 : 0;
+        if (hipStreamSynchronize(sts[j]) != hipSuccess) stream_fail = true;
+    (void)fail;
+    return stream_fail ? -1 : 0;
 }
 
 bool png_encode_gpu(hipStream_t st, int w, int h, int d, const uint8_t* src, std::vector<uint8_t>& out) {

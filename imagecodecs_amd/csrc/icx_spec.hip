@@ -55,6 +55,17 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     int last_round) {
     __shared__ int sh[1024];
     __shared__ int last[7];
+    if (round > 0) {  // a later round with nothing deferred (the usual case) plans nothing, at once
+        int any = 0;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) any |= spec[i].mode == 4;
+        if (!__syncthreads_or(any)) {
+            if (threadIdx.x == 0) {
+                totals[0] = totals[1] = totals[2] = 0;
+                tilepre[n] = wgpre[n] = wg2pre[n] = 0;
+            }
+            return;
+        }
+    }
     int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0, carry_a = 0;
     const int64_t pool_units = upool >> 12, wg_cap = lanes_cap / kLanes;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
@@ -138,7 +149,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             Desc& dd = desc[i];
             if (round == 0) dd.acbase = ((int64_t)carry_a + ea) * kGwChunk;
             dd.mapped = gwi;
-            // (cannot happen with the workspace's pool of 1.25 x coef_cap per slot: reported, not written)
+            // (cannot happen with the workspace's pool of 2.5 x coef_cap per slot: reported, not written)
             if (round == 0 && dd.acbase + region > pool_cap && dd.status == kPending) {
                 dd.status = kOutOfMem;
                 s.mode = 0;
@@ -1462,9 +1473,16 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     // left by the images before it is deferred to the next round instead of the sequential
     // kernel (a batch of 4:4:4 q100 photos at 1.3 B/px overflows a pool sized for 1 B/px). A round
     // with no deferred image costs only its launches (every kernel finds no work).
+    // Up to kMaxRounds rounds. Each round after the first finds the U pool empty, so it plans at
+    // least (pool - largest scan) bytes of the deferred images: with the pool at 2 B/px per slot
+    // (ws_per_slot) eight rounds hold any conforming group -- baseline JPEG's entropy data stays
+    // far below 8 B/px -- and only a scan larger than the whole pool is left to the sequential
+    // kernel. A round with nothing deferred is a handful of empty launches: k_spec_plan finds no
+    // deferred image and returns, every other kernel then finds no work, and rounds after the
+    // first launch 1/8 of the grid-stride workgroups (deferred images are the rare case).
     const int rounds = [] {  // (read per launch: tests vary it)
         const char* e = std::getenv("ICX_ROUNDS");
-        return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
+        return e ? std::max(1, std::min(kMaxRounds, std::atoi(e))) : kMaxRounds;
     }();
     for (int r = 0; r < rounds; ++r) launch_spec_round(ws, n, d_data, d_off, st, hook, r, r + 1 == rounds);
 }
@@ -1473,7 +1491,8 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
                        StageHook* hook, int round, int last) {
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
-    static const int g = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
+    static const int g0 = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
+    const int g = round == 0 ? g0 : std::max(64, g0 / 8);
     // Guess lanes start kGuessLead bits before their range (ICX_GUESS_LEAD overrides), so they are
     // resynchronised when they reach it and the count lanes splice at their first MCU start.
     // (per image: at most a quarter of a short lane, the lead is extra work on every lane)
@@ -1491,7 +1510,8 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
     B(kStUnstuff);
     hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
                        ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw, round, last);
-    hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
+    if (round == 0)  // (an image's tables serve every round)
+        hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
     hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
                        ws.totals, ws.tiles);
     hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,

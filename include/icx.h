@@ -215,8 +215,9 @@ void icx_png_encoder_destroy(icx_png_encoder* enc);
 int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, const uint8_t* d_src,
                           uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* hip_stream);
 /* n images (width x height x d each, at d_srcs[i] on the context's device) into d_out + i *
- * out_stride; out_sizes[i] = file size (or the bytes needed), status[i] = ICX_OK or ICX_OUT_OF_MEM
- * (the slot is too small). The batch form of png_encoder::saveToFile for device-resident images:
+ * out_stride; out_sizes[i] = file size (or the bytes needed), status[i] = ICX_OK, ICX_OUT_OF_MEM
+ * (the slot is too small) or ICX_INTERNAL_ERR (that image's own job failed: every other image still
+ * gets its status and size). Returns ICX_INTERNAL_ERR only when a stream failed. The batch form of png_encoder::saveToFile for device-resident images:
  * several images in flight (ICX_PNG_INFLIGHT, default 8), each on its own workspace and stream,
  * so some images' kernels run while the host reads back another's (colour statistics, stream
  * length, CRC). Returns when every file is written. */
