@@ -417,6 +417,10 @@ def main_png(args, wl, world, rank, local):
                 "kernel": PNG_STAGE_KERNEL.get(dom, dom), "launches_per_step": n,
                 "alg_bytes_per_launch": round(per_img), "avg_launch_ms": round(avg, 4),
                 "stage_ms": {k: round(v, 3) for k, v in stages.items()},
+                "stage_ms_note": ("per-image HIP events summed over the images; with the batch entry several "
+                                  "images run at once on their own streams, so the sums overlap and exceed the "
+                                  "wall time, and avg_launch_ms (hence achieved) understates the kernel's rate")
+                                 if not args.png_single else "per-image HIP events summed over the images",
                 "pipeline_frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
     out = {
         "metric": "megapixels/s PNG encode, 8192x8192 RGBA", "value": round(value, 2), "unit": "megapixels/s",

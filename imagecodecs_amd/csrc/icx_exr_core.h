@@ -267,6 +267,382 @@ ICX_HD bool exr_unrle(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) 
     return o == cap;
 }
 
+// ------------------------------------------------------------------------------------------ PIZ
+// DecompressPiz (:3228-3375), with TINYEXR_USE_PIZ 1 (the default, :126-128; codecs.cpp:27-29
+// leaves it on). The plan (icx_exr_plan.h) checks the chunk's range header (where DecompressPiz
+// returns false); the kernel runs the rest in phases around workgroup barriers:
+//   init   (all)  zero the code lengths and the direct table, reset the long-code lists, count
+//                 the range bitmap's values (maxValue, :3081-3094)
+//   unpack (one)  hufUncompress's header and hufUnpackEncTable (:2979-3016, :2466-2519)
+//   count  (all)  code lengths per length (hufCanonicalCodeTable's first loop, :2190-2192)
+//   build  (one)  the canonical codes in symbol order and hufBuildDecTable (:2181-2220, :2548-2632)
+//   decode (one)  hufDecode (:2804-2920) into the channel planes
+//   wavelet(all)  wav2Decode (:1995-2109), one level at a time, its 2x2 groups in parallel
+//   lut    (all)  reverseLutFromBitmap + applyLut + the line interleave (:3294-3372)
+// tinyexr ignores hufUncompress's result (:3317): a Huffman failure keeps what was decoded and
+// leaves the rest of the planes 0, and a failed table unpack leaves its raw code lengths for the
+// build (no canonical codes: every code is 0). Reads past the end of the file give 0 (tinyexr
+// reads the memory after its buffer; only damaged chunks get there).
+constexpr int kHufEncSize = 65537;
+constexpr int kHufDecBits = 14;
+constexpr int kHufDecSize = 1 << kHufDecBits;
+constexpr int kPizLens = 65540;  // code-length bytes (kHufEncSize, rounded to words)
+
+// A PIZ chunk's long-code lists (hufBuildDecTable's HufDec::p, kept in insertion order) in global
+// memory: per direct-table entry the first / last symbol, per symbol the next one and its code.
+struct PizWork {
+    int32_t head[kHufDecSize], tail[kHufDecSize];
+    int32_t next[kHufEncSize];
+    int32_t pad_;
+    uint64_t code[kHufEncSize];  // hcode (length | code << 6) of every listed symbol
+};
+
+// The file as the decoder's pointers see it: byte i, 0 past the end. One 16-byte aligned load
+// per 16 bytes read in order (the device file buffer holds 16 bytes of slack past the end).
+struct PizBytes {
+    const uint8_t* f;
+    int64_t n;
+    int64_t blk = -1;
+    uint32_t w[4] = {0, 0, 0, 0};
+    ICX_HD uint32_t operator()(int64_t i) {
+        if (i < 0 || i >= n) return 0u;
+        const int64_t b = i >> 4;
+        if (b != blk) {
+            const uint4 v = reinterpret_cast<const uint4*>(f)[b];
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            blk = b;
+        }
+        return (w[(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
+    }
+};
+
+struct PizHuf {
+    int32_t run;      // 0: hufUncompress returned before hufDecode (the planes stay 0)
+    int32_t canon;    // the table unpacked (canonical codes); 0: raw lengths, every code 0
+    int32_t im, iM;   // symbol range (iM: the run-length code)
+    int32_t nbits;    // hufDecode's input size in bits
+    int32_t pad_;
+    int64_t ptr;      // file offset of the codes
+};
+
+ICX_HD uint32_t piz_u32(PizBytes& F, int64_t p) { return F(p) | F(p + 1) << 8 | F(p + 2) << 16 | F(p + 3) << 24; }
+
+// hufUncompress's header + hufUnpackEncTable (one thread). lens[] must be zero (init phase).
+ICX_HD PizHuf piz_unpack(PizBytes& F, int64_t p0, int32_t ncomp, uint8_t* lens) {
+    PizHuf r{0, 0, 0, 0, 0, 0, 0};
+    if (ncomp == 0) return r;
+    const int32_t im = (int32_t)piz_u32(F, p0), iM = (int32_t)piz_u32(F, p0 + 4), nbits = (int32_t)piz_u32(F, p0 + 12);
+    if (im < 0 || im >= kHufEncSize || iM < 0 || iM >= kHufEncSize) return r;
+    const int64_t pc = p0 + 20;                 // *pcode
+    const int64_t ni = (int64_t)ncomp - 20;     // nCompressed - (ptr - compressed)
+    int64_t p = pc;
+    uint64_t c = 0;
+    int lc = 0;
+    auto bits = [&](int n) -> uint32_t {
+        while (lc < n) {
+            c = (c << 8) | F(p++);
+            lc += 8;
+        }
+        lc -= n;
+        return (uint32_t)(c >> lc) & ((1u << n) - 1u);
+    };
+    bool ok = true;
+    for (int s = im; s <= iM; ++s) {
+        if (p - pc >= ni) { ok = false; break; }
+        const uint32_t l = bits(6);
+        lens[s] = (uint8_t)l;
+        if (l == 63) {  // LONG_ZEROCODE_RUN
+            if (p - pc > ni) { ok = false; break; }
+            const int zr = (int)bits(8) + 6;  // + SHORTEST_LONG_RUN
+            if (s + zr > iM + 1) { ok = false; break; }
+            for (int k = 0; k < zr; ++k) lens[s++] = 0;
+            --s;
+        } else if (l >= 59) {  // SHORT_ZEROCODE_RUN
+            const int zr = (int)l - 59 + 2;
+            if (s + zr > iM + 1) { ok = false; break; }
+            for (int k = 0; k < zr; ++k) lens[s++] = 0;
+            --s;
+        }
+    }
+    const int64_t ptr = ok ? p : pc;
+    // nBits > 8 * (nCompressed - (ptr - compressed)): a ptrdiff_t (64-bit) product
+    if ((int64_t)nbits > 8 * ((int64_t)ncomp - (ptr - p0))) return r;
+    r.run = 1;
+    r.canon = ok;
+    r.im = im;
+    r.iM = iM;
+    r.nbits = nbits;
+    r.ptr = ptr;
+    return r;
+}
+
+// hufCanonicalCodeTable's first code per length, from the counts n[0..58] (in place).
+ICX_HD void piz_first_codes(uint64_t* n) {
+    uint64_t c = 0;
+    for (int i = 58; i > 0; --i) {
+        const uint64_t nc = (c + n[i]) >> 1;
+        n[i] = c;
+        c = nc;
+    }
+}
+
+// hufBuildDecTable over the canonical codes (one thread), stopping at its first failure as
+// tinyexr does (the failure itself is ignored). dec[] zero and w.head / w.tail -1 on entry;
+// nextc[l] = the first code of length l (piz_first_codes).
+ICX_HD void piz_build(const PizHuf& H, const uint8_t* lens, uint64_t* nextc, uint32_t* dec, PizWork& w) {
+    for (int s = H.im; s <= H.iM; ++s) {
+        const uint32_t l = lens[s];
+        uint64_t h = l;
+        if (H.canon && l > 0) h = (uint64_t)l | (nextc[l]++ << 6);
+        const int64_t cc = (int64_t)h >> 6;
+        const int ln = (int)(h & 63);
+        if ((cc >> ln) != 0) return;  // not an l-bit code
+        if (ln > kHufDecBits) {       // long code: a secondary entry
+            const int64_t e = cc >> (ln - kHufDecBits);
+            if (dec[e] >> 24) return;  // a short code is there
+            dec[e] += 1;               // (the list's length)
+            w.code[s] = h;
+            if (w.tail[e] < 0) w.head[e] = s;
+            else w.next[w.tail[e]] = s;
+            w.tail[e] = s;
+        } else if (ln) {
+            const int64_t e0 = cc << (kHufDecBits - ln);
+            for (int64_t k = 0; k < ((int64_t)1 << (kHufDecBits - ln)); ++k) {
+                if (dec[e0 + k] != 0) return;  // a short or a long code is there
+                dec[e0 + k] = (uint32_t)ln << 24 | (uint32_t)s;
+            }
+        }
+    }
+}
+
+// hufDecode (one thread) into out[0..no); returns the ushorts written (the rest stays 0).
+ICX_HD int64_t piz_decode(PizBytes& F, const PizHuf& H, const uint32_t* dec, const uint8_t* lens, const PizWork& w,
+                          uint16_t* out, int64_t no) {
+    uint64_t c = 0;
+    int lc = 0;
+    int64_t in = H.ptr;
+    const int64_t ie = H.ptr + ((int64_t)H.nbits + 7) / 8;  // (C division: toward zero)
+    const int rlc = H.iM;
+    int64_t o = 0;
+    uint32_t last = 0;
+    auto getcode = [&](int po) -> bool {
+        if (po == rlc) {
+            if (lc < 8) {
+                if (in >= ie) return false;
+                c = (c << 8) | F(in++);
+                lc += 8;
+            }
+            lc -= 8;
+            const int64_t cs = (int64_t)(((int64_t)c >> lc) & 0xFF);
+            if (o + cs > no || o < 1) return false;
+            for (int64_t k = 0; k < cs; ++k) out[o++] = (uint16_t)last;
+        } else if (o < no) {
+            out[o++] = (uint16_t)po;
+            last = (uint32_t)po;
+        } else {
+            return false;
+        }
+        return true;
+    };
+    while (in < ie) {
+        c = (c << 8) | F(in++);
+        lc += 8;
+        while (lc >= kHufDecBits) {
+            const uint32_t e = dec[((int64_t)c >> (lc - kHufDecBits)) & (kHufDecSize - 1)];
+            if (e >> 24) {
+                lc -= (int)(e >> 24);
+                if (!getcode((int)(e & 0xFFFFFF))) return o;
+            } else {
+                if (e == 0) return o;  // no code
+                int32_t sym = w.head[((int64_t)c >> (lc - kHufDecBits)) & (kHufDecSize - 1)];
+                uint32_t j = 0;
+                for (; j < e; ++j, sym = w.next[sym]) {
+                    const uint64_t h = w.code[sym];
+                    const int l = (int)(h & 63);
+                    while (lc < l && in < ie) {
+                        c = (c << 8) | F(in++);
+                        lc += 8;
+                    }
+                    if (lc >= l && ((int64_t)h >> 6) == (((int64_t)c >> (lc - l)) & (int64_t)((1ull << l) - 1))) {
+                        lc -= l;
+                        if (!getcode(sym)) return o;
+                        break;
+                    }
+                }
+                if (j == e) return o;  // not found
+            }
+        }
+    }
+    const int i = (8 - H.nbits) & 7;
+    c = (uint64_t)((int64_t)c >> i);
+    lc -= i;
+    while (lc > 0) {
+        const uint32_t e = dec[(c << (kHufDecBits - lc)) & (kHufDecSize - 1)];
+        if (!(e >> 24)) return o;
+        lc -= (int)(e >> 24);
+        if (!getcode((int)(e & 0xFFFFFF))) return o;
+    }
+    (void)lens;
+    return o;
+}
+
+// wav2Decode's levels: the largest power of two p2 <= min(nx, ny); then (p, p2) = (p2 / 2, p2),
+// halving down to p = 1.
+ICX_HD int piz_top_p2(int nx, int ny) {
+    const int n = nx < ny ? nx : ny;
+    int p = 1;
+    while (p <= n) p <<= 1;
+    return p >> 1;
+}
+
+ICX_HD void piz_wdec(bool w14, uint32_t l, uint32_t h, uint32_t& a, uint32_t& b) {
+    if (w14) {  // wdec14 (:1831-1844)
+        const int32_t ls = (int16_t)l, hs = (int16_t)h;
+        const int32_t ai = ls + (hs & 1) + (hs >> 1);
+        a = (uint32_t)ai & 0xFFFFu;
+        b = (uint32_t)(ai - hs) & 0xFFFFu;
+    } else {  // wdec16 (:1871-1879)
+        const int32_t m = (int32_t)l, d = (int32_t)h;
+        const int32_t bb = (m - (d >> 1)) & 0xFFFF;
+        a = (uint32_t)((d + bb - 32768) & 0xFFFF);
+        b = (uint32_t)bb;
+    }
+}
+
+// Items of one wavelet level: the J x K 2x2 groups, then the odd column's J pairs, then the odd
+// line's K pairs (each touches its own samples).
+ICX_HD int64_t piz_level_items(int nx, int ny, int p, int p2) {
+    const int64_t K = nx / p2, J = ny / p2;
+    return J * K + ((nx & p) ? J : 0) + ((ny & p) ? K : 0);
+}
+
+ICX_HD void piz_level_item(uint16_t* in, int nx, int ox, int ny, int oy, bool w14, int p, int p2, int64_t it) {
+    const int64_t K = nx / p2, J = ny / p2;
+    const int64_t ox1 = (int64_t)ox * p, oy1 = (int64_t)oy * p, ox2 = (int64_t)ox * p2, oy2 = (int64_t)oy * p2;
+    uint32_t i00, i01, i10, i11, a, b;
+    if (it < J * K) {
+        uint16_t* px = in + (it / K) * oy2 + (it % K) * ox2;
+        uint16_t *p01 = px + ox1, *p10 = px + oy1, *p11 = p10 + ox1;
+        piz_wdec(w14, *px, *p10, i00, i10);
+        piz_wdec(w14, *p01, *p11, i01, i11);
+        piz_wdec(w14, i00, i01, a, b);
+        *px = (uint16_t)a;
+        *p01 = (uint16_t)b;
+        piz_wdec(w14, i10, i11, a, b);
+        *p10 = (uint16_t)a;
+        *p11 = (uint16_t)b;
+        return;
+    }
+    it -= J * K;
+    if ((nx & p) && it < J) {  // odd column
+        uint16_t* px = in + it * oy2 + K * ox2;
+        piz_wdec(w14, *px, px[oy1], a, b);
+        px[oy1] = (uint16_t)b;
+        *px = (uint16_t)a;
+        return;
+    }
+    if (nx & p) it -= J;
+    uint16_t* px = in + J * oy2 + it * ox2;  // odd line
+    piz_wdec(w14, *px, px[ox1], a, b);
+    px[ox1] = (uint16_t)b;
+    *px = (uint16_t)a;
+}
+
+// The workgroup phases (thread t of T; tests/emu runs them with t = 0 .. T-1 in turn).
+ICX_HD void piz_inc(uint32_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicAdd(p, 1u);
+#else
+    ++*p;
+#endif
+}
+
+// init: code lengths and direct table zero, long-code lists empty, planes zero (tinyexr's
+// value-initialised tmpBuffer), per-length counts zero.
+ICX_HD void piz_init(int t, int T, uint8_t* lens, uint32_t* dec, PizWork& w, uint16_t* planes, int64_t nus, uint32_t* ncnt) {
+    for (int i = t; i < kPizLens / 4; i += T) reinterpret_cast<uint32_t*>(lens)[i] = 0;
+    for (int i = t; i < kHufDecSize; i += T) {
+        dec[i] = 0;
+        w.head[i] = -1;
+        w.tail[i] = -1;
+    }
+    for (int64_t i = t; i < nus; i += T) planes[i] = 0;
+    for (int i = t; i < 59; i += T) ncnt[i] = 0;
+}
+
+// Bit k of the chunk's range bitmap (bytes minNonZero .. maxNonZero from the file, 0 elsewhere;
+// value 0 is always in the LUT: reverseLutFromBitmap's i == 0).
+ICX_HD uint32_t piz_bitmap_byte(const uint8_t* file, int64_t bitmap, int32_t mnmx, int b) {
+    const int mn = mnmx & 0xFFFF, mx = (mnmx >> 16) & 0xFFFF;
+    uint32_t v = (b >= mn && b <= mx) ? file[bitmap + (b - mn)] : 0u;
+    return b == 0 ? (v | 1u) : v;
+}
+
+// Values of the LUT in thread t's range [256 t, 256 t + 256) (T = 256).
+ICX_HD uint32_t piz_lut_count(const uint8_t* file, int64_t bitmap, int32_t mnmx, int t) {
+    uint32_t n = 0;
+    for (int b = 32 * t; b < 32 * t + 32; ++b) n += (uint32_t)__builtin_popcount(piz_bitmap_byte(file, bitmap, mnmx, b));
+    return n;
+}
+
+// Thread t's LUT entries from `base` on (its range's values in order), and the zero tail past
+// the last value (total = values in the LUT).
+ICX_HD void piz_lut_fill(const uint8_t* file, int64_t bitmap, int32_t mnmx, int t, uint32_t base, uint16_t* lut) {
+    for (int b = 32 * t; b < 32 * t + 32; ++b) {
+        const uint32_t v = piz_bitmap_byte(file, bitmap, mnmx, b);
+        for (int k = 0; k < 8; ++k)
+            if (v >> k & 1u) lut[base++] = (uint16_t)(8 * b + k);
+    }
+}
+ICX_HD void piz_lut_tail(int t, int T, uint32_t total, uint16_t* lut) {
+    for (uint32_t k = total + (uint32_t)t; k < 65536u; k += (uint32_t)T) lut[k] = 0;
+}
+
+// count: code lengths per length (lengths 1..58; hufCanonicalCodeTable's counts).
+ICX_HD void piz_count(int t, int T, const uint8_t* lens, uint32_t* ncnt) {
+    for (int i = t; i < kHufEncSize; i += T) {
+        const uint32_t l = lens[i];
+        if (l > 0 && l <= 58) piz_inc(&ncnt[l]);
+    }
+}
+
+// One wavelet level (p, p2) over every channel plane: channel k has ctype[k] (HALF: one ushort
+// per sample, else two, each its own plane with stride 2), planes one after the other
+// (DecompressPiz's channelData, :3323-3352).
+ICX_HD void piz_wavelet_level(int t, int T, uint16_t* planes, const int32_t* ctype, int nch, int nx, int ny, bool w14,
+                              int p, int p2) {
+    const int64_t per = piz_level_items(nx, ny, p, p2);
+    int64_t st = 0;
+    for (int k = 0; k < nch; ++k) {
+        const int sz = ctype[k] == 1 ? 1 : 2;
+        for (int j = 0; j < sz; ++j)
+            for (int64_t it = t; it < per; it += T) piz_level_item(planes + st + j, nx, sz, ny, nx * sz, w14, p, p2, it);
+        st += (int64_t)nx * ny * sz;
+    }
+}
+
+// applyLut + the line interleave (:3358-3372): ushort i of the pixel data (line v, channel k,
+// sample u of its nx * size) = lut[the plane's ushort].
+ICX_HD void piz_interleave(int t, int T, const uint16_t* planes, const uint16_t* lut, const int32_t* ctype, int nch, int nx,
+                           int ny, uint16_t* out) {
+    int64_t line = 0;
+    for (int k = 0; k < nch; ++k) line += (int64_t)nx * (ctype[k] == 1 ? 1 : 2);
+    const int64_t n = line * ny;
+    for (int64_t i = t; i < n; i += T) {
+        const int64_t v = i / line;
+        int64_t r = i - v * line, st = 0;
+        for (int k = 0; k < nch; ++k) {
+            const int64_t m = (int64_t)nx * (ctype[k] == 1 ? 1 : 2);
+            if (r < m) {
+                out[i] = lut[planes[st + v * m + r]];
+                break;
+            }
+            r -= m;
+            st += m * ny;
+        }
+    }
+}
+
 // tinyexr's half_to_float (:966-987), bit for bit.
 ICX_HD uint32_t exr_half_bits(uint32_t h) {
     uint32_t o = (h & 0x7fffu) << 13;

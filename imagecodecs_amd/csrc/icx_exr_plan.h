@@ -30,17 +30,23 @@ uint64_t rd64(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 struct ExrChunk {
     int64_t src;        // file offset of the chunk's pixel data
     int64_t len;        // its size (data_len)
-    int64_t scratch;    // byte offset of the decompressed bytes in the scratch (mode 1)
+    int64_t scratch;    // byte offset of the decompressed bytes in the scratch (modes 1-3)
     int64_t out_len;    // width * lines * pixel_data_size
     int64_t produced;   // bytes the decompressor produced (device)
-    int32_t mode;       // 0 pixel bytes are the file's (NONE, or stored raw), 1 ZIP, 2 RLE
+    int32_t mode;       // 0 pixel bytes are the file's (NONE, or stored raw), 1 ZIP, 2 RLE, 3 PIZ
     int32_t width;      // samples per line of this chunk
     int32_t lines;      // lines it holds
+    int32_t piz_len;    // PIZ: the Huffman data's length field
+    int64_t piz_bitmap; // PIZ: file offset of the range bitmap's first byte (byte minNonZero)
+    int64_t piz_huf;    // PIZ: file offset of the Huffman data
+    int64_t piz_work;   // PIZ: scratch offset of the channel planes (out_len), then its PizWork
+    int32_t piz_mnmx;   // PIZ: minNonZero | maxNonZero << 16
     int32_t pad_;
 };
 
 struct ExrPlan {
     int w = 0, h = 0, nch = 0, pds = 0, comp = 0, tiled = 0, tx = 0, ty = 0, ntx = 0, line_order = 0;
+    int levels = 1;  // tiled: levels decoded (mip- / rip-mapped files: all of them; level 0 is output)
     int src[4] = {-1, -1, -1, -1};  // channel of R, G, B, A (-1: A = 1.0)
     std::vector<int32_t> type, offs;
     std::vector<ExrChunk> chunks;
@@ -48,6 +54,80 @@ struct ExrPlan {
     std::vector<int32_t> tile_h;  // tiled: the lines each chunk decoded (DecodeTiledPixelData's height)
     int64_t scratch = 0;
 };
+
+// Tiled levels (PrecalculateTileInfo / InitTileOffsets / LevelSize, tinyexr.h:4950-4979,
+// :5582-5802): per level in offset-table order its (lx, ly) and tiles across / down.
+struct ExrLevel {
+    int lx, ly;
+    int64_t nx, ny;
+};
+inline int exr_level_size(int64_t top, int level, int rounding) {  // LevelSize (:4967-4979)
+    const int64_t b = (int64_t)1 << level;
+    int64_t ls = top / b;
+    if (rounding == 1 && ls * b < top) ls += 1;
+    return (int)std::max<int64_t>(ls, 1);
+}
+inline int exr_log2(int64_t x, int rounding) {  // FloorLog2 / CeilLog2 (:5582-5614)
+    int y = 0, r = 0;
+    while (x > 1) {
+        if (x & 1) r = 1;
+        ++y;
+        x >>= 1;
+    }
+    return y + (rounding == 1 ? r : 0);
+}
+inline bool exr_levels(int64_t W, int64_t H, int mode, int rounding, int64_t tx, int64_t ty, std::vector<ExrLevel>& L) {
+    int nxl, nyl;
+    if (mode == 0) nxl = nyl = 1;
+    else if (mode == 1) nxl = nyl = exr_log2(std::max(W, H), rounding) + 1;
+    else if (mode == 2) { nxl = exr_log2(W, rounding) + 1; nyl = exr_log2(H, rounding) + 1; }
+    else return false;  // CalculateNumXLevels: -1
+    std::vector<int64_t> ntx(nxl), nty(nyl);
+    for (int i = 0; i < nxl; ++i) {  // CalculateNumTiles (:5692-5706)
+        const int64_t l = exr_level_size(W, i, rounding);
+        if (l > (int64_t)kIntMax - tx + 1) return false;
+        ntx[i] = (l + tx - 1) / tx;
+    }
+    for (int i = 0; i < nyl; ++i) {
+        const int64_t l = exr_level_size(H, i, rounding);
+        if (l > (int64_t)kIntMax - ty + 1) return false;
+        nty[i] = (l + ty - 1) / ty;
+    }
+    L.clear();
+    if (mode != 2) {
+        for (int l = 0; l < nxl; ++l) L.push_back({l, l, ntx[l], nty[l]});
+    } else {
+        for (int ly = 0; ly < nyl; ++ly)
+            for (int lx = 0; lx < nxl; ++lx) L.push_back({lx, ly, ntx[lx], nty[ly]});
+    }
+    return true;
+}
+
+// DecompressPiz's range header (:3232-3314): where it returns false the chunk fails (-1);
+// otherwise its fields go to the chunk. inLen == tmpBufSize (stored raw) is mode 0 before this.
+inline bool exr_piz_head(const uint8_t* buf, int64_t size, ExrChunk& c) {
+    const int64_t in_len = c.len, src = c.src;
+    if (in_len < 4) return false;
+    const uint32_t mn = buf[src] | buf[src + 1] << 8, mx = buf[src + 2] | buf[src + 3] << 8;
+    if (mx >= 8192) return false;  // BITMAP_SIZE
+    int64_t rd = 4;
+    if (mn <= mx) {
+        if ((int64_t)(mx - mn + 1) + rd > in_len) return false;
+        rd += mx - mn + 1;
+    } else if (!(mn == 8191 && mx == 0)) {
+        return false;
+    }
+    if (rd + 4 > in_len) return false;
+    const int32_t length = rd32(buf + src + rd);
+    rd += 4;
+    if ((uint64_t)(rd + (int64_t)length) > (uint64_t)in_len) return false;  // size_t((ptr - inPtr) + length)
+    c.piz_mnmx = (int32_t)(mn | mx << 16);
+    c.piz_bitmap = src + 4;
+    c.piz_huf = src + rd;
+    c.piz_len = length;
+    (void)size;
+    return true;
+}
 
 // ParseEXRVersionFromMemory + ParseEXRHeader + ConvertHeader + DecodeEXRImage's table reading +
 // DecodeChunk's per-chunk checks (tinyexr.h:8927-8982, :4441-4940, :6005-6199, :5163-5542).
@@ -61,7 +141,7 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
     std::vector<Ch> chans;
     int32_t dw[4] = {0, 0, 0, 0}, chunk_count = 0, comp = -1, line_order = 0;
     int64_t tile_x = -1, tile_y = -1;
-    int tile_mode = -1, tiled = 0;
+    int tile_mode = -1, tile_round = -1, tiled = 0;
     std::string type_attr;
     unsigned have = 0;  // required attributes seen
     enum { kComp = 1, kChans = 2, kDW = 4, kDisp = 8, kLO = 16, kPAR = 32, kSWC = 64, kSWW = 128, kName = 256, kType = 512 };
@@ -103,6 +183,7 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
             tile_x = xs;
             tile_y = ys;
             tile_mode = data[8] & 3;
+            tile_round = (data[8] >> 4) & 1;
             tiled = 1;
         } else if (name == "compression") {
             if (data[0] > 4) { ret = kExrUnsupportedFormat; break; }  // unknown / ZFP not built (:4568-4601)
@@ -164,17 +245,16 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
     const int64_t header_len = (size - 8) - rem;
     // LoadEXRFromMemory / DecodeEXRImage
     if (multipart || non_image) return kExrUnsupportedFeature;
-    if (comp == 4) return kExrUnsupportedFormat;  // PIZ: not in this build (TINYEXR_USE_PIZ 0)
     if (size <= 8) return kExrInvalidArgument;
     int64_t marker = header_len + 8;
-    const int nsb = comp == 3 ? 16 : 1;
+    const int nsb = comp == 3 ? 16 : comp == 4 ? 32 : 1;
     if (dw[2] < dw[0] || (int64_t)dw[2] - dw[0] == kIntMax) return kExrInvalidData;
     const int64_t W = (int64_t)dw[2] - dw[0] + 1;
     if (dw[3] < dw[1] || (int64_t)dw[3] - dw[1] == kIntMax) return kExrInvalidData;
     const int64_t H = (int64_t)dw[3] - dw[1] + 1;
     if (W > kThresh || H > kThresh) return kExrInvalidData;
     std::vector<uint64_t> offsets;
-    int64_t ntx = 0, nty = 0;
+    std::vector<ExrLevel> levels;
     auto read_offsets = [&](int64_t n) -> bool {
         // (a count the file cannot hold fails before any allocation: tinyexr's loop runs off the
         // buffer with the same kExrInvalidData; a bad_alloc here would cross the C ABI)
@@ -191,14 +271,36 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
     };
     if (tiled) {
         if (tile_x > kThresh || tile_y > kThresh) return kExrInvalidData;
-        if (tile_mode != 0) return kExrUnsupportedFeature;
         if (tile_x == 0 || tile_y == 0) return kExrInvalidData;  // (tinyexr divides by it)
-        ntx = (W + tile_x - 1) / tile_x;
-        nty = (H + tile_y - 1) / tile_y;
-        if (chunk_count > 0 && chunk_count != ntx * nty) return kExrInvalidData;
-        if (!read_offsets(ntx * nty)) return kExrInvalidData;
-        for (uint64_t o : offsets)
-            if (o == 0) return kExrInvalidData;  // ReconstructTileOffsets: out of scope
+        if (!exr_levels(W, H, tile_mode, tile_round, tile_x, tile_y, levels)) return kExrInvalidData;
+        int64_t nblocks = 0;
+        for (const ExrLevel& l : levels) nblocks += l.nx * l.ny;
+        if (chunk_count > 0 && chunk_count != nblocks) return kExrInvalidData;
+        if (!read_offsets(nblocks)) return kExrInvalidData;
+        if (std::find(offsets.begin(), offsets.end(), 0ull) != offsets.end()) {
+            // ReconstructTileOffsets (:5867-5974), single part, not deep: each chunk after the
+            // table goes to the place its own header names (places none names keep the table's)
+            const int nxl = tile_mode == 2 ? levels.back().lx + 1 : (int)levels.size();
+            const int nyl = tile_mode == 2 ? levels.back().ly + 1 : (int)levels.size();
+            std::vector<int64_t> lbase(levels.size() + 1, 0);
+            for (size_t l = 0; l < levels.size(); ++l) lbase[l + 1] = lbase[l] + levels[l].nx * levels[l].ny;
+            int64_t mk = marker;
+            for (int64_t k = 0; k < nblocks; ++k) {
+                const int64_t here = mk;
+                if (mk < 0 || mk + 16 >= size) return kExrInvalidData;
+                const int32_t tx_ = rd32(buf + mk), ty_ = rd32(buf + mk + 4), lx = rd32(buf + mk + 8), ly = rd32(buf + mk + 12);
+                mk += 16;
+                if (mk + 4 >= size) return kExrInvalidData;
+                mk += 4 + (int64_t)rd32(buf + mk);
+                if (lx < 0 || ly < 0 || tx_ < 0 || ty_ < 0) return kExrInvalidData;  // isValidTile (:5814-5865)
+                if (tile_mode == 0 && (lx != 0 || ly != 0)) return kExrInvalidData;
+                if (tile_mode != 0 && (lx >= nxl || ly >= nyl)) return kExrInvalidData;
+                const int64_t li = tile_mode == 0 ? 0 : tile_mode == 1 ? lx : (int64_t)lx + (int64_t)ly * nxl;  // LevelIndex
+                if (li >= (int64_t)levels.size()) return kExrInvalidData;
+                if (ty_ >= levels[li].ny || tx_ >= levels[li].nx) return kExrInvalidData;
+                offsets[(size_t)(lbase[li] + ty_ * levels[li].nx + tx_)] = (uint64_t)here;
+            }
+        }
     } else {
         const int64_t nb = chunk_count > 0 ? chunk_count : (H + nsb - 1) / nsb;
         if (!read_offsets(nb)) return kExrInvalidData;
@@ -239,42 +341,56 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
         c.width = width;
         c.lines = lines;
         c.out_len = (int64_t)width * lines * pds;
-        c.mode = comp == 0 ? 0 : (len == c.out_len ? 0 : (comp == 1 ? 2 : 1));
+        c.mode = comp == 0 ? 0 : (len == c.out_len ? 0 : (comp == 1 ? 2 : comp == 4 ? 3 : 1));
         if (comp == 0 && len < c.out_len) return -1;  // "Insufficient data size" (:4192-4196)
-        if (comp != 0 && c.out_len == 0) return -1;   // dstLen == 0 (:3801, :3943)
+        if (comp != 0 && c.out_len == 0) return -1;   // dstLen == 0 (:3801, :3943); PIZ: #90 (:3643)
+        if (c.mode == 3 && !exr_piz_head(buf, size, c)) return -1;
         if (c.mode != 0) {
             c.scratch = P.scratch;
             P.scratch += (c.out_len + 15) / 16 * 16;
+        }
+        if (c.mode == 3) {  // the channel planes, then the long-code lists
+            c.piz_work = P.scratch;
+            P.scratch += (c.out_len + 15) / 16 * 16 + (int64_t)(sizeof(PizWork) + 15) / 16 * 16;
         }
         P.chunks.push_back(c);
         return (int)P.chunks.size() - 1;
     };
     if (tiled) {
+        const int64_t ntx = levels[0].nx, nty = levels[0].ny;
         P.tx = (int)tile_x;
         P.ty = (int)tile_y;
         P.ntx = (int)ntx;
+        P.levels = (int)levels.size();
         P.map.assign((size_t)(ntx * nty), make_int2(-1, 0));
         P.tile_h.clear();
         std::vector<int2> coords;
-        for (size_t k = 0; k < offsets.size(); ++k) {  // DecodeTiledLevel (:5047-5133)
-            const int64_t o = (int64_t)offsets[k];
-            if (o + 20 > size) return kExrInvalidData;
-            const int64_t dsz = size - (o + 20);
-            const int32_t cx = rd32(buf + o), cy = rd32(buf + o + 4), lx = rd32(buf + o + 8), ly = rd32(buf + o + 12);
-            if (lx != 0 || ly != 0) return kExrInvalidData;
-            const int32_t dlen = rd32(buf + o + 16);
-            if (dlen < 2 || (int64_t)dlen > dsz) return kExrInvalidData;
-            // DecodeTiledPixelData (:4283-4319), in tinyexr's int arithmetic
-            if ((int64_t)tile_x * cx > W || (int64_t)tile_y * cy > H) return kExrInvalidData;
-            const int tw = ((int64_t)(cx + 1) * tile_x >= W) ? (int)(W - (int64_t)cx * tile_x) : (int)tile_x;
-            const int th = ((int64_t)(cy + 1) * tile_y >= H) ? (int)(H - (int64_t)cy * tile_y) : (int)tile_y;
-            const int ci = add_chunk(o + 20, dlen, tw, th);
-            if (ci < 0) return kExrInvalidData;
-            P.tile_h.push_back(th);
-            coords.push_back(make_int2(cx, cy));
+        // DecodeChunk's level loops (:5282-5354): every level's tiles are decoded and checked
+        // (DecodeTiledLevel :4981-5161); the RGBA output takes level 0, the first ntx * nty
+        // chunks (:6789-6828)
+        size_t k = 0;
+        for (const ExrLevel& L : levels) {
+            const int64_t lw = exr_level_size(W, L.lx, tile_round), lh = exr_level_size(H, L.ly, tile_round);
+            for (int64_t t = 0; t < L.nx * L.ny; ++t, ++k) {
+                const int64_t o = (int64_t)offsets[k];
+                if (o + 20 > size) return kExrInvalidData;
+                const int64_t dsz = size - (o + 20);
+                const int32_t cx = rd32(buf + o), cy = rd32(buf + o + 4), lx = rd32(buf + o + 8), ly = rd32(buf + o + 12);
+                if (lx != L.lx || ly != L.ly) return kExrInvalidData;
+                const int32_t dlen = rd32(buf + o + 16);
+                if (dlen < 2 || (int64_t)dlen > dsz) return kExrInvalidData;
+                // DecodeTiledPixelData (:4283-4319), in the level's size, tinyexr's int arithmetic
+                if ((int64_t)tile_x * cx > lw || (int64_t)tile_y * cy > lh) return kExrInvalidData;
+                const int tw = ((int64_t)(cx + 1) * tile_x >= lw) ? (int)(lw - (int64_t)cx * tile_x) : (int)tile_x;
+                const int th = ((int64_t)(cy + 1) * tile_y >= lh) ? (int)(lh - (int64_t)cy * tile_y) : (int)tile_y;
+                const int ci = add_chunk(o + 20, dlen, tw, th);
+                if (ci < 0) return kExrInvalidData;
+                P.tile_h.push_back(th);
+                if (k < (size_t)(ntx * nty)) coords.push_back(make_int2(cx, cy));
+            }
         }
-        // the RGBA loop (:6789-6828) visits tiles in order: the last tile at a position wins;
-        // negative origins are past the image as size_t
+        // the RGBA loop (:6789-6828) visits level 0's tiles in order: the last tile at a position
+        // wins; negative origins are past the image as size_t
         for (size_t k = 0; k < coords.size(); ++k) {
             const int64_t cx = coords[k].x, cy = coords[k].y;
             if (cx < 0 || cy < 0 || cx >= ntx || cy >= nty) continue;
@@ -329,6 +445,7 @@ ICX_HD uint32_t exr_byte(const uint8_t* file, const uint8_t* scratch, const ExrC
     const int64_t m = c.produced;
     if (p >= m) return 0;
     const uint8_t* t = scratch + c.scratch;
+    if (c.mode == 3) return t[p];  // PIZ: the pixel bytes in order (no predictor or reorder)
     return (p & 1) ? t[(m + 1) / 2 + (p >> 1)] : t[p >> 1];
 }
 

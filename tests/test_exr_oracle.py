@@ -2,7 +2,8 @@
 the fixtures against the oracle (oracle/exr_oracle.py), and the GPU path's own host plan,
 decompressors and per-pixel gather (icx_exr_plan.h / icx_exr_core.h, run on the CPU by
 tests/emu/exr_emu.cpp) against the oracle, bit for bit. PARITY UNPINNED (no EXR library here,
-tinyexr.h needs miniz): see the oracle's header."""
+tinyexr.h needs miniz): see the oracle's header. PIZ is in scope: the reference builds tinyexr
+with TINYEXR_USE_PIZ 1 (tinyexr.h:126-128, codecs.cpp:27-29)."""
 import ctypes as C
 import hashlib
 import json
@@ -155,6 +156,43 @@ def test_random_damage_same_result(seed):
             assert np.array_equal(eimg, oimg.view(np.uint32)), (seed, k)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_piz_and_levels_damage_same_result(seed):
+    """Random damage to PIZ chunks (range header, Huffman table and codes -- tinyexr ignores the
+    Huffman decoder's failures and keeps what it decoded) and to mip- / rip-mapped files: the GPU
+    path's logic returns the oracle's code and bits."""
+    rng = np.random.default_rng(200 + seed)
+    names = [n for n in sorted(MAN) if MAN[n]["code"] == 0 and ("piz" in n or n.startswith(("mip", "rip")))
+             and "w16" not in n and "longcodes" not in n]
+    for k in range(40):
+        data = bytearray(open(os.path.join(EXR, names[int(rng.integers(0, len(names)))]), "rb").read())
+        lo = len(data) // 3 if k % 2 else 0  # (half of the draws hit the chunk data only)
+        for _ in range(1 + k % 4):
+            data[int(rng.integers(lo, len(data)))] ^= int(rng.integers(1, 256))
+        data = bytes(data)
+        oc, ow, oh, oimg = O.decode(data)
+        ec, ew, eh, eimg = emu_decode(data)
+        assert (ec, ew, eh) == (oc, ow, oh), (seed, k)
+        if oc == 0:
+            assert np.array_equal(eimg, oimg.view(np.uint32)), (seed, k)
+
+
+def test_piz_wavelet_inverse():
+    """wav2Decode (oracle) inverts wav2Encode (writer) for 14- and 16-bit data, odd sizes and
+    strides 1 and 2 (the two halves of a FLOAT / UINT sample)."""
+    rng = np.random.default_rng(9)
+    for nx, ny in ((1, 1), (7, 3), (32, 32), (33, 17), (64, 5), (5, 64)):
+        for sz in (1, 2):
+            for top in (1 << 14, 1 << 16):
+                a = rng.integers(0, top, nx * ny * sz, dtype=np.int64).astype(np.uint16)
+                b = a.copy()
+                for j in range(sz):
+                    W.wav2_encode(b, j, nx, sz, ny, nx * sz, top - 1)
+                for j in range(sz):
+                    O.wav2_decode(b, j, nx, sz, ny, nx * sz, top - 1)
+                assert np.array_equal(a, b), (nx, ny, sz, top)
+
+
 def test_writer_roundtrip_every_layout():
     """tools/exrwrite.py -> oracle returns the written samples (HALF via float32, UINT bits,
     DECREASING_Y scanlines flipped as tinyexr places them)."""
@@ -164,9 +202,10 @@ def test_writer_roundtrip_every_layout():
     B = rng.standard_normal((h, w)).astype(np.float32)
     A = rng.integers(0, 2**32, (h, w), dtype=np.uint32)
     exp = np.stack([R.astype(np.float32), G.astype(np.float32), B, A.view(np.float32)], -1).view(np.uint32)
-    for comp in (W.NONE, W.RLE, W.ZIPS, W.ZIP):
-        for tiles in (None, (8, 4), (32, 32)):
-            data = W.write_exr([("R", R), ("G", G), ("B", B), ("A", A)], compression=comp, tiles=tiles, origin=(2, -7))
+    for comp in (W.NONE, W.RLE, W.ZIPS, W.ZIP, W.PIZ):
+        for tiles, levels in ((None, 0), ((8, 4), 0), ((32, 32), 0), ((8, 4), 1), ((16, 8), 2)):
+            data = W.write_exr([("R", R), ("G", G), ("B", B), ("A", A)], compression=comp, tiles=tiles, origin=(2, -7),
+                               levels=levels, rounding=levels == 2)
             code, ww, hh, img = O.decode(data)
             assert code == 0 and (ww, hh) == (w, h)
             assert np.array_equal(img.view(np.uint32), exp)

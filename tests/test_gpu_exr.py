@@ -42,17 +42,19 @@ def test_exr_fixture(ctx, name):
         assert sha(img) == e["sha256"]
 
 
-@pytest.mark.parametrize("comp,tiles", [(W.ZIP, None), (W.ZIPS, None), (W.RLE, None), (W.NONE, None), (W.ZIP, (64, 64)),
-                                        (W.RLE, (128, 32))])
-def test_exr_large_vs_oracle(ctx, comp, tiles):
+@pytest.mark.parametrize("comp,tiles,levels", [(W.ZIP, None, 0), (W.ZIPS, None, 0), (W.RLE, None, 0), (W.NONE, None, 0),
+                                               (W.ZIP, (64, 64), 0), (W.RLE, (128, 32), 0), (W.PIZ, None, 0),
+                                               (W.PIZ, (128, 64), 1), (W.ZIP, (64, 32), 2)])
+def test_exr_large_vs_oracle(ctx, comp, tiles, levels):
     """A 1000x700 half RGBA image (ZIP chunks of 16 lines = 22 KB of samples each, windows
-    reaching back past 32 KiB of output) decodes to the oracle's bits."""
+    reaching back past 32 KiB of output; PIZ chunks of 32 lines = 256 KB of samples) decodes to
+    the oracle's bits; mip- / rip-mapped files decode every level and output level 0."""
     rng = np.random.default_rng(comp * 10 + (tiles is not None))
-    h, w = 700, 1000
+    h, w = (700, 1000) if comp != W.PIZ else (350, 500)  # (the PIZ oracle is pure Python)
     y, x = np.mgrid[0:h, 0:w].astype(np.float32)
     chans = [(n, (np.sin(x * (0.01 + 0.003 * k)) * np.cos(y * 0.013) * 50 + rng.normal(0, 0.05, (h, w))).astype(np.float16))
              for k, n in enumerate("RGBA")]
-    data = W.write_exr(chans, compression=comp, tiles=tiles)
+    data = W.write_exr(chans, compression=comp, tiles=tiles, levels=levels)
     oc, ow, oh, oimg = O.decode(data)
     code, ww, hh, img = ctx.exr_decode(data)
     assert (code, ww, hh) == (oc, ow, oh) == (0, w, h)
@@ -68,6 +70,25 @@ def test_exr_random_damage(ctx):
         data = bytearray(open(os.path.join(EXR, names[int(rng.integers(0, len(names)))]), "rb").read())
         for _ in range(1 + k % 3):
             data[int(rng.integers(0, len(data)))] ^= int(rng.integers(1, 256))
+        data = bytes(data)
+        oc, ow, oh, oimg = O.decode(data)
+        code, w, h, img = ctx.exr_decode(data)
+        assert (code, w, h) == (oc, ow, oh), k
+        if oc == 0:
+            assert np.array_equal(img.view(np.uint32), oimg.view(np.uint32)), k
+
+
+def test_exr_piz_damage(ctx):
+    """Random damage to PIZ and level fixtures: the GPU's code and bits equal the oracle's
+    (damaged Huffman data decodes to what tinyexr keeps: it ignores hufUncompress's failure)."""
+    rng = np.random.default_rng(12)
+    names = [n for n in sorted(MAN) if MAN[n]["code"] == 0 and ("piz" in n or n.startswith(("mip", "rip")))
+             and "w16" not in n and "longcodes" not in n]
+    for k in range(60):
+        data = bytearray(open(os.path.join(EXR, names[int(rng.integers(0, len(names)))]), "rb").read())
+        lo = len(data) // 3 if k % 2 else 0
+        for _ in range(1 + k % 4):
+            data[int(rng.integers(lo, len(data)))] ^= int(rng.integers(1, 256))
         data = bytes(data)
         oc, ow, oh, oimg = O.decode(data)
         code, w, h, img = ctx.exr_decode(data)

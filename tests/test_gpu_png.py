@@ -165,3 +165,71 @@ def test_png_c5_8192_rgba(ctx):
     png = check(ctx, px, decode=False)
     ref = O.png_encode_zlib(px.tobytes(), w, h, 4, 6)
     assert len(png) <= 1.05 * len(ref), (len(png), len(ref))
+
+
+PNG_FIX = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "png")
+
+
+def _bmp(name):
+    """The reference's data/*.bmp (committed as data fixtures under tests/golden/png) as RGB."""
+    from PIL import Image
+    return np.asarray(Image.open(__import__("os").path.join(PNG_FIX, name)).convert("RGB"))
+
+
+def test_png_reference_anchor(ctx):
+    """the reference's one PNG anchor on the GPU path -- data/test.png's pixels
+    (opaque RGBA 499 x 289) encode as lodepng encodes them: palette colour type,
+    8-bit, the palette in first-seen order, filter 0 on every row; and decode back exactly."""
+    px = P.read_fixture_png(__import__("os").path.join(PNG_FIX, "test.png"))
+    h, w = px.shape[:2]
+    assert (w, h) == (499, 289) and px[..., 3].min() == 255
+    png = check(ctx, px)
+    I = P.info(png)
+    assert (I["colortype"], I["bitdepth"]) == (3, 8)
+    raw = zlib.decompress(I["idat"])
+    assert set(raw[:: w + 1]) == {0}
+    # first-seen order: palette entry k is the k-th distinct colour in raster order
+    flat = px.reshape(-1, 4)
+    _, first = np.unique(flat.view(np.uint32), return_index=True)
+    order = flat[np.sort(first)][:, :3]
+    assert I["plte"] == order.tobytes()
+
+
+def _size_vs_zlib(ctx, px, decode=True):
+    h, w, d = px.shape
+    png = check(ctx, px, decode)
+    I = P.info(png)
+    m = O.png_choose(px.tobytes(), w, h, d)
+    z6 = len(zlib.compress(O.png_filtered(px.tobytes(), w, h, d, m), 6))
+    return len(I["idat"]) / z6
+
+
+@pytest.mark.parametrize("name", ["test.bmp", "cat.bmp"])
+@pytest.mark.parametrize("alpha", [False, True])
+def test_png_size_real_content(ctx, name, alpha, capsys):
+    """IDAT size on the reference's own photographs (data/test.bmp, cat.bmp)
+    as RGB (opaque RGBA: lodepng drops alpha) and with a gradient alpha (RGBA kept), against
+    system zlib -6 on the identical filtered stream (the contract: within 5% of lodepng's size;
+    lodepng itself is unbuildable here, zlib -6 stands in)."""
+    rgb = _bmp(name)
+    h, w = rgb.shape[:2]
+    a = np.full((h, w, 1), 255, np.uint8) if not alpha else \
+        np.broadcast_to((np.arange(w) * 255 // max(1, w - 1)).astype(np.uint8)[None, :, None], (h, w, 1))
+    px = np.ascontiguousarray(np.concatenate([rgb, a], axis=2))
+    r = _size_vs_zlib(ctx, px)
+    with capsys.disabled():
+        print(f"\n  {name} {'RGBA' if alpha else 'RGB'} {w}x{h}: GPU IDAT / zlib-6 = {r:.3f}")
+    assert r <= 1.05, r
+
+
+def test_png_size_photo_4096(ctx, capsys):
+    """A 4096^2 photo-like image (tools/foreign.py photo: flat sky, noise band, hard edges,
+    stripes) with gradient alpha: IDAT size against zlib -6."""
+    from tools import foreign
+    rgb = foreign.photo(7101, 4096, 4096)
+    a = np.broadcast_to((np.arange(4096) * 255 // 4095).astype(np.uint8)[None, :, None], (4096, 4096, 1))
+    px = np.ascontiguousarray(np.concatenate([rgb, a], axis=2))
+    r = _size_vs_zlib(ctx, px, decode=False)
+    with capsys.disabled():
+        print(f"\n  photo 4096^2 RGBA: GPU IDAT / zlib-6 = {r:.3f}")
+    assert r <= 1.05, r

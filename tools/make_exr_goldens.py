@@ -78,12 +78,14 @@ def cases():
     c["missing_lineorder.exr"] = W.write_exr(rgba(96, 16, 16, "half"), compression=W.ZIP, drop=("lineOrder",))
     c["pxr24.exr"] = W.write_exr(rgba(96, 16, 16, "half"), compression=W.ZIP,
                                  attrs={"compression": W.attr("compression", "compression", bytes([5]))})
+    # a ZIP payload labelled PIZ: DecompressPiz reads it as a range header (INVALID_DATA or garbage)
     c["piz.exr"] = W.write_exr(rgba(96, 16, 16, "half"), compression=W.ZIP,
                                attrs={"compression": W.attr("compression", "compression", bytes([4]))})
     c["type_mismatch.exr"] = W.write_exr(rgba(96, 16, 16, "half"), compression=W.ZIP,
                                          extra_attrs=W.attr("type", "string", b"tiledimage"))
     c["multipart_flag.exr"] = W.write_exr(rgba(96, 16, 16, "half"), compression=W.ZIP, version_flags=0x10,
                                           extra_attrs=W.attr("name", "string", b"a") + W.attr("type", "string", b"scanlineimage"))
+    # the mipmap flag on a one-level file: the offset table is shorter than the levels need
     c["mipmap_tiles.exr"] = W.write_exr(rgba(97, 16, 16, "half"), compression=W.NONE, tiles=(8, 8),
                                         attrs={"tiles": W.attr("tiles", "tiledesc", struct.pack("<IIB", 8, 8, 1))})
     c["inverted_window.exr"] = W.write_exr(rgba(96, 16, 16, "half"), compression=W.ZIP,
@@ -98,7 +100,97 @@ def cases():
                                             raw_chunks=lambda i, d: d[:-2] if i == 7 else d)
     c["line_out_of_range.exr"] = W.write_exr(rgba(99, 16, 16, "half"), compression=W.ZIP, chunk_line=lambda i, y: y - 100)
     c["zip_zero_len.exr"] = W.write_exr(rgba(99, 16, 16, "half"), compression=W.ZIPS, raw_chunks=lambda i, d: b"" if i == 2 else d)
+    c.update(piz_and_level_cases())
     return c
+
+
+def smooth(h, w, kind, seed=0):
+    """Smooth planes quantised to 1/64 (the PIZ wavelet + Huffman compress them; noise would be
+    stored raw, Issue 40)."""
+    y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+    p = [np.round((np.sin(x * (0.05 + 0.01 * k) + k + seed) * np.cos(y * 0.07) * (4 + k)) * 64) / 64 for k in range(4)]
+    if kind == "half":
+        return [(n, a.astype(np.float16)) for n, a in zip("RGBA", p)]
+    if kind == "float":
+        return [(n, a.astype(np.float32)) for n, a in zip("RGBA", p)]
+    if kind == "uint":
+        return [(n, (np.abs(a) * 1000).astype(np.uint32)) for n, a in zip("RGBA", p)]
+    return [("R", p[0].astype(np.float16)), ("G", p[1].astype(np.float32)), ("B", p[2].astype(np.float16)),
+            ("A", (np.abs(p[3]) * 100).astype(np.uint32))]
+
+
+def piz_and_level_cases():
+    """PIZ (TINYEXR_USE_PIZ is on in the reference build, tinyexr.h:126-128) and mip- / rip-mapped
+    tiles (DecodeChunk decodes every level, :5282-5354; the output is level 0)."""
+    c = {}
+    for kind in ("half", "float", "uint", "mixed"):
+        c[f"scan_piz_{kind}.exr"] = W.write_exr(smooth(70, 90, kind, len(c)), compression=W.PIZ, origin=(4, -9))
+    c["scan_piz_desc.exr"] = W.write_exr(smooth(45, 61, "half", 1), compression=W.PIZ, line_order=1)
+    c["tile_piz_half.exr"] = W.write_exr(smooth(70, 90, "half", 2), compression=W.PIZ, tiles=(64, 32))
+    y, x = np.mgrid[0:40, 0:600]
+    h = (np.sin(x * 0.05) * np.cos(y * 0.1) * 8).astype(np.float16)
+    # > 16384 distinct values in a chunk: wdec16 (maxValue >= 1 << 14, :2003)
+    c["scan_piz_w16.exr"] = W.write_exr([("R", h), ("G", h), ("B", h), ("A", (x * 3 + y * 1801).astype(np.uint32))],
+                                        compression=W.PIZ)
+    h2 = h.copy()  # rare outliers: codes longer than the 14-bit direct table (:2574-2606, :2849-2887)
+    h2[::7, ::13] = np.float16(1234.5) + x[::7, ::13].astype(np.float16)
+    c["scan_piz_longcodes.exr"] = W.write_exr([("R", h2), ("G", h), ("B", h)], compression=W.PIZ)
+    z = np.zeros((33, 50), np.float16)  # bitmap empty: minNonZero 8191, maxNonZero 0 (Issue 194)
+    c["scan_piz_zero.exr"] = W.write_exr([("R", z), ("G", z), ("B", z)], compression=W.PIZ)
+    rng = np.random.default_rng(5)
+    c["scan_piz_raw.exr"] = W.write_exr([(n, rng.standard_normal((40, 30)).astype(np.float32)) for n in "RGB"],
+                                        compression=W.PIZ)  # (stored raw: not smaller, Issue 40)
+    # range header / length rejected by DecompressPiz (:3249-3314)
+    c["piz_bad_bitmap.exr"] = W.write_exr(smooth(40, 50, "half", 3), compression=W.PIZ,
+                                          raw_chunks=lambda i, d: d[:2] + b"\x00\x20" + d[4:] if i == 0 else d)
+    c["piz_bad_length.exr"] = W.write_exr(smooth(40, 50, "half", 4), compression=W.PIZ,
+                                          raw_chunks=lambda i, d: _piz_set_length(d, 10**6) if i == 0 else d)
+    # damaged Huffman data: tinyexr ignores hufUncompress's failure and keeps what was decoded
+    c["piz_damaged_codes.exr"] = W.write_exr(smooth(40, 50, "half", 5), compression=W.PIZ,
+                                             raw_chunks=lambda i, d: d[: len(d) * 2 // 3] + bytes(len(d) - len(d) * 2 // 3))
+    c["piz_short_length.exr"] = W.write_exr(smooth(40, 50, "half", 6), compression=W.PIZ,
+                                            raw_chunks=lambda i, d: _piz_set_length(d, 7) if i == 0 else d)
+    # levels
+    c["mip_none_half.exr"] = W.write_exr(smooth(45, 70, "half", 7), compression=W.NONE, tiles=(16, 16), levels=1)
+    c["mip_zip_mixed.exr"] = W.write_exr(smooth(45, 70, "mixed", 8), compression=W.ZIP, tiles=(16, 8), levels=1)
+    c["mip_piz_half.exr"] = W.write_exr(smooth(90, 70, "half", 9), compression=W.PIZ, tiles=(64, 32), levels=1)
+    c["mip_round_up.exr"] = W.write_exr(smooth(45, 70, "half", 10), compression=W.RLE, tiles=(16, 16), levels=1,
+                                        rounding=1)
+    c["rip_zips_half.exr"] = W.write_exr(smooth(45, 70, "half", 11), compression=W.ZIPS, tiles=(16, 16), levels=2)
+    c["rip_piz_round_up.exr"] = W.write_exr(smooth(45, 70, "float", 12), compression=W.PIZ, tiles=(64, 32), levels=2,
+                                            rounding=1)
+    c["mip_desc.exr"] = W.write_exr(smooth(21, 30, "half", 13), compression=W.NONE, tiles=(8, 8), levels=1, line_order=1)
+    # a level-1 tile naming the wrong level / damaged data in the last level: the read fails
+    # although level 0 is intact (:5085-5094, :5124-5127)
+    c["mip_wrong_level.exr"] = W.write_exr(smooth(45, 70, "half", 14), compression=W.ZIP, tiles=(16, 16), levels=1,
+                                           raw_chunks=None, offsets=None)
+    c["mip_wrong_level.exr"] = _patch_tile_level(c["mip_wrong_level.exr"], 1)
+    c["mip_damaged_last.exr"] = W.write_exr(smooth(45, 70, "half", 15), compression=W.ZIP, tiles=(16, 16), levels=1,
+                                            raw_chunks=lambda i, d: d[:-1] + bytes([d[-1] ^ 1]) if i == 19 else d)
+    c["tile_mode3.exr"] = W.write_exr(smooth(16, 16, "half", 16), compression=W.NONE, tiles=(8, 8),
+                                      attrs={"tiles": W.attr("tiles", "tiledesc", struct.pack("<IIB", 8, 8, 3))})
+    # tile offsets to reconstruct (:6100-6108, :5867-5974)
+    c["tile_offsets_zero.exr"] = W.write_exr(smooth(45, 70, "half", 17), compression=W.ZIP, tiles=(16, 16),
+                                             offsets=lambda o: [0] * len(o))
+    c["mip_offsets_zero.exr"] = W.write_exr(smooth(45, 70, "half", 18), compression=W.RLE, tiles=(16, 16), levels=1,
+                                            offsets=lambda o: [0 if k % 3 == 0 else v for k, v in enumerate(o)])
+    return c
+
+
+def _piz_set_length(d, n):
+    """The Huffman length field of a PIZ chunk payload (after the range header)."""
+    mn, mx = struct.unpack_from("<HH", d, 0)
+    at = 4 + (mx - mn + 1 if mn <= mx else 0)
+    return d[:at] + struct.pack("<i", n) + d[at + 4:]
+
+
+def _patch_tile_level(data, k):
+    """Tile chunk k's level field (lx) + 1: the table still names it at its level."""
+    code, info = O.parse_header(data)
+    marker = info["header_len"] + 8
+    o = struct.unpack_from("<Q", data, marker + 8 * k)[0]
+    lx = struct.unpack_from("<i", data, o + 8)[0]
+    return data[: o + 8] + struct.pack("<i", lx + 1) + data[o + 12:]
 
 
 def main():
