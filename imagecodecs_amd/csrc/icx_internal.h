@@ -14,7 +14,7 @@ namespace icx {
 // ---- speculative parallel entropy decode (icx_spec.hip) ----
 constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16 B)
 constexpr int kSubBytes = 2560;      // longest decode lane (unstuffed bytes per subsequence)
-constexpr int kMaxRounds = 8;        // entropy rounds per group (launch_spec_entropy; ICX_ROUNDS)
+constexpr int kMaxRounds = 4;        // entropy rounds per group (launch_spec_entropy; ICX_ROUNDS, at most 8)
 constexpr int kPoolPerSlotX4 = 10;   // coefficient pool: 2.5 x an image's blocks per workspace slot (icx_api.cpp)
 constexpr int kSubBytesSmall = 512;  // shortest: k_spec_plan sizes each image's lanes in between so
                                      // they fill whole 512-lane workgroups (icx_spec.hip)

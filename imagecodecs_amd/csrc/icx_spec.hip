@@ -539,10 +539,16 @@ __global__ __launch_bounds__(256) void k_step_tabs(int n, const Desc* __restrict
     StepSet& S = steps[i];
     for (int k = threadIdx.x; k < ScanTab::entries(); k += blockDim.x) S.scan.fill(h, k);
     for (int k = threadIdx.x; k < WriteTab::entries(); k += blockDim.x) S.write.fill(h, k);
+#ifdef ICX_EXP_GW8
+    for (int k = threadIdx.x; k < ScanTab11::entries(); k += blockDim.x) S.scan11.fill(h, k);
+#endif
     if (threadIdx.x == 0) {
         const Sel sel = make_sel(desc[i]);
         set_block_sel(S.scan, h, sel);
         set_block_sel(S.write, h, sel);
+#ifdef ICX_EXP_GW8
+        set_block_sel(S.scan11, h, sel);
+#endif
     }
 }
 
@@ -944,18 +950,32 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                                                 int64_t pool_cap, uint64_t* __restrict__ X, GwOut* __restrict__ gwo,
                                                 RecState* __restrict__ rec, int lead) {
     __shared__ WriteTab T;
+#ifdef ICX_EXP_GW8  // timing experiment only: 64-byte int8 slots (values truncated), 11-bit lead tables
+    constexpr int kSQ = 4;  // 16-byte quarters per slot
+    using LeadTab = ScanTab11;
+    typedef int8_t Cell;
+#else
+    constexpr int kSQ = 8;
+    using LeadTab = ScanTab;
+    typedef int16_t Cell;
+#endif
     union SlotsOrScan {  // the lead loop's scan tables, then the write loop's slots
-        ScanTab st;
-        int4 slots[NL][8];
+        LeadTab st;
+        int4 slots[NL][kSQ];
     };
-    static_assert(sizeof(ScanTab) <= sizeof(int4) * NL * 8, "scan tables fit the slots' LDS");
+    static_assert(sizeof(LeadTab) <= sizeof(int4) * NL * kSQ, "scan tables fit the slots' LDS");
     __shared__ SlotsOrScan L;
     __shared__ uint8_t done_lane[NL / 64][64];  // per wave: lanes that completed a block, by rank
     int cur = -1;
     const int total = totals[2];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int4* slot = &L.slots[threadIdx.x][0];
-    int16_t* sv = reinterpret_cast<int16_t*>(slot);
+    Cell* sv = reinterpret_cast<Cell*>(slot);
+#ifdef ICX_EXP_GW8
+    auto slot_cell = [](int t, int n) { return n ^ ((t & 3) << 4); };
+#else
+    auto slot_cell = [](int t, int n) { return slot_elem(t, n); };
+#endif
     int4* A = reinterpret_cast<int4*>(ac);
     const int32_t scratch = (int32_t)pool_cap;  // (a lane the pool could not hold writes here)
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
@@ -963,7 +983,11 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         SpecImg& s = spec[i];
         if (s.mode != 1) continue;  // uniform per workgroup
         __syncthreads();  // (the previous item's slots are done with)
+#ifdef ICX_EXP_GW8
+        stage_tab(L.st, steps[i].scan11);
+#else
         stage_tab(L.st, steps[i].scan);
+#endif
         __syncthreads();
         const int64_t j = (int64_t)(wg - wpre[i]) * NL + threadIdx.x;
         const Sel S = make_sel(desc[i]);
@@ -986,7 +1010,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         const uint64_t g0 = pack_state(s0 + r.used, b, 0);
         __syncthreads();  // every wave is done with the scan tables: the slots take their LDS
 #pragma unroll
-        for (int q = 0; q < 8; ++q) slot[q] = make_int4(0, 0, 0, 0);
+        for (int q = 0; q < kSQ; ++q) slot[q] = make_int4(0, 0, 0, 0);
         __builtin_amdgcn_wave_barrier();
         r.phase();  // the lead ran a lane-dependent number of lookups
         ErrBounds eb;
@@ -1063,8 +1087,8 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             if (owndc && cell == kDcEscape) dcv[addr] = pc;  // lane-local DC outside int16 (rare)
             const int n1 = o.w1 ? (o.c1 & 63) : min(z0, 63);
             const int n2 = o.w2 ? (o.c2 & 63) : (o.w1 ? min(o.c1 + 1, 63) : min(z0, 63));
-            sv[slot_elem(threadIdx.x, n2)] = (int16_t)(o.w2 ? o.v2 : 0);
-            sv[slot_elem(threadIdx.x, n1)] = (int16_t)(o.w1 ? (bs ? cell : o.v1) : 0);
+            sv[slot_cell(threadIdx.x, n2)] = (Cell)(o.w2 ? o.v2 : 0);
+            sv[slot_cell(threadIdx.x, n1)] = (Cell)(o.w1 ? (bs ? cell : o.v1) : 0);
             const bool done = live && z == 0;
             k += done ? 1 : 0;
             const uint64_t m = __ballot(done);
@@ -1075,19 +1099,20 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                 }
                 __builtin_amdgcn_wave_barrier();
                 const int cnt = __popcll(m);
-                for (int k0 = 0; k0 < cnt; k0 += 8) {
-                    const int e = k0 + (lane >> 3), q = lane & 7;
+                constexpr int kPer = 64 / kSQ;  // blocks per flush round
+                for (int k0 = 0; k0 < cnt; k0 += kPer) {
+                    const int e = k0 + lane / kSQ, q = lane % kSQ;
                     const int src = done_lane[wave][min(e, cnt - 1)];
                     const int bsrc = __shfl(addr, src);
                     if (e < cnt) {
                         const int sl = (wave << 6) | src;
                         int4* sp = &L.slots[sl][0];
-                        const int sq = q ^ (sl & 7);
+                        const int sq = q ^ (sl & (kSQ - 1));
 #ifndef ICX_EXP_NOSTORE  // timing experiment only: drop the coefficient stores
                         typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
                         const int4 v = sp[sq];
                         const i32x4 vv = {v.x, v.y, v.z, v.w};
-                        __builtin_nontemporal_store(vv, reinterpret_cast<i32x4*>(A) + (int64_t)bsrc * 8 + q);
+                        __builtin_nontemporal_store(vv, reinterpret_cast<i32x4*>(A) + (int64_t)bsrc * kSQ + q);
 #endif
                         sp[sq] = make_int4(0, 0, 0, 0);
                     }
@@ -1473,16 +1498,17 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     // left by the images before it is deferred to the next round instead of the sequential
     // kernel (a batch of 4:4:4 q100 photos at 1.3 B/px overflows a pool sized for 1 B/px). A round
     // with no deferred image costs only its launches (every kernel finds no work).
-    // Up to kMaxRounds rounds. Each round after the first finds the U pool empty, so it plans at
-    // least (pool - largest scan) bytes of the deferred images: with the pool at 2 B/px per slot
-    // (ws_per_slot) eight rounds hold any conforming group -- baseline JPEG's entropy data stays
-    // far below 8 B/px -- and only a scan larger than the whole pool is left to the sequential
-    // kernel. A round with nothing deferred is a handful of empty launches: k_spec_plan finds no
-    // deferred image and returns, every other kernel then finds no work, and rounds after the
-    // first launch 1/8 of the grid-stride workgroups (deferred images are the rare case).
+    // Up to kMaxRounds rounds (ICX_ROUNDS: 1..8). Each round after the first finds the U pool
+    // empty, so it plans at least (pool - largest scan) bytes of the deferred images: with the
+    // pool at 2 B/px per slot (ws_per_slot) four rounds hold a group averaging up to ~6 B/px of
+    // entropy data (a 4:4:4 q100 photo is 1.3-2.5), and only what is past that, or a scan larger
+    // than the whole pool, is left to the sequential kernel. A round with nothing deferred is a
+    // handful of empty launches (k_spec_plan finds no deferred image and returns, every other
+    // kernel then finds no work) with 1/32 of the grid-stride workgroups; each costs ~0.3% of a
+    // C3 step (measured: eight rounds 216.6-216.9 GP/s against 220.9-221.2 with one).
     const int rounds = [] {  // (read per launch: tests vary it)
         const char* e = std::getenv("ICX_ROUNDS");
-        return e ? std::max(1, std::min(kMaxRounds, std::atoi(e))) : kMaxRounds;
+        return e ? std::max(1, std::min(8, std::atoi(e))) : kMaxRounds;
     }();
     for (int r = 0; r < rounds; ++r) launch_spec_round(ws, n, d_data, d_off, st, hook, r, r + 1 == rounds);
 }
@@ -1492,7 +1518,7 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     static const int g0 = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
-    const int g = round == 0 ? g0 : std::max(64, g0 / 8);
+    const int g = round == 0 ? g0 : std::max(32, g0 / 32);
     // Guess lanes start kGuessLead bits before their range (ICX_GUESS_LEAD overrides), so they are
     // resynchronised when they reach it and the count lanes splice at their first MCU start.
     // (per image: at most a quarter of a short lane, the lead is extra work on every lane)

@@ -395,7 +395,8 @@ ICX_HD void set_block_sel(Tab& T, const Huff* H, const Sel& S) {
 // the lookup was a DC code (0 for an invalid one). Returns true on a decode error (jpeg_dec.h
 // :646, :669, :671), which ends the block deterministically so speculative lanes keep going;
 // on the true path an error makes the image NJ_SYNTAX_ERROR.
-ICX_HD bool scan_step(Reader& r, const ScanTab& T, const Huff* H, const Sel& S, int& b, int& z, int32_t& dcv) {
+template <class ScanT>
+ICX_HD bool scan_step(Reader& r, const ScanT& T, const Huff* H, const Sel& S, int& b, int& z, int32_t& dcv) {
     const bool dc = z == 0;
     uint32_t x;
     const uint32_t e = step_lookup(r, T, H, S, b, dc, x);

@@ -228,11 +228,17 @@ struct StepTab {
 // under 15.5 KB for two workgroups per CU.
 using ScanTab = StepTab<9, 12, 1280, true>;
 using WriteTab = StepTab<8, 10, 1280, false>;
+#ifdef ICX_EXP_GW8  // timing experiment only: an 11-bit scan table for k_gw_lane's lead
+using ScanTab11 = StepTab<9, 11, 1280, true>;
+#endif
 
 // One image's step tables in global memory (built by k_step_tabs from Desc::huff).
 struct StepSet {
     ScanTab scan;
     WriteTab write;
+#ifdef ICX_EXP_GW8
+    ScanTab11 scan11;
+#endif
 };
 
 }  // namespace icx

@@ -41,16 +41,17 @@ def _check(res, jpegs):
 
 @pytest.mark.parametrize("rounds,parallel", [(None, 16), ("1", None), ("3", 16)])
 def test_pool_overflow_deferred_to_next_round(ctx, monkeypatch, rounds, parallel):
-    """16 slots of 512^2, 16 images at 2.5 B/px: the U pool (18 slots x 512 KiB) holds about 14 of
-    them per round. The default rounds or three: all 16 on the parallel path. One round: the rest
-    go to the sequential kernel (the old behaviour) -- bit-exact either way."""
-    monkeypatch.delenv("ICX_UPOOL_BPP", raising=False)
+    """16 slots of 512^2 over two pipelines (8 each), 16 images at 2.5 B/px, the U pool cut to
+    1 B/px (10 slots x 256 KiB per pipeline: about 3 images a round). The default rounds or three:
+    all 16 on the parallel path. One round: the rest go to the sequential kernel (the old
+    behaviour) -- bit-exact either way."""
+    monkeypatch.setenv("ICX_UPOOL_BPP", "1")  # (so a pool holds ~3 of these images)
     if rounds is None:
         monkeypatch.delenv("ICX_ROUNDS", raising=False)
     else:
         monkeypatch.setenv("ICX_ROUNDS", rounds)
     jpegs = [S.synth_jpeg(6100 + k, 512, 512, "444", 100) for k in range(16)]
-    assert sum(len(j) for j in jpegs) > 18 * 2 * 512 * 512  # more than one pool's worth
+    assert sum(len(j) for j in jpegs) > 18 * 512 * 512  # more than one pool's worth
     b = icx.Batch(ctx, 16, 512, 512, group=16)
     res = b.decode_host(jpegs)
     st = b.path_stats()
@@ -77,18 +78,21 @@ def test_pool_overflow_beyond_rounds_is_exact(ctx, monkeypatch):
 
 
 def test_deep_batch_never_sequential(ctx, monkeypatch, capsys):
-    """eight 4096^2 4:4:4 q100 images (2.5 B/px) in one group whose U pool is cut
-    to 1 B/px (ICX_UPOOL_BPP=1: 10 x 16 MiB), so the batch is more than two pools deep. With the
+    """ten 4096^2 4:4:4 q100 images (2.5 B/px) in one group whose U pool is cut
+    to 1 B/px (ICX_UPOOL_BPP=1: 12 x 16 MiB), so the batch is more than two pools deep. With the
     default rounds every image takes the parallel path (sequential == 0), bit-exact, and the
     batch costs less than twice the time per compressed byte of a clean 4:2:0 q90 batch of the
     same size decoded in one round."""
     monkeypatch.delenv("ICX_ROUNDS", raising=False)
     monkeypatch.setenv("ICX_UPOOL_BPP", "1")
-    W = 4096
-    deep = [S.synth_jpeg(6500 + k, W, W, "444", 100) for k in range(8)]
-    clean = [S.synth_jpeg(6600 + k, W, W, "420", 90) for k in range(8)]
-    assert sum(len(j) for j in deep) > 2 * 10 * W * W
-    b = icx.Batch(ctx, 8, W, W, group=8)
+    monkeypatch.setenv("ICX_PIPES", "1")  # (one workspace of 10 slots: a 12-slot U pool)
+    W, N = 4096, 10
+    from multiprocessing.pool import ThreadPool
+    with ThreadPool(8) as p:  # (the generator is C through ctypes)
+        deep = p.map(lambda k: S.synth_jpeg(6500 + k, W, W, "444", 100), range(N))
+        clean = p.map(lambda k: S.synth_jpeg(6600 + k, W, W, "420", 90), range(N))
+    assert sum(len(j) for j in deep) > 2 * 12 * W * W  # more than two pools
+    b = icx.Batch(ctx, N, W, W, group=N)
 
     def run(batch):
         b.decode_host(batch)  # (warm)
@@ -99,12 +103,12 @@ def test_deep_batch_never_sequential(ctx, monkeypatch, capsys):
     t_clean, _ = run(clean)
     t_deep, res = run(deep)
     st = b.path_stats()
-    assert st == {"parallel": 8, "fallback": 0, "sequential": 0}, st
+    assert st == {"parallel": N, "fallback": 0, "sequential": 0}, st
     _check(res, deep)
     per_clean = t_clean / sum(len(j) for j in clean)
     per_deep = t_deep / sum(len(j) for j in deep)
     with capsys.disabled():
-        print(f"\n  8 x 4096^2: 4:2:0 q90 {t_clean * 1e3:.1f} ms ({sum(map(len, clean)) / 1e6:.0f} MB), "
+        print(f"\n  {N} x 4096^2: 4:2:0 q90 {t_clean * 1e3:.1f} ms ({sum(map(len, clean)) / 1e6:.0f} MB), "
               f"4:4:4 q100 over >2 pools {t_deep * 1e3:.1f} ms ({sum(map(len, deep)) / 1e6:.0f} MB)")
     assert per_deep < 2 * per_clean, (t_deep, t_clean)
     b.close()
