@@ -407,6 +407,7 @@ int icx_batch_stage_times(const icx_batch* b, const char** names, float* ms, int
     for (auto& r : b->hook->recs) {
         float t = 0;
         if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) acc[r.s] += t;
+        else (void)hipGetLastError();  // (not left for the caller's next check)
     }
     int k = 0;
     for (int s = 0; s < kStCount && k < cap; ++s, ++k) {

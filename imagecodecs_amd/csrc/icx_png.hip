@@ -481,10 +481,11 @@ __device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t di
 // One workgroup (4 waves) per 256 KiB block; each wave takes a 4 KiB segment at a time, stages
 // its two views in LDS, and walks it in 64-position windows: every lane scores the position
 // under it against the six structural candidates (left pixel, up to two pixels back, the pixel
-// above and its two neighbours), then the wave parses the window greedily with ballots -- the
-// literal run up to the first position with a match is emitted by all lanes at once, the match
-// by one. The tokens are those of a serial greedy parse (first match of length >= 3 per
-// position, longest over the candidates, never crossing the segment end).
+// above and its two neighbours), then the wave parses the window with ballots -- the literal
+// run up to the first position with a match is emitted by all lanes at once, the match by one.
+// The tokens are those of a serial parse with one-step lazy evaluation (a match of length >= 3
+// per position, longest over the candidates, never crossing the segment end; a match whose next
+// position has a longer one is deferred to it, as zlib's lazy matching does).
 __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
                                                   int bw, uint16_t* __restrict__ tok, uint32_t* __restrict__ ntok,
                                                   uint32_t* __restrict__ hist, uint32_t* __restrict__ adl,
@@ -563,8 +564,14 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
             const int wend = (int)min((int64_t)64, s1 - p0);  // live lanes of this window
             while (pos < p0 + wend) {  // wave-uniform
                 const int li = (int)(pos - p0);
-                const uint64_t m = cmask & (~0ull << li);
-                const int mi = m ? __ffsll((unsigned long long)m) - 1 : 64;
+                uint64_t m = cmask & (~0ull << li);
+                int mi = m ? __ffsll((unsigned long long)m) - 1 : 64;
+                // lazy evaluation (zlib's deflate_slow): a match start whose successor has a
+                // longer match becomes a literal, and the successor is considered in turn
+                while (mi + 1 < wend && __shfl(best, mi + 1) > __shfl(best, mi)) {
+                    m &= m - 1;
+                    mi = __ffsll((unsigned long long)m) - 1;
+                }
                 const int le = min(mi, wend);
                 if (lane >= li && lane < le) {  // the literal run li .. le-1
                     T[nt + (lane - li)] = (uint16_t)lit;
