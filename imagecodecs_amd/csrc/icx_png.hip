@@ -13,9 +13,11 @@
 //                    rows padded to whole bytes (preProcessScanlines)
 //   k_png_filter     one workgroup per row: the five filters, MINSUM scores, strict-< choice,
 //                    filtered row with its type byte
-//   k_png_lz77       one lane per 4 KiB segment: greedy LZ77 over fixed candidate distances
+//   k_png_lz77       one wave per 4 KiB segment: lazy LZ77 over fixed candidate distances
 //                    (1, pixel, 2 pixels, row above +-pixel), tokens + per-block histograms +
 //                    Adler-32 partials; 64 segments = one 256 KiB deflate block
+//   k_png_seam(_apply) join each segment's tokens to the previous segment's last match where
+//                    it runs past the boundary (re-parsed head), and fix the counts
 //   k_png_huff       one workgroup per block: length-limited Huffman codes (15/7 bits), the
 //                    dynamic block header bits
 //   k_png_segbits    bits per segment -> (scan) bit offsets
@@ -25,6 +27,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -35,6 +38,8 @@ namespace icx {
 namespace png {
 
 constexpr int kSeg = 4096;            // LZ77 / emit segment (bytes of the filtered stream), one lane each
+constexpr int kSlots = kSeg + 8;      // token slots per segment: up to kSeg - 1 literals + a match
+                                      // overhanging the segment end (16-byte multiple)
 constexpr int kSegPerBlock = 64;      // 256 KiB deflate blocks (lodepng's size at this scale, :1830)
 constexpr int kNLL = 286, kND = 30;   // literal/length and distance alphabets
 constexpr int kHdrWords = 96;         // per-block header bit buffer (<= 3072 bits)
@@ -426,15 +431,20 @@ __global__ __launch_bounds__(256) void k_png_filter(const uint8_t* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------- LZ77
-// Token: literal = byte value (< 256); match = 1<<31 | (len-3) << 15 | (dist-1).
+// Token slots (uint16): a literal is its byte value (< 256); a match is a length slot
+// 0x4000 | (len - 3) followed by a distance slot 0x8000 | (dist - 1).
+// A segment's matches start inside it but may run past its end (the overhang, < 258 bytes): the
+// stream is then parsed as one serial parse would, without the short match every segment
+// boundary would otherwise cost (k_png_seam joins the next segment's tokens to the overhang).
 // A wave's view of the filtered stream around its segment, staged in LDS: `near` covers
-// [s0 - kNear, s1) (the segment and the short candidate distances), `far` covers
-// [s0 - rowlen - kNear, s1 - rowlen + kNear) (the row above +- one pixel). Both start at a
-// 16-byte-aligned stream index so the staging is 16-byte loads. Every source byte a candidate
-// can compare (q - d + l with q + l < s1) lies in one of them: indices >= s0 - kNear in `near`,
-// the others (distances rowlen - bw .. rowlen + bw only) in `far`.
-constexpr int kNear = 16;                        // >= 2 * bw (bw <= 8)
-constexpr int kStage = kSeg + 2 * kNear + 32;    // bytes per staged view, 16-byte multiple (dword-read slack)
+// [s0 - kNear, s1 + kOver) (the segment, its overhang and the short candidate distances), `far`
+// covers [s0 - rowlen - kNear, s1 + kOver - rowlen + kNear) (the row above +- one pixel). Both
+// start at a 16-byte-aligned stream index so the staging is 16-byte loads. Every source byte a
+// candidate can compare (q - d + l with q + l < s1 + 258) lies in one of them: indices
+// >= s0 - kNear in `near`, the others (distances rowlen - bw .. rowlen + bw only) in `far`.
+constexpr int kNear = 16;                               // >= 2 * bw (bw <= 8)
+constexpr int kOver = 272;                              // >= 258: a match past the segment end
+constexpr int kStage = kSeg + kOver + 2 * kNear + 32;   // bytes per staged view, 16-byte multiple (dword-read slack)
 struct SegView {
     const uint8_t* nearp;  // LDS base, = stream index nb0
     const uint8_t* farp;   // LDS base, = stream index fb0
@@ -443,7 +453,8 @@ struct SegView {
         return i >= nlo ? nearp[i - nb0] : farp[i - fb0];
     }
     // bytes i .. i+3, byte i lowest (a far-view read never crosses the end of that view: far
-    // candidates compare below s1 - rowlen + bw, and the view runs 2 kNear + 32 bytes past it)
+    // candidates compare below s1 + 258 - rowlen + bw, and the view runs past it by more than
+    // kNear + 16)
     __device__ __forceinline__ uint32_t dword(int64_t i) const {
         const bool nr = i >= nlo;
         const int64_t o = nr ? i - nb0 : i - fb0;
@@ -484,18 +495,21 @@ __device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t di
 // above and its two neighbours), then the wave parses the window with ballots -- the literal
 // run up to the first position with a match is emitted by all lanes at once, the match by one.
 // The tokens are those of a serial parse with one-step lazy evaluation (a match of length >= 3
-// per position, longest over the candidates, never crossing the segment end; a match whose next
-// position has a longer one is deferred to it, as zlib's lazy matching does).
+// per position, longest over the candidates; a match whose next position in the window has a
+// longer one is deferred to it, as zlib's lazy matching does). The last match may run past the
+// segment end; its overhang goes to seam[4 seg] for k_png_seam.
 __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
                                                   int bw, uint16_t* __restrict__ tok, uint32_t* __restrict__ ntok,
                                                   uint32_t* __restrict__ hist, uint32_t* __restrict__ adl,
-                                                  uint16_t* __restrict__ seghist, uint32_t* __restrict__ segx) {
-    __shared__ uint32_t h_ll[kNLL], h_d[kND];
+                                                  uint16_t* __restrict__ seghist, uint32_t* __restrict__ segx,
+                                                  uint32_t* __restrict__ seam, uint32_t* __restrict__ blksym) {
+    __shared__ uint32_t h_ll[kNLL], h_d[kND], s_sym;
     __shared__ uint32_t s_h[4][kNLL + kND];  // per wave: the current segment's symbol counts
     __shared__ __attribute__((aligned(16))) uint8_t views[4][2][kStage];
     const int64_t blk = blockIdx.x;
     for (int i = threadIdx.x; i < kNLL; i += 256) h_ll[i] = 0;
     if (threadIdx.x < kND) h_d[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_sym = 1;  // + EOB
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int64_t cand[6] = {1, bw, 2 * bw, rowlen, rowlen - bw, rowlen + bw};
@@ -506,7 +520,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
         const int64_t seg = blk * kSegPerBlock + sl;
         if (seg >= nseg) break;  // wave-uniform
         const int64_t s0 = seg * kSeg, s1 = min(N, s0 + kSeg);
-        uint16_t* T = tok + s0;
+        uint16_t* T = tok + seg * kSlots;
         uint32_t* SH = s_h[wave];
         for (int i = lane; i < kNLL + kND; i += 64) SH[i] = 0;
         uint32_t xbits = 0;  // length / distance extra bits of the segment's matches (lane 0)
@@ -536,7 +550,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
             adl[2 * seg] = (uint32_t)(a1 % kAdlerMod);
             adl[2 * seg + 1] = (uint32_t)(a2 % kAdlerMod);
         }
-        uint32_t nt = 0;
+        uint32_t nt = 0, nm = 0;  // token slots, matches
         int64_t pos = s0;  // first position not yet covered by a token
         for (int64_t p0 = s0; p0 < s1; p0 += 64) {
             const int64_t q = p0 + lane;
@@ -545,7 +559,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
             if (q < s1) {
                 const uint32_t t4 = V.dword(q);
                 lit = t4 & 255u;
-                const int maxlen = (int)min((int64_t)258, s1 - q);
+                const int maxlen = (int)min((int64_t)258, N - q);
                 if (maxlen >= 3 && q >= pos) {  // positions under a previous match need no score
 #pragma unroll
                     for (int k = 0; k < 6; ++k) {
@@ -590,6 +604,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
                         xbits += kLenExtra[lc] + kDistExtra[dc];
                     }
                     nt += 2;
+                    nm += 1;
                     pos += len;
                 }
             }
@@ -597,6 +612,8 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
         if (lane == 0) {
             ntok[seg] = nt;
             segx[seg] = xbits;
+            seam[4 * seg] = (uint32_t)(pos - s1);  // the overhang
+            atomicAdd(&s_sym, nt - nm);
         }
         __builtin_amdgcn_wave_barrier();
         // the segment's counts: to HBM for k_png_segbits, into the block histogram for k_png_huff
@@ -612,6 +629,186 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
     uint32_t* H = hist + blk * (kNLL + kND);
     for (int i = threadIdx.x; i < kNLL; i += 256) H[i] = h_ll[i] + (i == 256 ? 1u : 0u);  // + EOB
     if (threadIdx.x < kND) H[kNLL + threadIdx.x] = h_d[threadIdx.x];
+    if (threadIdx.x == 0) blksym[blk] = s_sym;
+}
+
+// ------------------------------------------------------------------------------ seams
+// Segment B's tokens were parsed from its first byte, but the previous segment A's last match
+// may already cover B's first o bytes (A's overhang). k_png_seam re-parses B from s0 + o, the
+// same way (longest structural candidate, one-step lazy), until it reaches the start of one of
+// B's own tokens -- greedy parses resynchronise within a few tokens -- and B's tokens before that
+// are replaced by the re-parsed head (at most kHead slots). If no such join is found before B's
+// last token (which fixes B's own overhang), A's last match is cut back to A's end instead and B
+// keeps its tokens. seam[4 s + 0..3]: overhang, head skip (B's slots dropped), head slots, A cut.
+constexpr int kHead = 32;
+// Longest candidate match at q (lanes 0..5: candidate k at q; lanes 6..11: candidate k at q + 1)
+// in the segment's staged views, the candidate order deciding ties as in k_png_lz77;
+// -> (len, dist) at q and len at q + 1.
+__device__ __forceinline__ void seam_score(const SegView& V, int64_t N, int64_t q, const int64_t* cand, int lane,
+                                           int& len0, int& dist0, int& len1) {
+    int l = 0, d = 0;
+    if (lane < 12) {
+        const int64_t p = q + (lane >= 6), dd = cand[lane % 6];
+        const int maxlen = (int)min((int64_t)258, N - p);
+        if (dd && dd <= p && maxlen >= 3) {
+            l = match_len(V, p, dd, maxlen);
+            if (l < 3) l = 0;
+            d = (int)dd;
+        }
+    }
+    len0 = dist0 = len1 = 0;
+    for (int k = 0; k < 6; ++k) {
+        const int a = __shfl(l, k), b = __shfl(l, 6 + k);
+        if (a > len0) {
+            len0 = a;
+            dist0 = __shfl(d, k);
+        }
+        len1 = max(len1, b);
+    }
+}
+__device__ __forceinline__ void tok_counts(uint16_t* G, uint32_t* H, uint32_t& xbits, uint32_t t, uint32_t tnext, int sgn) {
+    if (t < 256) {
+        G[t] = (uint16_t)(G[t] + sgn);
+        atomicAdd(&H[t], (uint32_t)sgn);
+        return;
+    }
+    const int len = (int)(t & 255) + 3, dist = (int)(tnext & 0x7FFFu) + 1;
+    const int lc = len_code(len), dc = dist_code(dist);
+    G[257 + lc] = (uint16_t)(G[257 + lc] + sgn);
+    G[kNLL + dc] = (uint16_t)(G[kNLL + dc] + sgn);
+    atomicAdd(&H[257 + lc], (uint32_t)sgn);
+    atomicAdd(&H[kNLL + dc], (uint32_t)sgn);
+    xbits += (uint32_t)(sgn * (int)(kLenExtra[lc] + kDistExtra[dc]));
+}
+// One wave per segment B (the seam before it): B's two views staged as in k_png_lz77, then
+// the wave walks B's tokens while 12 lanes score each re-parse position.
+__global__ __launch_bounds__(256) void k_png_seam(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
+                                                  int bw, const uint16_t* __restrict__ tok,
+                                                  const uint32_t* __restrict__ ntok, uint32_t* __restrict__ seam,
+                                                  uint16_t* __restrict__ head, int join) {
+    __shared__ __attribute__((aligned(16))) uint8_t views[4][2][kStage];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+    if (b >= nseg) return;  // wave-uniform; no block barriers below
+    if (b == nseg - 1 && lane == 0) seam[4 * b + 3] = 0;  // no seam after the last segment
+    const uint32_t o = b > 0 ? seam[4 * (b - 1)] : 0u;
+    uint32_t skip = 0, nh = 0, cut = 0;
+    if (o) {
+        int64_t cand[6] = {1, bw, 2 * bw, rowlen, rowlen - bw, rowlen + bw};
+        for (int k = 0; k < 6; ++k)
+            if (cand[k] <= 0 || cand[k] > 32768) cand[k] = 0;
+        const int64_t s0 = b * kSeg;
+        SegView V;
+        V.nlo = s0 - kNear;
+        V.nb0 = V.nlo & ~(int64_t)15;
+        V.fb0 = (s0 - rowlen - kNear) & ~(int64_t)15;
+        V.nearp = views[wave][0];
+        V.farp = views[wave][1];
+        stage_view(F, N, V.nb0, views[wave][0], lane);
+        stage_view(F, N, V.fb0, views[wave][1], lane);
+        __builtin_amdgcn_wave_barrier();
+        const uint16_t* T = tok + b * kSlots;
+        const uint32_t nt = ntok[b];
+        const uint32_t last = (nt >= 2 && (T[nt - 1] & 0x8000u)) ? nt - 2 : nt - 1;  // B's last token slot
+        const bool final_seg = b == nseg - 1;
+        uint16_t* Hd = head + b * kHead;
+        uint32_t si = 0;      // B's token slot under consideration ...
+        int64_t bp = s0;      // ... and the stream position it starts at
+        int64_t q = s0 + o;   // the re-parse position
+        bool joined = false;
+        for (;;) {  // wave-uniform: every lane walks the same tokens
+            while (si <= last && bp < q) {
+                const uint32_t t = T[si];
+                if (t < 256) {
+                    bp += 1;
+                    si += 1;
+                } else {
+                    bp += (t & 255) + 3;
+                    si += 2;
+                }
+            }
+            if (si <= last && bp == q) {  // join B's own parse at slot si
+                joined = true;
+                break;
+            }
+            if (final_seg && q >= N) {  // the whole final segment re-parsed
+                si = nt;
+                joined = true;
+                break;
+            }
+            if ((si > last && !final_seg) || nh + 2 > kHead || !join) break;  // no join: cut A instead
+            int len0, dist0, len1;
+            seam_score(V, N, q, cand, lane, len0, dist0, len1);
+            if (len0 >= 3 && !(q + 1 < N && len1 > len0)) {
+                if (lane == 0) {
+                    Hd[nh] = (uint16_t)(0x4000u | (uint32_t)(len0 - 3));
+                    Hd[nh + 1] = (uint16_t)(0x8000u | (uint32_t)(dist0 - 1));
+                }
+                nh += 2;
+                q += len0;
+            } else {
+                if (lane == 0) Hd[nh] = V.at(q);
+                nh += 1;
+                q += 1;
+            }
+        }
+        if (joined) skip = si;
+        else {
+            nh = 0;
+            cut = 1;
+        }
+    }
+    if (lane == 0) {
+        seam[4 * b + 1] = skip;
+        seam[4 * b + 2] = nh;
+        if (b > 0) seam[4 * (b - 1) + 3] = cut;
+    }
+}
+// One lane per segment: the symbol counts (segment, block) and extra bits follow the seams --
+// the dropped head slots out, the re-parsed head in, and a cut last match shortened (or, under
+// three bytes, turned into its literals, in place).
+__global__ __launch_bounds__(256) void k_png_seam_apply(const uint8_t* __restrict__ F, int64_t N, int64_t nseg,
+                                                        uint16_t* __restrict__ tok, uint32_t* __restrict__ ntok,
+                                                        const uint32_t* __restrict__ seam, const uint16_t* __restrict__ head,
+                                                        uint16_t* __restrict__ seghist, uint32_t* __restrict__ segx,
+                                                        uint32_t* __restrict__ hist) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= nseg) return;
+    const uint32_t o = seam[4 * s], skip = seam[4 * s + 1], nh = seam[4 * s + 2], cut = seam[4 * s + 3];
+    if (!skip && !nh && !cut) return;
+    uint16_t* T = tok + s * kSlots;
+    uint16_t* G = seghist + s * (kNLL + kND);
+    uint32_t* H = hist + (s / kSegPerBlock) * (kNLL + kND);
+    uint32_t nt = ntok[s], xbits = segx[s];
+    for (uint32_t i = 0; i < skip;) {
+        const uint32_t t = T[i];
+        tok_counts(G, H, xbits, t, i + 1 < nt ? T[i + 1] : 0u, -1);
+        i += t < 256 ? 1 : 2;
+    }
+    const uint16_t* Hd = head + s * kHead;
+    for (uint32_t i = 0; i < nh;) {
+        const uint32_t t = Hd[i];
+        tok_counts(G, H, xbits, t, i + 1 < nh ? Hd[i + 1] : 0u, +1);
+        i += t < 256 ? 1 : 2;
+    }
+    if (cut) {  // the last token is a match ending o bytes past the segment end
+        const uint32_t t = T[nt - 2], d = T[nt - 1];
+        tok_counts(G, H, xbits, t, d, -1);
+        const int len = (int)(t & 255) + 3 - (int)o;
+        const int64_t p = min(N, (s + 1) * kSeg) - len;  // its start
+        if (len >= 3) {
+            T[nt - 2] = (uint16_t)(0x4000u | (uint32_t)(len - 3));
+            tok_counts(G, H, xbits, T[nt - 2], d, +1);
+        } else {
+            for (int k = 0; k < len; ++k) {
+                T[nt - 2 + k] = F[p + k];
+                tok_counts(G, H, xbits, F[p + k], 0u, +1);
+            }
+            nt -= 2 - len;
+        }
+    }
+    ntok[s] = nt;
+    segx[s] = xbits;
 }
 
 // ------------------------------------------------------------------------------ Huffman
@@ -732,8 +929,38 @@ struct BitW {
     }
 };
 
-// One workgroup per block, thread 0 builds everything (deterministic, tiny).
-__global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hist, int64_t nblk, BlockCodes* __restrict__ bc) {
+// Deflate blocks: k_png_lz77 counts symbols per 256 KiB base block; consecutive base blocks
+// with few tokens between them share one deflate block (one header), as zlib's blocks end at
+// kBlockTokens symbols (lit_bufsize at memLevel 8) -- highly compressible input would otherwise
+// pay a code-table header per 256 KiB. plan[2 b], plan[2 b + 1] = the first / last base block
+// of b's deflate block. One workgroup; thread 0 groups greedily over the base blocks' symbol
+// counts (k_png_lz77's, before the seams move a few tokens: the grouping only needs their size).
+constexpr uint32_t kBlockTokens = 16384;
+__global__ __launch_bounds__(256) void k_png_blockplan(const uint32_t* __restrict__ blksym, int64_t nblk,
+                                                       uint32_t* __restrict__ plan) {
+    extern __shared__ uint32_t cnt[];  // nblk symbol counts (host caps nblk for the LDS size)
+    for (int64_t b = threadIdx.x; b < nblk; b += 256) cnt[b] = blksym[b];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    int64_t first = 0;
+    uint32_t acc = 0;
+    for (int64_t b = 0; b <= nblk; ++b) {
+        if (b == nblk || (acc && acc + cnt[b] > kBlockTokens)) {
+            for (int64_t k = first; k < b; ++k) {
+                plan[2 * k] = (uint32_t)first;
+                plan[2 * k + 1] = (uint32_t)(b - 1);
+            }
+            first = b;
+            acc = 0;
+        }
+        if (b < nblk) acc += cnt[b];
+    }
+}
+
+// One workgroup per base block, thread 0 builds everything (deterministic, tiny); the base
+// blocks of one deflate block compute the same codes from the same summed counts.
+__global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hist, int64_t nblk,
+                                                 const uint32_t* __restrict__ plan, BlockCodes* __restrict__ bc) {
     __shared__ uint32_t f_ll[kNLL], f_d[kND];
     __shared__ uint16_t order[kNLL], order_d[kND];
     __shared__ uint32_t wt[2 * kNLL];
@@ -741,10 +968,14 @@ __global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hi
     __shared__ uint8_t l_ll[kNLL], l_d[kND];
     __shared__ uint8_t rle_sym[kNLL + kND];
     __shared__ uint8_t rle_ext[kNLL + kND];
-    const int64_t blk = blockIdx.x;
-    const uint32_t* H = hist + blk * (kNLL + kND);
-    for (int i = threadIdx.x; i < kNLL; i += 64) f_ll[i] = H[i];
-    if (threadIdx.x < kND) f_d[threadIdx.x] = H[kNLL + threadIdx.x];
+    const int64_t blk = blockIdx.x, gfirst = plan[2 * blk], glast = plan[2 * blk + 1];
+    for (int i = threadIdx.x; i < kNLL + kND; i += 64) {
+        uint32_t f = 0;
+        for (int64_t b = gfirst; b <= glast; ++b) f += hist[b * (kNLL + kND) + i];
+        if (i == 256) f -= (uint32_t)(glast - gfirst);  // one EOB per deflate block
+        if (i < kNLL) f_ll[i] = f;
+        else f_d[i - kNLL] = f;
+    }
     BlockCodes& B = bc[blk];
     for (int i = threadIdx.x; i < kHdrWords; i += 64) B.hdr[i] = 0;
     __syncthreads();
@@ -837,7 +1068,7 @@ __global__ __launch_bounds__(64) void k_png_huff(const uint32_t* __restrict__ hi
     int hclen = 19;
     while (hclen > 4 && l_cl[kClOrder[hclen - 1]] == 0) --hclen;
     BitW bw{B.hdr};
-    bw.put(blk == nblk - 1 ? 1u : 0u, 1);  // BFINAL
+    bw.put(glast == nblk - 1 ? 1u : 0u, 1);  // BFINAL
     bw.put(2u, 2);                          // BTYPE = dynamic
     bw.put((uint32_t)(hlit - 257), 5);
     bw.put((uint32_t)(hdist - 1), 5);
@@ -864,9 +1095,17 @@ __device__ __forceinline__ void stage_codes(const BlockCodes* __restrict__ bc, B
 
 // One wave per segment: the segment's symbol counts (from k_png_lz77) times the block's code
 // lengths, plus the extra bits of its matches -- no pass over the tokens.
+// A segment opens its deflate block (header) / closes it (EOB).
+__device__ __forceinline__ bool seg_opens(int64_t seg, const uint32_t* plan) {
+    return seg % kSegPerBlock == 0 && plan[2 * (seg / kSegPerBlock)] == (uint32_t)(seg / kSegPerBlock);
+}
+__device__ __forceinline__ bool seg_closes(int64_t seg, int64_t nseg, const uint32_t* plan) {
+    return seg == nseg - 1 ||
+           (seg % kSegPerBlock == kSegPerBlock - 1 && plan[2 * (seg / kSegPerBlock) + 1] == (uint32_t)(seg / kSegPerBlock));
+}
 __global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint16_t* __restrict__ seghist,
                                                      const uint32_t* __restrict__ segx, const BlockCodes* __restrict__ bc,
-                                                     unsigned long long* __restrict__ bits) {
+                                                     const uint32_t* __restrict__ plan, unsigned long long* __restrict__ bits) {
     __shared__ BlockCodes B;  // the four waves' segments share one block (kSegPerBlock % 4 == 0)
     stage_codes(bc, B);
     const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -879,8 +1118,8 @@ __global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint16_
     for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o);
     if (lane == 0) {
         unsigned long long t = (unsigned long long)b + segx[seg];
-        if (seg % kSegPerBlock == 0) t += B.hdr_bits;
-        if (seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1) t += B.ll_len[256];  // EOB
+        if (seg_opens(seg, plan)) t += B.hdr_bits;
+        if (seg_closes(seg, nseg, plan)) t += B.ll_len[256];  // EOB
         bits[seg] = t;
     }
 }
@@ -888,8 +1127,7 @@ __global__ __launch_bounds__(256) void k_png_segbits(int64_t nseg, const uint16_
 // Token slot i -> (bits, count), LSB-first: a literal; or, at a match's length slot, code, length
 // extra, distance code, distance extra (at most 15 + 5 + 15 + 13 = 48 bits); a distance slot
 // emits nothing (its match's length slot took it).
-__device__ __forceinline__ uint64_t token_code(const BlockCodes& B, const uint16_t* T, uint32_t i, int& nb) {
-    const uint32_t t = T[i];
+__device__ __forceinline__ uint64_t token_code(const BlockCodes& B, uint32_t t, uint32_t tnext, int& nb) {
     if (t < 256) {
         nb = B.ll_len[t];
         return B.ll_code[t];
@@ -898,7 +1136,7 @@ __device__ __forceinline__ uint64_t token_code(const BlockCodes& B, const uint16
         nb = 0;
         return 0;
     }
-    const int len = (int)(t & 255) + 3, dist = (int)(T[i + 1] & 0x7FFFu) + 1;
+    const int len = (int)(t & 255) + 3, dist = (int)(tnext & 0x7FFFu) + 1;
     const int lc = len_code(len), dc = dist_code(dist);
     uint64_t v = B.ll_code[257 + lc];
     int n = B.ll_len[257 + lc];
@@ -926,9 +1164,11 @@ __device__ __forceinline__ void or_bits(uint32_t* w, unsigned long long bitpos, 
     if (sh + nb > 32) atomicOr(w + wi + 1, (uint32_t)hi);
     if (sh + nb > 64) atomicOr(w + wi + 2, (uint32_t)(hi >> 32));
 }
-// The segment's bits into W (word 0 = output word w0; zeroed), starting at bit `pos`.
+// The segment's bits into W (word 0 = output word w0; zeroed), starting at bit `pos`: its nh
+// re-parsed head slots Hd, then its own slots T[0 .. nt).
 __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos, const BlockCodes& B,
-                                             const uint16_t* T, uint32_t nt, bool head, bool eob, int lane) {
+                                             const uint16_t* Hd, uint32_t nh, const uint16_t* T, uint32_t nt,
+                                             bool head, bool eob, int lane) {
     if (head) {  // the block header: its words, shifted into place
         const uint32_t hb = B.hdr_bits;
         for (uint32_t i = lane; i * 32 < hb; i += 64) {
@@ -937,10 +1177,13 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
         }
         pos += hb;
     }
-    for (uint32_t i0 = 0; i0 < nt; i0 += 64) {
+    const uint32_t n = nh + nt;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + lane;
         int nb = 0;
-        const uint64_t v = i < nt ? token_code(B, T, i, nb) : 0;
+        uint64_t v = 0;
+        if (i < nh) v = token_code(B, Hd[i], i + 1 < nh ? Hd[i + 1] : 0u, nb);
+        else if (i < n) v = token_code(B, T[i - nh], i + 1 < n ? T[i + 1 - nh] : 0u, nb);
         uint32_t inc;  // inclusive scan of nb over the wave (rocprim's DPP cross-lane scan)
         using WScan = rocprim::warp_scan<uint32_t, 64>;
         typename WScan::storage_type wst;  // empty for the cross-lane implementation
@@ -951,7 +1194,9 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
     if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
 }
 __global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint16_t* __restrict__ tok,
-                                                  const uint32_t* __restrict__ ntok, const BlockCodes* __restrict__ bc,
+                                                  const uint32_t* __restrict__ ntok, const uint32_t* __restrict__ seam,
+                                                  const uint16_t* __restrict__ hbuf, const BlockCodes* __restrict__ bc,
+                                                  const uint32_t* __restrict__ plan,
                                                   const unsigned long long* __restrict__ off,
                                                   const unsigned long long* __restrict__ bits, uint32_t* __restrict__ out,
                                                   unsigned long long base_bits) {
@@ -961,21 +1206,23 @@ __global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint16_t* 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t seg = (int64_t)blockIdx.x * 4 + wave;
     if (seg >= nseg) return;  // wave-uniform; no block barriers below
-    const uint16_t* T = tok + seg * kSeg;
-    const uint32_t nt = ntok[seg];
+    const uint32_t skip = seam[4 * seg + 1], nh = seam[4 * seg + 2];
+    const uint16_t* T = tok + seg * kSlots + skip;
+    const uint16_t* Hd = hbuf + seg * kHead;
+    const uint32_t nt = ntok[seg] - skip;
     const unsigned long long o0 = base_bits + off[seg], o1 = o0 + bits[seg];
     if (o1 == o0) return;
     const unsigned long long w0 = o0 >> 5, wl = (o1 - 1) >> 5;  // first / last output word
     const int nw = (int)(wl - w0 + 1);
-    const bool head = seg % kSegPerBlock == 0, eob = seg % kSegPerBlock == kSegPerBlock - 1 || seg == nseg - 1;
+    const bool head = seg_opens(seg, plan), eob = seg_closes(seg, nseg, plan);
     if (nw > kEmitWords) {  // straight into the (zeroed) output
-        emit_segment(out + w0, o0 & 31, B, T, nt, head, eob, lane);
+        emit_segment(out + w0, o0 & 31, B, Hd, nh, T, nt, head, eob, lane);
         return;
     }
     uint32_t* W = img[wave];
     for (int i = lane; i < nw; i += 64) W[i] = 0;
     __builtin_amdgcn_wave_barrier();
-    emit_segment(W, o0 & 31, B, T, nt, head, eob, lane);
+    emit_segment(W, o0 & 31, B, Hd, nh, T, nt, head, eob, lane);
     __builtin_amdgcn_wave_barrier();
     for (int i = lane; i < nw; i += 64) {
         const uint32_t v = W[i];
@@ -1105,7 +1352,11 @@ struct PngWs {
     unsigned long long *bits = nullptr, *off = nullptr;
     uint16_t* seghist = nullptr;  // per segment: literal/length and distance symbol counts
     uint32_t* segx = nullptr;     // per segment: extra bits of its matches
-    size_t seghist_cap = 0, segx_cap = 0;
+    uint32_t* seam = nullptr;     // per segment: overhang, head skip, head slots, cut (k_png_seam)
+    uint16_t* head = nullptr;     // per segment: kHead re-parsed head slots
+    uint32_t* plan = nullptr;     // per base block: first / last base block of its deflate block
+    uint32_t* blksym = nullptr;   // per base block: symbols k_png_lz77 counted (+ EOB)
+    size_t seghist_cap = 0, segx_cap = 0, seam_cap = 0, head_cap = 0, plan_cap = 0, blksym_cap = 0;
     void* tmp = nullptr;
     size_t tmp_cap = 0;
     struct PngHost* host = nullptr;  // pinned read-back buffer (PngJob)
@@ -1122,7 +1373,7 @@ struct PngWs {
         if (host) (void)hipHostFree(host);
         for (void* p : {(void*)st, (void*)set_key, (void*)set_idx, (void*)mode, (void*)conv, (void*)filt, (void*)tok,
                         (void*)ntok, (void*)hist, (void*)adl, (void*)crc, (void*)small, (void*)bc, (void*)bits,
-                        (void*)off, (void*)seghist, (void*)segx, tmp})
+                        (void*)off, (void*)seghist, (void*)segx, (void*)seam, (void*)head, (void*)plan, (void*)blksym, tmp})
             if (p) (void)hipFree(p);
     }
 };
@@ -1149,6 +1400,11 @@ void png_ws_destroy(PngWs* ws) { delete ws; }
         if ((call) != hipSuccess) return -1;        \
     } while (0)
 
+// ICX_PNG_SEAM=0: cut every overhanging match back to its segment end (no re-parsed heads).
+static int seam_join() {
+    const char* e = std::getenv("ICX_PNG_SEAM");
+    return !(e && e[0] == '0');
+}
 template <class T>
 static bool pgrow(T*& p, size_t bytes, size_t& cap) {
     if (p && bytes <= cap) return true;
@@ -1371,7 +1627,7 @@ int PngJob::issue_b() {
     nseg = (N + kSeg - 1) / kSeg;
     nblk = (nseg + kSegPerBlock - 1) / kSegPerBlock;
     size_t c5 = ws->seg_cap, c6 = ws->seg_cap, c7 = ws->seg_cap, c8 = ws->seg_cap;
-    if (!pgrow(ws->tok, (size_t)nseg * kSeg * 2, ws->tok_cap)) return -1;  // <= kSeg slots per segment
+    if (!pgrow(ws->tok, (size_t)nseg * kSlots * 2, ws->tok_cap)) return -1;
     if ((size_t)nseg * 8 > ws->seg_cap || !ws->ntok) {
         if (!pgrow(ws->ntok, (size_t)nseg * 8, c5) || !pgrow(ws->adl, (size_t)nseg * 8, c6) ||
             !pgrow(ws->bits, (size_t)nseg * 8, c7) || !pgrow(ws->off, (size_t)nseg * 8, c8))
@@ -1385,15 +1641,24 @@ int PngJob::issue_b() {
     if (!pgrow(ws->small, 64, c11)) return -1;
     mark(4);
     if (!pgrow(ws->seghist, (size_t)nseg * (kNLL + kND) * 2, ws->seghist_cap) ||
-        !pgrow(ws->segx, (size_t)nseg * 4, ws->segx_cap))
+        !pgrow(ws->segx, (size_t)nseg * 4, ws->segx_cap) || !pgrow(ws->seam, (size_t)nseg * 16, ws->seam_cap) ||
+        !pgrow(ws->head, (size_t)nseg * kHead * 2, ws->head_cap) || !pgrow(ws->plan, (size_t)nblk * 8, ws->plan_cap) ||
+        !pgrow(ws->blksym, (size_t)nblk * 4, ws->blksym_cap))
         return -1;
+    if (nblk > 16384) return -1;  // k_png_blockplan's LDS (64 KiB): images up to 4 GiB of filtered bytes
     hipLaunchKernelGGL(k_png_lz77, dim3((unsigned)nblk), dim3(256), 0, st, ws->filt, N, nseg, 1 + M.lb, M.bw, ws->tok,
-                       ws->ntok, ws->hist, ws->adl, ws->seghist, ws->segx);
+                       ws->ntok, ws->hist, ws->adl, ws->seghist, ws->segx, ws->seam, ws->blksym);
+    gwave = (unsigned)((nseg + 3) / 4);  // one wave per segment
+    hipLaunchKernelGGL(k_png_seam, dim3(gwave), dim3(256), 0, st, ws->filt, N, nseg, 1 + M.lb, M.bw, ws->tok, ws->ntok,
+                       ws->seam, ws->head, seam_join());
+    hipLaunchKernelGGL(k_png_seam_apply, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, st, ws->filt, N, nseg,
+                       ws->tok, ws->ntok, ws->seam, ws->head, ws->seghist, ws->segx, ws->hist);
     mark(5);
     mark(6);
-    hipLaunchKernelGGL(k_png_huff, dim3((unsigned)nblk), dim3(64), 0, st, ws->hist, nblk, ws->bc);
-    gwave = (unsigned)((nseg + 3) / 4);  // one wave per segment
-    hipLaunchKernelGGL(k_png_segbits, dim3(gwave), dim3(256), 0, st, nseg, ws->seghist, ws->segx, ws->bc, ws->bits);
+    hipLaunchKernelGGL(k_png_blockplan, dim3(1), dim3(256), (size_t)nblk * 4, st, ws->blksym, nblk, ws->plan);
+    hipLaunchKernelGGL(k_png_huff, dim3((unsigned)nblk), dim3(64), 0, st, ws->hist, nblk, ws->plan, ws->bc);
+    hipLaunchKernelGGL(k_png_segbits, dim3(gwave), dim3(256), 0, st, nseg, ws->seghist, ws->segx, ws->bc, ws->plan,
+                       ws->bits);
     size_t tb = 0;
     PNG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ws->bits, ws->off, (int)nseg, st));
     if (!pgrow(ws->tmp, tb, ws->tmp_cap)) return -1;
@@ -1425,7 +1690,7 @@ int PngJob::issue_c() {
     const unsigned long long base_bits = mis * 8;
     PNG_HIP(hipMemsetAsync(d_out + wbase, 0, ((dbytes + mis + 3) & ~3ull) + 4, st));
     mark(8);
-    hipLaunchKernelGGL(k_png_emit, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->bc, ws->off, ws->bits,
+    hipLaunchKernelGGL(k_png_emit, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->seam, ws->head, ws->bc, ws->plan, ws->off, ws->bits,
                        reinterpret_cast<uint32_t*>(d_out + wbase), base_bits);
     mark(9);
     // signature + IHDR/PLTE/tRNS + IDAT length/type + zlib header (78 01, :1932-1941)
