@@ -930,6 +930,13 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 // gives the IDCT each block's pool block and DC offset (k_gw_scan, k_gw_map). The per-lane logic
 // is icx_spec_core.h's gw_* / gc_*, which tests/emu/spec_emu.cpp runs lane by lane on the CPU.
 
+// A pointer every lane of the wave holds, as the compiler's uniform (SGPR) value.
+__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo);
+}
+
 // NL lanes per workgroup (the wg2pre numbering: kWriteLanesBig). Two loops per lane:
 //  1. the lead: from `lead` bits before the lane's start to its first block start at or after
 //     the start (g0), with the scan tables (runs of symbols per lookup; nothing is stored). The
@@ -1002,6 +1009,8 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         const uint32_t pre = act ? (uint32_t)(start - s0) : 0u, span = act ? (uint32_t)(end - s0) : 0u;
         Reader r;
         r.init(U + s.uoff, s.ulen, s0);
+        r.u = uniform_ptr(r.u);  // (one image per workgroup: the stream base and end chunk stay in SGPRs)
+        r.cmax = __builtin_amdgcn_readfirstlane(r.cmax);
         int b = 0, z = 0;
         {  // 1. the lead
             int32_t v;
