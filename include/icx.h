@@ -271,10 +271,12 @@ int icx_hdr_batch_stage_times(const icx_hdr_batch* b, const char** names, float*
  * one-channel image repeats its channel in all four; no A channel -> 1.0), data-window rows in
  * tinyexr's order. HALF samples are converted bit for bit (half_to_float), FLOAT copied, UINT
  * sample bits copied unconverted (tinyexr reads them through its float** view).
- * Scope: single-part scanline or one-level tiled files, NONE / RLE / ZIPS / ZIP compression;
- * PIZ -> ICX_EXR_UNSUPPORTED_FORMAT (tinyexr built with TINYEXR_USE_PIZ 0), multi-part, deep and
- * mip- / rip-mapped files -> ICX_EXR_UNSUPPORTED_FEATURE. Pixels no chunk wrote (tinyexr leaves
- * them uninitialised) are 0. */
+ * Scope: single-part scanline or tiled files, NONE / RLE / ZIPS / ZIP / PIZ compression (the
+ * reference builds tinyexr with TINYEXR_USE_PIZ 1, tinyexr.h:126-128); mip- and rip-mapped tiled
+ * files decode every level's tiles as DecodeChunk does (a failure in any level fails the read) and
+ * return level 0; a broken offset table is reconstructed from the chunk headers
+ * (ReconstructTileOffsets). Multi-part and deep files -> ICX_EXR_UNSUPPORTED_FEATURE. Pixels no
+ * chunk wrote (tinyexr leaves them uninitialised) are 0. */
 enum icx_exr_result {
     ICX_EXR_SUCCESS = 0,                /* TINYEXR_SUCCESS                          */
     ICX_EXR_INVALID_MAGIC_NUMBER = -1,  /* TINYEXR_ERROR_INVALID_MAGIC_NUMBER       */
