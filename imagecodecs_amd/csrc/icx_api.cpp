@@ -204,6 +204,9 @@ static void ws_free(GroupWs& ws) {
                     (void*)ws.repair, (void*)ws.steps, (void*)ws.map, (void*)ws.chunk_next, (void*)ws.pool_next,
                     (void*)ws.gw, (void*)ws.crec, (void*)ws.clist})
         if (p) (void)hipFree(p);
+    if (ws.h_defer) (void)hipHostFree(ws.h_defer);
+    if (ws.h_layout) (void)hipHostFree(ws.h_layout);
+    if (ws.ev_defer) (void)hipEventDestroy(ws.ev_defer);
     ws = GroupWs{};
 }
 
@@ -265,6 +268,11 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ICX_HIP(ctx, hipMalloc(&ws.gw, sizeof(GwOut) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.crec, sizeof(GcRec) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.clist, sizeof(int2) * ws.lanes_cap), false);
+    ICX_HIP(ctx, hipHostMalloc(&ws.h_defer, 2 * sizeof(int32_t), hipHostMallocDefault), false);
+    ws.h_defer[0] = ws.h_defer[1] = 0;
+    ICX_HIP(ctx, hipHostMalloc(&ws.h_layout, sizeof(int32_t), hipHostMallocDefault), false);
+    *ws.h_layout = 1;
+    ICX_HIP(ctx, hipEventCreateWithFlags(&ws.ev_defer, hipEventDisableTiming), false);
     return true;
 }
 
@@ -358,16 +366,34 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
         ICX_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), ICX_INTERNAL_ERR);
         b->front_done.push_back(e);
     }
-    int gi = 0;
-    for (int g0 = 0; g0 < n; g0 += per, ++gi) {
-        const int gn = std::min(per, n - g0);
-        const int p = gi % used;
+    // Entropy round 0 of the first group on each pipe goes out first; then, per group, the later
+    // rounds only while its previous round deferred an image (the host reads that count once the
+    // round's k_spec_plan has run: the call returns after the last group's planning, not after the
+    // decode), its back half, and round 0 of the group that follows on the same pipe.
+    auto front0 = [&](int g) {
+        const int g0 = g * per, p = g % used;
+        launch_decode_front(b->ws[p], std::min(per, n - g0), d_data, d_off + g0, d_size + g0, out_stride,
+                            p == 0 ? st : b->pst[p], b->hook.get(), stagger ? kFrontAll : kFrontFirst);
+    };
+    for (int g = 0; g < std::min(used, ng); ++g) {
+        if (stagger && g > 0) ICX_HIP(ctx, hipStreamWaitEvent(b->pst[g % used], b->front_done[g - 1], 0), ICX_INTERNAL_ERR);
+        front0(g);
+        if (stagger) ICX_HIP(ctx, hipEventRecord(b->front_done[g], g % used == 0 ? st : b->pst[g % used]), ICX_INTERNAL_ERR);
+    }
+    for (int g = 0; g < ng; ++g) {
+        const int g0 = g * per, gn = std::min(per, n - g0), p = g % used;
         hipStream_t ps = p == 0 ? st : b->pst[p];
-        if (stagger && gi > 0) ICX_HIP(ctx, hipStreamWaitEvent(ps, b->front_done[gi - 1], 0), ICX_INTERNAL_ERR);
-        launch_decode_front(b->ws[p], gn, d_data, d_off + g0, d_size + g0, out_stride, ps, b->hook.get());
-        if (stagger) ICX_HIP(ctx, hipEventRecord(b->front_done[gi], ps), ICX_INTERNAL_ERR);
+        if (!stagger) launch_decode_front(b->ws[p], gn, d_data, d_off + g0, d_size + g0, out_stride, ps, b->hook.get(),
+                                          kFrontRest);
         launch_decode_back(b->ws[p], gn, d_out + (uint64_t)g0 * out_stride, out_stride, d_status + g0, d_dims + 3 * g0,
-                           ps, b->hook.get());
+                           ps, b->hook.get(), !stagger);
+        const int gnext = g + used;
+        if (gnext < ng) {
+            hipStream_t pn = gnext % used == 0 ? st : b->pst[gnext % used];
+            if (stagger) ICX_HIP(ctx, hipStreamWaitEvent(pn, b->front_done[gnext - 1], 0), ICX_INTERNAL_ERR);
+            front0(gnext);
+            if (stagger) ICX_HIP(ctx, hipEventRecord(b->front_done[gnext], pn), ICX_INTERNAL_ERR);
+        }
     }
     for (int p = 1; p < used; ++p) {  // the caller's stream waits for every pipe
         ICX_HIP(ctx, hipEventRecord(b->join[p], b->pst[p]), ICX_INTERNAL_ERR);

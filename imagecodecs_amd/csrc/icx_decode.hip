@@ -1253,9 +1253,24 @@ __global__ __launch_bounds__(256, ICX_CONV_MINW) void k_convert_stream(const Des
 // blocks into LDS and converts those 16 rows from there -- the 16.8 MB luma plane per 4096^2
 // image never goes through HBM. Both use the lane-pair IDCT; the conversion is rows_kv, the same
 // code k_convert_stream runs, with the luma rows read from LDS.
-__device__ __forceinline__ bool fused420(const Desc& d) {
-    return d.status == kOk && d.nc == 3 && d.bpm == 6 && d.c[0].hs == 2 && d.c[0].vs == 2 && d.c[1].hs == 1 &&
-           d.c[1].vs == 1 && d.c[2].hs == 1 && d.c[2].vs == 1 && stream_kind(d) == 3;
+__device__ __forceinline__ bool fused420_shape(const Desc& d) {
+    return d.nc == 3 && d.bpm == 6 && d.c[0].hs == 2 && d.c[0].vs == 2 && d.c[1].hs == 1 && d.c[1].vs == 1 &&
+           d.c[2].hs == 1 && d.c[2].vs == 1 && stream_kind(d) == 3;
+}
+__device__ __forceinline__ bool fused420(const Desc& d) { return d.status == kOk && fused420_shape(d); }
+
+// After k_parse: whether the group holds an image that is not 4:2:0 in the fused420 layout
+// (pinned memory, read by the host once round 0's planning has run). Without one, the back half
+// skips the other samplings' kernels, which would all find no work (a dozen no-op launches per
+// group: ~2% of a C2 step).
+__global__ __launch_bounds__(256) void k_layout(int n, const Desc* __restrict__ desc, int32_t* __restrict__ out) {
+    int other = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const Desc& d = desc[i];
+        other |= (d.status == kPending || d.status == kOk) && !fused420_shape(d);
+    }
+    other = __syncthreads_or(other);
+    if (threadIdx.x == 0) *out = other;
 }
 
 // Lane-pair IDCT of one block: c = the block as stored (zig-zag int16), qw = its component's
@@ -1800,23 +1815,30 @@ __global__ void k_finalize(int n, const Desc* __restrict__ desc, int32_t* __rest
 
 // ---------------------------------------------------------------------------- launcher
 void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
-                         const uint64_t* d_size, uint64_t out_stride, hipStream_t st, StageHook* hook) {
+                         const uint64_t* d_size, uint64_t out_stride, hipStream_t st, StageHook* hook, int part) {
     if (n <= 0) return;
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
-    B(kStParse);
-    hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
-                       out_stride);
-    E(kStParse);
-    launch_spec_entropy(ws, n, d_data, d_off, st, hook);
+    if (part != kFrontRest) {
+        B(kStParse);
+        hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
+                           out_stride);
+        hipLaunchKernelGGL(k_layout, dim3(1), dim3(256), 0, st, n, ws.desc, ws.h_layout);
+        E(kStParse);
+    }
+    launch_spec_entropy(ws, n, d_data, d_off, st, hook, part);
+    if (part == kFrontFirst) return;
     B(kStEntropy);
     hipLaunchKernelGGL(k_entropy_seq, dim3(n), dim3(64), 0, st, n, d_data, d_off, ws.desc, ws.ac, ws.dc);
     E(kStEntropy);
 }
 
 void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
-                        int32_t* d_dims, hipStream_t st, StageHook* hook) {
+                        int32_t* d_dims, hipStream_t st, StageHook* hook, bool known_layout) {
     if (n <= 0) return;
+    // the other samplings' kernels, unless the host knows the group has none (k_layout, written
+    // before round 0's planning, whose event the host waits for here)
+    const bool other = !known_layout || hipEventSynchronize(ws.ev_defer) != hipSuccess || *ws.h_layout != 0;
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     const int tb = 64, nb = (n + tb - 1) / tb;
@@ -1838,12 +1860,12 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
         const int v = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 2;
         return (v >= 0 && v <= 3) ? v : 2;
     }();
-#ifndef ICX_EXP_ONLY420  // timing experiment only: the 4:2:0 kernels alone (other samplings undecoded)
-    hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes, ws.plane_cap,
-                       fuse);
-    hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
-                       ws.plane_cap);
-#endif
+    if (other || fuse == 0) {
+        hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes, ws.plane_cap,
+                           fuse);
+        hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
+                           ws.plane_cap);
+    }
     if (fuse == 1 || fuse == 2) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
         const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;
         hipLaunchKernelGGL(k_idct420c, dim3(std::max(cgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map,
@@ -1857,11 +1879,9 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     E(kStIdct);
     B(kStUpsample);
     const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, gwg / (3 * n)));
-#ifndef ICX_EXP_ONLY420
-    for (int p = 0; p < 6; ++p)
+    for (int p = 0; p < 6 && other; ++p)
         hipLaunchKernelGGL(k_upsample, dim3(ux, n * 3), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
                            ws.tmp_cap, p);
-#endif
     E(kStUpsample);
     B(kStConvert);
     const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, gwg / n));
@@ -1884,30 +1904,30 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     if (fuse == 1)
         hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap, d_out, out_stride);
-#ifndef ICX_EXP_ONLY420
-    hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride, fuse);
-    hipLaunchKernelGGL(k_convert_stream<1>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride, fuse);
-    hipLaunchKernelGGL(k_convert_stream<2>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride, fuse);
-    hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride, fuse);
-#endif
+    if (other) {
+        hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                           out_stride, fuse);
+        hipLaunchKernelGGL(k_convert_stream<1>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                           out_stride, fuse);
+        hipLaunchKernelGGL(k_convert_stream<2>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                           out_stride, fuse);
+        hipLaunchKernelGGL(k_convert_stream<4>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                           out_stride, fuse);
+    }
     // border lanes of the doubled layouts: ~3 lanes x (H / kSHE) strips per image
     const int64_t egw = (4 * ((ws.max_h + kSHE - 1) / kSHE) + 255) / 256;
     const int egx = (int)std::max<int64_t>(1, std::min<int64_t>(egw, 16384 / n));
     const int ego = (int)std::max<int64_t>(1, std::min<int64_t>(egw, gwg / n));
     hipLaunchKernelGGL(k_convert_edge<3>, dim3(egx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                        out_stride, fuse);
-#ifndef ICX_EXP_ONLY420
-    hipLaunchKernelGGL(k_convert_edge<1>, dim3(ego, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride, fuse);
-    hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride);
-    hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
-                       ws.tmp_cap, d_out, out_stride);
-#endif
+    if (other) {
+        hipLaunchKernelGGL(k_convert_edge<1>, dim3(ego, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                           out_stride, fuse);
+        hipLaunchKernelGGL(k_convert_fused, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                           out_stride);
+        hipLaunchKernelGGL(k_convert, dim3(cx, n), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
+                           ws.tmp_cap, d_out, out_stride);
+    }
     hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(tb), 0, st, n, ws.desc, d_status, d_dims);
     E(kStConvert);
 }
@@ -1916,7 +1936,7 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
                          const uint64_t* d_size, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
                          int32_t* d_dims, hipStream_t st, StageHook* hook) {
     launch_decode_front(ws, n, d_data, d_off, d_size, out_stride, st, hook);
-    launch_decode_back(ws, n, d_out, out_stride, d_status, d_dims, st, hook);
+    launch_decode_back(ws, n, d_out, out_stride, d_status, d_dims, st, hook, false);
 }
 
 }  // namespace icx

@@ -14,7 +14,7 @@ namespace icx {
 // ---- speculative parallel entropy decode (icx_spec.hip) ----
 constexpr int kTileBytes = 4096;   // raw bytes per unstuff tile (256 lanes x 16 B)
 constexpr int kSubBytes = 2560;      // longest decode lane (unstuffed bytes per subsequence)
-constexpr int kMaxRounds = 4;        // entropy rounds per group (launch_spec_entropy; ICX_ROUNDS, at most 8)
+constexpr int kMaxRounds = 8;        // entropy rounds per group at most (launch_spec_entropy; ICX_ROUNDS 1..8)
 constexpr int kPoolPerSlotX4 = 10;   // coefficient pool: 2.5 x an image's blocks per workspace slot (icx_api.cpp)
 constexpr int kSubBytesSmall = 512;  // shortest: k_spec_plan sizes each image's lanes in between so
                                      // they fill whole 512-lane workgroups (icx_spec.hip)
@@ -147,6 +147,9 @@ struct GroupWs {
     GwOut* gw = nullptr;               // [lanes_cap]
     GcRec* crec = nullptr;             // [lanes_cap]
     int2* clist = nullptr;             // [lanes_cap] per image, in its lane-record range: (image, lane) to count-decode
+    int32_t* h_defer = nullptr;        // pinned [2]: images the last k_spec_plan deferred, and gave restart-interval lanes
+    int32_t* h_layout = nullptr;       // pinned: the group has an image outside the fused 4:2:0 layout (k_layout)
+    hipEvent_t ev_defer = nullptr;     // after round 0's k_spec_plan
 };
 
 // Where block n of an image lives in its group's coefficient pool: the pool block and the offset
@@ -211,14 +214,24 @@ void launch_decode_group(const GroupWs& ws, int n, const uint8_t* d_data, const 
 // The same in two halves: front = parse, unstuff, entropy decode (latency-bound); back = IDCT,
 // upsample, convert, statuses (HBM-bound). The batch scheduler overlaps one group's back with the
 // next group's front on another stream.
+// part: kFrontAll every entropy round; kFrontFirst parse + round 0 (ws.h_defer holds round 0's
+// deferred-image count once ws.ev_defer has completed); kFrontRest the later rounds when that count
+// is not 0 (the caller has waited for ws.ev_defer), then the sequential kernel.
+enum { kFrontAll = 0, kFrontFirst = 1, kFrontRest = 2 };
 void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
-                         const uint64_t* d_size, uint64_t out_stride, hipStream_t st, StageHook* hook);
+                         const uint64_t* d_size, uint64_t out_stride, hipStream_t st, StageHook* hook,
+                         int part = kFrontAll);
+// known_layout: the host may wait for ws.ev_defer and read ws.h_layout (k_layout) to skip the
+// other samplings' kernels when the group has only fused-layout 4:2:0 images.
 void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
-                        int32_t* d_dims, hipStream_t st, StageHook* hook);
+                        int32_t* d_dims, hipStream_t st, StageHook* hook, bool known_layout = false);
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
-                         StageHook* hook);
+                         StageHook* hook, int part = kFrontAll);
+// piece: kRoundAll the whole round; kRoundHead up to its restart-interval write; kRoundTail that
+// write and the round's end; kRoundTailNoDri the end alone (no image got restart-interval lanes).
+enum { kRoundAll = 0, kRoundHead = 1, kRoundTail = 2, kRoundTailNoDri = 3 };
 void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
-                       StageHook* hook, int round, int last);
+                       StageHook* hook, int round, int last, int piece = kRoundAll);
 
 // Per-image result record (icx_records.hip; include/icx.h icx_record): status, dims and the
 // 64-bit weighted word sum of the decoded bytes.

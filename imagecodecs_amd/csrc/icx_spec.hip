@@ -52,21 +52,22 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
                                                     int64_t upool, int64_t lanes_cap, int sub_bytes, int64_t pool_cap,
                                                     unsigned long long* __restrict__ pool_next, int gw, int round,
-                                                    int last_round) {
+                                                    int last_round, int32_t* __restrict__ defer_out) {
     __shared__ int sh[1024];
     __shared__ int last[7];
-    if (round > 0) {  // a later round with nothing deferred (the usual case) plans nothing, at once
+    if (round > 0) {  // a later round with nothing deferred plans nothing, at once
         int any = 0;
         for (int i = threadIdx.x; i < n; i += blockDim.x) any |= spec[i].mode == 4;
         if (!__syncthreads_or(any)) {
             if (threadIdx.x == 0) {
                 totals[0] = totals[1] = totals[2] = 0;
                 tilepre[n] = wgpre[n] = wg2pre[n] = 0;
+                if (defer_out) defer_out[0] = defer_out[1] = 0;
             }
             return;
         }
     }
-    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0, carry_a = 0;
+    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0, carry_a = 0, carry_d = 0, carry_i = 0;
     const int64_t pool_units = upool >> 12, wg_cap = lanes_cap / kLanes;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
         const int i = i0 + threadIdx.x;
@@ -156,6 +157,8 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                 dd.mapped = 0;
             }
         }
+        carry_d += __syncthreads_count(mine && !ok && cand && !last_round);  // deferred to the next round
+        carry_i += __syncthreads_count(ok && desc[i].restart != 0);        // restart-interval lanes (mode 3)
         const int et = block_exclusive_scan(nt, sh);
         const int ew = block_exclusive_scan(nw, sh);
         const int ew2 = block_exclusive_scan(nw2, sh);
@@ -187,6 +190,12 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         // overflow chunks and count blocks from here (a later round goes on from where it is: the
         // earlier rounds' chunks hold their images' blocks)
         if (round == 0) *pool_next = (unsigned long long)carry_a * kGwChunk;
+        // images deferred to the next round, for the host (pinned memory: icx_jpeg_batch_decode
+        // launches a next round only while there are any)
+        if (defer_out) {
+            defer_out[0] = carry_d;
+            defer_out[1] = carry_i;
+        }
     }
 }
 
@@ -1502,28 +1511,47 @@ __global__ void k_spec_finish(int n, Desc* __restrict__ desc, SpecImg* __restric
 }
 
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
-                         StageHook* hook) {
+                         StageHook* hook, int part) {
     // Rounds over the group (k_spec_plan): an image that does not fit the U pool / lane records
     // left by the images before it is deferred to the next round instead of the sequential
     // kernel (a batch of 4:4:4 q100 photos at 1.3 B/px overflows a pool sized for 1 B/px). A round
     // with no deferred image costs only its launches (every kernel finds no work).
     // Up to kMaxRounds rounds (ICX_ROUNDS: 1..8). Each round after the first finds the U pool
     // empty, so it plans at least (pool - largest scan) bytes of the deferred images: with the
-    // pool at 2 B/px per slot (ws_per_slot) four rounds hold a group averaging up to ~6 B/px of
+    // pool at 2 B/px per slot (ws_per_slot) eight rounds hold a group averaging up to ~14 B/px of
     // entropy data (a 4:4:4 q100 photo is 1.3-2.5), and only what is past that, or a scan larger
     // than the whole pool, is left to the sequential kernel. A round with nothing deferred is a
     // handful of empty launches (k_spec_plan finds no deferred image and returns, every other
     // kernel then finds no work) with 1/32 of the grid-stride workgroups; each costs ~0.3% of a
-    // C3 step (measured: eight rounds 216.6-216.9 GP/s against 220.9-221.2 with one).
+    // C3 step (measured: eight rounds 216.6-216.9 GP/s against 220.9-221.2 with one). So the batch
+    // entry launches round 0 alone (part kFrontFirst) and later (part kFrontRest) each next round
+    // only while the previous round's k_spec_plan deferred an image (its count in pinned memory,
+    // ws.h_defer, read once ws.ev_defer has completed): rounds until nothing is deferred, at most
+    // ICX_ROUNDS. kFrontAll (the single-call paths) launches every round unconditionally.
     const int rounds = [] {  // (read per launch: tests vary it)
         const char* e = std::getenv("ICX_ROUNDS");
         return e ? std::max(1, std::min(8, std::atoi(e))) : kMaxRounds;
     }();
-    for (int r = 0; r < rounds; ++r) launch_spec_round(ws, n, d_data, d_off, st, hook, r, r + 1 == rounds);
+    if (part == kFrontFirst) {  // round 0 up to its restart-interval write (kFrontRest finishes it)
+        launch_spec_round(ws, n, d_data, d_off, st, hook, 0, rounds == 1, kRoundHead);
+        return;
+    }
+    if (part == kFrontRest) {  // round 0's tail: the restart-interval write only if its plan gave DRI lanes
+        const bool known = hipEventSynchronize(ws.ev_defer) == hipSuccess;
+        launch_spec_round(ws, n, d_data, d_off, st, hook, 0, rounds == 1,
+                          known && ws.h_defer[1] == 0 ? kRoundTailNoDri : kRoundTail);
+        if (!known) return;
+    }
+    for (int r = part == kFrontRest ? 1 : 0; r < rounds; ++r) {
+        if (part == kFrontRest) {  // the previous round's k_spec_plan: anything deferred?
+            if (hipEventSynchronize(ws.ev_defer) != hipSuccess || ws.h_defer[0] == 0) break;
+        }
+        launch_spec_round(ws, n, d_data, d_off, st, hook, r, r + 1 == rounds, kRoundAll);
+    }
 }
 
 void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
-                       StageHook* hook, int round, int last) {
+                       StageHook* hook, int round, int last, int piece) {
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     static const int g0 = std::getenv("ICX_EGRID") ? std::max(1, std::atoi(std::getenv("ICX_EGRID"))) : 2048;  // grid-stride launches: >> 256 CUs
@@ -1542,78 +1570,80 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
     // ICX_GW=0 / 1 forces one (read per launch: tests run both paths in one process).
     const char* gw_env = std::getenv("ICX_GW");
     const int gw = gw_env ? (std::atoi(gw_env) != 0) : ((int64_t)ws.max_w * ws.max_h > kGwMinPixels ? 1 : 0);
-    B(kStUnstuff);
-    hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
-                       ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw, round, last);
-    if (round == 0)  // (an image's tables serve every round)
-        hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
-    hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
-                       ws.totals, ws.tiles);
-    hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,
-                       ws.U);
-    hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
-                       ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.rst, ws.rst_cap);
-    E(kStUnstuff);
-    // Guess-write path (default; ICX_GW=0: guess, count, write)
-    if (gw) {
-        B(kStWrite);
-        hipLaunchKernelGGL(k_gw_lane<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                           ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.X, ws.gw,
-                           ws.rec, lead);
-        E(kStWrite);
+    const bool big = !gw && (std::getenv("ICX_BIG_WG") ? std::atoi(std::getenv("ICX_BIG_WG")) != 0 : true);
+    if (piece == kRoundAll || piece == kRoundHead) {
+        B(kStUnstuff);
+        hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
+                           ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw, round, last, ws.h_defer);
+        (void)hipEventRecord(ws.ev_defer, st);
+        if (round == 0)  // (an image's tables serve every round)
+            hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
+        hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
+                           ws.totals, ws.tiles);
+        hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,
+                           ws.U);
+        hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
+                           ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.rst, ws.rst_cap);
+        E(kStUnstuff);
+        // Guess-write path (default; ICX_GW=0: guess, count, write)
+        if (gw) {
+            B(kStWrite);
+            hipLaunchKernelGGL(k_gw_lane<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                               ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.X, ws.gw,
+                               ws.rec, lead);
+            E(kStWrite);
+            B(kStEntropy);
+            hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,
+                               ws.clist);
+            hipLaunchKernelGGL(k_gw_count, dim3(n), dim3(512), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
+                               ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair);
+            hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
+                               ws.rec, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
+            hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent);
+            hipLaunchKernelGGL(k_gw_tail, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.crec,
+                               ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.map);
+            hipLaunchKernelGGL(k_gw_map, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.gw, ws.crec,
+                               ws.rec, ws.ent, ws.chunk_next, ws.map);
+            E(kStEntropy);
+        } else {
         B(kStEntropy);
-        hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,
-                           ws.clist);
-        hipLaunchKernelGGL(k_gw_count, dim3(n), dim3(512), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
-                           ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair);
-        hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
-                           ws.rec, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
-        hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent);
-        hipLaunchKernelGGL(k_gw_tail, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.crec,
-                           ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.map);
-        hipLaunchKernelGGL(k_gw_map, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.gw, ws.crec,
-                           ws.rec, ws.ent, ws.chunk_next, ws.map);
+        // guess / count / write: 512-lane workgroups (tables amortised over more lanes), which each
+        // image's lanes fill (k_spec_plan); ICX_BIG_WG=0 selects 256-lane ones (experiments)
+        if (big) {
+            hipLaunchKernelGGL(k_spec_guess<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                               ws.totals, 2, ws.steps, ws.U, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
+            hipLaunchKernelGGL(k_spec_count<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
+                               ws.totals, 2, ws.steps, ws.U, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+        } else {
+            hipLaunchKernelGGL(k_spec_guess<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
+                               ws.totals, 1, ws.steps, ws.U, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
+            hipLaunchKernelGGL(k_spec_count<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
+                               ws.totals, 1, ws.steps, ws.U, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+        }
+        hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y,
+                           ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+        hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
         E(kStEntropy);
         B(kStWrite);
-        // restart intervals (DRI): one write lane per interval, 256-lane workgroups
-        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
+        if (big) {
+            // subsequences: 512-lane workgroups; restart intervals (DRI, typically one per MCU row, so
+            // a few hundred long lanes per image): 256-lane workgroups, which a 512-lane numbering
+            // would leave half idle
+            hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, 1, n, ws.desc, ws.spec,
+                               ws.wg2pre, ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
+        } else {
+            hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 0, n, ws.desc, ws.spec, ws.wgpre,
+                               ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
+        }
         E(kStWrite);
-    } else {
-    B(kStEntropy);
-    // guess / count / write: 512-lane workgroups (tables amortised over more lanes), which each
-    // image's lanes fill (k_spec_plan); ICX_BIG_WG=0 selects 256-lane ones (experiments)
-    static const bool big = std::getenv("ICX_BIG_WG") ? std::atoi(std::getenv("ICX_BIG_WG")) != 0 : true;
-    if (big) {
-        hipLaunchKernelGGL(k_spec_guess<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                           ws.totals, 2, ws.steps, ws.U, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
-        hipLaunchKernelGGL(k_spec_count<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                           ws.totals, 2, ws.steps, ws.U, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
-    } else {
-        hipLaunchKernelGGL(k_spec_guess<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, 1, ws.steps, ws.U, ws.X, ws.rec, ws.nrec, ws.guess_cnt, lead);
-        hipLaunchKernelGGL(k_spec_count<kLanes>, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, 1, ws.steps, ws.U, ws.X, ws.Y, ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
+        }
     }
-    hipLaunchKernelGGL(k_spec_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y,
-                       ws.rec, ws.nrec, ws.guess_cnt, ws.sub, ws.repair);
-    hipLaunchKernelGGL(k_spec_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.sub, ws.ent);
-    E(kStEntropy);
-    B(kStWrite);
-    if (big) {
-        // subsequences: 512-lane workgroups; restart intervals (DRI, typically one per MCU row, so
-        // a few hundred long lanes per image): 256-lane workgroups, which a 512-lane numbering
-        // would leave half idle
-        hipLaunchKernelGGL(k_spec_write<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, 1, n, ws.desc, ws.spec,
-                           ws.wg2pre, ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
+    if (piece == kRoundHead) return;
+    // the round's tail: restart intervals (DRI) -- one write lane per interval, 256-lane workgroups
+    // (the non-big three-pass launch above took them) -- and the round's end
+    if ((gw || big) && piece != kRoundTailNoDri)
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
                            ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
-    } else {
-        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 0, n, ws.desc, ws.spec, ws.wgpre,
-                           ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
-    }
-    E(kStWrite);
-    }
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
 }
 
