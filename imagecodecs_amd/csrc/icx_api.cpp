@@ -39,7 +39,10 @@ struct EventHook;
 // Up to kMaxPipes decode pipelines per batch, each a workspace + a stream: consecutive groups of
 // a call alternate between them, so one group's entropy kernels (latency/LDS-bound) run beside
 // another group's IDCT/convert (memory-bound) instead of after them.
-constexpr int kMaxPipes = 2;
+#ifndef ICX_MAX_PIPES  // (timing experiments: more pipelines)
+#define ICX_MAX_PIPES 2
+#endif
+constexpr int kMaxPipes = ICX_MAX_PIPES;
 struct icx_batch {
     icx_ctx* ctx = nullptr;
     int max_images = 0;
