@@ -26,11 +26,15 @@ int64_t ws_plane_cap(int w, int h) { return ws_coef_cap(w, h) * 64; }
 int64_t ws_tmp_cap(int w, int h) { return ((int64_t)w + 8) * ((int64_t)h + 8); }
 
 // ------------------------------------------------------------------------------ parse
+__device__ __forceinline__ bool fused420_shape(const Desc& d);  // (the 4:2:0 back half, below)
 // One 64-lane workgroup per image: zero the descriptor together, lane 0 walks the markers,
-// then all lanes fill the four 1024-entry fast Huffman tables.
+// then all lanes fill the four 1024-entry fast Huffman tables. `layout` (pinned memory, zeroed by
+// the host before the launch): set when an image that will be decoded is not 4:2:0 in the fused
+// layout -- the host reads it once the group's planning has run and launches the other
+// samplings' back-half kernels only then.
 __global__ __launch_bounds__(64) void k_parse(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                                               const uint64_t* __restrict__ size, Desc* __restrict__ desc, int max_w,
-                                              int max_h, uint64_t out_stride) {
+                                              int max_h, uint64_t out_stride, int32_t* __restrict__ layout) {
     const int i = blockIdx.x;
     if (i >= n) return;
     Desc& d = desc[i];
@@ -44,6 +48,7 @@ __global__ __launch_bounds__(64) void k_parse(int n, const uint8_t* __restrict__
             const int64_t out_bytes = (int64_t)d.W * d.H * (d.nc == 1 ? 1 : d.nc);
             if (d.W > max_w || d.H > max_h || out_bytes > (int64_t)out_stride) d.status = kOutOfMem;
         }
+        if (layout && d.status == kPending && !fused420_shape(d)) *layout = 1;
     }
     __syncthreads();
     if (d.status != kPending) return;
@@ -1259,19 +1264,7 @@ __device__ __forceinline__ bool fused420_shape(const Desc& d) {
 }
 __device__ __forceinline__ bool fused420(const Desc& d) { return d.status == kOk && fused420_shape(d); }
 
-// After k_parse: whether the group holds an image that is not 4:2:0 in the fused420 layout
-// (pinned memory, read by the host once round 0's planning has run). Without one, the back half
-// skips the other samplings' kernels, which would all find no work (a dozen no-op launches per
-// group: ~2% of a C2 step).
-__global__ __launch_bounds__(256) void k_layout(int n, const Desc* __restrict__ desc, int32_t* __restrict__ out) {
-    int other = 0;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        const Desc& d = desc[i];
-        other |= (d.status == kPending || d.status == kOk) && !fused420_shape(d);
-    }
-    other = __syncthreads_or(other);
-    if (threadIdx.x == 0) *out = other;
-}
+
 
 // Lane-pair IDCT of one block: c = the block as stored (zig-zag int16), qw = its component's
 // dequant table (zig-zag, 4 bytes per register), h = the lane's half; rowd[r] = pixels 4h..4h+3
@@ -1821,9 +1814,9 @@ void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const 
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };
     if (part != kFrontRest) {
         B(kStParse);
+        *ws.h_layout = 0;  // (k_parse sets it; the previous group on this workspace was read already)
         hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, st, n, d_data, d_off, d_size, ws.desc, ws.max_w, ws.max_h,
-                           out_stride);
-        hipLaunchKernelGGL(k_layout, dim3(1), dim3(256), 0, st, n, ws.desc, ws.h_layout);
+                           out_stride, ws.h_layout);
         E(kStParse);
     }
     launch_spec_entropy(ws, n, d_data, d_off, st, hook, part);
@@ -1836,8 +1829,8 @@ void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const 
 void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
                         int32_t* d_dims, hipStream_t st, StageHook* hook, bool known_layout) {
     if (n <= 0) return;
-    // the other samplings' kernels, unless the host knows the group has none (k_layout, written
-    // before round 0's planning, whose event the host waits for here)
+    // the other samplings' kernels, unless the host knows the group has none (k_parse's flag,
+    // written before round 0's planning, whose event the host waits for here)
     const bool other = !known_layout || hipEventSynchronize(ws.ev_defer) != hipSuccess || *ws.h_layout != 0;
     auto B = [&](Stage s) { if (hook) hook->begin(s, st); };
     auto E = [&](Stage s) { if (hook) hook->end(s, st); };

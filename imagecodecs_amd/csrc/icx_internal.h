@@ -148,7 +148,7 @@ struct GroupWs {
     GcRec* crec = nullptr;             // [lanes_cap]
     int2* clist = nullptr;             // [lanes_cap] per image, in its lane-record range: (image, lane) to count-decode
     int32_t* h_defer = nullptr;        // pinned [2]: images the last k_spec_plan deferred, and gave restart-interval lanes
-    int32_t* h_layout = nullptr;       // pinned: the group has an image outside the fused 4:2:0 layout (k_layout)
+    int32_t* h_layout = nullptr;       // pinned: the group has an image outside the fused 4:2:0 layout (k_parse)
     hipEvent_t ev_defer = nullptr;     // after round 0's k_spec_plan
 };
 
@@ -221,7 +221,7 @@ enum { kFrontAll = 0, kFrontFirst = 1, kFrontRest = 2 };
 void launch_decode_front(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off,
                          const uint64_t* d_size, uint64_t out_stride, hipStream_t st, StageHook* hook,
                          int part = kFrontAll);
-// known_layout: the host may wait for ws.ev_defer and read ws.h_layout (k_layout) to skip the
+// known_layout: the host may wait for ws.ev_defer and read ws.h_layout (k_parse) to skip the
 // other samplings' kernels when the group has only fused-layout 4:2:0 images.
 void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_stride, int32_t* d_status,
                         int32_t* d_dims, hipStream_t st, StageHook* hook, bool known_layout = false);
