@@ -462,8 +462,9 @@ struct SegView {
         return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(o & 3));
     }
 };
-__device__ __forceinline__ void stage_view(const uint8_t* __restrict__ F, int64_t N, int64_t b0, uint8_t* lds, int lane) {
-    for (int k = lane; k < kStage / 16; k += 64) {
+__device__ __forceinline__ void stage_view(const uint8_t* __restrict__ F, int64_t N, int64_t b0, uint8_t* lds, int lane,
+                                           int nbytes = kStage) {
+    for (int k = lane; k < nbytes / 16; k += 64) {
         const int64_t g = b0 + 16 * k;
         uint4 v;
         if (g >= 0 && g + 16 <= N) {
@@ -682,11 +683,19 @@ __device__ __forceinline__ void tok_counts(uint16_t* G, uint32_t* H, uint32_t& x
 }
 // One wave per segment B (the seam before it): B's two views staged as in k_png_lz77, then
 // the wave walks B's tokens while 12 lanes score each re-parse position.
+// The re-parse may run over the whole of B (a highly compressible segment joins only after a few
+// 258-byte matches); it walks B's first kSeamToks token slots from LDS. (Views of B's first KiB
+// only, cutting A's match where the head had not joined by then, were tried: C5 +1%, but the
+// reference's test.bmp with alpha went 1.042 -> 1.049 of zlib -6.)
+constexpr int kSeamStage = kStage;
+constexpr int kSeamReach = kSeg + kOver;  // (no limit inside the segment)
+constexpr int kSeamToks = 256;
 __global__ __launch_bounds__(256) void k_png_seam(const uint8_t* __restrict__ F, int64_t N, int64_t nseg, int64_t rowlen,
                                                   int bw, const uint16_t* __restrict__ tok,
                                                   const uint32_t* __restrict__ ntok, uint32_t* __restrict__ seam,
                                                   uint16_t* __restrict__ head, int join) {
-    __shared__ __attribute__((aligned(16))) uint8_t views[4][2][kStage];
+    __shared__ __attribute__((aligned(16))) uint8_t views[4][2][kSeamStage];
+    __shared__ uint16_t toks[4][kSeamToks];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t b = (int64_t)blockIdx.x * 4 + wave;
     if (b >= nseg) return;  // wave-uniform; no block barriers below
@@ -704,11 +713,13 @@ __global__ __launch_bounds__(256) void k_png_seam(const uint8_t* __restrict__ F,
         V.fb0 = (s0 - rowlen - kNear) & ~(int64_t)15;
         V.nearp = views[wave][0];
         V.farp = views[wave][1];
-        stage_view(F, N, V.nb0, views[wave][0], lane);
-        stage_view(F, N, V.fb0, views[wave][1], lane);
-        __builtin_amdgcn_wave_barrier();
+        stage_view(F, N, V.nb0, views[wave][0], lane, kSeamStage);
+        stage_view(F, N, V.fb0, views[wave][1], lane, kSeamStage);
         const uint16_t* T = tok + b * kSlots;
         const uint32_t nt = ntok[b];
+        for (int k = lane; k < kSeamToks; k += 64) toks[wave][k] = k < (int)nt ? T[k] : 0;
+        __builtin_amdgcn_wave_barrier();
+        auto tokat = [&](uint32_t i) { return i < (uint32_t)kSeamToks ? (uint32_t)toks[wave][i] : (uint32_t)T[i]; };
         const uint32_t last = (nt >= 2 && (T[nt - 1] & 0x8000u)) ? nt - 2 : nt - 1;  // B's last token slot
         const bool final_seg = b == nseg - 1;
         uint16_t* Hd = head + b * kHead;
@@ -718,7 +729,7 @@ __global__ __launch_bounds__(256) void k_png_seam(const uint8_t* __restrict__ F,
         bool joined = false;
         for (;;) {  // wave-uniform: every lane walks the same tokens
             while (si <= last && bp < q) {
-                const uint32_t t = T[si];
+                const uint32_t t = tokat(si);
                 if (t < 256) {
                     bp += 1;
                     si += 1;
@@ -736,7 +747,7 @@ __global__ __launch_bounds__(256) void k_png_seam(const uint8_t* __restrict__ F,
                 joined = true;
                 break;
             }
-            if ((si > last && !final_seg) || nh + 2 > kHead || !join) break;  // no join: cut A instead
+            if ((si > last && !final_seg) || nh + 2 > kHead || !join || q >= s0 + kSeamReach) break;  // no join: cut A
             int len0, dist0, len1;
             seam_score(V, N, q, cand, lane, len0, dist0, len1);
             if (len0 >= 3 && !(q + 1 < N && len1 > len0)) {
