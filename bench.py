@@ -87,6 +87,8 @@ WORKLOADS = {
                 desc="HDR read: 32 x 4096x4096 Radiance RGBE, new-style RLE scanlines -> 4 floats/px (readHdr)"),
     "hdrflat": dict(n=32, w=4096, h=4096, mode=1,
                     desc="HDR read: 32 x 4096x4096 Radiance RGBE, flat pixel data -> 4 floats/px (readHdr)"),
+    "exr": dict(n=32, w=2048, h=2048,
+                desc="EXR read: 32 x 2048x2048 half RGBA, ZIP scanline chunks -> 4 floats/px (readExr -> tinyexr)"),
 }
 
 # encode stage (icx_encoder_stage_times) -> kernels it times
@@ -571,6 +573,142 @@ def main_hdr(args, wl, world, rank, local):
         dist.destroy_process_group()
 
 
+def _exr_image(seed, w, h):
+    """Synthetic half RGBA EXR (ZIP): smooth waves plus noise, as tools/exr_time.py."""
+    from tools import exrwrite as EW
+    y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+    rng = np.random.default_rng(seed)
+    chans = [(c, (np.sin(x * (0.01 + 0.003 * k)) * np.cos(y * (0.013 + 0.001 * (seed % 5))) * 50 +
+                  rng.normal(0, 0.05, (h, w))).astype(np.float16)) for k, c in enumerate("RGBA")]
+    return EW.write_exr(chans, compression=EW.ZIP)
+
+
+def _oracle_exr(data):
+    from oracle import exr_oracle
+    t0 = time.perf_counter()
+    code, w, h, arr = exr_oracle.decode(data)
+    return time.perf_counter() - t0, code, hashlib.sha256(np.ascontiguousarray(arr).tobytes()).hexdigest(), w * h
+
+
+def main_exr(args, wl, world, rank, local):
+    """OpenEXR read (the row beside readHdr, tinyexr LoadEXRFromMemory): the files resident in HBM,
+    one icx_exr_decode_device_batch per step over the rank's files (headers and offset tables
+    planned on the host from their copies; every file's chunks inflated and un-predicted by one
+    launch, then converted per file on the GPU; floats written to HBM; the call synchronises)."""
+    from imagecodecs_amd import shard
+    n = args.images or wl["n"]
+    W, H = wl["w"], wl["h"]
+    first, _ = shard.shard_range(n * world, world, rank)
+    npool = min(args.pool, n, 4)
+    with ThreadPool(npool) as p:
+        files = p.map(lambda i: _exr_image(1234 + first + i, W, H), range(npool))
+    cpu, cpu_hashes = None, {}
+    if rank == 0 and not args.no_cpu:
+        probe_t = _oracle_exr(files[0])[0]
+        cores = args.cpu_cores
+        per_core = max(1, int(args.cpu_seconds / max(probe_t, 1e-3)))
+        per_core = max(1, min(per_core, 24))
+        sample = [files[i % npool] for i in range(per_core * cores)]
+        import multiprocessing as mp
+        t0 = time.perf_counter()
+        with mp.get_context("fork").Pool(cores) as p:  # (before any GPU use: fork is safe)
+            res = p.map(_oracle_exr, sample)
+        wall = time.perf_counter() - t0
+        cpu = {"value": round(sum(r[3] for r in res) / 1e6 / wall, 2), "unit": "megapixels/s", "cores": cores,
+               "kind": "port", "sample": f"{len(sample)} reads of the same files ({per_core} per core, {cores} processes), "
+                                         f"oracle/ tinyexr restatement (numpy + zlib), {wall:.1f} s wall"}
+        cpu_hashes = {i % npool: r[2] for i, r in enumerate(res)}
+
+    import ctypes as C
+    import torch
+    import imagecodecs_amd as icx
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    fl = [files[i % npool] for i in range(n)]
+    sizes = np.array([len(f) for f in fl], np.int64)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum((sizes[:-1] + 16 + 255) // 256 * 256)  # each file + 16 zero bytes, 256-aligned
+    blob = np.zeros(int(offs[-1] + sizes[-1] + 16), np.uint8)
+    for i, f in enumerate(fl):
+        blob[offs[i]: offs[i] + sizes[i]] = np.frombuffer(f, np.uint8)
+    d_data = torch.from_numpy(blob).to(dev)
+    per_img = W * H * 4
+    d_out = torch.empty(n * per_img, dtype=torch.float32, device=dev)
+    ctx = icx.Context(local)
+    L = icx.lib()
+    hbuf = [C.create_string_buffer(f, len(f)) for f in files]  # host copies the plans read
+    base_in, base_out = d_data.data_ptr(), d_out.data_ptr()
+    hp = (C.c_void_p * n)(*[C.cast(hbuf[i % npool], C.c_void_p) for i in range(n)])
+    dp = (C.c_void_p * n)(*[base_in + int(offs[i]) for i in range(n)])
+    szp = (C.c_size_t * n)(*[int(x) for x in sizes])
+    op = (C.c_void_p * n)(*[base_out + 4 * i * per_img for i in range(n)])
+    ofp = (C.c_size_t * n)(*([per_img] * n))
+    codes, ws_, hs_ = np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int32)
+
+    def step():  # one icx_exr_decode_device_batch over the rank's files
+        rc = L.icx_exr_decode_device_batch(ctx._p, n, hp, dp, szp, op, ofp, codes.ctypes.data, ws_.ctypes.data,
+                                           hs_.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"icx_exr_decode_device_batch: {rc}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ok_all = bool((codes == 0).all())
+    if world > 1:
+        st = torch.from_numpy(codes.copy()).to(dev)
+        ok_all = bool((shard.gather_results(st, dist).cpu().numpy() == 0).all())
+    checked = mismatches = 0
+    for i, hx in cpu_hashes.items():
+        got = hashlib.sha256(d_out[i * per_img: (i + 1) * per_img].cpu().numpy().tobytes()).hexdigest()
+        checked += 1
+        mismatches += got != hx
+    ms_step = elapsed / args.steps * 1e3
+    value = world * n * W * H / 1e6 / (elapsed / args.steps)
+    file_b = float(sizes.sum())
+    alg_bytes = file_b + n * W * H * 16.0  # read the files, write 4 floats per pixel
+    achieved = alg_bytes / (ms_step * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "kernel": "whole batch read (host plans, k_exr_unpack over all chunks, k_exr_convert per file)",
+            "launches_per_step": 1, "alg_bytes_per_launch": round(alg_bytes), "avg_launch_ms": round(ms_step, 4),
+            "pipeline_frac": round(achieved / HBM_PEAK_GBS, 5)}
+    out = {
+        "metric": "megapixels/s OpenEXR read, 2048x2048 half RGBA ZIP -> float", "value": round(value, 2),
+        "unit": "megapixels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f16->f32", "data": "synthetic (waves + noise, tools/exrwrite.py ZIP, seeded)",
+        "config": {"workload": wl["desc"], "images_per_gpu": n, "pool": npool, "width": W, "height": H,
+                   "file_bytes_per_pixel": round(file_b / (n * W * H), 4),
+                   "parallelism": f"dp{world} (images sharded; one RCCL all-gather of statuses after the timed steps)"},
+        "roofline": roof, "cpu_baseline": cpu,
+        "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -617,6 +755,8 @@ def main():
         return main_png(args, wl, world, rank, local)
     if args.workload.startswith("hdr"):
         return main_hdr(args, wl, world, rank, local)
+    if args.workload == "exr":
+        return main_exr(args, wl, world, rank, local)
     n = args.images or wl["n"]
     W, H = wl["w"], wl["h"]
 

@@ -108,6 +108,8 @@ _SIGS = {
     "icx_multi_shard": (_i32, [_vp, _i32, _i32, _vp]),
     "icx_exr_probe": (_i32, [_vp, _sz, C.POINTER(_i32), C.POINTER(_i32)]),
     "icx_exr_decode": (_i32, [_vp, _vp, _sz, C.POINTER(_vp), C.POINTER(_i32), C.POINTER(_i32)]),
+    "icx_exr_decode_device": (_i32, [_vp, _vp, _vp, _sz, _vp, _sz, C.POINTER(_i32), C.POINTER(_i32)]),
+    "icx_exr_decode_device_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 # icx_record (include/icx.h): per-image result record gathered across devices / ranks
@@ -275,6 +277,40 @@ class Context:
             arr = np.frombuffer(C.string_at(out.value, n * 4), np.float32).reshape(h.value, w.value, 4).copy()
             lib().icx_free(out)
         return code, w.value, h.value, arr
+
+    def exr_decode_device(self, data: bytes, d_data: int, d_out: int, out_floats: int):
+        """icx_exr_decode_device: the file resident on the device at ``d_data`` (its ``len(data)``
+        bytes + 16 zero bytes; ``data`` is the host copy the header is planned from), RGBA floats to
+        device memory ``d_out`` -> (code, w, h)."""
+        buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+        w, h = C.c_int(), C.c_int()
+        code = lib().icx_exr_decode_device(self._p, buf, C.c_void_p(d_data), len(data), C.c_void_p(d_out), out_floats,
+                                           C.byref(w), C.byref(h))
+        if code == EXR_INTERNAL_ERR:
+            raise ICXError("icx_exr_decode_device: " + _err(self._p))
+        return code, w.value, h.value
+
+    def exr_decode_device_batch(self, datas, d_ptrs, d_outs, out_floats):
+        """icx_exr_decode_device_batch over n files (host copies ``datas``, device copies at
+        ``d_ptrs`` each followed by 16 zero bytes, outputs at ``d_outs`` with ``out_floats`` room
+        each) -> (codes, widths, heights) as int32 arrays."""
+        n = len(datas)
+        bufs = [C.create_string_buffer(bytes(d), max(1, len(d))) for d in datas]
+        hp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in bufs])
+        dp = (C.c_void_p * n)(*d_ptrs)
+        sz = (C.c_size_t * n)(*[len(d) for d in datas])
+        op = (C.c_void_p * n)(*d_outs)
+        of = (C.c_size_t * n)(*out_floats)
+        codes = np.zeros(n, np.int32)
+        ws = np.zeros(n, np.int32)
+        hs = np.zeros(n, np.int32)
+        rc = lib().icx_exr_decode_device_batch(self._p, n, hp, dp, sz, op, of, codes.ctypes.data, ws.ctypes.data,
+                                               hs.ctypes.data)
+        if rc == EXR_INTERNAL_ERR:
+            raise ICXError("icx_exr_decode_device_batch: " + _err(self._p))
+        if rc != 0:
+            raise ICXError(f"icx_exr_decode_device_batch: code {rc}")
+        return codes, ws, hs
 
     def png_encode(self, width: int, height: int, d: int, src: bytes):
         """PNG bytes of an RGB8 (d=3) / RGBA8 (d=4) image (png_encoder::saveToFile), or None."""

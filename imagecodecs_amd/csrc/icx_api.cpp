@@ -32,6 +32,7 @@ struct icx_ctx {
     // staging for one-image calls
     uint8_t* d_in = nullptr;
     size_t d_in_cap = 0;
+    ExrWs* exr = nullptr;  // grow-only EXR read buffers (icx_exr.hip)
 };
 
 struct EventHook;
@@ -152,6 +153,7 @@ void icx_destroy(icx_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->single) icx_batch_destroy(c->single);
     if (c->d_in) (void)hipFree(c->d_in);
+    if (c->exr) exr_ws_destroy(c->exr);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -993,12 +995,66 @@ int icx_exr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out, 
     std::string err;
     int rc;
     try {  // (nothing may cross the C ABI: a host allocation failure is an internal error)
-        rc = exr_decode(ctx->stream, data, size, out, &ww, &hh, err);
+        if (!ctx->exr) ctx->exr = exr_ws_create();
+        rc = exr_decode(ctx->stream, *ctx->exr, data, size, nullptr, nullptr, 0, out, &ww, &hh, err);
     } catch (const std::exception& e) {
         err = std::string("icx_exr_decode: ") + e.what();
         rc = ICX_EXR_INTERNAL_ERR;
     }
     if (rc == ICX_EXR_INTERNAL_ERR) ctx->err = err.empty() ? "icx_exr_decode: HIP failure" : err;
+    if (rc == ICX_EXR_SUCCESS) {
+        if (w) *w = ww;
+        if (h) *h = hh;
+    }
+    return rc;
+}
+
+int icx_exr_decode_device_batch(icx_ctx* ctx, int n, const uint8_t* const* data, const uint8_t* const* d_data,
+                                const size_t* sizes, float* const* d_out, const size_t* out_floats, int32_t* codes,
+                                int32_t* widths, int32_t* heights) {
+    if (!ctx) return ICX_EXR_INTERNAL_ERR;
+    if (n < 0 || (n > 0 && (!data || !d_data || !sizes || !d_out || !out_floats || !codes || !widths || !heights)))
+        return ICX_EXR_INVALID_ARGUMENT;
+    for (int i = 0; i < n; ++i)
+        if (!data[i] || !d_data[i] || !d_out[i]) return ICX_EXR_INVALID_ARGUMENT;
+    if (n == 0) return ICX_EXR_SUCCESS;
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_EXR_INTERNAL_ERR);
+    const RoctxRange range("icx_exr_decode_device_batch");
+    std::string err;
+    int rc;
+    try {
+        if (!ctx->exr) ctx->exr = exr_ws_create();
+        rc = exr_decode_batch(ctx->stream, *ctx->exr, n, data, d_data, sizes, d_out, out_floats, codes, widths, heights, err);
+    } catch (const std::exception& e) {
+        err = std::string("icx_exr_decode_device_batch: ") + e.what();
+        rc = ICX_EXR_INTERNAL_ERR;
+    }
+    if (rc != 0) {
+        ctx->err = err.empty() ? "icx_exr_decode_device_batch: HIP failure" : err;
+        return ICX_EXR_INTERNAL_ERR;
+    }
+    return ICX_EXR_SUCCESS;
+}
+
+int icx_exr_decode_device(icx_ctx* ctx, const uint8_t* data, const uint8_t* d_data, size_t size, float* d_out,
+                          size_t out_floats, int* w, int* h) {
+    if (w) *w = 0;
+    if (h) *h = 0;
+    if (!ctx) return ICX_EXR_INTERNAL_ERR;
+    if (!data || !d_data || !d_out) return ICX_EXR_INVALID_ARGUMENT;
+    ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_EXR_INTERNAL_ERR);
+    const RoctxRange range("icx_exr_decode_device");
+    int ww = 0, hh = 0;
+    std::string err;
+    int rc;
+    try {
+        if (!ctx->exr) ctx->exr = exr_ws_create();
+        rc = exr_decode(ctx->stream, *ctx->exr, data, size, d_data, d_out, out_floats, nullptr, &ww, &hh, err);
+    } catch (const std::exception& e) {
+        err = std::string("icx_exr_decode_device: ") + e.what();
+        rc = ICX_EXR_INTERNAL_ERR;
+    }
+    if (rc == ICX_EXR_INTERNAL_ERR) ctx->err = err.empty() ? "icx_exr_decode_device: HIP failure" : err;
     if (rc == ICX_EXR_SUCCESS) {
         if (w) *w = ww;
         if (h) *h = hh;

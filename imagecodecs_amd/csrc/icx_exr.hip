@@ -31,7 +31,8 @@
 
 namespace icx {
 
-// Per compressed chunk: decompress (lane 0), then the predictor as a workgroup prefix sum.
+// Per compressed chunk (of any image of the call: `file` is the first file's device address, a
+// chunk's own at + c.base): decompress (lane 0), then the predictor as a workgroup prefix sum.
 __global__ __launch_bounds__(256) void k_exr_unpack(const uint8_t* __restrict__ file, ExrChunk* __restrict__ ch,
                                                     const int32_t* __restrict__ list, uint8_t* __restrict__ scratch,
                                                     int32_t* __restrict__ fail) {
@@ -44,14 +45,15 @@ __global__ __launch_bounds__(256) void k_exr_unpack(const uint8_t* __restrict__ 
     if (threadIdx.x == 0) {
         int64_t m = 0;
         bool ok;
+        const uint8_t* f = file + c.base + c.src;
         if (c.mode == 1) {
-            ok = exr_inflate(file + c.src, c.len, t, c.out_len, &m, st, win);
+            ok = exr_inflate(f, c.len, t, c.out_len, &m, st, win);
         } else {
-            ok = exr_unrle(file + c.src, c.len, t, c.out_len);
+            ok = exr_unrle(f, c.len, t, c.out_len);
             m = c.out_len;
         }
         if (!ok) {
-            atomicOr(fail, 1);
+            atomicOr(fail + c.img, 1);
             m = 0;
         }
         produced = m;
@@ -158,86 +160,209 @@ __global__ __launch_bounds__(256) void k_exr_convert(const uint8_t* __restrict__
         reinterpret_cast<uint4*>(out)[px] = exr_pixel(file, scratch, ch, map, tile_h, ctype, coffs, cv, px);
 }
 
-// The whole read: returns a tinyexr code; *out_rgba = malloc'd w*h*4 floats on success.
-int exr_decode(hipStream_t st, const uint8_t* data, size_t size, float** out_rgba, int* width, int* height,
-               std::string& err) {
-    ExrPlan P;
-    const int rc = exr_plan(data, (int64_t)size, P);
-    if (rc != kExrOk) return rc;
-    const int64_t npx = (int64_t)P.w * P.h;
-    uint8_t *d_file = nullptr, *d_scr = nullptr;
-    ExrChunk* d_ch = nullptr;
-    int2* d_map = nullptr;
-    int32_t *d_list = nullptr, *d_plist = nullptr, *d_fail = nullptr, *d_th = nullptr, *d_ty = nullptr, *d_of = nullptr;
-    float* d_out = nullptr;
-    std::vector<int32_t> list, plist;  // inflate / RLE chunks; PIZ chunks
-    for (size_t k = 0; k < P.chunks.size(); ++k) {
-        if (P.chunks[k].mode == 3) plist.push_back((int32_t)k);
-        else if (P.chunks[k].mode != 0) list.push_back((int32_t)k);
+// Grow-only device buffers of one context's EXR reads (icx_ctx::exr): one arena carved per call
+// into the file copy (host-input reads), scratch, chunk table, maps, work lists, failure flags and
+// output, plus pinned failure flags.
+struct ExrWs {
+    uint8_t* arena = nullptr;
+    size_t cap = 0;
+    int32_t* h_fail = nullptr;
+    size_t h_cap = 0;
+    ~ExrWs() {
+        if (arena) (void)hipFree(arena);
+        if (h_fail) (void)hipHostFree(h_fail);
     }
-    std::vector<int32_t> th = P.tile_h.empty() ? std::vector<int32_t>(1, 0) : P.tile_h;
-    int res = -100;
-    int32_t fail = 0;
-    float* host = nullptr;
-    const size_t nout = (size_t)npx * 4 * sizeof(float);
-    auto ok = [&](hipError_t e) { return e == hipSuccess; };
-    // (the file + 16 zero bytes: the PIZ reader loads whole aligned 16-byte words)
-    if (ok(hipMalloc(&d_file, size + 16)) && ok(hipMemsetAsync(d_file + size, 0, 16, st)) &&
-        ok(hipMalloc(&d_scr, (size_t)std::max<int64_t>(16, P.scratch))) &&
-        ok(hipMalloc(&d_ch, sizeof(ExrChunk) * std::max<size_t>(1, P.chunks.size()))) &&
-        ok(hipMalloc(&d_map, sizeof(int2) * P.map.size())) &&
-        ok(hipMalloc(&d_list, sizeof(int32_t) * std::max<size_t>(1, list.size()))) &&
-        ok(hipMalloc(&d_plist, sizeof(int32_t) * std::max<size_t>(1, plist.size()))) &&
-        ok(hipMalloc(&d_fail, sizeof(int32_t))) && ok(hipMalloc(&d_th, sizeof(int32_t) * th.size())) &&
-        ok(hipMalloc(&d_ty, sizeof(int32_t) * P.nch)) && ok(hipMalloc(&d_of, sizeof(int32_t) * P.nch)) &&
-        ok(hipMalloc(&d_out, nout)) &&
-        ok(hipMemcpyAsync(d_file, data, size, hipMemcpyHostToDevice, st)) &&
-        ok(hipMemcpyAsync(d_ch, P.chunks.data(), sizeof(ExrChunk) * P.chunks.size(), hipMemcpyHostToDevice, st)) &&
-        ok(hipMemcpyAsync(d_map, P.map.data(), sizeof(int2) * P.map.size(), hipMemcpyHostToDevice, st)) &&
-        ok(hipMemcpyAsync(d_list, list.data(), sizeof(int32_t) * list.size(), hipMemcpyHostToDevice, st)) &&
-        ok(hipMemcpyAsync(d_plist, plist.data(), sizeof(int32_t) * plist.size(), hipMemcpyHostToDevice, st)) &&
-        ok(hipMemcpyAsync(d_th, th.data(), sizeof(int32_t) * th.size(), hipMemcpyHostToDevice, st)) &&
-        ok(hipMemcpyAsync(d_ty, P.type.data(), sizeof(int32_t) * P.nch, hipMemcpyHostToDevice, st)) &&
-        ok(hipMemcpyAsync(d_of, P.offs.data(), sizeof(int32_t) * P.nch, hipMemcpyHostToDevice, st)) &&
-        ok(hipMemsetAsync(d_fail, 0, sizeof(int32_t), st))) {
-        if (!list.empty()) hipLaunchKernelGGL(k_exr_unpack, dim3((unsigned)list.size()), dim3(256), 0, st, d_file, d_ch, d_list, d_scr, d_fail);
-        if (!plist.empty())
-            hipLaunchKernelGGL(k_exr_piz, dim3((unsigned)plist.size()), dim3(256), 0, st, d_file, (int64_t)size, d_ch, d_plist,
-                               d_ty, P.nch, d_scr);
-        ExrConv cv{};
-        cv.w = P.w; cv.h = P.h; cv.nch = P.nch; cv.pds = P.pds; cv.tiled = P.tiled; cv.tx = P.tx; cv.ty = P.ty;
-        cv.ntx = P.ntx; cv.line_order = P.line_order;
-        for (int k = 0; k < 4; ++k) cv.src[k] = P.src[k];
-        const unsigned grid = (unsigned)std::min<int64_t>(8192, (npx + 255) / 256);
-        hipLaunchKernelGGL(k_exr_convert, dim3(std::max(1u, grid)), dim3(256), 0, st, d_file, d_scr, d_ch, d_map, d_th, d_ty,
-                           d_of, cv, d_out);
-        if (ok(hipGetLastError()) && ok(hipMemcpyAsync(&fail, d_fail, sizeof(int32_t), hipMemcpyDeviceToHost, st)) &&
-            ok(hipStreamSynchronize(st))) {
-            if (fail) {
-                res = kExrInvalidData;  // "Invalid/Corrupted data found when decoding pixels" (:5512-5524)
-            } else {
-                host = (float*)std::malloc(nout);
-                if (host && ok(hipMemcpy(host, d_out, nout, hipMemcpyDeviceToHost))) {
-                    *out_rgba = host;
-                    *width = P.w;
-                    *height = P.h;
-                    host = nullptr;
-                    res = kExrOk;
-                } else {
-                    err = "icx_exr_decode: host allocation or copy failed";
-                }
-            }
-        } else {
-            err = "icx_exr_decode: HIP failure";
+};
+ExrWs* exr_ws_create() { return new ExrWs(); }
+void exr_ws_destroy(ExrWs* w) { delete w; }
+
+// n reads in one pass: every file planned on the host (header, offset table, chunk headers), then
+// one k_exr_unpack launch over all files' compressed chunks (each workgroup one chunk, so a batch
+// keeps thousands in flight where one 2048^2 file has 128), PIZ chunks per file, and a conversion
+// per file. d_data[i]: file i on the device (sizes[i] bytes + 16 zero bytes), or nullptr when
+// `upload` (then it is copied from data[i] into the arena). d_out[i]: its floats, or nullptr (into
+// the arena; *arena_out[i] then says where). codes[i]: tinyexr's code per file. Returns 0, or -100
+// with err set (a device failure, or an output buffer too small).
+static int exr_batch(hipStream_t st, ExrWs& ws, int n, const uint8_t* const* data, const uint8_t* const* d_data_in,
+                     const size_t* sizes, float* const* d_out_in, const size_t* out_floats, int32_t* codes,
+                     int32_t* widths, int32_t* heights, float** arena_out, std::string& err) {
+    std::vector<ExrPlan> P((size_t)n);
+    std::vector<int64_t> cbase((size_t)n, 0), sbase((size_t)n, 0);
+    std::vector<ExrChunk> chunks;
+    std::vector<int32_t> list;                            // inflate / RLE chunks (global indices)
+    std::vector<std::vector<int32_t>> plist((size_t)n);   // PIZ chunks per file (global indices)
+    int64_t scr = 0;
+    for (int i = 0; i < n; ++i) {
+        widths[i] = heights[i] = 0;
+        codes[i] = exr_plan(data[i], (int64_t)sizes[i], P[i]);
+        if (codes[i] != kExrOk) continue;
+        if (d_out_in && d_out_in[i] && (size_t)P[i].w * P[i].h * 4 > out_floats[i]) {
+            err = "icx_exr_decode_device: output buffer too small";
+            return -100;
         }
-    } else {
-        err = "icx_exr_decode: device allocation or copy failed";
+        cbase[i] = (int64_t)chunks.size();
+        sbase[i] = scr;
+        for (size_t k = 0; k < P[i].chunks.size(); ++k) {
+            ExrChunk c = P[i].chunks[k];
+            c.scratch += scr;
+            c.piz_work += scr;
+            c.img = i;
+            const int32_t g = (int32_t)chunks.size();
+            if (c.mode == 3) plist[(size_t)i].push_back(g);
+            else if (c.mode != 0) list.push_back(g);
+            chunks.push_back(c);
+        }
+        scr += (P[i].scratch + 255) / 256 * 256;
     }
-    std::free(host);
-    for (void* q : {(void*)d_file, (void*)d_scr, (void*)d_ch, (void*)d_map, (void*)d_list, (void*)d_plist, (void*)d_fail, (void*)d_th,
-                    (void*)d_ty, (void*)d_of, (void*)d_out})
-        if (q) (void)hipFree(q);
-    return res;
+    // arena layout (256-byte aligned pieces)
+    size_t at = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = at;
+        at += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    std::vector<size_t> o_file((size_t)n, 0), o_map((size_t)n), o_th((size_t)n), o_ty((size_t)n), o_of((size_t)n),
+        o_plist((size_t)n), o_out((size_t)n, 0);
+    std::vector<std::vector<int32_t>> th((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        if (!d_data_in) o_file[i] = take(sizes[i] + 16);
+        if (codes[i] != kExrOk) continue;
+        th[i] = P[i].tile_h.empty() ? std::vector<int32_t>(1, 0) : P[i].tile_h;
+        o_map[i] = take(sizeof(int2) * std::max<size_t>(1, P[i].map.size()));
+        o_th[i] = take(sizeof(int32_t) * th[i].size());
+        o_ty[i] = take(sizeof(int32_t) * P[i].nch);
+        o_of[i] = take(sizeof(int32_t) * P[i].nch);
+        o_plist[i] = take(sizeof(int32_t) * std::max<size_t>(1, plist[i].size()));
+        if (!d_out_in || !d_out_in[i]) o_out[i] = take((size_t)P[i].w * P[i].h * 4 * sizeof(float));
+    }
+    const size_t o_scr = take((size_t)std::max<int64_t>(16, scr));
+    const size_t o_ch = take(sizeof(ExrChunk) * std::max<size_t>(1, chunks.size()));
+    const size_t o_list = take(sizeof(int32_t) * std::max<size_t>(1, list.size()));
+    const size_t o_fail = take(sizeof(int32_t) * (size_t)std::max(1, n));
+    auto ok = [&](hipError_t e) { return e == hipSuccess; };
+    if (at > ws.cap) {
+        if (ws.arena) (void)hipFree(ws.arena);
+        ws.arena = nullptr;
+        ws.cap = 0;
+        if (!ok(hipMalloc(&ws.arena, at))) {
+            err = "icx_exr_decode: device allocation failed";
+            return -100;
+        }
+        ws.cap = at;
+    }
+    if ((size_t)std::max(1, n) > ws.h_cap) {
+        if (ws.h_fail) (void)hipHostFree(ws.h_fail);
+        ws.h_fail = nullptr;
+        ws.h_cap = 0;
+        if (!ok(hipHostMalloc(&ws.h_fail, sizeof(int32_t) * (size_t)std::max(1, n), hipHostMallocDefault))) {
+            ws.h_fail = nullptr;
+            err = "icx_exr_decode: pinned allocation failed";
+            return -100;
+        }
+        ws.h_cap = (size_t)std::max(1, n);
+    }
+    uint8_t* A = ws.arena;
+    std::vector<const uint8_t*> dfile((size_t)n);
+    for (int i = 0; i < n; ++i) dfile[i] = d_data_in ? d_data_in[i] : A + o_file[i];
+    // chunk file bases relative to the first file's device address (k_exr_unpack)
+    for (ExrChunk& c : chunks) c.base = (int64_t)(dfile[(size_t)c.img] - dfile[0]);
+    uint8_t* d_scr = A + o_scr;
+    ExrChunk* d_ch = reinterpret_cast<ExrChunk*>(A + o_ch);
+    int32_t* d_list = reinterpret_cast<int32_t*>(A + o_list);
+    int32_t* d_fail = reinterpret_cast<int32_t*>(A + o_fail);
+    bool good = true;
+    // (a file + 16 zero bytes: the PIZ reader loads whole aligned 16-byte words)
+    for (int i = 0; i < n && good && !d_data_in; ++i)
+        good = ok(hipMemcpyAsync(A + o_file[i], data[i], sizes[i], hipMemcpyHostToDevice, st)) &&
+               ok(hipMemsetAsync(A + o_file[i] + sizes[i], 0, 16, st));
+    good = good && ok(hipMemcpyAsync(d_ch, chunks.data(), sizeof(ExrChunk) * chunks.size(), hipMemcpyHostToDevice, st)) &&
+           ok(hipMemcpyAsync(d_list, list.data(), sizeof(int32_t) * list.size(), hipMemcpyHostToDevice, st)) &&
+           ok(hipMemsetAsync(d_fail, 0, sizeof(int32_t) * (size_t)std::max(1, n), st));
+    for (int i = 0; i < n && good; ++i) {
+        if (codes[i] != kExrOk) continue;
+        good = ok(hipMemcpyAsync(A + o_map[i], P[i].map.data(), sizeof(int2) * P[i].map.size(), hipMemcpyHostToDevice, st)) &&
+               ok(hipMemcpyAsync(A + o_th[i], th[i].data(), sizeof(int32_t) * th[i].size(), hipMemcpyHostToDevice, st)) &&
+               ok(hipMemcpyAsync(A + o_ty[i], P[i].type.data(), sizeof(int32_t) * P[i].nch, hipMemcpyHostToDevice, st)) &&
+               ok(hipMemcpyAsync(A + o_of[i], P[i].offs.data(), sizeof(int32_t) * P[i].nch, hipMemcpyHostToDevice, st)) &&
+               ok(hipMemcpyAsync(A + o_plist[i], plist[i].data(), sizeof(int32_t) * plist[i].size(), hipMemcpyHostToDevice, st));
+    }
+    if (!good) {
+        err = "icx_exr_decode: device copy failed";
+        return -100;
+    }
+    if (!list.empty() && n > 0)
+        hipLaunchKernelGGL(k_exr_unpack, dim3((unsigned)list.size()), dim3(256), 0, st, dfile[0], d_ch, d_list, d_scr, d_fail);
+    for (int i = 0; i < n; ++i) {
+        if (codes[i] != kExrOk || plist[i].empty()) continue;
+        hipLaunchKernelGGL(k_exr_piz, dim3((unsigned)plist[i].size()), dim3(256), 0, st, dfile[i], (int64_t)sizes[i], d_ch,
+                           reinterpret_cast<const int32_t*>(A + o_plist[i]), reinterpret_cast<const int32_t*>(A + o_ty[i]),
+                           P[i].nch, d_scr);
+    }
+    for (int i = 0; i < n; ++i) {
+        if (codes[i] != kExrOk) continue;
+        const int64_t npx = (int64_t)P[i].w * P[i].h;
+        float* out = d_out_in && d_out_in[i] ? d_out_in[i] : reinterpret_cast<float*>(A + o_out[i]);
+        if (arena_out) arena_out[i] = out;
+        ExrConv cv{};
+        cv.w = P[i].w; cv.h = P[i].h; cv.nch = P[i].nch; cv.pds = P[i].pds; cv.tiled = P[i].tiled; cv.tx = P[i].tx;
+        cv.ty = P[i].ty; cv.ntx = P[i].ntx; cv.line_order = P[i].line_order;
+        for (int k = 0; k < 4; ++k) cv.src[k] = P[i].src[k];
+        const unsigned grid = (unsigned)std::min<int64_t>(8192, (npx + 255) / 256);
+        hipLaunchKernelGGL(k_exr_convert, dim3(std::max(1u, grid)), dim3(256), 0, st, dfile[i], d_scr, d_ch + cbase[i],
+                           reinterpret_cast<const int2*>(A + o_map[i]), reinterpret_cast<const int32_t*>(A + o_th[i]),
+                           reinterpret_cast<const int32_t*>(A + o_ty[i]), reinterpret_cast<const int32_t*>(A + o_of[i]), cv,
+                           out);
+    }
+    if (!ok(hipGetLastError()) ||
+        !ok(hipMemcpyAsync(ws.h_fail, d_fail, sizeof(int32_t) * (size_t)std::max(1, n), hipMemcpyDeviceToHost, st)) ||
+        !ok(hipStreamSynchronize(st))) {
+        err = "icx_exr_decode: HIP failure";
+        return -100;
+    }
+    for (int i = 0; i < n; ++i) {
+        if (codes[i] != kExrOk) continue;
+        if (ws.h_fail[i]) {
+            codes[i] = kExrInvalidData;  // "Invalid/Corrupted data found when decoding pixels" (:5512-5524)
+        } else {
+            widths[i] = P[i].w;
+            heights[i] = P[i].h;
+        }
+    }
+    return 0;
+}
+
+// One read. Host input (d_file == nullptr): the file is copied to the device, and on success
+// *out_rgba = malloc'd w*h*4 floats. Device input: d_file holds the same size bytes plus 16 zero
+// bytes, and the floats go to d_out (out_floats of room). Returns a tinyexr code.
+int exr_decode(hipStream_t st, ExrWs& ws, const uint8_t* data, size_t size, const uint8_t* d_file, float* d_out,
+               size_t out_floats, float** out_rgba, int* width, int* height, std::string& err) {
+    int32_t code = 0, w = 0, h = 0;
+    float* aout = nullptr;
+    float* const outs[1] = {d_out};
+    const uint8_t* const ins[1] = {d_file};
+    const int rc = exr_batch(st, ws, 1, &data, d_file ? ins : nullptr, &size, d_file ? outs : nullptr, &out_floats, &code,
+                             &w, &h, &aout, err);
+    if (rc != 0) return rc;
+    if (code != kExrOk) return code;
+    if (!d_file) {
+        const size_t nout = (size_t)w * h * 4 * sizeof(float);
+        float* host = (float*)std::malloc(std::max<size_t>(1, nout));
+        if (!host || hipMemcpy(host, aout, nout, hipMemcpyDeviceToHost) != hipSuccess) {
+            std::free(host);
+            err = "icx_exr_decode: host allocation or copy failed";
+            return -100;
+        }
+        *out_rgba = host;
+    }
+    *width = w;
+    *height = h;
+    return kExrOk;
+}
+
+int exr_decode_batch(hipStream_t st, ExrWs& ws, int n, const uint8_t* const* data, const uint8_t* const* d_data,
+                     const size_t* sizes, float* const* d_out, const size_t* out_floats, int32_t* codes, int32_t* widths,
+                     int32_t* heights, std::string& err) {
+    return exr_batch(st, ws, n, data, d_data, sizes, d_out, out_floats, codes, widths, heights, nullptr, err);
 }
 
 int exr_probe(const uint8_t* data, size_t size, int* width, int* height) {

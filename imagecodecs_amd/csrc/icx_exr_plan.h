@@ -41,7 +41,8 @@ struct ExrChunk {
     int64_t piz_huf;    // PIZ: file offset of the Huffman data
     int64_t piz_work;   // PIZ: scratch offset of the channel planes (out_len), then its PizWork
     int32_t piz_mnmx;   // PIZ: minNonZero | maxNonZero << 16
-    int32_t pad_;
+    int32_t img;        // batch reads: the chunk's image (its failure flag)
+    int64_t base;       // batch reads: its file's device address minus the first file's (k_exr_unpack)
 };
 
 struct ExrPlan {

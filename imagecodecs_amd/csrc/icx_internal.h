@@ -305,8 +305,14 @@ void launch_hdr_decode(const HdrWs& ws, int n, const uint8_t* d_data, const uint
 
 // ---- OpenEXR read (icx_exr.hip) ----
 // tinyexr's LoadEXRFromMemory; returns its code (-100: HIP failure, err says which).
-int exr_decode(hipStream_t st, const uint8_t* data, size_t size, float** out_rgba, int* width, int* height,
-               std::string& err);
+struct ExrWs;
+ExrWs* exr_ws_create();
+void exr_ws_destroy(ExrWs* w);
+int exr_decode(hipStream_t st, ExrWs& ws, const uint8_t* data, size_t size, const uint8_t* d_file, float* d_out,
+               size_t out_floats, float** out_rgba, int* width, int* height, std::string& err);
+int exr_decode_batch(hipStream_t st, ExrWs& ws, int n, const uint8_t* const* data, const uint8_t* const* d_data,
+                     const size_t* sizes, float* const* d_out, const size_t* out_floats, int32_t* codes, int32_t* widths,
+                     int32_t* heights, std::string& err);
 int exr_probe(const uint8_t* data, size_t size, int* width, int* height);
 
 }  // namespace icx

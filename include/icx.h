@@ -297,6 +297,22 @@ int icx_exr_probe(const uint8_t* data, size_t size, int* width, int* height);
 /* One image, host in / host out: *out_rgba receives a malloc()'d width*height*4 float buffer
  * (free with icx_free). Returns an icx_exr_result. */
 int icx_exr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out_rgba, int* width, int* height);
+/* The same read with the file already resident on the device (batch pipelines, benchmarks): the
+ * header and offset table are planned from the host copy `data`; the kernels read the device copy
+ * `d_data` (the same `size` bytes followed by 16 zero bytes) and write width*height*4 floats to
+ * `d_out` (room for `out_floats`; too little -> ICX_EXR_INTERNAL_ERR). Synchronises with the
+ * context's stream; returns an icx_exr_result. */
+int icx_exr_decode_device(icx_ctx* ctx, const uint8_t* data, const uint8_t* d_data, size_t size, float* d_out,
+                          size_t out_floats, int* width, int* height);
+/* n such reads in one call: every file is planned on the host, then the compressed chunks of all
+ * n files are decompressed by one launch (a workgroup per chunk) before each file is converted --
+ * one 2048^2 ZIP file has 128 chunks, a batch keeps thousands in flight. codes[i] gets file i's
+ * icx_exr_result, widths[i] / heights[i] its size (0 when it fails). Returns ICX_EXR_SUCCESS when
+ * the call ran (per-file results in codes), ICX_EXR_INVALID_ARGUMENT for a null pointer, or
+ * ICX_EXR_INTERNAL_ERR (HIP failure, an output buffer too small; see icx_last_error). */
+int icx_exr_decode_device_batch(icx_ctx* ctx, int n, const uint8_t* const* data, const uint8_t* const* d_data,
+                                const size_t* sizes, float* const* d_out, const size_t* out_floats, int32_t* codes,
+                                int32_t* widths, int32_t* heights);
 
 #ifdef __cplusplus
 }

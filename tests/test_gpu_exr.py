@@ -110,3 +110,63 @@ def test_image_read_exr(tmp_path):
     q.write_bytes(open(os.path.join(EXR, "zip_bad_adler.exr"), "rb").read())
     with pytest.raises(RuntimeError):
         icx.Image().read(str(q))
+
+
+def test_exr_decode_device_matches_host_entry(ctx):
+    """icx_exr_decode_device (file resident on the device, floats to device memory) returns the
+    host entry's code and the same float bits on every fixture that decodes (scanline, tiled,
+    PIZ, mip / rip levels) and on those whose pixel data fails; an output buffer one float short is
+    a call-level error."""
+    import torch
+    dev = torch.device("cuda", 0)
+    for name in sorted(MAN):
+        data = open(os.path.join(EXR, name), "rb").read()
+        code, w, h, img = ctx.exr_decode(data)
+        if code not in (0, icx.EXR_INVALID_DATA):
+            continue
+        d_file = torch.zeros(len(data) + 16, dtype=torch.uint8, device=dev)
+        d_file[:len(data)] = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
+        pw, ph = icx.exr_probe(data)[1:3] if code != 0 else (w, h)
+        n = max(1, pw * ph * 4)
+        d_out = torch.full((n,), -1.0, dtype=torch.float32, device=dev)
+        c2, w2, h2 = ctx.exr_decode_device(data, d_file.data_ptr(), d_out.data_ptr(), n)
+        assert c2 == code, name
+        if code == 0:
+            assert (w2, h2) == (w, h), name
+            got = d_out.cpu().numpy().reshape(h, w, 4)
+            assert sha(got) == sha(img), name
+    data = open(os.path.join(EXR, "scan_zip_half.exr"), "rb").read()
+    code, w, h, _ = ctx.exr_decode(data)
+    assert code == 0
+    d_file = torch.zeros(len(data) + 16, dtype=torch.uint8, device=dev)
+    d_file[:len(data)] = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
+    d_out = torch.zeros(w * h * 4, dtype=torch.float32, device=dev)
+    with pytest.raises(icx.ICXError):
+        ctx.exr_decode_device(data, d_file.data_ptr(), d_out.data_ptr(), w * h * 4 - 1)
+
+
+def test_exr_decode_device_batch_matches_single(ctx):
+    """icx_exr_decode_device_batch over every fixture at once (planning failures, pixel-data
+    failures, scanline / tiled / PIZ / level files mixed in one call): per-file codes, sizes and
+    float bits equal the single-file host entry's."""
+    import torch
+    dev = torch.device("cuda", 0)
+    names = sorted(MAN)
+    datas = [open(os.path.join(EXR, nm), "rb").read() for nm in names]
+    ref = [ctx.exr_decode(d) for d in datas]
+    files, outs, room = [], [], []
+    for d, nm in zip(datas, names):
+        f = torch.zeros(len(d) + 16, dtype=torch.uint8, device=dev)
+        if len(d):
+            f[:len(d)] = torch.from_numpy(np.frombuffer(d, np.uint8).copy()).to(dev)
+        files.append(f)
+        pw, ph = icx.exr_probe(d)[1:3]
+        n = max(1, pw * ph * 4)
+        outs.append(torch.full((n,), -1.0, dtype=torch.float32, device=dev))
+        room.append(n)
+    codes, ws, hs = ctx.exr_decode_device_batch(datas, [f.data_ptr() for f in files], [o.data_ptr() for o in outs], room)
+    for k, (nm, (code, w, h, img)) in enumerate(zip(names, ref)):
+        assert codes[k] == code, nm
+        if code == 0:
+            assert (ws[k], hs[k]) == (w, h), nm
+            assert sha(outs[k].cpu().numpy()[: w * h * 4].reshape(h, w, 4)) == sha(img), nm
