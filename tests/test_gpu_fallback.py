@@ -140,3 +140,33 @@ def test_sequential_fallback_cost(ctx, capsys):
         print(f"\n  64 x 512^2: clean {t_clean * 1e3:.1f} ms, with 2 sequential images {t_bad * 1e3:.1f} ms")
     assert t_bad < t_clean + 0.5, (t_bad, t_clean)
     b.close()
+
+
+def test_full_group_half_flat_photos_stay_parallel(ctx):
+    """a full group of 4096^2 photos whose top half is flat (a gradient with no
+    noise: a few bits per block, so the lanes over it hold thousands of blocks each and overflow
+    their static slots into the coefficient pool's tail) and whose bottom half is textured: every
+    image stays on the parallel path (fallback == 0, sequential == 0), bit-exact (four of them
+    checked against the oracle)."""
+    import numpy as np
+    from multiprocessing.pool import ThreadPool
+    from tools import foreign
+    W, N = 4096, 24
+
+    def make(k):
+        px = foreign.photo(6700 + k, W, W)
+        g = np.linspace(40, 220, W // 2, dtype=np.float32)[:, None]
+        px[: W // 2, :, 0] = g.astype(np.uint8)
+        px[: W // 2, :, 1] = (g * 0.8 + 20).astype(np.uint8)
+        px[: W // 2, :, 2] = (255 - g).astype(np.uint8)
+        return S.jpeg(px, "420", 90)
+
+    with ThreadPool(8) as p:
+        jpegs = p.map(make, range(N))
+    b = icx.Batch(ctx, N, W, W, group=N)
+    res = b.decode_host(jpegs)
+    st = b.path_stats()
+    assert st == {"parallel": N, "fallback": 0, "sequential": 0}, st
+    assert all(r[0] == 0 for r in res)
+    _check(res[:4], jpegs[:4])
+    b.close()
