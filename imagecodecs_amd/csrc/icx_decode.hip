@@ -832,7 +832,37 @@ struct CPl {
     const uint8_t* p;
     int w, h, s;
 };
-__device__ __forceinline__ uint32_t ld4(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+// Timing experiment ICX_NT_BACK (bit 0: plane and coefficient loads, bit 1: IDCT plane stores)
+// marked non-temporal (streamed past L2, so the other pipeline's entropy lanes keep their U lines).
+#ifndef ICX_NT_BACK
+#define ICX_NT_BACK 0
+#endif
+template <class T>
+__device__ __forceinline__ T nt_ld(const T* p) {
+#if ICX_NT_BACK & 1
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void nt_st(T v, T* p) {
+#if ICX_NT_BACK & 2
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ int4 nt_ld(const int4* p) {
+#if ICX_NT_BACK & 1
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i v = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+    return int4{v.x, v.y, v.z, v.w};
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint32_t ld4(const uint8_t* p) { return nt_ld(reinterpret_cast<const uint32_t*>(p)); }
 __device__ __forceinline__ int bt(uint32_t v, int i) { return (v >> (8 * i)) & 255; }
 // Packs four 0..255 values with v_perm_b32. (A shift/or pack of clamped taps lets the compiler
 // form gfx950's v_ashr_pk_u8_i32, whose result's upper half was observed to leak into the
@@ -1361,12 +1391,12 @@ __device__ __forceinline__ void load_qw(const uint8_t* qz, uint32_t (&qw)[16]) {
 // and a half never reads the other half's private chunks): 6 loads per lane instead of 8.
 __device__ __forceinline__ void load_block(const int16_t* ac, int64_t blk, int h, int4 (&c)[8]) {
     const int4* src = reinterpret_cast<const int4*>(ac + blk * 64);
-    c[0] = src[h ? 4 : 0];
-    c[1] = src[1];
-    c[2] = src[2];
-    c[3] = src[h ? 7 : 3];
-    c[5] = src[5];
-    c[6] = src[6];
+    c[0] = nt_ld(src + (h ? 4 : 0));
+    c[1] = nt_ld(src + 1);
+    c[2] = nt_ld(src + 2);
+    c[3] = nt_ld(src + (h ? 7 : 3));
+    c[5] = nt_ld(src + 5);
+    c[6] = nt_ld(src + 6);
     c[4] = c[0];
     c[7] = c[3];
 }
@@ -1453,7 +1483,7 @@ __global__ __launch_bounds__(256, ICX_IDCT_C_MINW) void k_idct420c(const Desc* _
         uint8_t* const rowp = Pc + (int64_t)mby * 8 * stride;
         const uint32_t lo = ccoff + (uint32_t)(mx * 8 + 4 * h);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(rowp + (lo + (uint32_t)(r * stride))) = rowd[r];
+        for (int r = 0; r < 8; ++r) nt_st(rowd[r], reinterpret_cast<uint32_t*>(rowp + (lo + (uint32_t)(r * stride))));
     };
     idct_units(ac, d, h, wid, nw, nunits, pendf, unit);
 }
@@ -1492,7 +1522,7 @@ __global__ __launch_bounds__(256, ICX_IDCT_Y_MINW) void k_idct420y(const Desc* _
         uint8_t* const rowp = Py + (int64_t)mby * 16 * stride;  // (as in k_idct420c)
         const uint32_t lo = (uint32_t)(sby * 8 * stride + mx * 16 + sbx * 8 + 4 * h);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint32_t*>(rowp + (lo + (uint32_t)(r * stride))) = rowd[r];
+        for (int r = 0; r < 8; ++r) nt_st(rowd[r], reinterpret_cast<uint32_t*>(rowp + (lo + (uint32_t)(r * stride))));
     };
     idct_units(ac, d, h, wid, nw, nunits, pendf, unit);
 }
