@@ -134,7 +134,7 @@ def test_ext_device_batch(ctx, q, sub, w, h):
     imgs = [S.rgb(300 + k, w, h, 3) for k in range(5)]
     d_src = [torch.from_numpy(px).cuda() for px in imgs]
     want = [O.jpeg_encode(q, sub, w, h, 3, px.tobytes()) for px in imgs]
-    stride = max(len(x) for x in want) + 64
+    stride = (max(len(x) for x in want) + 64) | 1  # odd: images 1.. start at every byte alignment
     d_out = torch.full((5 * stride,), 0xAB, dtype=torch.uint8, device="cuda")
     enc = icx.Encoder(ctx)
     st, sizes = enc.encode_device_batch(q, sub, w, h, 3, [t.data_ptr() for t in d_src], d_out.data_ptr(), stride)
