@@ -532,6 +532,248 @@ __global__ __launch_bounds__(256) void k_ustf_write(int n, const uint8_t* __rest
     }
 }
 
+// ---- one-pass unstuff (k_ustf_one: count, scan and write in one launch) ----
+// A wave takes tiles in ticket order (an atomic counter), so every tile with a smaller ticket is
+// held by a wave that is running or done, and takes its next ticket once its tile's aggregate is
+// out. It compacts its tile's kept bytes into LDS, publishes
+// the tile's aggregate (kept bytes, restart markers, whether the data ends in it), then looks back
+// over the image's earlier tiles -- 64 at a time, one per lane, nearest first -- until it meets an
+// inclusive prefix (or the image's first tile), publishes its own inclusive prefix and writes its
+// bytes at that offset. The tile that ends the data (or the image's last tile) sets the image's
+// length, markers, error position and lane count and writes the reader padding (k_ustf_scan's
+// work). A state word is 2 flag bits (1 aggregate, 2 inclusive), an end bit, 21 bits of restart
+// markers and 40 bits of kept bytes (scan_len < 2^40); the array is zeroed before each launch.
+constexpr uint64_t kTsAgg = 1, kTsInc = 2;
+constexpr int kTsRstBits = 21;
+__device__ __forceinline__ uint64_t ts_pack(uint64_t flag, bool end, int64_t nrst, int64_t kept) {
+    return flag << 62 | (uint64_t)end << 61 | (uint64_t)nrst << 40 | (uint64_t)kept;
+}
+__device__ __forceinline__ int64_t ts_kept(uint64_t v) { return (int64_t)(v & (((uint64_t)1 << 40) - 1)); }
+__device__ __forceinline__ int64_t ts_rst(uint64_t v) { return (int64_t)((v >> 40) & ((1u << kTsRstBits) - 1)); }
+__device__ __forceinline__ bool ts_end(uint64_t v) { return (v >> 61) & 1; }
+__device__ __forceinline__ long long wave_sum_ll(long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+// The image owning flat tile t: the largest i with pre[i] <= t (pre non-decreasing, pre[0] <= t),
+// two rounds of one load per lane for n <= 4096 images.
+__device__ __forceinline__ int find_image_wave(const int32_t* pre, int n, int t, int lane) {
+    if (n > 4096) return find_image(pre, n, t);
+    const int step = (n + 63) >> 6;
+    const int k = lane * step;
+    const uint64_t m = __ballot(k < n && pre[min(k, n - 1)] <= t);
+    const int base = (63 - __clzll((long long)m)) * step;
+    const int k2 = base + lane;
+    const uint64_t m2 = __ballot(lane < step && k2 < n && pre[min(k2, n - 1)] <= t);
+    return base + 63 - __clzll((long long)m2);
+}
+constexpr int kTsSpinMax = 1 << 22;  // a predecessor that never publishes: the image gives up
+
+__global__ __launch_bounds__(256) void k_ustf_one(int n, const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                  const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
+                                                  const int32_t* __restrict__ tilepre, const int32_t* __restrict__ totals,
+                                                  uint64_t* __restrict__ tstate, uint8_t* __restrict__ U,
+                                                  int64_t* __restrict__ rst, int64_t rst_cap) {
+    constexpr int kBufW = kTileBytes / 4 + 8;
+    __shared__ uint32_t sbuf_all[4][kBufW];
+    const int lane = threadIdx.x & 63;
+    uint32_t* sbuf = sbuf_all[threadIdx.x >> 6];
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(sbuf);
+    const int total = totals[0];
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(tstate + total);  // (one word past the tiles)
+    auto take = [&]() {
+        int v = 0;
+        if (lane == 0) v = (int)atomicAdd(ticket, 1u);
+        return __builtin_amdgcn_readfirstlane(__shfl(v, 0));
+    };
+    // Relaxed (monotonic) agent-scope accesses: a state word carries everything a reader uses, so
+    // no ordering with other data is needed -- and an acquire / release at agent scope invalidates /
+    // writes back the whole L2 of the XCD on gfx950 (40x slower at C3: every spin iteration
+    // emptied the cache under the other waves' tiles).
+    auto ts_load = [&](int q) { return __hip_atomic_load(tstate + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto ts_store = [&](int q, uint64_t v) {
+        if (lane == 0) __hip_atomic_store(tstate + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    TileImg im, imn;
+    TileChunks tc, tn;
+    int t = take();
+    if (t < total) {
+        im.set(find_image_wave(tilepre, n, t, lane), data, off, desc, spec, tilepre);
+        tc.load(im.R, im.L, im.t0(t), lane);
+    }
+    while (t < total) {  // wave-uniform
+        const int i = im.i;
+        SpecImg& s = spec[i];
+        const bool on = s.mode == 1 || s.mode == 3;
+        const uint8_t* R = im.R;
+        const int64_t L = im.L;
+        const int64_t t0 = im.t0(t);
+        for (int k = lane; k < kBufW / 4; k += 64) reinterpret_cast<uint4*>(sbuf)[k] = make_uint4(0u, 0u, 0u, 0u);
+        __builtin_amdgcn_wave_barrier();
+        int32_t giveup = 0;
+        int kept = 0, nrst = 0, end_err = 0;
+        bool own_end = false;
+        for (int r = 0; on && r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
+            const int64_t a = t0 + r * 1024 + lane * 16;
+            RstSink rs0{0, 0, nullptr, 0, 0};
+            const ChunkIn c = tc.next(a, lane);
+            const Ustf16 u = ustf16<true>(R, L, a, c.D, c.nx, c.prun, &giveup, &rs0);
+            const long long e = __any(u.end_at >= 0) ? wave_min_ll(u.end_at >= 0 ? (long long)u.end_at : LLONG_MAX)
+                                                     : LLONG_MAX;
+            const bool before = u.end_at >= 0 ? u.end_at <= e : a < e;
+            const int k = before ? u.kept : 0;
+            const int incl = wave_incl_scan(k);
+            nrst += before ? rs0.n : 0;
+            if (k) {  // (as k_ustf_write)
+                const int ob = kept + incl - k, q = ob >> 2, sft = ob & 3;
+                const uint32_t* d = u.out;
+                if (k == 16 && (ob & 15) == 0) {
+                    reinterpret_cast<uint4*>(sbuf)[q >> 2] = make_uint4(d[0], d[1], d[2], d[3]);
+                } else if (sft == 0) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) atomicOr(&sbuf[q + j], d[j]);
+                } else {
+                    atomicOr(&sbuf[q], d[0] << (8 * sft));
+#pragma unroll
+                    for (int j = 1; j < 4; ++j) atomicOr(&sbuf[q + j], __builtin_amdgcn_alignbyte(d[j], d[j - 1], 4 - sft));
+                    atomicOr(&sbuf[q + 4], d[3] >> (32 - 8 * sft));
+                }
+            }
+            kept += __shfl(incl, 63);
+            if (e != LLONG_MAX) {  // wave-uniform: the data ends in this round
+                const uint64_t owner = __ballot(u.end_at >= 0 && u.end_at == e);
+                end_err = __shfl(u.end_err, __ffsll((long long)owner) - 1);
+                own_end = true;
+                break;
+            }
+        }
+        nrst = __any(nrst) ? wave_sum(nrst) : 0;
+        if (__any(giveup) && lane == 0) atomicOr(&s.err, kSpecGiveUp);
+        ts_store(t, ts_pack(kTsAgg, own_end, min(nrst, (1 << kTsRstBits) - 1), kept));
+        // The next ticket only now: a wave holding a ticket it has not scanned would make every
+        // look-back that reaches that tile wait for this wave's whole current tile (and so on
+        // down the tickets: a serial chain). Its image and chunks load during the look-back.
+        const int tnx = take();
+        if (tnx < total) {
+            imn.set(find_image_wave(tilepre, n, tnx, lane), data, off, desc, spec, tilepre);
+            tn.load(imn.R, imn.L, imn.t0(tnx), lane);
+        }
+        // look back: the prefix before this tile (pk bytes, pr markers) and whether the data ended
+        // before it (pe)
+        int64_t pk = 0, pr = 0, ak = 0, ar = 0;
+        bool pe = false, ae = false, stuck = false;
+        for (int p = t - 1;; p -= 64) {  // wave-uniform
+            const int q = p - lane;
+            uint64_t v = ts_pack(kTsInc, false, 0, 0);  // before the image's first tile: prefix 0
+            if (q >= im.t_first) {
+                int spins = 0;
+                for (v = ts_load(q); (v >> 62) == 0 && spins < kTsSpinMax; ++spins) {
+                    __builtin_amdgcn_s_sleep(1);
+                    v = ts_load(q);
+                }
+                if ((v >> 62) == 0) {
+                    stuck = true;
+                    v = ts_pack(kTsInc, false, 0, 0);
+                }
+            }
+            const uint64_t mi = __ballot((v >> 62) == kTsInc);
+            const int m = mi ? __ffsll((long long)mi) - 1 : 64;  // nearest inclusive prefix
+            const uint64_t vm = __shfl(v, m & 63);
+            if (m < 64 && ts_end(vm)) {  // the data ended at or before it: its prefix is final
+                pk = ts_kept(vm);
+                pr = ts_rst(vm);
+                pe = true;
+                break;
+            }
+            // the farthest (earliest) tile below m whose data ends: the tiles nearer than it
+            // follow the end and count for nothing, nor does what nearer windows summed
+            const uint64_t me = __ballot(lane < m && ts_end(v));
+            const int e = me ? 63 - __clzll((long long)me) : -1;
+            const bool in = lane < m && lane >= (e < 0 ? 0 : e);
+            const int64_t wk = wave_sum_ll(in ? ts_kept(v) : 0), wr = wave_sum_ll(in ? ts_rst(v) : 0);
+            if (e >= 0) { ak = wk; ar = wr; ae = true; }
+            else { ak += wk; ar += wr; }
+            if (m < 64) {
+                pk = ts_kept(vm) + ak;
+                pr = ts_rst(vm) + ar;
+                pe = ae;
+                break;
+            }
+        }
+        if (__any(stuck) && lane == 0) atomicOr(&s.err, kSpecGiveUp);
+        const int64_t ik = pe ? pk : pk + kept, ir = pe ? pr : pr + nrst;
+        if (ir >= (1 << kTsRstBits) && lane == 0) atomicOr(&s.err, kSpecGiveUp);
+        ts_store(t, ts_pack(kTsInc, pe || own_end, min<int64_t>(ir, (1 << kTsRstBits) - 1), ik));
+        __builtin_amdgcn_wave_barrier();
+        if (on && !pe) {
+            const int64_t obase = pk;
+            if (nrst) {  // restart markers to the image's list in stream order (DRI images): a second
+                         // walk of the tile (now in L2), placing them at the known prefix
+                TileChunks t2;
+                t2.load(R, L, t0, lane);
+                int kk = 0, nr_done = 0;
+                int32_t gdummy = 0;
+                for (int r = 0; r < kTileBytes / 1024 && t0 + r * 1024 < L; ++r) {
+                    const int64_t a = t0 + r * 1024 + lane * 16;
+                    RstSink rs0{0, 0, nullptr, 0, 0};
+                    const ChunkIn c = t2.next(a, lane);
+                    const Ustf16 u = ustf16<false>(R, L, a, c.D, c.nx, c.prun, &gdummy, &rs0);
+                    const long long e = __any(u.end_at >= 0) ? wave_min_ll(u.end_at >= 0 ? (long long)u.end_at : LLONG_MAX)
+                                                             : LLONG_MAX;
+                    const bool before = u.end_at >= 0 ? u.end_at <= e : a < e;
+                    const int k = before ? u.kept : 0;
+                    const int incl = wave_incl_scan(k);
+                    const int nr = before ? rs0.n : 0;
+                    if (__any(nr)) {
+                        const int rincl = wave_incl_scan(nr);
+                        if (nr) {
+                            RstSink rs{0, obase + kk + (incl - k), rst + (int64_t)i * rst_cap, (int32_t)(pr + nr_done + rincl - nr),
+                                       (int32_t)min<int64_t>(rst_cap, INT32_MAX)};
+                            (void)ustf16<false>(R, L, a, c.D, c.nx, c.prun, &gdummy, &rs);
+                        }
+                        nr_done += __shfl(rincl, 63);
+                    }
+                    kk += __shfl(incl, 63);
+                    if (e != LLONG_MAX) break;
+                }
+            }
+            // copy out (as k_ustf_write)
+            const int64_t nout = kept;
+            uint8_t* dst = U + s.uoff + obase;
+            const int head = (int)min<int64_t>(nout, (16 - (obase & 15)) & 15);
+            const int nunit = (int)((nout - head) >> 4);
+            const int tail0 = head + nunit * 16;
+            if (lane < head) dst[lane] = sb[lane];
+            if (lane < nout - tail0) dst[tail0 + lane] = sb[tail0 + lane];
+            for (int u = lane; u < nunit; u += 64) {
+                const int b0 = head + 16 * u, shb = (b0 & 3) * 8;
+                const uint32_t* q = sbuf + (b0 >> 2);
+                uint32_t v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (uint32_t)((((uint64_t)q[j + 1] << 32) | q[j]) >> shb);
+                *reinterpret_cast<uint4*>(dst + b0) = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+            if (own_end || t == im.t_end - 1) {  // the data's end: the image's stream is complete
+                const int64_t ulen = obase + kept;
+                uint8_t* u = U + s.uoff;
+                for (int64_t p = ulen + lane; p < u_pad_end(ulen); p += 64) u[p] = 0xFF;
+                if (lane == 0) {
+                    s.ulen = ulen;
+                    s.nrst = (int32_t)ir;
+                    s.errpos = own_end && end_err ? ulen : INT64_MAX;
+                    const int64_t nsub = ulen > 0 ? (ulen + s.sub_bytes - 1) / s.sub_bytes : 1;
+                    s.nsub = s.mode == 3 ? s.nint : (int32_t)nsub;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        t = tnx;
+        tc = tn;
+        im = imn;
+    }
+}
+
 // -------------------------------------------------------------------- entropy lanes
 // Step tables (icx_step.h), one set per image, built once per group from the parsed Huffman
 // tables; each workgroup below stages the format it decodes with into LDS.
@@ -1578,12 +1820,22 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
         (void)hipEventRecord(ws.ev_defer, st);
         if (round == 0)  // (an image's tables serve every round)
             hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
-        hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
-                           ws.totals, ws.tiles);
-        hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,
-                           ws.U);
-        hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
-                           ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.rst, ws.rst_cap);
+        // ICX_USTF1=1: the one-pass unstuff (k_ustf_one, its tile states in the tile records' memory:
+        // 8 bytes per tile plus the ticket, of 24 per tile); otherwise count, scan, write
+        const char* one_env = std::getenv("ICX_USTF1");
+        if (one_env && std::atoi(one_env) != 0) {
+            uint64_t* ts = reinterpret_cast<uint64_t*>(ws.tiles);
+            (void)hipMemsetAsync(ts, 0, sizeof(uint64_t) * (size_t)(ws.tiles_cap + 2), st);
+            hipLaunchKernelGGL(k_ustf_one, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.totals,
+                               ts, ws.U, ws.rst, ws.rst_cap);
+        } else {
+            hipLaunchKernelGGL(k_ustf_count, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
+                               ws.totals, ws.tiles);
+            hipLaunchKernelGGL(k_ustf_scan, dim3(n), dim3(256), 0, st, n, ws.spec, ws.tiles, ws.tile_obase, ws.tile_rbase,
+                               ws.U);
+            hipLaunchKernelGGL(k_ustf_write, dim3(g), dim3(256), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre,
+                               ws.totals, ws.tiles, ws.tile_obase, ws.tile_rbase, ws.U, ws.rst, ws.rst_cap);
+        }
         E(kStUnstuff);
         // Guess-write path (default; ICX_GW=0: guess, count, write)
         if (gw) {
