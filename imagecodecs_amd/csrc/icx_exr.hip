@@ -3,7 +3,7 @@
 //
 // The host parses the header and the offset table and checks every chunk header the way tinyexr
 // does (a few hundred bytes of control data); the device does the pixel work:
-//   k_exr_unpack   one workgroup per compressed chunk: lane 0 inflates (ZIP / ZIPS) or run-decodes
+//   k_exr_unpack   one wave per compressed chunk: lane 0 inflates (ZIP / ZIPS; 16 KiB LDS ring) or run-decodes
 //                  (RLE) into the chunk's scratch, then the workgroup undoes the byte predictor
 //                  with a prefix sum (tinyexr.h:1469-1479 / :1726-1736)
 //   k_exr_convert  one thread per output pixel: the row / tile map names the chunk (and line) that
@@ -33,12 +33,17 @@ namespace icx {
 
 // Per compressed chunk (of any image of the call: `file` is the first file's device address, a
 // chunk's own at + c.base): decompress (lane 0), then the predictor as a workgroup prefix sum.
-__global__ __launch_bounds__(256) void k_exr_unpack(const uint8_t* __restrict__ file, ExrChunk* __restrict__ ch,
+// One wave per chunk, a 16 KiB LDS ring (exr_inflate<kExrWinDev>): ~20 KiB of LDS, so eight chunks
+// per CU inflate at once (four with the 32 KiB window and 256-thread workgroups: 375 MP/s at the
+// exr bench before).
+constexpr int kExrWinDev = 16384;
+constexpr int kUnpackThreads = 64;
+__global__ __launch_bounds__(kUnpackThreads) void k_exr_unpack(const uint8_t* __restrict__ file, ExrChunk* __restrict__ ch,
                                                     const int32_t* __restrict__ list, uint8_t* __restrict__ scratch,
                                                     int32_t* __restrict__ fail) {
     __shared__ InfState st;
-    __shared__ uint8_t win[kExrWin];
-    __shared__ uint32_t part[256];
+    __shared__ uint8_t win[kExrWinDev];
+    __shared__ uint32_t part[kUnpackThreads];
     __shared__ int64_t produced;
     ExrChunk& c = ch[list[blockIdx.x]];
     uint8_t* t = scratch + c.scratch;
@@ -47,7 +52,7 @@ __global__ __launch_bounds__(256) void k_exr_unpack(const uint8_t* __restrict__ 
         bool ok;
         const uint8_t* f = file + c.base + c.src;
         if (c.mode == 1) {
-            ok = exr_inflate(f, c.len, t, c.out_len, &m, st, win);
+            ok = exr_inflate<kExrWinDev>(f, c.len, t, c.out_len, &m, st, win);
         } else {
             ok = exr_unrle(f, c.len, t, c.out_len);
             m = c.out_len;
@@ -63,15 +68,15 @@ __global__ __launch_bounds__(256) void k_exr_unpack(const uint8_t* __restrict__ 
     const int64_t m = produced;
     if (m == 0) return;
     // t'[i] = t[0] + sum_{k=1..i} (t[k] - 128) mod 256: each thread one contiguous segment
-    const int64_t seg = (m + 255) / 256;
+    const int64_t seg = (m + kUnpackThreads - 1) / kUnpackThreads;
     const int64_t a = min<int64_t>(m, (int64_t)threadIdx.x * seg), b = min<int64_t>(m, a + seg);
     uint32_t sum = 0;
     for (int64_t k = a; k < b; ++k) sum += k == 0 ? t[0] : (uint32_t)t[k] - 128u;
     part[threadIdx.x] = sum;
     __syncthreads();
-    if (threadIdx.x == 0) {  // (256 partial sums: a serial scan is cheap next to the inflate)
+    if (threadIdx.x == 0) {  // (64 partial sums: a serial scan is cheap next to the inflate)
         uint32_t run = 0;
-        for (int k = 0; k < 256; ++k) {
+        for (int k = 0; k < kUnpackThreads; ++k) {
             const uint32_t v = part[k];
             part[k] = run;
             run += v;
@@ -291,7 +296,7 @@ static int exr_batch(hipStream_t st, ExrWs& ws, int n, const uint8_t* const* dat
         return -100;
     }
     if (!list.empty() && n > 0)
-        hipLaunchKernelGGL(k_exr_unpack, dim3((unsigned)list.size()), dim3(256), 0, st, dfile[0], d_ch, d_list, d_scr, d_fail);
+        hipLaunchKernelGGL(k_exr_unpack, dim3((unsigned)list.size()), dim3(kUnpackThreads), 0, st, dfile[0], d_ch, d_list, d_scr, d_fail);
     for (int i = 0; i < n; ++i) {
         if (codes[i] != kExrOk || plist[i].empty()) continue;
         hipLaunchKernelGGL(k_exr_piz, dim3((unsigned)plist[i].size()), dim3(256), 0, st, dfile[i], (int64_t)sizes[i], d_ch,

@@ -131,9 +131,13 @@ ICX_HD int inf_decode(BitIn& in, const InfTab& h) {
 }
 
 // mz_uncompress(dst, &cap, src, n): true and *produced = output bytes, or false. `win` is a
-// kExrWin-byte window (match sources; written as the output is).
+// W-byte ring of the latest output (match sources; written as the output is). With W below the
+// deflate window (the GPU's 16 KiB LDS ring: twice the decoders per CU), a match from farther back
+// reads the bytes from dst, where they were stored at least W bytes of output ago.
+template <int W = kExrWin>
 ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* produced, InfState& st,
                         uint8_t* win) {
+    static_assert(W >= 16 && (W & (W - 1)) == 0 && W <= kExrWin, "a power-of-two ring");
     *produced = 0;
     if (n < 2) return false;
     const uint32_t cmf = src[0], flg = src[1];
@@ -143,7 +147,7 @@ ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap
     uint32_t a1 = 1, a2 = 0, nm = 0;  // Adler-32, reduced every 5552 bytes (zlib's NMAX)
     uint32_t acc = 0;                 // output bytes gathered into 32-bit stores (dst 4-byte aligned)
     auto put = [&](uint8_t b) {
-        win[out & (kExrWin - 1)] = b;
+        win[out & (W - 1)] = b;
         acc |= (uint32_t)b << (8 * (out & 3));
         if ((out & 3) == 3) {
             *reinterpret_cast<uint32_t*>(dst + (out & ~(int64_t)3)) = acc;
@@ -227,7 +231,20 @@ ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap
             const int64_t dist = Deflate::kDBase[di] + (int64_t)in.bits(Deflate::kDExt[di]);
             if (in.past_end() || dist > out) return false;
             if (out + len > cap) return false;
-            for (int j = 0; j < len; ++j) put(win[(out - dist) & (kExrWin - 1)]);
+            if (W == kExrWin || dist <= W) {
+                for (int j = 0; j < len; ++j) put(win[(out - dist) & (W - 1)]);
+            } else {  // from the output (complete 4-byte words: dist > W >= 16), four loads at a time
+                int j = 0;
+                for (; j + 4 <= len; j += 4) {
+                    const uint8_t* q = dst + (out - dist);
+                    const uint8_t b0 = q[0], b1 = q[1], b2 = q[2], b3 = q[3];
+                    put(b0);
+                    put(b1);
+                    put(b2);
+                    put(b3);
+                }
+                for (; j < len; ++j) put(dst[out - dist]);
+            }
         }
     }
     if (out & 3) {  // the last partial word (dst holds cap bytes: write only what is ours)

@@ -59,6 +59,13 @@ int emu_exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, in
     return exr_inflate(src, n, dst, cap, produced, *st, win.data()) ? 1 : 0;
 }
 
+// The GPU's form: a 16 KiB ring, farther matches read back from dst (k_exr_unpack).
+int emu_exr_inflate_ring(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* produced) {
+    auto st = std::make_unique<InfState>();
+    std::vector<uint8_t> win(16384);
+    return exr_inflate<16384>(src, n, dst, cap, produced, *st, win.data()) ? 1 : 0;
+}
+
 // The whole read: the tinyexr code; on success w*h*4 float bits in out (cap_px pixels at most).
 int emu_exr_decode(const uint8_t* data, int64_t size, uint32_t* out, int64_t cap_px, int* w, int* h) {
     ExrPlan P;

@@ -35,6 +35,8 @@ def emu():
         L.emu_exr_decode.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.emu_exr_inflate.restype = C.c_int
         L.emu_exr_inflate.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+        L.emu_exr_inflate_ring.restype = C.c_int
+        L.emu_exr_inflate_ring.argtypes = L.emu_exr_inflate.argtypes
         _L = L
     return _L
 
@@ -48,11 +50,13 @@ def emu_decode(data: bytes, cap=1 << 22):
     return code, w.value, h.value, img
 
 
-def emu_inflate(src: bytes, cap: int):
+def emu_inflate(src: bytes, cap: int, ring: bool = False):
+    """ring: the GPU's form (16 KiB LDS ring, farther matches read back from the output)."""
     dst = np.zeros(max(1, cap), np.uint8)
     n = C.c_int64()
     buf = C.create_string_buffer(bytes(src), max(1, len(src)))
-    ok = emu().emu_exr_inflate(buf, len(src), dst.ctypes.data, cap, C.byref(n))
+    f = emu().emu_exr_inflate_ring if ring else emu().emu_exr_inflate
+    ok = f(buf, len(src), dst.ctypes.data, cap, C.byref(n))
     return dst[: n.value].tobytes() if ok else None
 
 
@@ -100,27 +104,42 @@ def _zstreams():
     return out
 
 
-def test_inflate_matches_zlib():
+@pytest.mark.parametrize("ring", [False, True])
+def test_inflate_matches_zlib(ring):
     """exr_inflate == zlib on stored, fixed and dynamic blocks, windows past 32 KiB, and an output
-    capacity of exactly / one short of / more than the data."""
+    capacity of exactly / one short of / more than the data; with the full window and in the
+    GPU's form (16 KiB ring, matches from farther back read from the output)."""
     for raw, z in _zstreams():
-        assert emu_inflate(z, len(raw)) == raw
-        assert emu_inflate(z, len(raw) + 100) == raw
+        assert emu_inflate(z, len(raw), ring) == raw
+        assert emu_inflate(z, len(raw) + 100, ring) == raw
         if raw:
-            assert emu_inflate(z, len(raw) - 1) is None  # (mz_uncompress: MZ_BUF_ERROR)
+            assert emu_inflate(z, len(raw) - 1, ring) is None  # (mz_uncompress: MZ_BUF_ERROR)
 
 
-def test_inflate_corrupt_streams():
+def test_inflate_far_matches_ring():
+    """Streams whose matches reach 16-32 KiB back (a 24 KiB random block repeated, odd lengths): the
+    GPU's ring form reads them from the output, bit-exact to zlib."""
+    rng = np.random.default_rng(11)
+    for size, tail in ((24 << 10, 7), ((20 << 10) + 3, 1), (30 << 10, 5)):
+        block = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        raw = block + block + block[: size // 3 + tail]
+        z = zlib.compress(raw, 9)
+        assert emu_inflate(z, len(raw), True) == raw
+        assert emu_inflate(z, len(raw), False) == raw
+
+
+@pytest.mark.parametrize("ring", [False, True])
+def test_inflate_corrupt_streams(ring):
     """Truncated streams, bad check bits, a preset dictionary, a wrong Adler-32 and random byte
-    damage: fail whenever zlib fails, else produce zlib's bytes."""
+    damage: fail whenever zlib fails, else produce zlib's bytes (both window forms)."""
     rng = np.random.default_rng(4)
     agree = total = 0
     for raw, z in _zstreams()[::3]:
-        assert emu_inflate(z[:-1], len(raw) + 10) is None
-        assert emu_inflate(z[: len(z) // 2], len(raw) + 10) is None or len(raw) == 0
-        assert emu_inflate(bytes([z[0], z[1] ^ 1]) + z[2:], len(raw)) is None
-        assert emu_inflate(bytes([z[0], z[1] | 0x20]) + z[2:], len(raw)) is None
-        assert emu_inflate(z[:-1] + bytes([z[-1] ^ 0x40]), len(raw)) is None
+        assert emu_inflate(z[:-1], len(raw) + 10, ring) is None
+        assert emu_inflate(z[: len(z) // 2], len(raw) + 10, ring) is None or len(raw) == 0
+        assert emu_inflate(bytes([z[0], z[1] ^ 1]) + z[2:], len(raw), ring) is None
+        assert emu_inflate(bytes([z[0], z[1] | 0x20]) + z[2:], len(raw), ring) is None
+        assert emu_inflate(z[:-1] + bytes([z[-1] ^ 0x40]), len(raw), ring) is None
         for _ in range(20):
             b = bytearray(z)
             b[int(rng.integers(2, len(b)))] ^= int(rng.integers(1, 256))
@@ -130,7 +149,7 @@ def test_inflate_corrupt_streams():
                 ref = ref if d.eof and not d.unconsumed_tail else None
             except zlib.error:
                 ref = None
-            got = emu_inflate(bytes(b), len(raw) + 64)
+            got = emu_inflate(bytes(b), len(raw) + 64, ring)
             total += 1
             agree += got == ref
     # (the two decoders differ only on streams zlib and miniz themselves disagree about: an

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 end measurement on one box: the whole GPU suite, smoke, C3 bench at the driver's
 # settings with rocprofv3 stats, PMC traffic of k_gw_lane and of the whole pipeline (every kernel
-# of a 512-image step), C2 at the driver's settings, C5 batch. Stops at the first GPU fault,
+# of a 512-image step; only with PMC=1), C2 at the driver's settings, C5 batch, EXR batch. Stops at the first GPU fault,
 # abort or time limit.
 R="$GRAFT_REPO_ROOT"; [ -n "$R" ] || R=$(pwd)
 cd "$R"; mkdir -p gpurun_out
@@ -17,10 +17,12 @@ rc=$?; echo "c3: $(cut -c1-160 $O/bench_c3.json)"; stop $rc
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu --no-pcie > "$O/bench_c3_rocprof.json" 2> "$O/rocprof.err"
 rc=$?; echo "rocprof rc=$rc"; stop $rc
-timeout -k 10 1200 python3 "$R/tools/pmc_traffic.py" run --out "$O/traffic.json" --pipeline-out "$O/pipeline_traffic.json" > "$O/pmc.log" 2>&1
-rc=$?; echo "pmc rc=$rc: $(tail -1 $O/pmc.log | cut -c1-200)"; stop $rc
+[ -n "$PMC" ] && timeout -k 10 1200 python3 "$R/tools/pmc_traffic.py" run --out "$O/traffic.json" --pipeline-out "$O/pipeline_traffic.json" > "$O/pmc.log" 2>&1
+rc=$?; [ -n "$PMC" ] && echo "pmc rc=$rc: $(tail -1 $O/pmc.log | cut -c1-200)" && stop $rc
 cd "$R"
 timeout -k 10 600 python3 bench.py --workload c2 --steps 20 --warmup 5 > "$O/bench_c2.json" 2> "$O/bench_c2.err"
 rc=$?; echo "c2: $(cut -c1-160 $O/bench_c2.json)"; stop $rc
 timeout -k 10 600 python3 bench.py --workload c5 --steps 5 --warmup 1 > "$O/bench_c5.json" 2> "$O/bench_c5.err"
 rc=$?; echo "c5: $(cut -c1-160 $O/bench_c5.json)"; stop $rc
+timeout -k 10 600 python3 bench.py --workload exr --steps 5 --warmup 2 > "$O/bench_exr.json" 2> "$O/bench_exr.err"
+rc=$?; echo "exr: $(cut -c1-160 $O/bench_exr.json)"; stop $rc
