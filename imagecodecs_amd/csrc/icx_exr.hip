@@ -3,7 +3,7 @@
 //
 // The host parses the header and the offset table and checks every chunk header the way tinyexr
 // does (a few hundred bytes of control data); the device does the pixel work:
-//   k_exr_unpack   one wave per compressed chunk: lane 0 inflates (ZIP / ZIPS; 16 KiB LDS ring) or run-decodes
+//   k_exr_unpack   one wave per compressed chunk: the wave inflates (ZIP / ZIPS; wave-uniform, 16 KiB LDS ring) or lane 0 run-decodes
 //                  (RLE) into the chunk's scratch, then the workgroup undoes the byte predictor
 //                  with a prefix sum (tinyexr.h:1469-1479 / :1726-1736)
 //   k_exr_convert  one thread per output pixel: the row / tile map names the chunk (and line) that
@@ -47,16 +47,16 @@ __global__ __launch_bounds__(kUnpackThreads) void k_exr_unpack(const uint8_t* __
     __shared__ int64_t produced;
     ExrChunk& c = ch[list[blockIdx.x]];
     uint8_t* t = scratch + c.scratch;
+    const uint8_t* f = file + c.base + c.src;
+    bool ok = true;
+    int64_t m = 0;
+    if (c.mode == 1) {  // (wave-uniform) the whole wave runs the inflate, lane 0 stores
+        ok = exr_inflate<kExrWinDev>(f, c.len, t, c.out_len, &m, st, win);
+    } else if (threadIdx.x == 0) {
+        ok = exr_unrle(f, c.len, t, c.out_len);
+        m = c.out_len;
+    }
     if (threadIdx.x == 0) {
-        int64_t m = 0;
-        bool ok;
-        const uint8_t* f = file + c.base + c.src;
-        if (c.mode == 1) {
-            ok = exr_inflate<kExrWinDev>(f, c.len, t, c.out_len, &m, st, win);
-        } else {
-            ok = exr_unrle(f, c.len, t, c.out_len);
-            m = c.out_len;
-        }
         if (!ok) {
             atomicOr(fail + c.img, 1);
             m = 0;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kUnpackThreads) void k_exr_unpack(const uint8_t* __
         c.produced = m;
     }
     __syncthreads();
-    const int64_t m = produced;
+    m = produced;
     if (m == 0) return;
     // t'[i] = t[0] + sum_{k=1..i} (t[k] - 128) mod 256: each thread one contiguous segment
     const int64_t seg = (m + kUnpackThreads - 1) / kUnpackThreads;

@@ -19,6 +19,25 @@ namespace icx {
 
 constexpr int kExrWin = 32768;  // deflate window
 
+// Wave-uniform inflate on the GPU: all 64 lanes of k_exr_unpack's wave run one chunk's decode, and
+// every value read from memory is made wave-uniform (readfirstlane), so the decoder's state sits in
+// SGPRs and its loop runs as scalar instructions (one lane doing it alone ran every step as a
+// full-wave VALU op); stores are lane 0's. On the host: the identity, and every store.
+ICX_HD uint32_t exr_uni(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_readfirstlane(v);
+#else
+    return v;
+#endif
+}
+ICX_HD bool exr_lane0() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0u;
+#else
+    return true;
+#endif
+}
+
 struct Deflate {  // RFC 1951 §3.2.5-3.2.7 length / distance bases and extra bits, code-length order
     static constexpr uint16_t kLBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
                                             35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -57,6 +76,7 @@ struct BitIn {
             if (pos + j < n) w |= (uint32_t)s[pos + j] << (8 * j);
             else over += 8;
         }
+        w = exr_uni(w);
         buf |= (uint64_t)w << cnt;
         pos += 4;
         cnt += 32;
@@ -106,7 +126,7 @@ ICX_HD bool inf_build(InfTab& h, const uint8_t* len, int n) {
 
 ICX_HD int inf_decode(BitIn& in, const InfTab& h) {
     in.fill(16);
-    const uint32_t e = h.fast[in.buf & ((1u << kInfFast) - 1u)];
+    const uint32_t e = exr_uni(h.fast[in.buf & ((1u << kInfFast) - 1u)]);
     if (e) {
         in.buf >>= e & 15u;
         in.cnt -= (int)(e & 15u);
@@ -117,11 +137,11 @@ ICX_HD int inf_decode(BitIn& in, const InfTab& h) {
     for (int l = 1; l <= 15; ++l) {
         code |= (int)(w & 1u);
         w >>= 1;
-        const int count = h.count[l];
+        const int count = (int)exr_uni(h.count[l]);
         if (code - count < first) {
             in.buf >>= l;
             in.cnt -= l;
-            return h.sym[index + (code - first)];
+            return (int)exr_uni(h.sym[index + (code - first)]);
         }
         index += count;
         first = (first + count) << 1;
@@ -140,17 +160,18 @@ ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap
     static_assert(W >= 16 && (W & (W - 1)) == 0 && W <= kExrWin, "a power-of-two ring");
     *produced = 0;
     if (n < 2) return false;
-    const uint32_t cmf = src[0], flg = src[1];
+    const uint32_t cmf = exr_uni(src[0]), flg = exr_uni(src[1]);
     if ((cmf * 256u + flg) % 31u != 0 || (flg & 32u) || (cmf & 15u) != 8) return false;
     BitIn in{src, n, 2, 0ull, 0, 0};
     int64_t out = 0;
     uint32_t a1 = 1, a2 = 0, nm = 0;  // Adler-32, reduced every 5552 bytes (zlib's NMAX)
     uint32_t acc = 0;                 // output bytes gathered into 32-bit stores (dst 4-byte aligned)
+    const bool l0 = exr_lane0();
     auto put = [&](uint8_t b) {
-        win[out & (W - 1)] = b;
+        if (l0) win[out & (W - 1)] = b;
         acc |= (uint32_t)b << (8 * (out & 3));
         if ((out & 3) == 3) {
-            *reinterpret_cast<uint32_t*>(dst + (out & ~(int64_t)3)) = acc;
+            if (l0) *reinterpret_cast<uint32_t*>(dst + (out & ~(int64_t)3)) = acc;
             acc = 0;
         }
         ++out;
@@ -201,7 +222,7 @@ ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap
                 int rep;
                 if (sym == 16) {
                     if (k == 0) return false;
-                    v = st.len[k - 1];
+                    v = (uint8_t)exr_uni(st.len[k - 1]);
                     rep = 3 + (int)in.bits(2);
                 } else if (sym == 17) {
                     rep = 3 + (int)in.bits(3);
@@ -232,23 +253,25 @@ ICX_HD bool exr_inflate(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap
             if (in.past_end() || dist > out) return false;
             if (out + len > cap) return false;
             if (W == kExrWin || dist <= W) {
-                for (int j = 0; j < len; ++j) put(win[(out - dist) & (W - 1)]);
+                for (int j = 0; j < len; ++j) put((uint8_t)exr_uni(win[(out - dist) & (W - 1)]));
             } else {  // from the output (complete 4-byte words: dist > W >= 16), four loads at a time
                 int j = 0;
                 for (; j + 4 <= len; j += 4) {
                     const uint8_t* q = dst + (out - dist);
-                    const uint8_t b0 = q[0], b1 = q[1], b2 = q[2], b3 = q[3];
+                    const uint8_t b0 = (uint8_t)exr_uni(q[0]), b1 = (uint8_t)exr_uni(q[1]), b2 = (uint8_t)exr_uni(q[2]),
+                                  b3 = (uint8_t)exr_uni(q[3]);
                     put(b0);
                     put(b1);
                     put(b2);
                     put(b3);
                 }
-                for (; j < len; ++j) put(dst[out - dist]);
+                for (; j < len; ++j) put((uint8_t)exr_uni(dst[out - dist]));
             }
         }
     }
     if (out & 3) {  // the last partial word (dst holds cap bytes: write only what is ours)
-        for (int64_t k = out & ~(int64_t)3; k < out; ++k) dst[k] = (uint8_t)(acc >> (8 * (k & 3)));
+        for (int64_t k = out & ~(int64_t)3; k < out; ++k)
+            if (l0) dst[k] = (uint8_t)(acc >> (8 * (k & 3)));
     }
     a1 %= 65521u;
     a2 %= 65521u;
