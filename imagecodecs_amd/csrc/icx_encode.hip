@@ -114,7 +114,51 @@ __global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ s
         return 0.5f * r - 0.4187f * g - 0.0813f * b;
     };
     constexpr int kHalf = kRunPx / 2;
-    if (L.sub) {  // 2x2 quads; chroma = ((a + b) + (c + d)) * 0.25f of the per-pixel values
+    // RGB rows 4-byte aligned (3 bytes per pixel, w % 4 == 0, src aligned): a thread takes two
+    // quads (4 x 2 pixels) with three dword loads per row instead of 12 byte loads
+    const bool rows4 = comps == 3 && (w & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 3) == 0;
+    if (L.sub && rows4) {
+        for (int pr = t; pr < kHalf * 4; pr += 256) {
+            const int qy = pr / (kHalf / 2), qx = 2 * (pr - qy * (kHalf / 2));
+            if (2 * qx >= wpx) continue;
+            const int x = x0 + 2 * qx, y = y0 + 2 * qy;
+            uint32_t rw[2][3];  // rows y, y + 1: pixels x .. x + 3 (edge-clamped past the image)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                if (x + 3 < w && y + r < h) {
+                    const uint32_t* q = reinterpret_cast<const uint32_t*>(src + ((int64_t)(y + r) * w + x) * 3);
+                    rw[r][0] = q[0]; rw[r][1] = q[1]; rw[r][2] = q[2];
+                } else {
+                    uint8_t b[12];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint8_t* pp = pix(x + k, y + r);
+                        b[3 * k] = pp[0]; b[3 * k + 1] = pp[1]; b[3 * k + 2] = pp[2];
+                    }
+#pragma unroll
+                    for (int d = 0; d < 3; ++d)
+                        rw[r][d] = (uint32_t)b[4 * d] | (uint32_t)b[4 * d + 1] << 8 | (uint32_t)b[4 * d + 2] << 16 | (uint32_t)b[4 * d + 3] << 24;
+                }
+            }
+            const uint8_t* B0 = reinterpret_cast<const uint8_t*>(rw[0]);
+            const uint8_t* B1 = reinterpret_cast<const uint8_t*>(rw[1]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (2 * (qx + j) >= wpx) break;
+                const uint8_t *p00 = B0 + 6 * j, *p10 = B0 + 6 * j + 3, *p01 = B1 + 6 * j, *p11 = B1 + 6 * j + 3;
+                float* Y = S + 2 * qy * kRunPx + 2 * (qx + j);
+                Y[0] = ycc(p00, 0);
+                Y[1] = ycc(p10, 0);
+                Y[kRunPx] = ycc(p01, 0);
+                Y[kRunPx + 1] = ycc(p11, 0);
+#pragma unroll
+                for (int c = 1; c < 3; ++c) {
+                    const float a = ycc(p00, c), b = ycc(p10, c), cc = ycc(p01, c), d = ycc(p11, c);
+                    S[16 * kRunPx + (c - 1) * 8 * kHalf + qy * kHalf + qx + j] = ((a + b) + (cc + d)) * 0.25f;
+                }
+            }
+        }
+    } else if (L.sub) {  // 2x2 quads; chroma = ((a + b) + (c + d)) * 0.25f of the per-pixel values
         for (int qd = t; qd < kHalf * 8; qd += 256) {
             const int qy = qd / kHalf, qx = qd - qy * kHalf;
             if (2 * qx >= wpx) continue;
