@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 end measurement on one box: the whole GPU suite, smoke, C3 bench at the driver's
 # settings with rocprofv3 stats, PMC traffic of k_gw_lane and of the whole pipeline (every kernel
-# of a 512-image step; only with PMC=1), C2 at the driver's settings, C5 batch, EXR batch. Stops at the first GPU fault,
+# of a 512-image step; only with PMC=1), C2 at the driver's settings, C5 batch, EXR batch, C4 encode. Stops at the first GPU fault,
 # abort or time limit.
 R="$GRAFT_REPO_ROOT"; [ -n "$R" ] || R=$(pwd)
 cd "$R"; mkdir -p gpurun_out
@@ -26,3 +26,5 @@ timeout -k 10 600 python3 bench.py --workload c5 --steps 5 --warmup 1 > "$O/benc
 rc=$?; echo "c5: $(cut -c1-160 $O/bench_c5.json)"; stop $rc
 timeout -k 10 600 python3 bench.py --workload exr --steps 5 --warmup 2 > "$O/bench_exr.json" 2> "$O/bench_exr.err"
 rc=$?; echo "exr: $(cut -c1-160 $O/bench_exr.json)"; stop $rc
+timeout -k 10 600 python3 bench.py --workload c4 --steps 10 --warmup 2 > "$O/bench_c4.json" 2> "$O/bench_c4.err"
+rc=$?; echo "c4: $(cut -c1-160 $O/bench_c4.json)"; stop $rc
