@@ -175,6 +175,34 @@ __global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ s
                 S[16 * kRunPx + (c - 1) * 8 * kHalf + qy * kHalf + qx] = ((a + b) + (cc + d)) * 0.25f;
             }
         }
+    } else if (rows4) {  // 4:4:4, aligned RGB rows: four pixels per thread, three dword loads
+        for (int i = t; i < kRunPx * 2; i += 256) {
+            const int yy = i / (kRunPx / 4), xx = 4 * (i - yy * (kRunPx / 4));
+            if (xx >= wpx) continue;
+            const int x = x0 + xx, y = y0 + yy;
+            uint32_t rw[3];
+            if (x + 3 < w && y < h) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(src + ((int64_t)y * w + x) * 3);
+                rw[0] = q[0]; rw[1] = q[1]; rw[2] = q[2];
+            } else {
+                uint8_t b[12];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint8_t* pp = pix(x + k, y);
+                    b[3 * k] = pp[0]; b[3 * k + 1] = pp[1]; b[3 * k + 2] = pp[2];
+                }
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+                    rw[d] = (uint32_t)b[4 * d] | (uint32_t)b[4 * d + 1] << 8 | (uint32_t)b[4 * d + 2] << 16 | (uint32_t)b[4 * d + 3] << 24;
+            }
+            const uint8_t* B = reinterpret_cast<const uint8_t*>(rw);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (xx + k >= wpx) break;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) S[c * 8 * kRunPx + yy * kRunPx + xx + k] = ycc(B + 3 * k, c);
+            }
+        }
     } else {
         for (int i = t; i < kRunPx * 8; i += 256) {
             const int yy = i / kRunPx, xx = i - yy * kRunPx;
