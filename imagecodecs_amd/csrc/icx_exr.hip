@@ -15,9 +15,10 @@
 //                  wavelet levels and the range LUT (icx_exr_core.h PIZ section)
 // Scope (tinyexr returns otherwise): single-part scanline images, and tiled ones
 // with one level, mipmap or ripmap levels (every level is decoded and checked, level 0 is the
-// output, as LoadEXRFromMemory does); NONE / RLE / ZIPS / ZIP / PIZ. Multi-part / deep ->
-// UNSUPPORTED_FEATURE, PXR24 / B44 / ZFP -> UNSUPPORTED_FORMAT. Pixels no chunk wrote
-// (tinyexr: uninitialised memory) are 0.
+// output, as LoadEXRFromMemory does); NONE / RLE / ZIPS / ZIP / PIZ. The multi-part / deep
+// version bits are decoded as one part, as LoadEXRFromMemory does (only the tile-offset walk
+// differs); PXR24 / B44 / ZFP -> UNSUPPORTED_FORMAT. Pixels no chunk wrote (tinyexr:
+// uninitialised memory) are 0.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -90,13 +91,17 @@ __global__ __launch_bounds__(kUnpackThreads) void k_exr_unpack(const uint8_t* __
     }
 }
 
-// One workgroup per PIZ chunk: the phases of icx_exr_core.h's PIZ section around barriers. The
+// A PIZ chunk per workgroup item: the phases of icx_exr_core.h's PIZ section around barriers. The
 // Huffman tables live in LDS (code lengths 64 KiB + the 14-bit direct table 64 KiB), then the same
-// LDS holds the 64 Ki-entry range LUT; the channel planes and the long-code lists are the chunk's
-// scratch. One thread walks the Huffman stream (a serial bit stream), the workgroup does the rest.
+// LDS holds the 64 Ki-entry range LUT; the channel planes are the chunk's scratch. The long-code
+// lists (PizWork, 0.9 MB) are not per chunk: the grid is at most kPizSlots workgroups (the LDS
+// allows one per CU), each walks the list of chunks with its own slot of a fixed pool, so the
+// memory does not grow with the chunk count (a file of many tiny tiles). One thread walks the
+// Huffman stream (a serial bit stream), the workgroup does the rest.
+constexpr int kPizSlots = 256;
 __global__ __launch_bounds__(256) void k_exr_piz(const uint8_t* __restrict__ file, int64_t fsize, ExrChunk* __restrict__ ch,
-                                                 const int32_t* __restrict__ list, const int32_t* __restrict__ ctype, int nch,
-                                                 uint8_t* __restrict__ scratch) {
+                                                 const int32_t* __restrict__ list, int nlist, const int32_t* __restrict__ ctype,
+                                                 int nch, uint8_t* __restrict__ scratch, PizWork* __restrict__ pool) {
     struct Tabs {
         uint8_t lens[kPizLens];
         uint32_t dec[kHufDecSize];
@@ -111,49 +116,52 @@ __global__ __launch_bounds__(256) void k_exr_piz(const uint8_t* __restrict__ fil
     __shared__ uint32_t part[256];
     __shared__ PizHuf H;
     const int t = threadIdx.x, T = blockDim.x;
-    ExrChunk& c = ch[list[blockIdx.x]];
-    uint16_t* planes = reinterpret_cast<uint16_t*>(scratch + c.piz_work);
-    PizWork& w = *reinterpret_cast<PizWork*>(scratch + c.piz_work + (c.out_len + 15) / 16 * 16);
-    uint16_t* out = reinterpret_cast<uint16_t*>(scratch + c.scratch);
-    const int64_t nus = c.out_len / 2;
-    piz_init(t, T, L.t.lens, L.t.dec, w, planes, nus, ncnt);
-    part[t] = piz_lut_count(file, c.piz_bitmap, c.piz_mnmx, t);
-    __syncthreads();
-    if (t == 0) {
-        PizBytes F{file, fsize};
-        H = piz_unpack(F, c.piz_huf, c.piz_len, L.t.lens);
-    }
-    __syncthreads();
-    if (H.run) {  // (uniform)
-        if (H.canon) piz_count(t, T, L.t.lens, ncnt);
+    PizWork& w = pool[blockIdx.x];
+    for (int item = blockIdx.x; item < nlist; item += gridDim.x) {
+        __syncthreads();  // (the previous item is done with the LDS tables and the slot)
+        ExrChunk& c = ch[list[item]];
+        uint16_t* planes = reinterpret_cast<uint16_t*>(scratch + c.piz_work);
+        uint16_t* out = reinterpret_cast<uint16_t*>(scratch + c.scratch);
+        const int64_t nus = c.out_len / 2;
+        piz_init(t, T, L.t.lens, L.t.dec, w, planes, nus, ncnt);
+        part[t] = piz_lut_count(file, c.piz_bitmap, c.piz_mnmx, t);
         __syncthreads();
         if (t == 0) {
-            for (int l = 0; l < 59; ++l) nextc[l] = ncnt[l];
-            piz_first_codes(nextc);
-            piz_build(H, L.t.lens, nextc, L.t.dec, w);
             PizBytes F{file, fsize};
-            piz_decode(F, H, L.t.dec, L.t.lens, w, planes, nus);
+            H = piz_unpack(F, c.piz_huf, c.piz_len, L.t.lens);
         }
         __syncthreads();
-    }
-    // the LUT over the tables' LDS: thread t's values from the exclusive prefix of the counts
-    uint32_t base = 0, total = 0;
-    for (int k = 0; k < T; ++k) {
-        const uint32_t v = part[k];
-        base += k < t ? v : 0u;
-        total += v;
-    }
-    piz_lut_fill(file, c.piz_bitmap, c.piz_mnmx, t, base, L.lut);
-    piz_lut_tail(t, T, total, L.lut);
-    const bool w14 = ((total - 1u) & 0xFFFFu) < (1u << 14);  // maxValue < 1 << 14
-    int p2 = piz_top_p2(c.width, c.lines);
-    for (int p = p2 >> 1; p >= 1; p2 = p, p >>= 1) {
-        piz_wavelet_level(t, T, planes, ctype, nch, c.width, c.lines, w14, p, p2);
+        if (H.run) {  // (uniform)
+            if (H.canon) piz_count(t, T, L.t.lens, ncnt);
+            __syncthreads();
+            if (t == 0) {
+                for (int l = 0; l < 59; ++l) nextc[l] = ncnt[l];
+                piz_first_codes(nextc);
+                piz_build(H, L.t.lens, nextc, L.t.dec, w);
+                PizBytes F{file, fsize};
+                piz_decode(F, H, L.t.dec, L.t.lens, w, planes, nus);
+            }
+            __syncthreads();
+        }
+        // the LUT over the tables' LDS: thread t's values from the exclusive prefix of the counts
+        uint32_t base = 0, total = 0;
+        for (int k = 0; k < T; ++k) {
+            const uint32_t v = part[k];
+            base += k < t ? v : 0u;
+            total += v;
+        }
+        piz_lut_fill(file, c.piz_bitmap, c.piz_mnmx, t, base, L.lut);
+        piz_lut_tail(t, T, total, L.lut);
+        const bool w14 = ((total - 1u) & 0xFFFFu) < (1u << 14);  // maxValue < 1 << 14
+        int p2 = piz_top_p2(c.width, c.lines);
+        for (int p = p2 >> 1; p >= 1; p2 = p, p >>= 1) {
+            piz_wavelet_level(t, T, planes, ctype, nch, c.width, c.lines, w14, p, p2);
+            __syncthreads();
+        }
         __syncthreads();
+        piz_interleave(t, T, planes, L.lut, ctype, nch, c.width, c.lines, out);
+        if (t == 0) c.produced = c.out_len;
     }
-    __syncthreads();
-    piz_interleave(t, T, planes, L.lut, ctype, nch, c.width, c.lines, out);
-    if (t == 0) c.produced = c.out_len;
 }
 
 __global__ __launch_bounds__(256) void k_exr_convert(const uint8_t* __restrict__ file, const uint8_t* __restrict__ scratch,
@@ -241,6 +249,9 @@ static int exr_batch(hipStream_t st, ExrWs& ws, int n, const uint8_t* const* dat
         if (!d_out_in || !d_out_in[i]) o_out[i] = take((size_t)P[i].w * P[i].h * 4 * sizeof(float));
     }
     const size_t o_scr = take((size_t)std::max<int64_t>(16, scr));
+    size_t npiz = 0;  // PizWork slots: one per k_exr_piz workgroup of the largest launch
+    for (int i = 0; i < n; ++i) npiz = std::max(npiz, std::min(plist[i].size(), (size_t)kPizSlots));
+    const size_t o_pizw = take(sizeof(PizWork) * std::max<size_t>(1, npiz));
     const size_t o_ch = take(sizeof(ExrChunk) * std::max<size_t>(1, chunks.size()));
     const size_t o_list = take(sizeof(int32_t) * std::max<size_t>(1, list.size()));
     const size_t o_fail = take(sizeof(int32_t) * (size_t)std::max(1, n));
@@ -299,9 +310,11 @@ static int exr_batch(hipStream_t st, ExrWs& ws, int n, const uint8_t* const* dat
         hipLaunchKernelGGL(k_exr_unpack, dim3((unsigned)list.size()), dim3(kUnpackThreads), 0, st, dfile[0], d_ch, d_list, d_scr, d_fail);
     for (int i = 0; i < n; ++i) {
         if (codes[i] != kExrOk || plist[i].empty()) continue;
-        hipLaunchKernelGGL(k_exr_piz, dim3((unsigned)plist[i].size()), dim3(256), 0, st, dfile[i], (int64_t)sizes[i], d_ch,
-                           reinterpret_cast<const int32_t*>(A + o_plist[i]), reinterpret_cast<const int32_t*>(A + o_ty[i]),
-                           P[i].nch, d_scr);
+        const unsigned g = (unsigned)std::min(plist[i].size(), (size_t)kPizSlots);
+        hipLaunchKernelGGL(k_exr_piz, dim3(g), dim3(256), 0, st, dfile[i], (int64_t)sizes[i], d_ch,
+                           reinterpret_cast<const int32_t*>(A + o_plist[i]), (int)plist[i].size(),
+                           reinterpret_cast<const int32_t*>(A + o_ty[i]), P[i].nch, d_scr,
+                           reinterpret_cast<PizWork*>(A + o_pizw));
     }
     for (int i = 0; i < n; ++i) {
         if (codes[i] != kExrOk) continue;

@@ -39,7 +39,8 @@ struct ExrChunk {
     int32_t piz_len;    // PIZ: the Huffman data's length field
     int64_t piz_bitmap; // PIZ: file offset of the range bitmap's first byte (byte minNonZero)
     int64_t piz_huf;    // PIZ: file offset of the Huffman data
-    int64_t piz_work;   // PIZ: scratch offset of the channel planes (out_len), then its PizWork
+    int64_t piz_work;   // PIZ: scratch offset of the channel planes (out_len); the long-code lists
+                        // (PizWork) come from a fixed pool, one per resident k_exr_piz workgroup
     int32_t piz_mnmx;   // PIZ: minNonZero | maxNonZero << 16
     int32_t img;        // batch reads: the chunk's image (its failure flag)
     int64_t base;       // batch reads: its file's device address minus the first file's (k_exr_unpack)
@@ -244,8 +245,8 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
         ret = kExrInvalidHeader;  // ConvertHeader (:4829-4876), whatever ParseEXRHeader returned
     if (ret != kExrOk) return ret;
     const int64_t header_len = (size - 8) - rem;
-    // LoadEXRFromMemory / DecodeEXRImage
-    if (multipart || non_image) return kExrUnsupportedFeature;
+    // LoadEXRFromMemory / DecodeEXRImage (no multi-part / deep rejection here: only LoadEXR has
+    // one, :6268-6270; the flags reach only ReconstructTileOffsets below)
     if (size <= 8) return kExrInvalidArgument;
     int64_t marker = header_len + 8;
     const int nsb = comp == 3 ? 16 : comp == 4 ? 32 : 1;
@@ -279,8 +280,10 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
         if (chunk_count > 0 && chunk_count != nblocks) return kExrInvalidData;
         if (!read_offsets(nblocks)) return kExrInvalidData;
         if (std::find(offsets.begin(), offsets.end(), 0ull) != offsets.end()) {
-            // ReconstructTileOffsets (:5867-5974), single part, not deep: each chunk after the
-            // table goes to the place its own header names (places none names keep the table's)
+            // ReconstructTileOffsets (:5867-5974): each chunk after the table goes to the place its
+            // own header names (places none names keep the table's). The version flags reach it
+            // (:6101-6103): a multi-part chunk's 4-byte part number is skipped (the offset kept is
+            // the one before it), a deep chunk's two int64 sizes and payloads are skipped.
             const int nxl = tile_mode == 2 ? levels.back().lx + 1 : (int)levels.size();
             const int nyl = tile_mode == 2 ? levels.back().ly + 1 : (int)levels.size();
             std::vector<int64_t> lbase(levels.size() + 1, 0);
@@ -288,11 +291,24 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
             int64_t mk = marker;
             for (int64_t k = 0; k < nblocks; ++k) {
                 const int64_t here = mk;
+                if (multipart) {
+                    if (mk < 0 || mk + 4 >= size) return kExrInvalidData;
+                    mk += 4;
+                }
                 if (mk < 0 || mk + 16 >= size) return kExrInvalidData;
                 const int32_t tx_ = rd32(buf + mk), ty_ = rd32(buf + mk + 4), lx = rd32(buf + mk + 8), ly = rd32(buf + mk + 12);
                 mk += 16;
-                if (mk + 4 >= size) return kExrInvalidData;
-                mk += 4 + (int64_t)rd32(buf + mk);
+                if (non_image) {
+                    if (mk + 16 >= size) return kExrInvalidData;
+                    uint64_t pot, ps;
+                    std::memcpy(&pot, buf + mk, 8);
+                    std::memcpy(&ps, buf + mk + 8, 8);
+                    mk = (int64_t)((uint64_t)mk + 16u + pot + ps + 8u);
+                    if (mk >= size || mk < 0) return kExrInvalidData;
+                } else {
+                    if (mk + 4 >= size) return kExrInvalidData;
+                    mk += 4 + (int64_t)rd32(buf + mk);
+                }
                 if (lx < 0 || ly < 0 || tx_ < 0 || ty_ < 0) return kExrInvalidData;  // isValidTile (:5814-5865)
                 if (tile_mode == 0 && (lx != 0 || ly != 0)) return kExrInvalidData;
                 if (tile_mode != 0 && (lx >= nxl || ly >= nyl)) return kExrInvalidData;
@@ -352,7 +368,7 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
         }
         if (c.mode == 3) {  // the channel planes, then the long-code lists
             c.piz_work = P.scratch;
-            P.scratch += (c.out_len + 15) / 16 * 16 + (int64_t)(sizeof(PizWork) + 15) / 16 * 16;
+            P.scratch += (c.out_len + 15) / 16 * 16;
         }
         P.chunks.push_back(c);
         return (int)P.chunks.size() - 1;
@@ -381,9 +397,11 @@ inline int exr_plan(const uint8_t* buf, int64_t size, ExrPlan& P) {
                 const int32_t dlen = rd32(buf + o + 16);
                 if (dlen < 2 || (int64_t)dlen > dsz) return kExrInvalidData;
                 // DecodeTiledPixelData (:4283-4319), in the level's size, tinyexr's int arithmetic
-                if ((int64_t)tile_x * cx > lw || (int64_t)tile_y * cy > lh) return kExrInvalidData;
-                const int tw = ((int64_t)(cx + 1) * tile_x >= lw) ? (int)(lw - (int64_t)cx * tile_x) : (int)tile_x;
-                const int th = ((int64_t)(cy + 1) * tile_y >= lh) ? (int)(lh - (int64_t)cy * tile_y) : (int)tile_y;
+                // (32-bit products: a damaged coordinate wraps as in the reference build)
+                auto m32 = [](int64_t a, int64_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); };
+                if (m32(tile_x, cx) > lw || m32(tile_y, cy) > lh) return kExrInvalidData;
+                const int tw = (m32((uint32_t)cx + 1u, tile_x) >= lw) ? (int32_t)((uint32_t)lw - (uint32_t)m32(cx, tile_x)) : (int)tile_x;
+                const int th = (m32((uint32_t)cy + 1u, tile_y) >= lh) ? (int32_t)((uint32_t)lh - (uint32_t)m32(cy, tile_y)) : (int)tile_y;
                 const int ci = add_chunk(o + 20, dlen, tw, th);
                 if (ci < 0) return kExrInvalidData;
                 P.tile_h.push_back(th);

@@ -278,7 +278,8 @@ int icx_hdr_batch_stage_times(const icx_hdr_batch* b, const char** names, float*
  * reference builds tinyexr with TINYEXR_USE_PIZ 1, tinyexr.h:126-128); mip- and rip-mapped tiled
  * files decode every level's tiles as DecodeChunk does (a failure in any level fails the read) and
  * return level 0; a broken offset table is reconstructed from the chunk headers
- * (ReconstructTileOffsets). Multi-part and deep files -> ICX_EXR_UNSUPPORTED_FEATURE. Pixels no
+ * (ReconstructTileOffsets, where the multi-part and deep version bits change the chunk walk;
+ * LoadEXRFromMemory does not reject them, only LoadEXR does, tinyexr.h:6268-6270). Pixels no
  * chunk wrote (tinyexr leaves them uninitialised) are 0. */
 enum icx_exr_result {
     ICX_EXR_SUCCESS = 0,                /* TINYEXR_SUCCESS                          */

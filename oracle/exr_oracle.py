@@ -2,23 +2,28 @@
 :6645-6860) for single-part scanline and tiled images (one level, mipmap or ripmap levels), NONE /
 RLE / ZIPS / ZIP / PIZ compression. Only tests/ may import it; libicx never does.
 
-PARITY UNPINNED: tinyexr.h cannot be built here -- it needs miniz (TINYEXR_USE_MINIZ, codecs.cpp:28),
-which /root/reference does not ship, or an external zlib -- and the reference holds no .exr file.
-This module is pinned only by its own round trips of tools/exrwrite.py files and by following
-tinyexr's code line by line; zlib's inflate stands in for miniz's mz_uncompress (both are RFC 1950
-/ 1951 decoders that check the Adler-32; a valid stream inflates to the same bytes). PIZ is
-restated from tinyexr's own sources (its build has TINYEXR_USE_PIZ 1, :126-128, which
-codecs.cpp:27-29 does not override), so it needs no third-party code.
+PINNED to the reference: tinyexr.h compiles here in place through its own documented zlib route
+(TINYEXR_USE_MINIZ 0 with the system <zlib.h>, tinyexr.h:109-112, 664-671; oracle/ref/ref_exr_tu.cc,
+`make -C oracle ref`), and tests/test_exr_oracle.py checks this module against that build on every
+fixture and on seeded damage (codes and every float the reference defines; tests/exrref.py). For
+NONE / RLE / PIZ chunks and all header and offset logic the inflate library is not on the path;
+ZIP / ZIPS go through zlib in both, standing in for the reference's un-vendored miniz (both are
+RFC 1950 / 1951 decoders that check the Adler-32: a valid stream inflates to the same bytes). PIZ
+is tinyexr's own code (its build has TINYEXR_USE_PIZ 1, :126-128, which codecs.cpp:27-29 does not
+override).
 
 What it returns where tinyexr's result is undefined or out of this build's scope (the GPU path
 does the same):
-* rows / tile pixels no chunk wrote are 0.0 (tinyexr: uninitialised malloc memory); a NONE
+* rows / tile pixels no chunk wrote are 0.0 (tinyexr: uninitialised malloc memory; the manifest
+  lists them per fixture, "ref_undefined_rows", from the reference build); a NONE
   chunk whose block index lies past the image (chunkCount > lines: tinyexr writes outside its
   buffer) is a decode failure (INVALID_DATA);
 * bytes a damaged PIZ chunk makes the decoder read past the end of the file are 0 (tinyexr reads
   the memory after its buffer); a tile-offset reconstruction that walks before the file fails;
-* multi-part / deep files -> UNSUPPORTED_FEATURE, PXR24 / B44 / ZFP -> UNSUPPORTED_FORMAT; a tile
-  size of 0 -> INVALID_DATA (tinyexr divides by it).
+* PXR24 / B44 / ZFP -> UNSUPPORTED_FORMAT; a tile size of 0 -> INVALID_DATA (tinyexr divides by
+  it). The multi-part and deep version bits are NOT rejected (LoadEXRFromMemory decodes such a
+  file as one part; only LoadEXR refuses them, :6268-6270): they change only how
+  ReconstructTileOffsets walks the chunks.
 """
 import struct
 import zlib
@@ -39,6 +44,10 @@ NONE, RLE, ZIPS, ZIP, PIZ = 0, 1, 2, 3, 4
 SIZE = {UINT: 4, HALF: 2, FLOAT: 4}
 THRESH = 1024 * 8192  # TINYEXR_DIMENSION_THRESHOLD (:3628)
 INT_MAX = 2**31 - 1
+
+
+def _w32(x):  # two's-complement int32 wrap-around
+    return ((x + 2**31) % 2**32) - 2**31
 
 
 def _i32(b, o):
@@ -687,11 +696,14 @@ def _level_index(lx, ly, mode, nxl):  # LevelIndex (:4950-4965)
     return {0: 0, 1: lx, 2: lx + ly * nxl}.get(mode, -1)
 
 
-def _reconstruct_tile_offsets(buf, marker, levels, mode, offs):
-    """ReconstructTileOffsets (:5867-5974) for a single-part, non-deep file: walk the chunks after
-    the offset table and put each at the place its own header names (places no chunk names keep
-    the table's value). None on failure (a marker moved before the file by a negative size also
-    fails: tinyexr reads outside its buffer)."""
+def _reconstruct_tile_offsets(buf, marker, levels, mode, offs, multipart=False, deep=False):
+    """ReconstructTileOffsets (:5867-5974): walk the chunks after the offset table and put each at
+    the place its own header names (places no chunk names keep the table's value). The version
+    flags reach it from LoadEXRFromMemory (:6101-6103): a multi-part file's chunk starts with a
+    4-byte part number that is skipped (the offset recorded is the one before it, :5876-5886);
+    a deep one has two int64 sizes after the coordinates, and the walk skips both payloads and
+    the unpacked size (:5911-5931). None on failure (a marker moved before the file by a
+    negative size also fails: tinyexr reads outside its buffer)."""
     size = len(buf)
     offs = [list(o) for o in offs]
     nxl = max(l[0] for l in levels) + 1
@@ -699,13 +711,25 @@ def _reconstruct_tile_offsets(buf, marker, levels, mode, offs):
     for _, _, nx, ny in levels:
         for _ in range(nx * ny):
             here = marker
+            if multipart:
+                if marker < 0 or marker + 4 >= size:
+                    return None
+                marker += 4
             if marker < 0 or marker + 16 >= size:
                 return None
             tx_, ty_, lx, ly = struct.unpack_from("<iiii", buf, marker)
             marker += 16
-            if marker + 4 >= size:
-                return None
-            marker += 4 + _i32(buf, marker)
+            if deep:
+                if marker + 16 >= size:
+                    return None
+                pot, ps = struct.unpack_from("<qq", buf, marker)
+                marker += 16 + pot + ps + 8
+                if marker >= size or marker < 0:
+                    return None
+            else:
+                if marker + 4 >= size:
+                    return None
+                marker += 4 + _i32(buf, marker)
             # isValidTile (:5814-5865)
             if lx < 0 or ly < 0 or tx_ < 0 or ty_ < 0:
                 return None
@@ -731,8 +755,8 @@ def decode(buf):
     code, info = parse_header(buf)
     if code != SUCCESS:
         return code, 0, 0, None
-    if info["multipart"] or info["non_image"]:
-        return UNSUPPORTED_FEATURE, 0, 0, None
+    # (LoadEXRFromMemory has no multi-part / deep rejection: only LoadEXR does, :6268-6270; the
+    # flags reach only the tile-offset reconstruction below)
     comp = info["compression"]
     size = len(buf)
     if size <= 8:
@@ -785,7 +809,7 @@ def decode(buf):
             offs.append(flat[k:k + nx * ny])
             k += nx * ny
         if any(o == 0 for o in flat):
-            offs = _reconstruct_tile_offsets(buf, marker, levels, mode, offs)
+            offs = _reconstruct_tile_offsets(buf, marker, levels, mode, offs, info["multipart"], info["non_image"])
             if offs is None:
                 return INVALID_DATA, 0, 0, None
     else:
@@ -833,11 +857,13 @@ def decode(buf):
                     continue
                 data = buf[o + 20:o + 20 + dlen]
                 # DecodeTiledPixelData (:4283-4319), in the level's size
-                if tx * cx > lw or ty * cy > lh:
+                # (int arithmetic: a damaged tile coordinate's product wraps as it does in the
+                # reference build's 32-bit multiplies)
+                if _w32(tx * cx) > lw or _w32(ty * cy) > lh:
                     ok = False
                 else:
-                    w = lw - cx * tx if (cx + 1) * tx >= lw else tx
-                    h = lh - cy * ty if (cy + 1) * ty >= lh else ty
+                    w = _w32(lw - _w32(cx * tx)) if _w32(_w32(cx + 1) * tx) >= lw else tx
+                    h = _w32(lh - _w32(cy * ty)) if _w32(_w32(cy + 1) * ty) >= lh else ty
                     ok = _decode_pixels(planes, chans, offs_c, pds, data, comp, info["line_order"], w, ty, tx, 0, 0, h,
                                         buf, o + 20)
                 if not ok:

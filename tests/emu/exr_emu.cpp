@@ -16,7 +16,9 @@ using namespace icx;
 static void emu_piz(const uint8_t* fpad, int64_t size, ExrChunk& c, uint8_t* scratch, const ExrPlan& P) {
     const int T = 256;
     uint16_t* planes = reinterpret_cast<uint16_t*>(scratch + c.piz_work);
-    PizWork& w = *reinterpret_cast<PizWork*>(scratch + c.piz_work + (c.out_len + 15) / 16 * 16);
+    static thread_local std::unique_ptr<PizWork> slot;  // (the kernel's pool slot: reused across chunks)
+    if (!slot) slot.reset(new PizWork);
+    PizWork& w = *slot;
     uint16_t* out = reinterpret_cast<uint16_t*>(scratch + c.scratch);
     const int64_t nus = c.out_len / 2;
     std::vector<uint8_t> lens(kPizLens);

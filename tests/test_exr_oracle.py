@@ -1,14 +1,19 @@
 """CPU tests of the OpenEXR read (Image::readExr -> tinyexr LoadEXRFromMemory, tinyexr.h:6645):
-the fixtures against the oracle (oracle/exr_oracle.py), and the GPU path's own host plan,
-decompressors and per-pixel gather (icx_exr_plan.h / icx_exr_core.h, run on the CPU by
-tests/emu/exr_emu.cpp) against the oracle, bit for bit. PARITY UNPINNED (no EXR library here,
-tinyexr.h needs miniz): see the oracle's header. PIZ is in scope: the reference builds tinyexr
-with TINYEXR_USE_PIZ 1 (tinyexr.h:126-128, codecs.cpp:27-29)."""
+the oracle (oracle/exr_oracle.py) against the reference's own tinyexr compiled in place
+(oracle/_ref/libref_exr.so: tinyexr's zlib route, TINYEXR_USE_MINIZ 0, tinyexr.h:109-112, 664-671)
+on every fixture and on seeded damage; the fixtures against the manifest; and the GPU path's own
+host plan, decompressors and per-pixel gather (icx_exr_plan.h / icx_exr_core.h, run on the CPU by
+tests/emu/exr_emu.cpp) against the oracle, bit for bit. Parity: pinned to the reference build for
+NONE / RLE / PIZ chunks and all header and offset logic; ZIP / ZIPS inflate through the system
+zlib in place of the reference's un-vendored miniz (both check the Adler-32, so a valid stream
+inflates to the same bytes). PIZ is in scope: the reference builds tinyexr with TINYEXR_USE_PIZ 1
+(tinyexr.h:126-128, codecs.cpp:27-29)."""
 import ctypes as C
 import hashlib
 import json
 import os
 import subprocess
+import sys
 import zlib
 
 import numpy as np
@@ -230,3 +235,46 @@ def test_writer_roundtrip_every_layout():
             assert np.array_equal(img.view(np.uint32), exp)
             lo = W.write_exr([("R", R), ("G", G), ("B", B), ("A", A)], compression=comp, line_order=1)
             assert np.array_equal(O.decode(lo)[3].view(np.uint32), exp[::-1])
+
+
+REFERENCE = "/root/reference/tinyexr.h"
+
+
+def _exrref(*args):
+    """tests/exrref.py in its own process (the allocator settings it needs act at start-up)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    env = dict(os.environ, GLIBC_TUNABLES="glibc.malloc.tcache_count=0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "exrref.py"), *args], env=env, check=True,
+                       capture_output=True, text=True, timeout=600)
+    return json.loads(r.stdout)
+
+
+@pytest.mark.skipif(not os.path.exists(REFERENCE), reason="the reference (container only)")
+def test_oracle_vs_live_tinyexr_fixtures():
+    """Every fixture: the reference build's code and every float it defines equal the oracle's;
+    the rows it leaves uninitialised are exactly the manifest's (the oracle writes 0.0 there)."""
+    rep = _exrref("fixtures")
+    assert rep["checked"] == len(MAN)
+    assert rep["failures"] == {}
+    for name, e in MAN.items():
+        assert rep["undefined_rows"].get(name, []) == e["ref_undefined_rows"], name
+
+
+@pytest.mark.skipif(not os.path.exists(REFERENCE), reason="the reference (container only)")
+@pytest.mark.parametrize("seed", [1, 2])
+def test_oracle_vs_live_tinyexr_damage(seed):
+    """Seeded variants of every fixture (version flags: tiled / deep / multi-part bits flipped;
+    1-3 bytes replaced; truncation) give the reference's code and floats."""
+    rep = _exrref("fuzz", str(seed), "4")
+    assert rep["checked"] > 8 * len(MAN)
+    assert rep["failures"] == {}
+
+
+def test_multipart_and_deep_flags_reach_only_tile_offsets():
+    """LoadEXRFromMemory (tinyexr.h:6645-6683) has no multi-part / deep rejection (LoadEXR's is at
+    :6268-6270): a single-part file with either version bit decodes; the bits change only how
+    ReconstructTileOffsets walks the chunks (:5876-5931)."""
+    for name in ("multipart_flag.exr", "multipart_tiled.exr", "deep_flag_scan.exr"):
+        assert MAN[name]["code"] == 0, name
+    for name in ("multipart_tiles_zero.exr", "deep_tiles_zero.exr"):
+        assert MAN[name]["code"] == O.INVALID_DATA, name

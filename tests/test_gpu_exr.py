@@ -1,7 +1,7 @@
 """GPU tests of the OpenEXR read (Image::readExr -> tinyexr LoadEXRFromMemory, tinyexr.h:6645) through
 the C ABI (icx_exr_decode): every fixture's code and RGBA float bits equal the manifest (the
-oracle's result), larger images and random damage equal the oracle live. PARITY UNPINNED (see
-oracle/exr_oracle.py)."""
+oracle's result), larger images and random damage equal the oracle live. The oracle is pinned to
+the reference's tinyexr compiled in place (tests/test_exr_oracle.py, oracle/exr_oracle.py)."""
 import hashlib
 import json
 import os
@@ -170,3 +170,39 @@ def test_exr_decode_device_batch_matches_single(ctx):
         if code == 0:
             assert (ws[k], hs[k]) == (w, h), nm
             assert sha(outs[k].cpu().numpy()[: w * h * 4].reshape(h, w, 4)) == sha(img), nm
+
+
+def test_exr_piz_many_small_tiles(ctx):
+    """PIZ files of many small tiles (4x4 tiles, mipmapped: 341 chunks per 64x64 file, more than
+    k_exr_piz's 256 pool slots, so workgroups walk several chunks with one reused long-code
+    slot), alone and three in one batch call: the oracle's bits (the per-chunk
+    PizWork used to grow the scratch with the chunk count)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    datas, refs = [], []
+    for k in range(2):
+        rng = np.random.default_rng(50 + k)
+        y, x = np.mgrid[0:64, 0:64].astype(np.float32)
+        chans = [(n, (np.sin(x * (0.02 + 0.01 * j)) * np.cos(y * 0.03) * 9 + rng.normal(0, 0.1, x.shape)).astype(np.float16))
+                 for j, n in enumerate("RGBA")]
+        d = W.write_exr(chans, compression=W.PIZ, tiles=(4, 4), levels=1)
+        oc, ow, oh, oimg = O.decode(d)
+        assert (oc, ow, oh) == (0, 64, 64)
+        code, w, h, img = ctx.exr_decode(d)
+        assert (code, w, h) == (0, 64, 64)
+        assert sha(img) == sha(oimg)
+        datas.append(d)
+        refs.append(oimg)
+    datas.append(datas[0])  # (three files in the call, two of them the same bytes)
+    refs.append(refs[0])
+    files = []
+    for d in datas:
+        f = torch.zeros(len(d) + 16, dtype=torch.uint8, device=dev)
+        f[:len(d)] = torch.from_numpy(np.frombuffer(d, np.uint8).copy()).to(dev)
+        files.append(f)
+    outs = [torch.zeros(64 * 64 * 4, dtype=torch.float32, device=dev) for _ in datas]
+    codes, ws, hs = ctx.exr_decode_device_batch(datas, [f.data_ptr() for f in files], [o.data_ptr() for o in outs],
+                                                [64 * 64 * 4] * 3)
+    assert list(codes) == [0, 0, 0]
+    for o, r in zip(outs, refs):
+        assert sha(o.cpu().numpy().reshape(64, 64, 4)) == sha(r)

@@ -155,7 +155,7 @@ def huf_compress(raw):
     iM = int(np.nonzero(freq)[0][-1]) + 1  # the run-length pseudo-symbol
     freq[iM] = 1
     lens = _huf_lengths(freq)
-    hcode = np.zeros(65537, np.int64)
+    hcode = [0] * 65537  # (a list: the loops below walk up to 64 Ki entries per chunk)
     for sym, ln in lens.items():
         hcode[sym] = ln
     # hufCanonicalCodeTable (:2181-2220)

@@ -4,8 +4,10 @@ covering every compression / pixel type / layout the GPU read takes, and files t
 each check, with the oracle's result (oracle/exr_oracle.py: code, size, sha256 of the RGBA float
 bits). TEST INFRASTRUCTURE (container-only; the GPU box only reads the committed files).
 
-Parity is unpinned (oracle/exr_oracle.py header): no EXR library is importable here and
-tinyexr.h does not build without miniz."""
+Pinned: every file is also loaded by the reference's own tinyexr, compiled in place with its
+zlib route (oracle/Makefile `ref`), and the oracle must agree with it on every code and every
+float the reference defines (ref_check); the rows it leaves uninitialised are listed per file
+("ref_undefined_rows", where the oracle and the GPU write 0.0)."""
 import hashlib
 import json
 import os
@@ -85,6 +87,18 @@ def cases():
                                          extra_attrs=W.attr("type", "string", b"tiledimage"))
     c["multipart_flag.exr"] = W.write_exr(rgba(96, 16, 16, "half"), compression=W.ZIP, version_flags=0x10,
                                           extra_attrs=W.attr("name", "string", b"a") + W.attr("type", "string", b"scanlineimage"))
+    # LoadEXRFromMemory accepts the multi-part and deep version bits (only LoadEXR rejects them,
+    # tinyexr.h:6268-6270); they reach ReconstructTileOffsets (:5876-5931): a zeroed table walks
+    # the chunks skipping a part number (multi-part) or two deep sizes and their payloads
+    nt = W.attr("name", "string", b"a") + W.attr("type", "string", b"tiledimage")
+    c["multipart_tiled.exr"] = W.write_exr(smooth(24, 40, "half", 31), compression=W.ZIP, tiles=(16, 16),
+                                           version_flags=0x12, extra_attrs=nt)
+    c["multipart_tiles_zero.exr"] = W.write_exr(smooth(24, 40, "half", 32), compression=W.ZIP, tiles=(16, 16),
+                                                version_flags=0x12, extra_attrs=nt, offsets=lambda o: [0] * len(o))
+    c["deep_flag_scan.exr"] = W.write_exr(rgba(98, 16, 16, "half"), compression=W.RLE, version_flags=0x08,
+                                          extra_attrs=W.attr("name", "string", b"d") + W.attr("type", "string", b"scanlineimage"))
+    c["deep_tiles_zero.exr"] = W.write_exr(smooth(24, 40, "half", 33), compression=W.NONE, tiles=(16, 16),
+                                           version_flags=0x0A, extra_attrs=nt, offsets=lambda o: [0] * len(o))
     # the mipmap flag on a one-level file: the offset table is shorter than the levels need
     c["mipmap_tiles.exr"] = W.write_exr(rgba(97, 16, 16, "half"), compression=W.NONE, tiles=(8, 8),
                                         attrs={"tiles": W.attr("tiles", "tiledesc", struct.pack("<IIB", 8, 8, 1))})
@@ -193,6 +207,23 @@ def _patch_tile_level(data, k):
     return data[: o + 8] + struct.pack("<i", lx + 1) + data[o + 12:]
 
 
+def ref_check():
+    """The reference's tinyexr (oracle/_ref, built in place) over the written files, in its own
+    process (tests/exrref.py): every code and every defined float must equal the oracle's, and
+    the rows the reference leaves uninitialised are recorded in the manifest."""
+    import subprocess
+    if not os.path.exists("/root/reference/tinyexr.h"):
+        raise SystemExit("the reference is needed to pin the EXR manifest (container only)")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    env = dict(os.environ, GLIBC_TUNABLES="glibc.malloc.tcache_count=0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "exrref.py"), "fixtures"], env=env, check=True,
+                       capture_output=True, text=True)
+    rep = json.loads(r.stdout)
+    if rep["failures"]:
+        raise SystemExit(f"oracle differs from the reference build: {rep['failures']}")
+    return rep["undefined_rows"]
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     man = {}
@@ -200,9 +231,12 @@ def main():
         all_cases = cases()
     for name, data in all_cases.items():
         open(os.path.join(OUT, name), "wb").write(data)
+    undef = ref_check()
+    for name, data in all_cases.items():
         code, w, h, img = O.decode(data)
         man[name] = {"code": code, "w": w, "h": h,
-                     "sha256": hashlib.sha256(img.tobytes()).hexdigest() if img is not None else None}
+                     "sha256": hashlib.sha256(img.tobytes()).hexdigest() if img is not None else None,
+                     "ref_undefined_rows": undef.get(name, [])}
     json.dump(man, open(os.path.join(ROOT, "tests", "golden", "exr_manifest.json"), "w"), indent=1, sort_keys=True)
     ok = sum(1 for v in man.values() if v["code"] == 0)
     print(f"{len(man)} files ({ok} decode, {len(man) - ok} rejected)")
