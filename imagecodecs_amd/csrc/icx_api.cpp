@@ -365,6 +365,16 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     // pipe's stream, so it runs beside group g-1's back half (IDCT, convert: HBM-bound) instead
     // of in lockstep with it.
     const bool stagger = b->stagger && used > 1;
+    // Host waits (the deferred-image count and the layout flag read from pinned memory after
+    // each group's plan) only when the call runs eagerly: under stream capture (hipGraph) a
+    // host wait would invalidate the capture, so every entropy round and every layout's back
+    // half is enqueued unconditionally (kFrontAll; empty rounds find no work). ICX_HOST_WAIT=0
+    // forces that form without capture.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    ICX_HIP(ctx, hipStreamIsCapturing(st, &cap), ICX_INTERNAL_ERR);
+    const char* hw = std::getenv("ICX_HOST_WAIT");  // (read per call: tests vary it)
+    const bool no_wait_env = hw && std::atoi(hw) == 0;
+    const bool host_wait = !stagger && cap == hipStreamCaptureStatusNone && !no_wait_env;
     const int ng = (n + per - 1) / per;
     while (stagger && (int)b->front_done.size() < ng) {
         hipEvent_t e;
@@ -378,7 +388,7 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     auto front0 = [&](int g) {
         const int g0 = g * per, p = g % used;
         launch_decode_front(b->ws[p], std::min(per, n - g0), d_data, d_off + g0, d_size + g0, out_stride,
-                            p == 0 ? st : b->pst[p], b->hook.get(), stagger ? kFrontAll : kFrontFirst);
+                            p == 0 ? st : b->pst[p], b->hook.get(), host_wait ? kFrontFirst : kFrontAll);
     };
     for (int g = 0; g < std::min(used, ng); ++g) {
         if (stagger && g > 0) ICX_HIP(ctx, hipStreamWaitEvent(b->pst[g % used], b->front_done[g - 1], 0), ICX_INTERNAL_ERR);
@@ -388,10 +398,10 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     for (int g = 0; g < ng; ++g) {
         const int g0 = g * per, gn = std::min(per, n - g0), p = g % used;
         hipStream_t ps = p == 0 ? st : b->pst[p];
-        if (!stagger) launch_decode_front(b->ws[p], gn, d_data, d_off + g0, d_size + g0, out_stride, ps, b->hook.get(),
-                                          kFrontRest);
+        if (host_wait) launch_decode_front(b->ws[p], gn, d_data, d_off + g0, d_size + g0, out_stride, ps, b->hook.get(),
+                                           kFrontRest);
         launch_decode_back(b->ws[p], gn, d_out + (uint64_t)g0 * out_stride, out_stride, d_status + g0, d_dims + 3 * g0,
-                           ps, b->hook.get(), !stagger);
+                           ps, b->hook.get(), host_wait);
         const int gnext = g + used;
         if (gnext < ng) {
             hipStream_t pn = gnext % used == 0 ? st : b->pst[gnext % used];

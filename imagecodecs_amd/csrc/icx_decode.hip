@@ -411,6 +411,42 @@ __device__ __forceinline__ void idct_col_full(const int32_t (&v)[8], int32_t (&o
     o[6] = cl(x3 - x2);
     o[7] = cl(x7 - x1);
 }
+// idct_col_full before its clip: o[r] = the value whose clip8(o >> 14) is the pixel, the +128
+// level shift folded into x0's rounding constant (every output holds x0's constant exactly once:
+// (x >> 14) + 128 == (x + (128 << 14)) >> 14), so sat4<14> packs four of them with the clip.
+__device__ __forceinline__ void idct_col_raw(const int32_t (&v)[8], int32_t (&o)[8]) {
+    int32_t x0 = (v[0] << 8) + 8192 + (128 << 14), x1 = v[4] << 8, x2 = v[6], x3 = v[2];
+    int32_t x4 = v[1], x5 = v[7], x6 = v[5], x7 = v[3], x8;
+    x8 = m24(kW7, x4 + x5) + 4;
+    x4 = (x8 + m24(kW1 - kW7, x4)) >> 3;
+    x5 = (x8 - m24(kW1 + kW7, x5)) >> 3;
+    x8 = m24(kW3, x6 + x7) + 4;
+    x6 = (x8 - m24(kW3 - kW5, x6)) >> 3;
+    x7 = (x8 - m24(kW3 + kW5, x7)) >> 3;
+    x8 = x0 + x1;
+    x0 -= x1;
+    x1 = m24(kW6, x3 + x2) + 4;
+    x2 = (x1 - m24(kW2 + kW6, x2)) >> 3;
+    x3 = (x1 + m24(kW2 - kW6, x3)) >> 3;
+    x1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = x0 + x2;
+    x0 -= x2;
+    x2 = (wmul(181, x4 + x5) + 128) >> 8;  // (32-bit: as in idct_col)
+    x4 = (wmul(181, x4 - x5) + 128) >> 8;
+    o[0] = x7 + x1;
+    o[1] = x3 + x2;
+    o[2] = x0 + x4;
+    o[3] = x8 + x6;
+    o[4] = x8 - x6;
+    o[5] = x0 - x4;
+    o[6] = x3 - x2;
+    o[7] = x7 - x1;
+}
 __device__ __forceinline__ int32_t pair_swap(int32_t x) {  // the other lane of the pair (DPP quad_perm [1,0,3,2])
     return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
 }
@@ -917,6 +953,21 @@ __device__ __forceinline__ uint32_t dtap(uint32_t biased, int32_t k) {
     const int32_t v = dot4_i8(biased, k, 128 * 128 + 64) >> 7;
     return (uint32_t)min(max(v, 0), 255);
 }
+// Four clipped bytes in one dword from four int32 values: byte i = clip8(v_i >> SH), by gfx950's
+// v_ashr_pk_u8_i32 (D[7:0] = sat_u8(S0 >> S2), D[15:8] = sat_u8(S1 >> S2)). It writes only the
+// low half of D and keeps the high half, and with op_sel:[0,0,0,1] writes the high half and keeps
+// the low one (tools/probe/ashr_pk.hip, measured on the box) -- the kept half is why the compiler's
+// own use of it had leaked bytes. Two instructions per dword replace four shifts,
+// four clamps and three byte permutes.
+template <int SH>
+__device__ __forceinline__ uint32_t sat4(int32_t v0, int32_t v1, int32_t v2, int32_t v3) {
+    uint32_t r;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, %5\n\tv_ashr_pk_u8_i32 %0, %3, %4, %5 op_sel:[0,0,0,1]"
+        : "=&v"(r) : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "i"(SH));
+    return r;
+}
+// dtap before its shift and clip: the biased dot (sat4<7> finishes it)
+__device__ __forceinline__ int32_t dtap_raw(uint32_t biased, int32_t k) { return dot4_i8(biased, k, 128 * 128 + 64); }
 
 template <bool KH>
 __device__ __forceinline__ uint32_t chroma_make(const CPl& c, int r, int M, bool fast, const CRaw& raw) {
@@ -926,7 +977,7 @@ __device__ __forceinline__ uint32_t chroma_make(const CPl& c, int r, int M, bool
         const uint64_t b = w >> ((M & 1) ? 0 : 16);  // bytes b0..b5 = samples 2M-2 .. 2M+3 (biased)
         const uint32_t w0 = (uint32_t)b, w1 = (uint32_t)(b >> 8), w2 = (uint32_t)(b >> 16);
         // tap4(b3,b2,b1,b0), tap4(b1,b2,b3,b4), tap4(b4,b3,b2,b1), tap4(b2,b3,b4,b5)
-        return pack4(dtap(w0, kTapRev), dtap(w1, kTapFwd), dtap(w1, kTapRev), dtap(w2, kTapFwd));
+        return sat4<7>(dtap_raw(w0, kTapRev), dtap_raw(w1, kTapFwd), dtap_raw(w1, kTapRev), dtap_raw(w2, kTapFwd));
     }
     const uint8_t* row = c.p + (int64_t)r * c.s;
     const int n2 = c.w << 1, s = c.s;
@@ -959,33 +1010,27 @@ __device__ __forceinline__ uint32_t vtap_odd(int k, int h, uint32_t w1, uint32_t
 // YCbCr -> RGB of a lane's 4 pixels (jpeg_dec.h:834-853, ycc_to_rgb) as three dwords of packed
 // RGB. Each channel is one or two v_dot2 on 16-bit pairs: (Y, cb) and (Y, cr) per pixel, with
 // the -128 offsets folded into the constant, e.g. R = 256*Y + 359*cr + (128 - 359*128) =
-// (Y << 8) + 359*(cr - 128) + 128. Clamping the numerator to [0, 65535] and taking its byte 1
-// equals clip8(numerator >> 8), so no shift is needed.
+// (Y << 8) + 359*(cr - 128) + 128; sat4<8> takes clip8(numerator >> 8) of four of them at once.
 typedef short icx_short2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ icx_short2 as_s2(uint32_t v) { return __builtin_bit_cast(icx_short2, v); }
 __device__ __forceinline__ void ycc4_to_rgb(uint32_t yv, uint32_t cb, uint32_t cr, uint32_t (&w)[3]) {
     // (Y, c) weight pairs as packed int16: (256, 359), (256, -88), (0, -183), (256, 454)
     constexpr uint32_t kR = 256u | (359u << 16), kG1 = 256u | ((uint32_t)(uint16_t)-88 << 16),
                        kG2 = (uint32_t)(uint16_t)-183 << 16, kB = 256u | (454u << 16);
-    uint32_t R[4], G[4], B[4];
+    int32_t R[4], G[4], B[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t sel = (uint32_t)i | (0x0cu << 8) | ((uint32_t)(4 + i) << 16) | (0x0cu << 24);
         const uint32_t yb = __builtin_amdgcn_perm(cb, yv, sel);  // (Y_i, cb_i)
         const uint32_t yr = __builtin_amdgcn_perm(cr, yv, sel);  // (Y_i, cr_i)
-        const int rn = dot2_i16(yr, kR, 128 - 359 * 128);
-        const int gn = dot2_i16(yr, kG2, dot2_i16(yb, kG1, 128 + (88 + 183) * 128));
-        const int bn = dot2_i16(yb, kB, 128 - 454 * 128);
-        R[i] = (uint32_t)min(max(rn, 0), 65535);
-        G[i] = (uint32_t)min(max(gn, 0), 65535);
-        B[i] = (uint32_t)min(max(bn, 0), 65535);
+        R[i] = dot2_i16(yr, kR, 128 - 359 * 128);
+        G[i] = dot2_i16(yr, kG2, dot2_i16(yb, kG1, 128 + (88 + 183) * 128));
+        B[i] = dot2_i16(yb, kB, 128 - 454 * 128);
     }
-    // byte 1 of each: [R0 G0 B0 R1] [G1 B1 R2 G2] [B2 R3 G3 B3]
-    auto two = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x0c0c0501u); };  // (lo.b1, hi.b1)
-    auto cat = [](uint32_t lo2, uint32_t hi2) { return __builtin_amdgcn_perm(hi2, lo2, 0x05040100u); };
-    w[0] = cat(two(R[0], G[0]), two(B[0], R[1]));
-    w[1] = cat(two(G[1], B[1]), two(R[2], G[2]));
-    w[2] = cat(two(B[2], R[3]), two(G[3], B[3]));
+    // [R0 G0 B0 R1] [G1 B1 R2 G2] [B2 R3 G3 B3]
+    w[0] = sat4<8>(R[0], G[0], B[0], R[1]);
+    w[1] = sat4<8>(G[1], B[1], R[2], G[2]);
+    w[2] = sat4<8>(B[2], R[3], G[3], B[3]);
 }
 
 struct StreamOut {
@@ -1083,8 +1128,8 @@ __device__ __forceinline__ void kv_rows(KvWin& w, const CPl& c1, const CPl& c2, 
         for (int i = 0; i < 4; ++i)  // O = (E >> 8) | new row's byte i << 24
             oc[i] = __builtin_amdgcn_perm(nb, cc[i], 0x00030201u | ((uint32_t)(4 + i) << 24));
         if (k >= 2 && k <= h - 3) {  // both outputs interior (wave-uniform)
-            ev = pack4(dtap(cc[0], kTapRev), dtap(cc[1], kTapRev), dtap(cc[2], kTapRev), dtap(cc[3], kTapRev));
-            od = pack4(dtap(oc[0], kTapFwd), dtap(oc[1], kTapFwd), dtap(oc[2], kTapFwd), dtap(oc[3], kTapFwd));
+            ev = sat4<7>(dtap_raw(cc[0], kTapRev), dtap_raw(cc[1], kTapRev), dtap_raw(cc[2], kTapRev), dtap_raw(cc[3], kTapRev));
+            od = sat4<7>(dtap_raw(oc[0], kTapFwd), dtap_raw(oc[1], kTapFwd), dtap_raw(oc[2], kTapFwd), dtap_raw(oc[3], kTapFwd));
         } else {
             ev = vtap_even(k, h, w0, w1, w2, w3);
             od = vtap_odd(k, h, w1, w2, w3, nrow);
@@ -1349,6 +1394,19 @@ __device__ __forceinline__ void pair_idct(const int4 (&c)[8], const uint32_t (&q
             C[4 + i][jj] = h ? keep : got;
         }
     }
+    if (fast) {  // the four columns' unclipped outputs, then clip and pack a row's four bytes at once
+        int32_t o[4][8];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            int32_t col[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) col[r] = C[r][jj];
+            idct_col_raw(col, o[jj]);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) rowd[r] = sat4<14>(o[0][r], o[1][r], o[2][r], o[3][r]);
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 8; ++r) rowd[r] = 0;
 #pragma unroll
@@ -1356,17 +1414,10 @@ __device__ __forceinline__ void pair_idct(const int4 (&c)[8], const uint32_t (&q
         int32_t col[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) col[r] = C[r][jj];
-        if (fast) {
-            int32_t o[8];
-            idct_col_full(col, o);
+        uint8_t o[8];
+        idct_col<false>(col, o);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) rowd[r] |= (uint32_t)o[r] << (8 * jj);
-        } else {
-            uint8_t o[8];
-            idct_col<false>(col, o);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) rowd[r] |= (uint32_t)o[r] << (8 * jj);
-        }
+        for (int r = 0; r < 8; ++r) rowd[r] |= (uint32_t)o[r] << (8 * jj);
     }
 }
 // A dequant table (64 bytes of Desc::q, 4-byte aligned) into registers straight from global

@@ -13,6 +13,29 @@
 
 namespace icx {
 
+// A 16-byte load that the compiler emits as global_load_dwordx4 whatever it knows about p.
+// A pointer rebuilt from integers (readfirstlane'd bases, pointers carried through loop phis)
+// loses its address space, and the load becomes flat_load_dwordx4. A flat load counts in BOTH
+// vmcnt and lgkmcnt and completes out of order, so every s_waitcnt lgkmcnt(0) of a later LDS
+// read then also waits for it: a prefetch issued ahead of its use turns into a full memory
+// latency at the next LDS lookup.
+typedef unsigned int icx_u32x4 __attribute__((ext_vector_type(4)));
+ICX_HD uint4 gload16(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const icx_u32x4 v = *(const __attribute__((address_space(1))) icx_u32x4*)(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+ICX_HD uint32_t gload4(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(1))) uint32_t*)(p);
+#else
+    return *reinterpret_cast<const uint32_t*>(p);
+#endif
+}
+
 enum : int32_t {
     kOk = 0, kNoJpeg = 1, kUnsupported = 2, kOutOfMem = 3, kInternalErr = 4, kSyntaxError = 5,
     kPending = 6  // headers parsed, entropy-coded segment not yet decoded (internal)

@@ -263,17 +263,17 @@ struct TileChunks {
         // zero-selected past the data: a load inside a branch gets its own vmcnt(0) at the join.
         const int64_t alast = ((int64_t)(ustf_align(R) + L - 1) & ~(int64_t)15) - ustf_align(R);
         auto ld = [&](int64_t a) {
-            const uint4 v = *reinterpret_cast<const uint4*>(R + (a < L ? a : alast));
+            const uint4 v = gload16(R + (a < L ? a : alast));
             return a < L ? v : make_uint4(0u, 0u, 0u, 0u);
         };
         const int64_t a0 = t0 + lane * 16;
         V0 = ld(a0); V1 = ld(a0 + 1024); V2 = ld(a0 + 2048); V3 = ld(a0 + 3072);
         // R[t0-4 .. t0) (headers before the scan when t0 < 1: inside the file, unused), and the
         // dword after the tile
-        const uint32_t p = *reinterpret_cast<const uint32_t*>(R + t0 - 4);
+        const uint32_t p = gload4(R + t0 - 4);
         pw = t0 >= 1 ? p : 0u;
         const int64_t an = t0 + kTileBytes;
-        const uint32_t q = *reinterpret_cast<const uint32_t*>(R + (an < L ? an : alast));
+        const uint32_t q = gload4(R + (an < L ? an : alast));
         nx3 = an < L ? q : 0u;
         r = 0;
     }
@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             bi += done ? 1 : 0;
             act = ok && (!done || bi < bend);
             used_end = done ? r.used : used_end;  // (the reader keeps moving once the lane is idle)
-            const uint64_t m = __ballot(done);
+            const uint64_t m = wave_ballot(done);
             if (m) {  // wave-uniform; every lane takes part
                 if (done) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -1351,7 +1351,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             sv[slot_cell(threadIdx.x, n1)] = (Cell)(o.w1 ? (bs ? cell : o.v1) : 0);
             const bool done = live && z == 0;
             k += done ? 1 : 0;
-            const uint64_t m = __ballot(done);
+            const uint64_t m = wave_ballot(done);
             if (m) {  // wave-uniform: flush the completed blocks, 8 per round
                 if (done) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

@@ -234,11 +234,21 @@ ICX_HD int dri_end_kind(const uint8_t* U, int64_t ulen, int64_t errpos, int64_t 
 }
 
 // Wave-wide helpers that are the identity on the host (the CPU emulator runs one lane).
+// (__builtin_amdgcn_ballot_w64 on the bool itself: the lane mask a compare leaves in an SGPR pair is
+// used as it is; HIP's __any(int) / __ballot(int) first turn the bool into a 0 / 1 VGPR and compare it
+// again, two VALU per vote.)
 ICX_HD bool wave_any(bool p) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return __any(p);
+    return __builtin_amdgcn_ballot_w64(p) != 0;
 #else
     return p;
+#endif
+}
+ICX_HD uint64_t wave_ballot(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(p);
+#else
+    return p ? 1u : 0u;
 #endif
 }
 
@@ -266,7 +276,7 @@ struct Reader {
     int64_t base;      // bit position at init
     uint32_t used;     // bits consumed since init (32-bit loop tests in the lane loops)
     ICX_HD uint4 load(uint32_t c) const {
-        return *reinterpret_cast<const uint4*>(u + (size_t)(c < cmax ? c : cmax) * 16);
+        return gload16(u + (size_t)(c < cmax ? c : cmax) * 16);
     }
     ICX_HD static void expand(const uint4& v, uint64_t& h, uint64_t& l) {
         h = ((uint64_t)__builtin_bswap32(v.x) << 32) | __builtin_bswap32(v.y);

@@ -90,10 +90,15 @@ void icx_batch_destroy(icx_batch* b);
  *   d_dims      n*3 int32 {width, height, ncomp} (ncomp 3 colour / 1 gray; 0s on error)
  * An image larger than the batch limits, or whose pixels exceed out_stride, gets
  * ICX_OUT_OF_MEM. Work is enqueued on `stream` (a hipStream_t; NULL = the context's
- * stream). The call does not wait for the decode: it returns once every group's entropy planning
- * has run on the device (it reads how many images a group's planning deferred to a further
- * entropy round, and enqueues that round only when there are any). Returns ICX_OK or a
- * call-level error. */
+ * stream). The call does not wait for the decode, but when the stream is not capturing it does
+ * wait on the host for each group's entropy planning, and so for all work enqueued on `stream`
+ * before the call (it reads how many images a group's planning deferred to a further entropy
+ * round, and enqueues that round only when there are any): do not make `stream` wait on an
+ * event the caller records only after this call. Under stream capture (hipStreamBeginCapture,
+ * e.g. to build a hipGraph of the decode) the call never waits: every entropy round and every
+ * layout's back half is enqueued unconditionally (rounds with nothing to do find no work), so the
+ * captured graph is complete; ICX_HOST_WAIT=0 selects that form without capture. Returns ICX_OK
+ * or a call-level error. */
 int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint64_t* d_offsets,
                           const uint64_t* d_sizes, uint8_t* d_out, uint64_t out_stride,
                           int32_t* d_status, int32_t* d_dims, void* stream);

@@ -170,3 +170,49 @@ def test_full_group_half_flat_photos_stay_parallel(ctx):
     assert all(r[0] == 0 for r in res)
     _check(res[:4], jpegs[:4])
     b.close()
+
+
+@pytest.mark.parametrize("how", ["capture", "env"])
+def test_batch_decode_without_host_waits(ctx, monkeypatch, how):
+    """icx_jpeg_batch_decode waits on the host for each group's plan (to launch only
+    the entropy rounds a group needs). Under stream capture it must not: the decode is captured
+    into a graph (every round and every layout's back half enqueued), replayed, and gives the
+    oracle's pixels on a batch deep enough to need several rounds; ICX_HOST_WAIT=0 takes the same
+    form eagerly."""
+    import numpy as np
+    import torch
+    dev = torch.device("cuda", 0)
+    monkeypatch.setenv("ICX_UPOOL_BPP", "1")  # (a pool holds ~3 of these images: several rounds)
+    if how == "env":
+        monkeypatch.setenv("ICX_HOST_WAIT", "0")
+    jpegs = [S.synth_jpeg(6300 + k, 512, 512, "444", 100) for k in range(12)] + \
+            [S.synth_jpeg(6320 + k, 512, 384, "420", 90) for k in range(4)]
+    n = len(jpegs)
+    sizes = [len(j) for j in jpegs]
+    offs = np.cumsum([0] + sizes[:-1]).astype(np.int64)
+    data = torch.from_numpy(np.frombuffer(b"".join(jpegs), np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_sz = torch.from_numpy(np.array(sizes, np.int64)).to(dev)
+    stride = 512 * 512 * 3
+    out = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    dims = torch.zeros((n, 3), dtype=torch.int32, device=dev)
+    b = icx.Batch(ctx, n, 512, 512, group=16)
+    args = (n, data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), out.data_ptr(), stride, st.data_ptr(), dims.data_ptr())
+    if how == "capture":
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            b.decode_device(*args, torch.cuda.current_stream(dev).cuda_stream)
+        assert int(st[0].item()) == -1  # captured, not run
+        g.replay()
+    else:
+        b.decode_device(*args, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert b.path_stats() == {"parallel": n, "fallback": 0, "sequential": 0}
+    st, dims, out = st.cpu().numpy(), dims.cpu().numpy(), out.cpu().numpy()
+    for i, j in enumerate(jpegs):
+        code, w, h, nc, pix = O.decode(j)
+        assert st[i] == code == 0 and tuple(dims[i]) == (w, h, nc)
+        assert out[i * stride: i * stride + w * h * nc].tobytes() == pix
+    b.close()

@@ -31,6 +31,16 @@ def main():
               f"{100*g(k,'SQ_WAIT_INST_ANY')/wc:6.1f} | {g(k,'SQ_INSTS_VALU')/w:15.0f} {g(k,'SQ_INSTS_SALU')/w:7.0f} "
               f"{g(k,'SQ_INSTS_LDS')/w:6.0f} | {100*g(k,'SQ_ACTIVE_INST_VALU')/wc:4.1f} {100*g(k,'SQ_ACTIVE_INST_LDS')/wc:4.1f} "
               f"{100*g(k,'SQ_ACTIVE_INST_SCA')/wc:4.1f} {100*g(k,'SQ_ACTIVE_INST_VMEM')/wc:4.1f}")
+    dump_all(agg, kernels)
+
+
+def dump_all(agg, kernels):
+    """Every counter collected, per kernel (raw sums; GRBM_* are chip-wide ticks summed over XCDs)."""
+    names = sorted({c for _, c in agg})
+    print()
+    for k in kernels[:12]:
+        vals = ", ".join(f"{c}={agg[(k, c)]:.4g}" for c in names if (k, c) in agg)
+        print(f"{k}: {vals}")
 
 
 if __name__ == "__main__":
