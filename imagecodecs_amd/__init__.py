@@ -37,7 +37,8 @@ RESULT_NAMES = ["NJ_OK", "NJ_NO_JPEG", "NJ_UNSUPPORTED", "NJ_OUT_OF_MEM", "NJ_IN
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # ICX_LIB selects another build of the same library (e.g. an instrumented variant); it is
 # still the HIP library, there is no other implementation to select.
-LIB_PATH = os.environ.get("ICX_LIB") or os.path.join(_HERE, "lib", "libicx.so")
+_DEFAULT_LIB = os.path.join(_HERE, "lib", "libicx.so")
+LIB_PATH = os.environ.get("ICX_LIB") or _DEFAULT_LIB
 _LIB = None
 
 
@@ -105,6 +106,7 @@ _SIGS = {
     "icx_multi_destroy": (None, [_vp]),
     "icx_multi_decode_host": (_i32, [_vp, _i32, _vp, _vp, _vp, _u64, _vp, _vp]),
     "icx_multi_last_error": (C.c_char_p, [_vp]),
+    "icx_multi_gather": (C.c_char_p, [_vp]),
     "icx_multi_shard": (_i32, [_vp, _i32, _i32, _vp]),
     "icx_exr_probe": (_i32, [_vp, _sz, C.POINTER(_i32), C.POINTER(_i32)]),
     "icx_exr_decode": (_i32, [_vp, _vp, _sz, C.POINTER(_vp), C.POINTER(_i32), C.POINTER(_i32)]),
@@ -152,7 +154,12 @@ def lib():
         _share_hip_runtime_with_torch()
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:
+                if LIB_PATH != _DEFAULT_LIB:
+                    continue  # (an older build loaded by ICX_LIB for an A/B: that entry is unusable)
+                raise
             fn.restype = res
             fn.argtypes = args
         _LIB = L
@@ -467,7 +474,8 @@ def multi_shard(sizes, ndev: int) -> np.ndarray:
 
 class Multi:
     """Multi-GPU decode in one process (icx_multi_*): the batch is split over `devices` by
-    compressed size, one host thread per device, records and pixels gathered to host memory."""
+    compressed size, one host thread per device; the records are gathered over RCCL when the
+    devices are distinct (`gather` says which), the pixels copied to host memory."""
 
     def __init__(self, devices, max_width: int, max_height: int):
         devs = (C.c_int * len(devices))(*devices)
@@ -476,6 +484,10 @@ class Multi:
             raise ICXError("icx_multi_create failed: " + _err(None))
         self.devices = list(devices)
         self.max_width, self.max_height = max_width, max_height
+
+    @property
+    def gather(self) -> str:
+        return lib().icx_multi_gather(self._p).decode()
 
     def close(self):
         if getattr(self, "_p", None):

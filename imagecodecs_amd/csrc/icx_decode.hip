@@ -1578,6 +1578,185 @@ __global__ __launch_bounds__(256, ICX_IDCT_Y_MINW) void k_idct420y(const Desc* _
     idct_units(ac, d, h, wid, nw, nunits, pendf, unit);
 }
 
+#ifndef ICX_IDCT1_MINW
+#define ICX_IDCT1_MINW 4
+#endif
+#ifndef ICX_IDCT1_PF
+#define ICX_IDCT1_PF 0
+#endif
+// ---------------------------------------------------- one-lane-per-block 4:2:0 IDCT (mode 4)
+// One lane transforms one whole block in registers: no pair hand-off (the lane-pair IDCT spends
+// a select per coefficient on which half of the block a lane holds, and a DPP swap plus two
+// selects per output of the row pass on the quadrant exchange), every row and column pass
+// within the lane. A wave's unit is 64 horizontally adjacent blocks of one block row of a plane
+// (512 pixels), so each of the block's 8 row stores is one 8-byte store per lane and the wave
+// writes 512 contiguous bytes per instruction. Dequant reads the int16 cell and the 8-bit table
+// entry by SDWA into one 24-bit multiply; clip and pack by sat4<14>. NanoJPEG's own row / column
+// code (shortcuts and 32-bit wrap-around, jpeg_dec.h:350-442) runs for a block whose dequantized
+// coefficients reach 2^14, as in pair_idct (a per-lane branch: valid streams do not take it).
+__device__ __forceinline__ void load_block8(const int16_t* ac, int64_t blk, int4 (&c)[8]) {
+    const int4* src = reinterpret_cast<const int4*>(ac + blk * 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = nt_ld(src + k);
+}
+// rowd[2r], rowd[2r+1] = the 8 pixels of row r
+__device__ __forceinline__ void block_idct(const int4 (&c)[8], const uint32_t (&qw)[16], const int32_t* dcv,
+                                           const BlkLoc& loc, uint32_t (&rowd)[16]) {
+    auto qt = [&](int z) { return (int32_t)((qw[z >> 2] >> (8 * (z & 3))) & 0xFFu); };
+    auto coef = [&](int z) {
+        const int4& w = c[z >> 3];
+        const int e = z & 7;
+        const uint32_t d32 = (uint32_t)(e < 2 ? w.x : e < 4 ? w.y : e < 6 ? w.z : w.w);
+        return (int32_t)(int16_t)(d32 >> (16 * (e & 1)));
+    };
+    int32_t R[8][8];
+    int32_t hi = 0, lo = 0;
+#pragma unroll
+    for (int n = 1; n < 64; ++n) {
+        const int z = kZigOfNatC[n];
+        R[n >> 3][n & 7] = m24(coef(z), qt(z));  // int16 x 8-bit: exact
+        hi = max(hi, R[n >> 3][n & 7]);
+        lo = min(lo, R[n >> 3][n & 7]);
+    }
+    R[0][0] = wmul(blk_dc((int16_t)c[0].x, dcv, loc), qt(0));  // the absolute DC
+    hi = max(hi, R[0][0]);
+    lo = min(lo, R[0][0]);
+    if (hi < (1 << 14) && lo > -(1 << 14)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) idct_row_full(R[i]);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {  // columns 4 half .. 4 half + 3, then their row dwords
+            int32_t o[4][8];  // o[column][row], unclipped
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                int32_t col[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) col[r] = R[r][4 * half + jj];
+                idct_col_raw(col, o[jj]);
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) rowd[2 * r + half] = sat4<14>(o[0][r], o[1][r], o[2][r], o[3][r]);
+        }
+    } else {  // the reference code, shortcuts and 32-bit wrap-around included
+#pragma unroll
+        for (int i = 0; i < 8; ++i) idct_row<false>(R[i]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rowd[r] = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            int32_t col[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) col[r] = R[r][j];
+            uint8_t ob[8];
+            idct_col<false>(col, ob);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) rowd[2 * r + (j >> 2)] |= (uint32_t)ob[r] << (8 * (j & 3));
+        }
+    }
+}
+// Units of one plane: `ucols` units of 64 blocks per block row, `nby` block rows; unit u's lane
+// takes block column bx = (u % ucols) * 64 + lane, clamped to the row (a lane past the row's end
+// transforms its last block again and stores the same bytes at the same place: every lane
+// stores). blkn(bx, by) = the block's index in the image's MCU order. Software-pipelined like
+// idct_units: the next unit's block is loaded during this one, its map entry the unit before.
+template <class BlkN>
+__device__ __forceinline__ void plane_units(const Desc& d, const int16_t* ac, const int32_t* dcv, const uint2* map,
+                                            const uint32_t (&qw)[16], uint8_t* P, int stride, uint32_t nbx,
+                                            uint32_t nby, uint32_t wid, uint32_t nw, BlkN blkn) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ucols = (nbx + 63) >> 6, nunits = ucols * nby;
+    if (wid >= nunits) return;
+    auto pend = [&](uint32_t u) {
+        u = min(u, nunits - 1);  // (past the end: harmless reloads)
+        const uint32_t by = u / ucols;
+        const uint32_t bx = min(((u - by * ucols) << 6) + lane, nbx - 1);
+        return blk_pend(d, map, blkn(bx, by));
+    };
+    auto unit = [&](uint32_t u, const int4 (&c)[8], const BlkLoc& l) {
+        const uint32_t by = u / ucols, bx0 = (u - by * ucols) << 6;
+        const uint32_t bx = min(bx0 + lane, nbx - 1);
+        uint32_t rowd[16];
+        block_idct(c, qw, dcv, l, rowd);
+        // the unit's row base is wave-uniform; a lane adds its 32-bit column offset
+        uint8_t* const rowp = P + (int64_t)by * 8 * stride + (int64_t)bx0 * 8;
+        const uint32_t lo = (bx - bx0) * 8;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint2 v = make_uint2(rowd[2 * r], rowd[2 * r + 1]);
+            nt_st(v, reinterpret_cast<uint2*>(rowp + (lo + (uint32_t)(r * stride))));
+        }
+    };
+#if ICX_IDCT1_PF  // the next unit's block loaded during this one (two register sets)
+    int4 ca[8], cb[8];
+    BlkLoc la = blk_resolve(d, pend(wid)), lb;
+    load_block8(ac, la.blk, ca);
+    BlkPend pa, pb = pend(wid + nw);
+    auto step = [&](uint32_t u, const int4 (&D)[8], const BlkLoc& lD, int4 (&Dn)[8], BlkLoc& lDn, const BlkPend& Pn,
+                    BlkPend& Pa) {
+        lDn = blk_resolve(d, Pn);
+        load_block8(ac, lDn.blk, Dn);
+        Pa = pend(u + 2 * nw);
+        unit(u, D, lD);
+    };
+    for (uint32_t u = wid;;) {
+        step(u, ca, la, cb, lb, pb, pa);
+        if ((u += nw) >= nunits) break;
+        step(u, cb, lb, ca, la, pa, pb);
+        if ((u += nw) >= nunits) break;
+    }
+#else  // only the map entry one unit ahead: the block's loads wait out their latency (other waves run)
+    BlkPend p = pend(wid);
+    for (uint32_t u = wid; u < nunits; u += nw) {
+        const BlkLoc l = blk_resolve(d, p);
+        int4 c[8];
+        load_block8(ac, l.blk, c);
+        p = pend(u + nw);
+        unit(u, c, l);
+    }
+#endif
+}
+// All three planes of fused420 images: gridDim.x workgroups per image walk the luma units, then
+// the Cb and Cr units (one grid-stride sequence over the three planes' units).
+__global__ __launch_bounds__(256, ICX_IDCT1_MINW) void k_idct420s(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                                                   const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                                                   uint8_t* __restrict__ planes, int64_t plane_cap) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (!fused420(d)) return;
+    const uint32_t wave = (uint32_t)wave_index();
+    const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t wid = chunk0 * 4 + wave, nw = gridDim.x * 4;
+    const uint32_t mbw = (uint32_t)d.mbw, mbh = (uint32_t)d.mbh;
+    uint8_t* const slot = planes + (int64_t)img * plane_cap;
+    // luma: 2 x 2 blocks per MCU (k = 2 sby + sbx), block rows 2 mbh
+    const uint32_t ynbx = 2 * mbw, yunits = ((ynbx + 63) >> 6) * (2 * mbh);
+    const uint32_t cnbx = mbw, cunits = ((cnbx + 63) >> 6) * mbh;
+    // The three planes' units are one sequence (luma, Cb, Cr); a wave takes units wid, wid + nw, ...
+    // of it, i.e. in a plane whose units start at `base` the local units first(base), + nw, ...
+    auto first = [&](uint32_t base) { return wid >= base ? wid - base : (base - wid + nw - 1) / nw * nw + wid - base; };
+    uint32_t qw[16];
+    auto uniform_q = [&]() {  // (one table per unit: scalar registers, read by SDWA)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) qw[k] = __builtin_amdgcn_readfirstlane(qw[k]);
+    };
+    if (wid < yunits) {  // (wave-uniform)
+        load_qw_g(d.q[d.c[0].tq], qw);
+        uniform_q();
+        plane_units(d, ac, dcv, map, qw, slot, d.c[0].stride, ynbx, 2 * mbh, wid, nw, [&](uint32_t bx, uint32_t by) {
+            return (int64_t)(((by >> 1) * mbw + (bx >> 1)) * 6 + ((by & 1) << 1) + (bx & 1));
+        });
+    }
+#pragma unroll
+    for (uint32_t cc = 0; cc < 2; ++cc) {
+        const uint32_t f = first(yunits + cc * cunits);
+        if (f >= cunits) continue;
+        load_qw_g(d.q[d.c[1 + cc].tq], qw);
+        uniform_q();
+        plane_units(d, ac, dcv, map, qw, slot + comp_plane_off(d, 1 + cc), d.c[1 + cc].stride, cnbx, mbh, f, nw,
+                    [&](uint32_t bx, uint32_t by) { return (int64_t)((by * mbw + bx) * 6 + 4 + cc); });
+    }
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // global stores (__syncthreads would also wait vmcnt(0), i.e. for every RGB store in flight).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -1930,15 +2109,23 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     // slower beside the second pipeline: DESIGN.md §4); mode 0 leaves them to k_idct. ICX_FUSE420
     // overrides the mode (tests, experiments).
     // (any value other than 0, 1, 2 is the default: an unknown mode would leave 4:2:0 luma untransformed)
+    // Mode 4 (default): all three planes by the one-lane-per-block IDCT k_idct420s, then the
+    // stream conversion as in mode 2.
     const int fuse = [] {  // (read per launch: tests switch modes within one process)
-        const int v = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 2;
-        return (v >= 0 && v <= 3) ? v : 2;
+        const int v = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 4;
+        return (v >= 0 && v <= 4) ? v : 4;
     }();
     if (other || fuse == 0) {
         hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes, ws.plane_cap,
                            fuse);
         hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap);
+    }
+    if (fuse == 4) {  // 4:2:0: 64 blocks of a block row per wave unit, luma then chroma units
+        const int64_t units = (maxblk / 6) * 6 / 64 + 3;
+        const int sgx = (int)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 16384 / n)) & ~7;
+        hipLaunchKernelGGL(k_idct420s, dim3(std::max(sgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map,
+                           ws.planes, ws.plane_cap);
     }
     if (fuse == 1 || fuse == 2) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
         const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;

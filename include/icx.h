@@ -141,8 +141,12 @@ void* icx_ctx_stream(const icx_ctx* ctx); /* the context's hipStream_t */
 
 /* Multi-GPU batch decode in one process: the batch is split over `ndev` devices by
  * compressed size (greedy longest-first, icx_multi_shard), one host thread per device decodes
- * its shard with its own context, workspace and stream, and the records and pixels are
- * gathered into host memory. Every image of every device may be up to max_width x max_height. */
+ * its shard with its own context, workspace and stream, and computes its per-image records on
+ * the device. The records are gathered over RCCL (one communicator per device, ncclCommInitAll;
+ * one grouped ncclAllGather of every shard's records padded to the largest shard) when the
+ * devices are distinct and librccl.so loads, else through host memory (ICX_MULTI_RCCL=0 forces
+ * that); each device copies its images' pixels to the caller's host buffers. Every image of
+ * every device may be up to max_width x max_height. */
 typedef struct icx_multi icx_multi;
 icx_multi* icx_multi_create(const int* devices, int ndev, int max_width, int max_height);
 void icx_multi_destroy(icx_multi* m);
@@ -152,6 +156,8 @@ void icx_multi_destroy(icx_multi* m);
 int icx_multi_decode_host(icx_multi* m, int n, const uint8_t* const* jpegs, const size_t* sizes,
                           uint8_t* const* outs, uint64_t out_stride, icx_record* records, int32_t* shard_of);
 const char* icx_multi_last_error(const icx_multi* m);
+/* How the records are gathered: "rccl", or "host (<reason>)". */
+const char* icx_multi_gather(const icx_multi* m);
 /* The split: shard_of[i] in [0, ndev) for n images of the given compressed sizes. */
 int icx_multi_shard(const size_t* sizes, int n, int ndev, int32_t* shard_of);
 

@@ -30,10 +30,26 @@ def _expect(j):
     return (code, w, h, n, shard.checksum64(pix)) if code == 0 else (code, 0, 0, 0, 0)
 
 
-@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def _all_devices():
+    import torch
+    n = torch.cuda.device_count()
+    return list(range(n)) if n > 1 else None
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], "all"])
 def test_multi_decode_records_and_pixels(devices):
+    """The records gather: RCCL over distinct devices (all of a multi-GPU box), host memory for one
+    device or a device listed twice (RCCL needs distinct GPUs), with the same records either way."""
+    if devices == "all":
+        devices = _all_devices()
+        if devices is None:
+            pytest.skip("one GPU: the RCCL gather needs distinct devices")
     jpegs = _jobs()
     m = icx.Multi(devices, 1024, 1024)
+    if len(set(devices)) > 1:
+        assert m.gather == "rccl", m.gather
+    else:
+        assert m.gather.startswith("host ("), m.gather
     rec, owner, pix = m.decode_host(jpegs)
     assert list(owner) == list(icx.multi_shard([len(j) for j in jpegs], len(devices)))
     assert list(owner) == [next(r for r, p in enumerate(shard.shard_by_size([len(j) for j in jpegs], len(devices)))
