@@ -1084,7 +1084,6 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644); a second
             // symbol is only paired when its own peek stays clear of the error byte
             const uint32_t u0 = r.used;
-            const int z0 = z;
             const WriteOut o = write_step(r, T, H, S, b, z, (int32_t)u0 > err_pair);
             // Bookkeeping by selects, not per-lane branches (each divergent `if` cost its exec-mask
             // save / restore and a branch in every iteration).
@@ -1099,15 +1098,15 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             const int32_t cell = dc_cell(pc);
             if (okdc && cell == kDcEscape) D[bi] = pc;  // DC outside int16 (corrupt streams only)
             // Both slot writes always issue (zig-zag order; k_idct reorders). A symbol that writes
-            // nothing stores 0 at a coefficient the block has not reached: the cursor z0 (EOB), or
+            // nothing stores 0 at a coefficient the block has not reached: the cursor (EOB), or
             // the one after the first symbol (no pair) -- which is that symbol's own cell when it
             // was coefficient 63, so the pair's cell is written first and the first symbol's
             // value lands last. A lane that stopped scribbles in its own slot, which is zeroed
             // before its next use.
-            const int n1 = o.w1 ? (o.c1 & 63) : min(z0, 63);
-            const int n2 = o.w2 ? (o.c2 & 63) : (o.w1 ? min(o.c1 + 1, 63) : min(z0, 63));
-            sv[slot_elem(threadIdx.x, n2)] = (int16_t)(o.w2 ? o.v2 : 0);
-            sv[slot_elem(threadIdx.x, n1)] = (int16_t)(o.w1 ? (dc ? cell : o.v1) : 0);
+            // (v1 is 0 for EOB and invalid codes; an invalid DC code fails the lane, so its cell
+            // is never stored)
+            sv[slot_elem(threadIdx.x, o.n2)] = (int16_t)(o.w2 ? o.v2 : 0);
+            sv[slot_elem(threadIdx.x, o.n1)] = (int16_t)(dc ? cell : o.v1);
             const bool done = ok && z == 0;
             const int64_t bdone = bi;
             bi += done ? 1 : 0;
@@ -1334,7 +1333,6 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             ci = bs ? S.comp(b) : ci;
             // one lookup (every lane: the reader moves on idle lanes too, see k_spec_write)
             const uint32_t u0 = r.used;
-            const int z0 = z;
             const WriteOut o = write_step(r, T, H, S, b, z, eb.near(u0));
             const bool fail = eb.fail(u0, o.err, r.used);
             err = live && fail && err == INT32_MAX ? k : err;
@@ -1345,10 +1343,10 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             ds2 = owndc && ci == 2 ? pc : ds2;
             const int32_t cell = dc_cell(pc);
             if (owndc && cell == kDcEscape) dcv[addr] = pc;  // lane-local DC outside int16 (rare)
-            const int n1 = o.w1 ? (o.c1 & 63) : min(z0, 63);
-            const int n2 = o.w2 ? (o.c2 & 63) : (o.w1 ? min(o.c1 + 1, 63) : min(z0, 63));
-            sv[slot_cell(threadIdx.x, n2)] = (Cell)(o.w2 ? o.v2 : 0);
-            sv[slot_cell(threadIdx.x, n1)] = (Cell)(o.w1 ? (bs ? cell : o.v1) : 0);
+            // (v1 is 0 for EOB and invalid codes; an invalid DC code is a decode error, so that
+            // block is a discarded speculative one or the image fails)
+            sv[slot_cell(threadIdx.x, o.n2)] = (Cell)(o.w2 ? o.v2 : 0);
+            sv[slot_cell(threadIdx.x, o.n1)] = (Cell)(bs ? cell : o.v1);
             const bool done = live && z == 0;
             k += done ? 1 : 0;
             const uint64_t m = wave_ballot(done);

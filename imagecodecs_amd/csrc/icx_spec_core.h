@@ -437,6 +437,12 @@ struct WriteOut {
     int c1, c2;
     bool w1, w2;  // write v1 at c1 / v2 at c2
     bool err;
+    // Slot cells for a block assembled in place (k_gw_lane, k_spec_write): v1 goes to n1, then
+    // (v2 if w2, else 0) to n2, n2 written first. n1 = c1 when w1, else the unreached cursor z;
+    // n2 = c2 when w2, else the first cell past symbol 1 (when that is 64, cell 63, which the
+    // n1 write then overwrites). Clamped to 63 where c1 would pass it, which only a decode
+    // error does (the block is then garbage: a discarded speculative one, or a failing image).
+    int n1, n2;
 };
 template <class Tab>
 ICX_HD WriteOut write_step(Reader& r, const Tab& T, const Huff* H, const Sel& S, int& b, int& z, bool near_err) {
@@ -454,6 +460,12 @@ ICX_HD WriteOut write_step(Reader& r, const Tab& T, const Huff* H, const Sel& S,
     o.c2 = o.c1 + (int)zad2;
     o.w1 = !st_eob1(e) && !st_err1(e);
     o.w2 = pair && !eob2;
+    {  // (zad1 = 0 exactly for EOB / invalid codes, and a pair's second symbol has zad2 >= 1)
+        const int zn1 = z + (int)zad1;
+        const int n1 = zn1 - (zad1 != 0u ? 1 : 0), n2 = zn1 + (o.w2 ? (int)zad2 - 1 : 0);
+        o.n1 = n1 < 63 ? n1 : 63;
+        o.n2 = n2 < 63 ? n2 : 63;
+    }
     const bool eob = pair ? eob2 != 0 : st_eob1(e) != 0;
     const int zn = z + (int)zad1 + (pair ? (int)zad2 : 0);
     o.err = st_err1(e) || (zn > 64 && !eob);

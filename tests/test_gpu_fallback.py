@@ -117,8 +117,14 @@ def test_deep_batch_never_sequential(ctx, monkeypatch, capsys):
 def test_sequential_fallback_cost(ctx, capsys):
     """A 64-image 512^2 batch with one non-conforming 18-blocks-per-MCU image and one DRI image
     whose restart marker NanoJPEG reads where no lane starts: both decode exactly (the only two),
-    on the sequential kernel, and what they add is one image's serial walk each (~60 ms for a
-    512^2 y44 image on one MI355X lane, ~4 MP/s), not a per-batch cost."""
+    on the sequential kernel, and what they add is one image's serial walk each (~40-60 ms for a
+    512^2 image on one MI355X lane), not a per-batch cost.
+
+    The two walks run side by side (the batch's two pipelines, one image each): the time they
+    add to the clean batch stays under 1.5x the slower one decoded alone. Two walks that
+    serialise (70 -> 149 ms between rounds; a kernel trace of this test in round 5
+    showed them overlapped, 60 and 41 ms) add their sum and fail. Each time is the best of three
+    calls, so a host hiccup in one call does not decide it."""
     clean = [S.synth_jpeg(6300 + k % 8, 512, 512, "420", 90) for k in range(64)]
     bad = list(clean)
     bad[5] = S.synth_jpeg(6399, 512, 512, "y44", 90)
@@ -126,19 +132,25 @@ def test_sequential_fallback_cost(ctx, capsys):
     b = icx.Batch(ctx, 64, 512, 512)
 
     def run(batch):
-        b.decode_host(batch)  # (warm)
-        t0 = time.perf_counter()
-        res = b.decode_host(batch)
-        return time.perf_counter() - t0, res
+        res = b.decode_host(batch)  # (warm)
+        best = float("inf")
+        for _ in range(3):
+            t0 = time.perf_counter()
+            b.decode_host(batch)
+            best = min(best, time.perf_counter() - t0)
+        return best, res
 
     t_clean, _ = run(clean)
     t_bad, res = run(bad)
-    st = b.path_stats()
+    st = b.path_stats()  # (of the last call)
     assert st["parallel"] == 62 and st["fallback"] + st["sequential"] == 2, st
     _check(res, bad)
+    t_one = [run([bad[k]])[0] for k in (5, 40)]  # each walk alone
+    added = t_bad - t_clean
     with capsys.disabled():
-        print(f"\n  64 x 512^2: clean {t_clean * 1e3:.1f} ms, with 2 sequential images {t_bad * 1e3:.1f} ms")
-    assert t_bad < t_clean + 0.5, (t_bad, t_clean)
+        print(f"\n  64 x 512^2: clean {t_clean * 1e3:.1f} ms, with 2 sequential images {t_bad * 1e3:.1f} ms "
+              f"(+{added * 1e3:.1f}); alone {t_one[0] * 1e3:.1f} / {t_one[1] * 1e3:.1f} ms")
+    assert added < 1.5 * max(t_one), (t_bad, t_clean, t_one)
     b.close()
 
 
