@@ -643,8 +643,6 @@ int icx_jpeg_encode_with_func(icx_ctx* ctx, icx_write_func* func, void* context,
 struct icx_encoder {
     icx_ctx* ctx = nullptr;
     EncWs* ws = nullptr;
-    EncWs* ws2 = nullptr;         // second workspace + stream of the batch entry (created on use)
-    hipStream_t st2 = nullptr;
 };
 
 icx_encoder* icx_encoder_create(icx_ctx* ctx) {
@@ -659,20 +657,12 @@ void icx_encoder_destroy(icx_encoder* enc) {
     if (!enc) return;
     (void)hipSetDevice(enc->ctx->device);
     enc_ws_destroy(enc->ws);
-    if (enc->ws2) enc_ws_destroy(enc->ws2);
-    if (enc->st2) (void)hipStreamDestroy(enc->st2);
     delete enc;
 }
 
 int icx_encoder_stage_times(icx_encoder* enc, const char** names, float* ms, int cap) {
     if (!enc || cap <= 0) return 0;
-    const int k = enc_ws_stage_times(enc->ws, names, ms, cap);
-    if (enc->ws2 && ms) {  // the batch entry's second workspace: summed
-        float m2[8] = {};
-        const int k2 = enc_ws_stage_times(enc->ws2, nullptr, m2, std::min(cap, 8));
-        for (int i = 0; i < std::min(k, k2); ++i) ms[i] += m2[i];
-    }
-    return k;
+    return enc_ws_stage_times(enc->ws, names, ms, cap);
 }
 
 int icx_jpeg_encode_device(icx_encoder* enc, int quality, int subsampling, int width, int height,
@@ -706,12 +696,10 @@ int icx_jpeg_encode_device_batch(icx_encoder* enc, int n, int quality, int subsa
         if ((int64_t)width * height > 0 && !d_srcs[i]) { ctx->err = "null buffer"; return ICX_UNSUPPORTED; }
     if (n > 0 && out_stride && !d_out) { ctx->err = "null buffer"; return ICX_UNSUPPORTED; }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_INTERNAL_ERR);
-    if (!enc->ws2) enc->ws2 = enc_ws_create();
-    if (!enc->st2) ICX_HIP(ctx, hipStreamCreateWithFlags(&enc->st2, hipStreamNonBlocking), ICX_INTERNAL_ERR);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
     std::vector<int32_t> rc(n > 0 ? n : 1);
-    if (jpeg_encode_device_batch(st, enc->st2, enc->ws, enc->ws2, n, quality, subsampling, width, height,
-                                 num_components, d_srcs, d_out, out_stride, out_sizes, rc.data()) < 0) {
+    if (jpeg_encode_device_batch(st, enc->ws, n, quality, subsampling, width, height, num_components, d_srcs, d_out,
+                                 out_stride, out_sizes, rc.data()) < 0) {
         ctx->err = "HIP failure in jpeg_encode_device_batch";
         return ICX_INTERNAL_ERR;
     }

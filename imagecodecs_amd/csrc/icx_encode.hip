@@ -1,18 +1,22 @@
 // icx_encode.hip -- gfx950 JPEG encoder: tiny_jpeg-exact (jpeg_enc.h:786-1175) and the C4
 // extension (4:2:0 / 4:4:4, IJG quality; defined by oracle/tje_oracle.c or_jpeg_encode).
 //
-//   k_enc_units   gather + float RGB->YCbCr (+ 2x2 chroma mean for 4:2:0) staged in LDS per
-//                 512-pixel run, then one lane per data unit: AAN float FDCT + quantize + the
-//                 AC bit length (jpeg_enc.h:1094-1126, 656-817, 851-887)
-//   k_enc_count   adds the DC code length of every unit       (jpeg_enc.h:831-849)
-//   (scan)        exclusive prefix sum of unit bit lengths -> bit offsets (hipCUB)
-//   k_enc_emit    pack each unit's codes at its bit offset    (jpeg_enc.h:613-643)
-//   k_stuff_*     FF -> FF 00 byte stuffing by count/scan/copy (jpeg_enc.h:634-638)
+//   k_enc_run        one workgroup per 512-pixel run of an MCU row, any number of images per
+//                    launch: gather + float RGB->YCbCr (+ 2x2 chroma mean for 4:2:0) staged in LDS,
+//                    one lane per data unit: AAN float FDCT, quantise, code lengths (jpeg_enc.h
+//                    :1094-1126, 656-817, 831-887); a decoupled look-back over the image's earlier
+//                    runs gives the run's bit offset and the DC predictors across runs; every lane
+//                    then packs its unit's codes at its offset (:613-643)
+//   k_stuff_count_b  FF -> FF 00 byte stuffing by count / scan (hipCUB, one per batch) / copy
+//   k_stuff_write_b  (:634-638), the header and EOI written with the stream
 // Built with -ffp-contract=off: every float op rounds exactly like the reference build.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "icx_internal.h"
@@ -34,15 +38,9 @@ struct EncLayout {
     int sub;                 // chroma units average 2x2 pixels
     int8_t comp[6], bx[6], by[6];
     int8_t prevk[6];         // previous unit of the same component in the MCU, or -1
+    int8_t firstk[3];        // first unit of each component in an MCU
     int8_t lastk[3];         // last unit of each component in an MCU
 };
-__device__ __forceinline__ int64_t pred_unit(const EncLayout& L, int64_t u) {  // DC predictor source
-    const int64_t m = u / L.upm;
-    const int k = (int)(u - m * L.upm);
-    if (L.prevk[k] >= 0) return m * L.upm + L.prevk[k];
-    return m > 0 ? (m - 1) * L.upm + L.lastk[L.comp[k]] : -1;
-}
-
 // AAN float FDCT on 8 samples at stride S (tjei_fdct, jpeg_enc.h:667-712), in registers.
 template <int S>
 __device__ __forceinline__ void fdct8(float* p) {
@@ -85,25 +83,111 @@ __device__ __forceinline__ void vli(int v, int& nb, uint32_t& bits) {  // jpeg_e
     bits = (uint32_t)v & ((1u << nb) - 1u);
 }
 
-// A workgroup owns a 512-pixel run of one MCU row (64 MCUs at 4:4:4, 32 at 4:2:0; 192 data units
-// either way). Phase 1: all lanes read the run's pixels (coalesced, edge-clamped as
-// jpeg_enc.h:1106-1111) and write the samples the units use to LDS -- Y per pixel, Cb/Cr per pixel
-// (4:4:4) or per 2x2 mean (4:2:0), each with the reference's float expression and order
-// (:1118-1120). Phase 2: one lane per data unit: 8x8 samples from LDS, AAN FDCT, quantise
-// (:806-817), the zig-zag block as eight 16-byte stores, and the AC part of its Huffman bit length
-// (the DC part needs the previous unit's DC: k_enc_count adds it).
+// One workgroup per run: 512 pixels of one MCU row (64 MCUs at 4:4:4, 32 at 4:2:0; 192 data
+// units either way), runs in stream order within an image, taken by ticket so a run's
+// predecessors are always resident. The whole entropy-coded stream of the run is produced here:
+//   1. all lanes read the run's pixels (coalesced, edge-clamped as jpeg_enc.h:1106-1111) and write
+//      the samples the units use to LDS -- Y per pixel, Cb/Cr per pixel (4:4:4) or per 2x2 mean
+//      (4:2:0), each with the reference's float expression and order (:1118-1120);
+//   2. one lane per data unit: 8x8 samples from LDS, AAN FDCT, quantise (:806-817), the AC part of
+//      its Huffman bit length (:851-887) and its DC value;
+//   3. the DC code lengths (:831-849) of every unit whose predecessor (the previous unit of its
+//      component in stream order) is in the run, the run's bit count without its first units'
+//      DC codes (A), and its first / last DC of each component, published as look-back records;
+//   4. decoupled look-back (wave 0) over earlier runs of the image for the stream bits before the
+//      run, whose last DCs also give the first units' DC codes; the run's inclusive count is
+//      published at once;
+//   5. a block scan of the unit bit lengths, and every lane packs its unit's codes (DC diff, then
+//      per nonzero AC coefficient a ZRL per 16 preceding zeros, the (run, size) symbol and the
+//      amplitude bits, EOB unless coefficient 63 is nonzero: tjei_encode_and_write_MCU,
+//      :831-887) at its bit offset (:613-643) from registers: no coefficient round trip.
+// The coefficients never leave registers, and the count / scan / emit passes are this one launch.
 constexpr int kRunPx = 512;
-__global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ src, int w, int h, int comps,
-                                                   EncLayout L, int runs_per_row, const EncTables* __restrict__ T,
-                                                   int16_t* __restrict__ zz, uint64_t* __restrict__ nbits) {
-    __shared__ float S[3 * 8 * kRunPx];  // 4:4:4: Y|Cb|Cr, 8 x 512 each; 4:2:0: Y 16 x 512 | Cb|Cr 8 x 256
+struct EncBatch {
+    const uint8_t* const* srcs;  // device array: image i's RGB pixels
+    int w, h, comps;
+    int runs_per_row, runs;      // per image
+    uint64_t wwords;             // words per image in `words` (its stride)
+};
+// Look-back records, one per run of an image: three 8-byte granules, each written once by one
+// agent-scope (sc1) 8-byte store with its own valid bit, so readers need no ordering
+// (MI355X_MICROARCH.md, inter-workgroup visibility: self-tagged granules).
+struct RunRec {
+    unsigned long long agg;   // [63] valid, [62:42] A, [41:0] first DC per component (14-bit, +8192)
+    unsigned long long last;  // [63] valid, [41:0] last DC per component
+    unsigned long long inc;   // [63] valid, [62:0] stream bits up to and including the run
+};
+constexpr unsigned long long kGValid = 1ull << 63;
+__device__ __forceinline__ unsigned long long g_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Waits for a record another (earlier, hence resident) workgroup publishes; bounded (about a
+// second), so a defect cannot hang the GPU: on expiry it raises *fail (the host reports a HIP
+// failure) and returns a valid, wrong record.
+__device__ __forceinline__ unsigned long long g_wait(const unsigned long long* p, unsigned* fail) {
+    unsigned long long v;
+    for (int it = 0; !((v = g_load(p)) & kGValid); ++it) {
+        if (it == (1 << 22)) {
+            atomicOr(fail, 1u);
+            return kGValid | ((8192ull << 28) | (8192ull << 14) | 8192ull);
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return v;
+}
+__device__ __forceinline__ int dc_field(unsigned long long g, int c) { return (int)((g >> (14 * c)) & 0x3FFFu) - 8192; }
+__device__ __forceinline__ int dc_bits(const uint8_t (&dcl)[2][16], int c, int diff) {  // jpeg_enc.h:834-849
+    const int mag = diff < 0 ? -diff : diff;
+    const int nb = mag ? 32 - __clz(mag) : 0;
+    return dcl[c ? 1 : 0][nb] + nb;
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor((unsigned long long)v, o);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const EncTables* __restrict__ T,
+                                                 RunRec* __restrict__ recs, unsigned* __restrict__ ticket,  // [0] ticket, [1] look-back expired
+                                                 uint32_t* __restrict__ words, uint64_t* __restrict__ info) {
+    // the run's samples (4:4:4: Y|Cb|Cr, 8 x 512 each; 4:2:0: Y 16 x 512 | Cb|Cr 8 x 256), then
+    // (once every lane holds its unit) the code tables, code << 8 | length
+    __shared__ union {
+        float S[3 * 8 * kRunPx];
+        uint32_t tab[4][256];
+    } U;
     __shared__ float pq[2][64];
     __shared__ uint8_t aclen[2][256];
-    const int t = threadIdx.x;
+    __shared__ uint8_t dcl[2][16];
+    __shared__ int32_t dcs[256];
+    __shared__ uint32_t wsum[4];
+    __shared__ int s_tk;
+    __shared__ unsigned long long s_excl;
+    __shared__ int32_t s_lprev[3];
+    float* S = U.S;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) s_tk = (int)atomicAdd(ticket, 1u);
     if (t < 128) pq[t >> 6][t & 63] = T->pq[t >> 6][t & 63];
     aclen[0][t] = T->len[1][t];
     aclen[1][t] = T->len[3][t];
-    const int my = blockIdx.x / runs_per_row, rx = blockIdx.x - my * runs_per_row;
+    if (t < 32) dcl[t >> 4][t & 15] = (t & 15) < 12 ? T->len[(t >> 4) ? 2 : 0][t & 15] : 0;
+    __syncthreads();
+    // (the grid is exactly one workgroup per run of the batch; the ticket is made wave-uniform so
+    // the run's geometry and source pointer stay in SGPRs)
+    const int tk = __builtin_amdgcn_readfirstlane(s_tk);
+    const int img = tk / B.runs, run = tk - img * B.runs;
+    const uint8_t* src = B.srcs[img];
+    const int w = B.w, h = B.h, comps = B.comps;
+    RunRec* R = recs + (int64_t)img * B.runs;
+    const int my = run / B.runs_per_row, rx = run - my * B.runs_per_row;
     const int x0 = rx * kRunPx, y0 = my * L.ms;
     const int mcu0 = x0 / L.ms, nm = min(kRunPx / L.ms, L.mbw - mcu0), wpx = nm * L.ms;
     auto pix = [&](int x, int y) { return src + ((int64_t)min(y, h - 1) * w + min(x, w - 1)) * comps; };
@@ -114,7 +198,7 @@ __global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ s
         return 0.5f * r - 0.4187f * g - 0.0813f * b;
     };
     constexpr int kHalf = kRunPx / 2;
-    // RGB rows 4-byte aligned (3 bytes per pixel, w % 4 == 0, src aligned): a thread takes two
+    // 1. RGB rows 4-byte aligned (3 bytes per pixel, w % 4 == 0, src aligned): a thread takes two
     // quads (4 x 2 pixels) with three dword loads per row instead of 12 byte loads
     const bool rows4 = comps == 3 && (w & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 3) == 0;
     if (L.sub && rows4) {
@@ -195,12 +279,12 @@ __global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ s
                 for (int d = 0; d < 3; ++d)
                     rw[d] = (uint32_t)b[4 * d] | (uint32_t)b[4 * d + 1] << 8 | (uint32_t)b[4 * d + 2] << 16 | (uint32_t)b[4 * d + 3] << 24;
             }
-            const uint8_t* B = reinterpret_cast<const uint8_t*>(rw);
+            const uint8_t* Bq = reinterpret_cast<const uint8_t*>(rw);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (xx + k >= wpx) break;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) S[c * 8 * kRunPx + yy * kRunPx + xx + k] = ycc(B + 3 * k, c);
+                for (int c = 0; c < 3; ++c) S[c * 8 * kRunPx + yy * kRunPx + xx + k] = ycc(Bq + 3 * k, c);
             }
         }
     } else {
@@ -213,156 +297,212 @@ __global__ __launch_bounds__(256) void k_enc_units(const uint8_t* __restrict__ s
         }
     }
     __syncthreads();
-    if (t >= nm * L.upm) return;
-    const int ml = t / L.upm, k = t - ml * L.upm, c = L.comp[k];
-    const float* base;
-    int pitch = kRunPx;
-    if (!L.sub) base = S + c * 8 * kRunPx + ml * 8;
-    else if (c == 0) base = S + L.by[k] * 8 * kRunPx + ml * 16 + L.bx[k] * 8;
-    else { base = S + 16 * kRunPx + (c - 1) * 8 * kHalf + ml * 8; pitch = kHalf; }
+    // 2. one lane per data unit (lanes past the run's units idle to the barriers)
+    const int nunits = nm * L.upm;
+    const bool act = t < nunits;
+    const int ml = act ? t / L.upm : 0, k = act ? t - ml * L.upm : 0, c = L.comp[k];
     float f[64];
+    {
+        const float* base;
+        int pitch = kRunPx;
+        if (!L.sub) base = S + c * 8 * kRunPx + ml * 8;
+        else if (c == 0) base = S + L.by[k] * 8 * kRunPx + ml * 16 + L.bx[k] * 8;
+        else { base = S + 16 * kRunPx + (c - 1) * 8 * kHalf + ml * 8; pitch = kHalf; }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const float4 lo = *reinterpret_cast<const float4*>(base + r * pitch);
-        const float4 hi = *reinterpret_cast<const float4*>(base + r * pitch + 4);
-        f[8 * r + 0] = lo.x; f[8 * r + 1] = lo.y; f[8 * r + 2] = lo.z; f[8 * r + 3] = lo.w;
-        f[8 * r + 4] = hi.x; f[8 * r + 5] = hi.y; f[8 * r + 6] = hi.z; f[8 * r + 7] = hi.w;
+        for (int r = 0; r < 8; ++r) {
+            const float4 lo = *reinterpret_cast<const float4*>(base + r * pitch);
+            const float4 hi = *reinterpret_cast<const float4*>(base + r * pitch + 4);
+            f[8 * r + 0] = lo.x; f[8 * r + 1] = lo.y; f[8 * r + 2] = lo.z; f[8 * r + 3] = lo.w;
+            f[8 * r + 4] = hi.x; f[8 * r + 5] = hi.y; f[8 * r + 6] = hi.z; f[8 * r + 7] = hi.w;
+        }
     }
+    __syncthreads();  // every lane holds its samples: the code tables take the samples' LDS (below)
 #pragma unroll
     for (int r = 0; r < 8; ++r) fdct8<1>(f + 8 * r);
 #pragma unroll
     for (int q = 0; q < 8; ++q) fdct8<8>(f + q);
-    const float* pqc = pq[c ? 1 : 0];
-    int o[64];
+    uint32_t cw[32];  // the quantised block, zig-zag order, two coefficients per word
+    {
+        const float* pqc = pq[c ? 1 : 0];
+        int o[64];
 #pragma unroll
-    for (int i = 0; i < 64; ++i) {  // jpeg_enc.h:806-817
-        float v = f[i];
-        v *= pqc[i];
-        v = floorf(v + 1024 + 0.5f);
-        v -= 1024;
-        o[zig_of_nat(i)] = (int)v;
+        for (int i = 0; i < 64; ++i) {  // jpeg_enc.h:806-817
+            float v = f[i];
+            v *= pqc[i];
+            v = floorf(v + 1024 + 0.5f);
+            v -= 1024;
+            o[zig_of_nat(i)] = (int)v;
+        }
+#pragma unroll
+        for (int q = 0; q < 32; ++q) cw[q] = ((uint32_t)o[2 * q] & 0xFFFFu) | ((uint32_t)o[2 * q + 1] << 16);
     }
-    const int64_t u = ((int64_t)my * L.mbw + mcu0 + ml) * L.upm + k;
-    int4* dst = reinterpret_cast<int4*>(zz + u * 64);
-    auto pk = [](int a, int b) { return (int)(((uint32_t)a & 0xFFFFu) | ((uint32_t)b << 16)); };
+    // (the whole block is quantised before the length loop reads it, and stays 32 packed
+    // registers until the emit: left alone, the compiler interleaves the FDCT with that loop and
+    // keeps the unpacked coefficients alive across the look-back, 250+ VGPRs)
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-        dst[q] = make_int4(pk(o[8 * q], o[8 * q + 1]), pk(o[8 * q + 2], o[8 * q + 3]), pk(o[8 * q + 4], o[8 * q + 5]),
-                           pk(o[8 * q + 6], o[8 * q + 7]));
+    for (int q = 0; q < 32; ++q) asm volatile("" : "+v"(cw[q]));
+    auto coef = [&](int i) { return (int)(int16_t)(cw[i >> 1] >> (16 * (i & 1))); };
     // AC codes (jpeg_enc.h:851-887): a ZRL per 16 zeros before a nonzero coefficient, (run, size)
     // symbol + amplitude bits, EOB unless coefficient 63 is nonzero
-    const uint8_t* al = aclen[c ? 1 : 0];
     uint32_t bits = 0;
-    int run = 0;
+    {
+        const uint8_t* al = aclen[c ? 1 : 0];
+        int zr = 0;
 #pragma unroll
-    for (int i = 1; i < 64; ++i) {
-        const int v = (int16_t)o[i];
-        if (v) {
-            const int mag = v < 0 ? -v : v, nb = 32 - __clz(mag);
-            bits += (uint32_t)((run >> 4) * al[0xF0] + al[((run & 15) << 4) | nb] + nb);
-            run = 0;
-        } else {
-            ++run;
+        for (int i = 1; i < 64; ++i) {
+            const int v = coef(i);
+            if (v) {
+                const int mag = v < 0 ? -v : v, nb = 32 - __clz(mag);
+                bits += (uint32_t)((zr >> 4) * al[0xF0] + al[((zr & 15) << 4) | nb] + nb);
+                zr = 0;
+            } else {
+                ++zr;
+            }
+        }
+        if (!coef(63)) bits += al[0];
+    }
+    const int dc = coef(0);
+    dcs[t] = act ? dc : 0;
+    for (int i = t; i < 4 * 256; i += 256) U.tab[i >> 8][i & 255] = (uint32_t)T->code[i >> 8][i & 255] << 8 | T->len[i >> 8][i & 255];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) asm volatile("" : "+v"(cw[q]));
+    __syncthreads();
+    // 3. DC codes of the units whose predecessor is in the run (:834: the predictor never resets)
+    const bool first = L.prevk[k] < 0 && ml == 0;  // the run's first unit of its component
+    const int pt = L.prevk[k] >= 0 ? ml * L.upm + L.prevk[k] : (ml - 1) * L.upm + L.lastk[c];
+    int pred = first ? 0 : dcs[pt];
+    if (act && !first) bits += (uint32_t)dc_bits(dcl, c, dc - pred);
+    if (!act) bits = 0;
+    {
+        const uint32_t s = wave_sum32(bits);  // (first units: AC only so far)
+        if (lane == 0) wsum[wv] = s;
+    }
+    __syncthreads();
+    // 4. look-back (wave 0): the run's A, first and last DCs go out first
+    if (wv == 0) {
+        const uint32_t A = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        unsigned long long F = 0, Lr = 0;
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) {
+            F |= (unsigned long long)(dcs[L.firstk[cc]] + 8192) << (14 * cc);
+            Lr |= (unsigned long long)(dcs[(nm - 1) * L.upm + L.lastk[cc]] + 8192) << (14 * cc);
+        }
+        if (lane == 0) {
+            g_store(&R[run].agg, kGValid | (unsigned long long)A << 42 | F);
+            g_store(&R[run].last, kGValid | Lr);
+        }
+        // bits before the run: sum the T of the runs back to the nearest inclusive one, where
+        // T(j) = A(j) + the DC codes of j's first units, predicted from run j - 1's last DCs
+        unsigned long long excl = 0;
+        for (int hi = run - 1;; hi -= 64) {
+            const int j = hi - lane;
+            unsigned long long gi = 0;
+            bool inc = j < 0;  // (before the image: an inclusive count of 0)
+            if (!inc) {
+                gi = g_load(&R[j].inc);
+                inc = (gi & kGValid) != 0;
+            }
+            const uint64_t m = __ballot(inc);
+            const int stop = m ? __ffsll((unsigned long long)m) - 1 : 64;
+            unsigned long long v = 0;
+            if (lane < stop) {
+                const unsigned long long ga = g_wait(&R[j].agg, ticket + 1);
+                const unsigned long long gl = j > 0 ? g_wait(&R[j - 1].last, ticket + 1) : kGValid | ((8192ull << 28) | (8192ull << 14) | 8192ull);
+                v = (ga >> 42) & 0x1FFFFFull;
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) v += (unsigned long long)dc_bits(dcl, cc, dc_field(ga, cc) - dc_field(gl, cc));
+            } else if (lane == stop) {
+                v = j < 0 ? 0 : gi & ~kGValid;
+            }
+            excl += wave_sum64(v);
+            if (m) break;
+        }
+        if (lane == 0) {
+            const unsigned long long gl = run > 0 ? g_wait(&R[run - 1].last, ticket + 1) : kGValid | ((8192ull << 28) | (8192ull << 14) | 8192ull);
+            unsigned long long Tr = A;
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) {
+                s_lprev[cc] = dc_field(gl, cc);
+                Tr += (unsigned long long)dc_bits(dcl, cc, dc_field(F, cc) - dc_field(gl, cc));
+            }
+            g_store(&R[run].inc, kGValid | (excl + Tr));
+            s_excl = excl;
+            if (run == B.runs - 1) info[(int64_t)img * 4] = (excl + Tr + 7) / 8;  // stream bytes (:1161-1165)
         }
     }
-    if (!(int16_t)o[63]) bits += al[0];
-    nbits[u] = bits;
-}
-
-// Adds the DC code length (jpeg_enc.h:834-849) to the AC bits k_enc_units stored.
-__global__ __launch_bounds__(256) void k_enc_count(const int16_t* __restrict__ zz, int64_t nunits, EncLayout L,
-                                                   const EncTables* __restrict__ T, uint64_t* __restrict__ nbits) {
-    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nunits) return;
-    const int c = L.comp[u % L.upm], td = c ? 2 : 0;
-    const int64_t pu = pred_unit(L, u);
-    const int pred = pu >= 0 ? zz[pu * 64] : 0;  // DC predictor never resets (:834-835)
-    const int diff = zz[u * 64] - pred;
-    int nb = 0;
-    uint32_t bits;
-    if (diff) vli(diff, nb, bits);
-    nbits[u] += (uint64_t)(T->len[td][nb] + nb);
-}
-
-// Stream words hold bits MSB-first: word k covers stream bits [32k, 32k+32). One lane per unit:
-// its zig-zag block is loaded once (eight 16-byte loads) and walked with a fully unrolled
-// coefficient loop, so every coefficient is a register; code tables come from LDS. Codes are
-// appended to a 64-bit accumulator and every completed word is stored; only words shared with a
-// neighbouring unit (the first, when the unit starts mid-word, and the last) use atomicOr.
-// Code order as tjei_encode_and_write_MCU (jpeg_enc.h:831-887): DC diff (never reset), then per
-// nonzero AC coefficient a ZRL per 16 preceding zeros, the (run, size) symbol and its amplitude
-// bits, and EOB unless coefficient 63 is nonzero.
-__global__ __launch_bounds__(256) void k_enc_emit(const int16_t* __restrict__ zz, int64_t nunits, EncLayout L,
-                                                  const EncTables* __restrict__ T, const uint64_t* __restrict__ off,
-                                                  const uint64_t* __restrict__ nbits, uint64_t cap_bits,
-                                                  uint32_t* __restrict__ words) {
-    __shared__ uint32_t tab[4][256];  // code << 8 | len
-    for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i >> 8][i & 255] = (uint32_t)T->code[i >> 8][i & 255] << 8 | T->len[i >> 8][i & 255];
     __syncthreads();
-    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nunits || off[u] + nbits[u] + 32 > cap_bits) return;  // past the words buffer: host re-runs
-    const int c = L.comp[u % L.upm];
-    const int64_t pu = pred_unit(L, u);
-    const int pred = pu >= 0 ? zz[pu * 64] : 0;
-    const int4* src = reinterpret_cast<const int4*>(zz + u * 64);
-    uint32_t w[32];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int4 v = src[q];
-        w[4 * q] = (uint32_t)v.x; w[4 * q + 1] = (uint32_t)v.y; w[4 * q + 2] = (uint32_t)v.z; w[4 * q + 3] = (uint32_t)v.w;
+    if (first) {
+        pred = s_lprev[c];
+        if (act) bits += (uint32_t)dc_bits(dcl, c, dc - pred);
     }
-    auto coef = [&](int i) { return (int)(int16_t)(w[i >> 1] >> (16 * (i & 1))); };
-    const uint32_t* td = tab[c ? 2 : 0];
-    const uint32_t* ta = tab[c ? 3 : 1];
-    const uint64_t pos = off[u];
-    uint32_t* wp = words + (pos >> 5);
+    // 5. block exclusive scan of the unit lengths -> bit offsets
+    uint32_t incl = bits;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;  // (wave 0 read the A sums before the barrier above)
+    __syncthreads();
+    uint32_t before = incl - bits;
+    for (int q = 0; q < wv; ++q) before += wsum[q];
+    const uint64_t pos = s_excl + before;
+    const uint64_t cap_bits = B.wwords * 32;
+    if (!act || pos + bits + 32 > cap_bits) return;  // past the words buffer: the host runs it again
+    const uint32_t* td = U.tab[c ? 2 : 0];
+    const uint32_t* ta = U.tab[c ? 3 : 1];
+    uint32_t* wp = words + (int64_t)img * B.wwords + (pos >> 5);
     const int o0 = (int)(pos & 31);
     uint64_t acc = 0;
-    int nacc = o0;        // the first o0 bits of the first word belong to the previous unit (zeros here)
-    bool first = true;
+    int nacc = o0;  // the first o0 bits of the first word belong to the previous unit (zeros here)
+    bool firstw = true;
     auto put = [&](int n, uint32_t v) {
         acc = (acc << n) | (v & ((1u << n) - 1u));
         nacc += n;
         if (nacc >= 32) {
             const uint32_t word = (uint32_t)(acc >> (nacc - 32));
-            if (first && o0) atomicOr(wp, word);
+            if (firstw && o0) atomicOr(wp, word);  // shared with the previous unit
             else *wp = word;
-            first = false;
+            firstw = false;
             ++wp;
             nacc -= 32;
         }
     };
     auto code = [&](uint32_t e) { put((int)(e & 255), e >> 8); };
     int nb;
-    uint32_t bits;
-    const int diff = coef(0) - pred;
+    uint32_t vb;
+    const int diff = dc - pred;
     if (diff) {
-        vli(diff, nb, bits);
+        vli(diff, nb, vb);
         code(td[nb]);
-        put(nb, bits);
+        put(nb, vb);
     } else {
         code(td[0]);
     }
-    int run = 0;
+    int zr = 0;
 #pragma unroll
     for (int i = 1; i < 64; ++i) {
         const int v = coef(i);
         if (v) {
-            for (int z = run >> 4; z > 0; --z) code(ta[0xF0]);
-            vli(v, nb, bits);
-            code(ta[((run & 15) << 4) | nb]);
-            put(nb, bits);
-            run = 0;
+            for (int z = zr >> 4; z > 0; --z) code(ta[0xF0]);
+            vli(v, nb, vb);
+            code(ta[((zr & 15) << 4) | nb]);
+            put(nb, vb);
+            zr = 0;
         } else {
-            ++run;
+            ++zr;
         }
     }
     if (!coef(63)) code(ta[0]);
     if (nacc > 0) atomicOr(wp, (uint32_t)(acc << (32 - nacc)));  // shared with the next unit
 }
 
-// 16 stream bytes (4 words, one 16-byte load) per lane: adjacent lanes write adjacent output.
+// FF -> FF 00 byte stuffing (jpeg_enc.h:634-638) of a batch's streams: 16 stream bytes (4 words,
+// one 16-byte load) per lane, a workgroup per 4 KB; k_stuff_count_b counts each workgroup's FF
+// bytes, one scan over the batch gives every workgroup's stuffed offset, k_stuff_write_b recounts
+// per lane, scans in the workgroup and copies.
 constexpr int kStuffChunk = 16;
+constexpr int kStuffWg = 256 * kStuffChunk;
 __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t t, uint64_t nbytes, uint32_t (&w)[4]) {
     const uint64_t b0 = (uint64_t)t * kStuffChunk;
     if (b0 + kStuffChunk <= nbytes) {
@@ -373,64 +513,85 @@ __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t t, ui
         for (int q = 0; q < 4; ++q) w[q] = b0 + 4 * q < nbytes ? words[(b0 >> 2) + q] : 0u;
     }
 }
-
-// info[0] = stream bytes (k_enc_size), info[1] = stuffed bytes (k_stuff_total)
-__global__ void k_enc_size(const uint64_t* __restrict__ off, const uint64_t* __restrict__ nbits, int64_t nunits,
-                           uint64_t* __restrict__ info) {
-    info[0] = (off[nunits - 1] + nbits[nunits - 1] + 7) / 8;  // final partial byte zero-padded (:1161-1165)
-}
-__global__ __launch_bounds__(256) void k_zero_words(uint32_t* __restrict__ words, uint64_t cap_words,
-                                                    const uint64_t* __restrict__ info) {
-    const uint64_t n = min<uint64_t>(cap_words, (info[0] + 3) / 4 + 1);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        words[i] = 0;
-}
-__global__ __launch_bounds__(256) void k_stuff_count(const uint32_t* __restrict__ words, const uint64_t* __restrict__ info,
-                                                     uint32_t* __restrict__ cnt, int64_t nchunks) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nchunks) return;
-    const uint64_t nbytes = info[0];
-    const uint64_t b0 = (uint64_t)t * kStuffChunk;
-    if (b0 >= nbytes) { cnt[t] = 0; return; }
-    const int nb = (int)min<uint64_t>(kStuffChunk, nbytes - b0);
-    uint32_t w[4];
-    chunk_words(words, t, nbytes, w);
+__device__ __forceinline__ uint32_t chunk_ff(const uint32_t (&w)[4], int nb) {
     uint32_t n = 0;
 #pragma unroll
     for (int i = 0; i < kStuffChunk; ++i) n += (i < nb && ((w[i >> 2] >> (24 - 8 * (i & 3))) & 255u) == 255u);
-    cnt[t] = n;
+    return n;
 }
-
-__global__ void k_stuff_total(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ base, int64_t nchunks,
-                              uint64_t* __restrict__ info) {
-    info[1] = info[0] + base[nchunks - 1] + cnt[nchunks - 1];
+// the image's stream bytes, clamped to its words buffer (an image past it is encoded again)
+__device__ __forceinline__ uint64_t stream_bytes(const uint64_t* info, int img, uint64_t wwords) {
+    return min<uint64_t>(info[(int64_t)img * 4], wwords * 4);
 }
-// The file header (SOI .. SOS, < 1 KiB) as a kernel argument: written with the stream, only when
-// the whole file fits, without a host sync.
+__global__ __launch_bounds__(256) void k_stuff_count_b(const uint32_t* __restrict__ words, uint64_t wwords,
+                                                       const uint64_t* __restrict__ info, int nwg,
+                                                       uint32_t* __restrict__ wsum) {
+    __shared__ uint32_t s[4];
+    const int img = blockIdx.y, t = threadIdx.x;
+    const uint64_t nbytes = stream_bytes(info, img, wwords);
+    const int64_t ch = (int64_t)blockIdx.x * 256 + t;
+    const uint64_t b0 = (uint64_t)ch * kStuffChunk;
+    uint32_t n = 0;
+    if (b0 < nbytes) {
+        uint32_t w[4];
+        chunk_words(words + (int64_t)img * wwords, ch, nbytes, w);
+        n = chunk_ff(w, (int)min<uint64_t>(kStuffChunk, nbytes - b0));
+    }
+    n = wave_sum32(n);
+    if ((t & 63) == 0) s[t >> 6] = n;
+    __syncthreads();
+    if (t == 0) {
+        wsum[(int64_t)img * nwg + blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+        if (img == (int)gridDim.y - 1 && (int)blockIdx.x == nwg - 1) wsum[(int64_t)gridDim.y * nwg] = 0;  // scan tail
+    }
+}
+// The file header (SOI .. SOS, < 1 KiB) as a kernel argument.
 struct HdrArg {
     uint8_t b[1024];
     int n;
 };
-__global__ void k_put_header(HdrArg h, uint8_t* __restrict__ file, const uint64_t* __restrict__ info, uint64_t cap_e,
-                             int eoi, uint64_t wbytes) {
-    if (info[1] + (eoi ? 2 : 0) > cap_e || info[0] + 4 > wbytes) return;
-    for (int i = threadIdx.x; i < h.n; i += blockDim.x) file[i] = h.b[i];
-}
-// Writes the stuffed stream only when it fits in `cap` bytes (and, with eoi, the EOI marker after it).
-__global__ __launch_bounds__(256) void k_stuff_write(const uint32_t* __restrict__ words, const uint64_t* __restrict__ info,
-                                                     const uint32_t* __restrict__ base, int64_t nchunks, uint64_t cap,
-                                                     int eoi, uint8_t* __restrict__ out) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t nbytes = info[0], total = info[1];
-    // nothing is written unless the whole stream fits in cap and every unit was emitted
-    if (t >= nchunks || total + (eoi ? 2 : 0) > cap || nbytes + 4 > (uint64_t)nchunks * kStuffChunk) return;
-    if (eoi && t == 0) { out[total] = 0xFF; out[total + 1] = 0xD9; }
-    const uint64_t b0 = (uint64_t)t * kStuffChunk;
-    if (b0 >= nbytes) return;
-    const int nb = (int)min<uint64_t>(kStuffChunk, nbytes - b0);
-    uint32_t w[4];
-    chunk_words(words, t, nbytes, w);
-    uint8_t* o = out + b0 + base[t];
+// Writes image img's stuffed stream (after its header when hdr.n > 0, and EOI after it with eoi)
+// only when the whole file fits in cap bytes past out + img * stride; info[4 img + 1] = stuffed
+// bytes either way.
+__global__ __launch_bounds__(256) void k_stuff_write_b(const uint32_t* __restrict__ words, uint64_t wwords,
+                                                       uint64_t* __restrict__ info, int nwg,
+                                                       const uint32_t* __restrict__ wbase, HdrArg hdr,
+                                                       uint8_t* __restrict__ out, uint64_t stride, uint64_t cap, int eoi) {
+    __shared__ uint32_t s[4];
+    const int img = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint64_t nbytes_raw = info[(int64_t)img * 4];
+    const uint64_t nbytes = min<uint64_t>(nbytes_raw, wwords * 4);
+    const uint32_t* base = wbase + (int64_t)img * nwg;
+    const uint64_t total = nbytes + (uint32_t)(base[nwg] - base[0]);
+    if (blockIdx.x == 0 && t == 0) info[(int64_t)img * 4 + 1] = total;
+    const uint64_t need = (uint64_t)hdr.n + total + (eoi ? 2 : 0);
+    if (need > cap || nbytes_raw + 4 > wwords * 4) return;  // (uniform per workgroup)
+    uint8_t* o0 = out + (int64_t)img * stride;
+    if (blockIdx.x == 0) {
+        for (int i = t; i < hdr.n; i += 256) o0[i] = hdr.b[i];
+        if (eoi && t == 0) { o0[hdr.n + total] = 0xFF; o0[hdr.n + total + 1] = 0xD9; }
+    }
+    const int64_t ch = (int64_t)blockIdx.x * 256 + t;
+    const uint64_t b0 = (uint64_t)ch * kStuffChunk;
+    uint32_t w[4] = {0, 0, 0, 0};
+    int nb = 0;
+    if (b0 < nbytes) {
+        chunk_words(words + (int64_t)img * wwords, ch, nbytes, w);
+        nb = (int)min<uint64_t>(kStuffChunk, nbytes - b0);
+    }
+    const uint32_t n = chunk_ff(w, nb);
+    uint32_t incl = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s[wv] = incl;
+    __syncthreads();
+    if (!nb) return;
+    uint32_t before = incl - n + (base[blockIdx.x] - base[0]);
+    for (int q = 0; q < wv; ++q) before += s[q];
+    uint8_t* o = o0 + hdr.n + b0 + before;
 #pragma unroll
     for (int i = 0; i < kStuffChunk; ++i) {
         if (i >= nb) break;
@@ -550,11 +711,12 @@ static EncLayout make_layout(int subsampling, int w) {
         const int8_t comp[6] = {0, 0, 0, 0, 1, 2}, bx[6] = {0, 1, 0, 1, 0, 0}, by[6] = {0, 0, 1, 1, 0, 0};
         const int8_t prevk[6] = {-1, 0, 1, 2, -1, -1};
         for (int k = 0; k < 6; ++k) { L.comp[k] = comp[k]; L.bx[k] = bx[k]; L.by[k] = by[k]; L.prevk[k] = prevk[k]; }
+        L.firstk[0] = 0; L.firstk[1] = 4; L.firstk[2] = 5;
         L.lastk[0] = 3; L.lastk[1] = 4; L.lastk[2] = 5;
     } else {  // 4:4:4 (tiny_jpeg's only layout)
         L.upm = 3;
         L.ms = 8;
-        for (int k = 0; k < 3; ++k) { L.comp[k] = (int8_t)k; L.prevk[k] = -1; L.lastk[k] = (int8_t)k; }
+        for (int k = 0; k < 3; ++k) { L.comp[k] = (int8_t)k; L.prevk[k] = -1; L.firstk[k] = L.lastk[k] = (int8_t)k; }
     }
     L.mbw = (w + L.ms - 1) / L.ms;
     return L;
@@ -602,34 +764,44 @@ static void ijg_table(const uint8_t* base, int q, uint8_t* out) {  // IJG jpeg_q
 }
 
 // ----------------------------------------------------------------------- device pipeline
+// A batch of images (same geometry and settings) is encoded by one fused launch and the stuffing
+// pair, whatever the batch size:
+//   memset     the words buffers (image i's at words + i * wwords), look-back records, ticket
+//   k_enc_run  every run of every image (units, DC chain, look-back scan, emit); info[4i] = stream
+//              bytes
+//   k_stuff_count_b, one scan over the batch, k_stuff_write_b: stuffed stream (with header and EOI
+//              when asked) at out + i * stride, only when it fits; info[4i + 1] = stuffed bytes
+//   info -> pinned host memory, one host wait per batch
+// An image whose stream outgrew its words buffer (sized from the images before) is encoded again
+// with a buffer of its measured size.
 struct EncWs {
     EncTables* T = nullptr;
-    int16_t* zz = nullptr;
-    uint64_t *nb = nullptr, *off = nullptr;
-    int64_t units_cap = 0;
+    RunRec* recs = nullptr;
+    size_t recs_cap = 0;
+    unsigned* ticket = nullptr;
     uint32_t* words = nullptr;
-    uint64_t words_cap = 0;  // bytes
-    uint32_t *cnt = nullptr, *base = nullptr;
-    int64_t chunks_cap = 0;
-    uint64_t* info = nullptr;  // device: stream bytes, stuffed bytes
-    uint64_t* hinfo = nullptr; // pinned host copy of info, valid when `fin` completes
-    hipEvent_t fin = nullptr;
-    uint64_t est_bytes = 0;    // words-buffer estimate from the images so far
-    uint64_t wbytes = 0;       // words buffer of the job in flight
-    int64_t nunits = 0;        // data units of the job in flight
+    size_t words_cap = 0;        // bytes
+    uint32_t *wsum = nullptr, *wbase = nullptr;
+    size_t wsum_cap = 0, wbase_cap = 0;
+    uint64_t* info = nullptr;    // device: 4 per image (stream bytes, stuffed bytes)
+    uint64_t* hinfo = nullptr;   // pinned host copy
+    size_t info_cap = 0;         // images
+    const uint8_t** srcs = nullptr;  // device array of source pointers
+    size_t srcs_cap = 0;
+    uint64_t est_bytes = 0;      // words-buffer estimate per image from the images so far
     void* tmp = nullptr;
     size_t tmp_cap = 0;
-    // per-stage HIP events of the last entropy pass (icx_encoder_stage_times): units, count,
-    // scan, emit, stuff; ms[] accumulates over calls until read
-    hipEvent_t ev[10] = {};  // stage i spans ev[2i] .. ev[2i+1]
-    float ms[5] = {};
+    // per-stage HIP events of the last batch (icx_encoder_stage_times): encode, stuff; ms[]
+    // accumulates over calls until read
+    hipEvent_t ev[4] = {};
+    float ms[2] = {};
     ~EncWs() {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
-        for (void* p : {(void*)T, (void*)zz, (void*)nb, (void*)off, (void*)words, (void*)cnt, (void*)base, (void*)info, tmp})
+        for (void* p : {(void*)T, (void*)recs, (void*)ticket, (void*)words, (void*)wsum, (void*)wbase, (void*)info,
+                        (void*)srcs, tmp})
             if (p) (void)hipFree(p);
         if (hinfo) (void)hipHostFree(hinfo);
-        if (fin) (void)hipEventDestroy(fin);
     }
 };
 EncWs* enc_ws_create() {
@@ -638,9 +810,9 @@ EncWs* enc_ws_create() {
         if (hipEventCreate(&e) != hipSuccess) e = nullptr;
     return ws;
 }
-const char* const kEncStageNames[5] = {"units", "count", "scan", "emit", "stuff"};
+const char* const kEncStageNames[2] = {"encode", "stuff"};
 int enc_ws_stage_times(EncWs* ws, const char** names, float* ms, int cap) {
-    const int k = cap < 5 ? cap : 5;
+    const int k = cap < 2 ? cap : 2;
     for (int i = 0; i < k; ++i) {
         if (names) names[i] = kEncStageNames[i];
         if (ms) ms[i] = ws->ms[i];
@@ -666,141 +838,163 @@ static bool grow(Ptr*& p, size_t need, size_t& cap_bytes) {
     return true;
 }
 
-// One image's entropy-coded data is produced in two launches-only phases and one collect:
-//   enc_front  units, bit counts, scan, stream size (info[0], device)
-//   enc_tail   words (sized from the images before: the stream's size is known on the device
-//              only), emit, stuffing, stuffed size (info[1]); writes d_out only when the whole
-//              result fits in cap (and, with hdr / eoi, the header before it and EOI after it);
-//              info -> pinned host memory, event `fin`
-//   enc_collect  waits for `fin`: 1 = done (*n = stuffed bytes), 0 = the stream outgrew the words
-//              buffer (nothing written; run enc_tail again: est_bytes now holds its size), -1 = HIP
-//              failure
-// So an image costs one host wait, and a caller with two workspaces on two streams can issue
-// image i+1 before waiting for image i.
-static bool enc_front(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables* T, const uint8_t* d_src, int w,
-                      int h, int comps) {
+// Images per launch: the words buffers of one launch stay within this many bytes.
+constexpr uint64_t kEncWordsBudget = 4ull << 30;
+
+// Encodes n images (device sources srcs[i], w x h x comps) into out + i * stride: hdr (if any),
+// the stuffed stream, EOI (with eoi), only when all of it fits in `cap` bytes; nbytes[i] = stream
+// bytes, total[i] = stuffed bytes. wbytes: words buffer per image. Returns false on a HIP failure.
+static bool enc_launch(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables& T, int n,
+                       const uint8_t* const* srcs, int w, int h, int comps, uint64_t wbytes, uint8_t* out,
+                       uint64_t stride, uint64_t cap, bool eoi, const HdrArg& hdr, uint64_t* nbytes, uint64_t* total) {
     const int64_t mbh = (h + L.ms - 1) / L.ms;
-    const int64_t nunits = (int64_t)L.mbw * mbh * L.upm;
-    ws.nunits = nunits;
-    size_t c0 = ws.units_cap * 128, c1 = ws.units_cap * 8, c2 = c1;
-    if (nunits > ws.units_cap) {
-        if (!grow(ws.zz, (size_t)nunits * 128, c0) || !grow(ws.nb, (size_t)nunits * 8, c1) ||
-            !grow(ws.off, (size_t)nunits * 8, c2))
-            return false;
-        ws.units_cap = nunits;
-    }
-    if (!ws.T) ENC_HIP(hipMalloc(&ws.T, sizeof(EncTables)));
-    if (!ws.info) ENC_HIP(hipMalloc(&ws.info, 4 * sizeof(uint64_t)));
-    if (!ws.hinfo) ENC_HIP(hipHostMalloc(&ws.hinfo, 4 * sizeof(uint64_t)));
-    if (!ws.fin) ENC_HIP(hipEventCreateWithFlags(&ws.fin, hipEventDisableTiming));
-    if (T) ENC_HIP(hipMemcpyAsync(ws.T, T, sizeof *T, hipMemcpyHostToDevice, st));
-    const int TB = 256;
-    const int gu = (int)((nunits + TB - 1) / TB);
-    const bool ev = ws.ev[9] != nullptr;
-    auto mark = [&](int i) {
-        if (ev) (void)hipEventRecord(ws.ev[i], st);
-    };
-    mark(0);
     const int runs_per_row = (L.mbw * L.ms + kRunPx - 1) / kRunPx;
-    hipLaunchKernelGGL(k_enc_units, dim3((unsigned)(runs_per_row * mbh)), dim3(TB), 0, st, d_src, w, h, comps, L,
-                       runs_per_row, ws.T, ws.zz, ws.nb);
-    mark(1);
-    mark(2);
-    hipLaunchKernelGGL(k_enc_count, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.nb);
-    mark(3);
-    mark(4);
+    const int64_t runs = (int64_t)runs_per_row * mbh;
+    const uint64_t wwords = wbytes / 4;
+    const int nwg = (int)((wbytes + kStuffWg - 1) / kStuffWg);
+    if (!ws.T) ENC_HIP(hipMalloc(&ws.T, sizeof(EncTables)));
+    if (!ws.ticket) ENC_HIP(hipMalloc(&ws.ticket, 2 * sizeof(unsigned)));
+    if (!grow(ws.recs, sizeof(RunRec) * runs * n, ws.recs_cap) || !grow(ws.words, wbytes * n, ws.words_cap) ||
+        !grow(ws.wsum, sizeof(uint32_t) * ((size_t)nwg * n + 1), ws.wsum_cap) ||
+        !grow(ws.wbase, sizeof(uint32_t) * ((size_t)nwg * n + 1), ws.wbase_cap))
+        return false;
+    if (!grow(ws.srcs, sizeof(uint8_t*) * n, ws.srcs_cap)) return false;
+    if ((size_t)n > ws.info_cap) {
+        if (ws.info) (void)hipFree(ws.info);
+        if (ws.hinfo) (void)hipHostFree(ws.hinfo);
+        ws.info = nullptr;
+        ws.hinfo = nullptr;
+        ws.info_cap = 0;
+        ENC_HIP(hipMalloc(&ws.info, sizeof(uint64_t) * 4 * n));
+        ENC_HIP(hipHostMalloc(&ws.hinfo, sizeof(uint64_t) * (4 * n + 1)));
+        ws.info_cap = n;
+    }
+    ENC_HIP(hipMemcpyAsync(ws.T, &T, sizeof T, hipMemcpyHostToDevice, st));
+    ENC_HIP(hipMemcpyAsync(ws.srcs, srcs, sizeof(uint8_t*) * n, hipMemcpyHostToDevice, st));
+    const bool ev = ws.ev[3] != nullptr;
+    if (ev) ENC_HIP(hipEventRecord(ws.ev[0], st));
+    ENC_HIP(hipMemsetAsync(ws.words, 0, wbytes * n, st));
+    ENC_HIP(hipMemsetAsync(ws.recs, 0, sizeof(RunRec) * runs * n, st));
+    ENC_HIP(hipMemsetAsync(ws.ticket, 0, 2 * sizeof(unsigned), st));
+    EncBatch B;
+    B.srcs = ws.srcs;
+    B.w = w;
+    B.h = h;
+    B.comps = comps;
+    B.runs_per_row = runs_per_row;
+    B.runs = (int)runs;
+    B.wwords = wwords;
+    hipLaunchKernelGGL(k_enc_run, dim3((unsigned)(runs * n)), dim3(256), 0, st, B, L, ws.T, ws.recs, ws.ticket, ws.words,
+                       ws.info);
+    if (ev) ENC_HIP(hipEventRecord(ws.ev[1], st));
+    if (ev) ENC_HIP(hipEventRecord(ws.ev[2], st));
+    hipLaunchKernelGGL(k_stuff_count_b, dim3(nwg, n), dim3(256), 0, st, ws.words, wwords, ws.info, nwg, ws.wsum);
     size_t tmp_b = 0;
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, ws.nb, ws.off, (int)nunits, st));
+    const int ns = nwg * n + 1;
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, ws.wsum, ws.wbase, ns, st));
     if (!grow(ws.tmp, tmp_b, ws.tmp_cap)) return false;
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b, ws.nb, ws.off, (int)nunits, st));
-    mark(5);
-    hipLaunchKernelGGL(k_enc_size, dim3(1), dim3(1), 0, st, ws.off, ws.nb, nunits, ws.info);
-    return hipGetLastError() == hipSuccess;
-}
-
-static bool enc_tail(hipStream_t st, EncWs& ws, const EncLayout& L, int w, int h, int comps, uint8_t* d_out,
-                     uint64_t cap, bool eoi, const HdrArg* hdr) {
-    const int TB = 256;
-    const int64_t nunits = ws.nunits;
-    const int gu = (int)((nunits + TB - 1) / TB);
-    const bool ev = ws.ev[9] != nullptr;
-    auto mark = [&](int i) {
-        if (ev) (void)hipEventRecord(ws.ev[i], st);
-    };
-    const uint64_t est = ws.est_bytes ? ws.est_bytes : std::max<uint64_t>(65536, (uint64_t)w * h * comps / 4);
-    const uint64_t wbytes = (est + 4 + 15) / 16 * 16;
-    if (!grow(ws.words, wbytes, ws.words_cap)) return false;
-    ws.wbytes = wbytes;
-    const int64_t nchunks = (int64_t)(wbytes / kStuffChunk);
-    size_t cc = ws.chunks_cap * 4, cb = cc;
-    if (nchunks > ws.chunks_cap) {
-        if (!grow(ws.cnt, (size_t)nchunks * 4, cc) || !grow(ws.base, (size_t)nchunks * 4, cb)) return false;
-        ws.chunks_cap = nchunks;
-    }
-    hipLaunchKernelGGL(k_zero_words, dim3(1024), dim3(TB), 0, st, ws.words, (uint64_t)(wbytes / 4), ws.info);
-    mark(6);
-    hipLaunchKernelGGL(k_enc_emit, dim3(gu), dim3(TB), 0, st, ws.zz, nunits, L, ws.T, ws.off, ws.nb,
-                       (uint64_t)wbytes * 8, ws.words);
-    mark(7);
-    mark(8);
-    const int gc = (int)((nchunks + TB - 1) / TB);
-    hipLaunchKernelGGL(k_stuff_count, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.cnt, nchunks);
-    size_t tmp_b2 = 0;
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
-    if (!grow(ws.tmp, tmp_b2, ws.tmp_cap)) return false;
-    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b2, ws.cnt, ws.base, (int)nchunks, st));
-    hipLaunchKernelGGL(k_stuff_total, dim3(1), dim3(1), 0, st, ws.cnt, ws.base, nchunks, ws.info);
-    hipLaunchKernelGGL(k_stuff_write, dim3(gc), dim3(TB), 0, st, ws.words, ws.info, ws.base, nchunks, cap,
-                       eoi ? 1 : 0, d_out);
-    if (hdr)
-        hipLaunchKernelGGL(k_put_header, dim3(1), dim3(256), 0, st, *hdr, d_out - hdr->n, ws.info, cap, eoi ? 1 : 0,
-                           (uint64_t)wbytes);
-    mark(9);
+    ENC_HIP(hipcub::DeviceScan::ExclusiveSum(ws.tmp, tmp_b, ws.wsum, ws.wbase, ns, st));
+    hipLaunchKernelGGL(k_stuff_write_b, dim3(nwg, n), dim3(256), 0, st, ws.words, wwords, ws.info, nwg, ws.wbase, hdr, out,
+                       stride, cap, eoi ? 1 : 0);
+    if (ev) ENC_HIP(hipEventRecord(ws.ev[3], st));
     ENC_HIP(hipGetLastError());
-    ENC_HIP(hipMemcpyAsync(ws.hinfo, ws.info, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    ENC_HIP(hipEventRecord(ws.fin, st));
-    return true;
-}
-
-static int enc_collect(EncWs& ws, uint64_t* n) {
-    if (hipEventSynchronize(ws.fin) != hipSuccess) return -1;
-    const uint64_t nbytes = ws.hinfo[0];
-    if (nbytes + 4 > ws.wbytes) {  // the stream outgrew the words buffer: nothing was written
-        ws.est_bytes = nbytes + nbytes / 4;
-        return 0;
+    ENC_HIP(hipMemcpyAsync(ws.hinfo, ws.info, sizeof(uint64_t) * 4 * n, hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipMemcpyAsync(ws.hinfo + 4 * n, ws.ticket + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    ENC_HIP(hipStreamSynchronize(st));
+    if (*reinterpret_cast<const unsigned*>(ws.hinfo + 4 * n)) return false;  // a look-back wait expired
+    for (int i = 0; i < n; ++i) {
+        nbytes[i] = ws.hinfo[4 * i];
+        total[i] = ws.hinfo[4 * i + 1];
     }
-    ws.est_bytes = std::max(ws.est_bytes, nbytes + nbytes / 4);
-    *n = ws.hinfo[1];
-    if (ws.ev[9]) {
-        for (int i = 0; i < 5; ++i) {
+    if (ev) {
+        for (int i = 0; i < 2; ++i) {
             float t = 0.f;
             if (hipEventElapsedTime(&t, ws.ev[2 * i], ws.ev[2 * i + 1]) == hipSuccess) ws.ms[i] += t;
         }
     }
-    return 1;
+    return true;
 }
 
-// Entropy-coded data of the image at d_src (device) -> d_out[0 .. *n) (stuffed bytes); with eoi,
-// FF D9 follows it, with hdr the header precedes it (all only when they fit in cap). Returns false
-// on a HIP failure.
-static bool encode_entropy(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables& T, const uint8_t* d_src,
-                           int w, int h, int comps, uint8_t* d_out, uint64_t cap, uint64_t* n, bool eoi = false,
-                           const HdrArg* hdr = nullptr) {
-    *n = 0;
-    const int64_t mbh = (h + L.ms - 1) / L.ms;
-    if ((int64_t)L.mbw * mbh * L.upm == 0 || w == 0 || h == 0) return true;
-    if (!enc_front(st, ws, L, &T, d_src, w, h, comps)) return false;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        if (!enc_tail(st, ws, L, w, h, comps, d_out, cap, eoi, hdr)) return false;
-        const int rc = enc_collect(ws, n);
-        if (rc < 0) return false;
-        if (rc > 0) return true;
+// The batch encode behind every entry point: images in launches of at most kEncWordsBudget bytes
+// of words buffers; an image whose stream did not fit its words buffer is encoded again alone.
+// sizes[i] = header + stuffed bytes (+ 2 with eoi); fits[i] = it was written.
+static bool enc_batch(hipStream_t st, EncWs& ws, const EncLayout& L, const EncTables& T, int n,
+                      const uint8_t* const* srcs, int w, int h, int comps, uint8_t* out, uint64_t stride, uint64_t cap,
+                      bool eoi, const HdrArg& hdr, uint64_t* sizes, bool* fits) {
+    const uint64_t est = ws.est_bytes ? ws.est_bytes : std::max<uint64_t>(65536, (uint64_t)w * h * comps / 4);
+    const uint64_t wbytes = (est + 4 + kStuffWg - 1) / kStuffWg * kStuffWg;
+    int per = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n, kEncWordsBudget / wbytes));
+    if (const char* e = std::getenv("ICX_ENC_BATCH")) per = std::max(1, std::min(per, std::atoi(e)));  // (tests)
+    std::vector<uint64_t> nb(per), tot(per);
+    for (int i0 = 0; i0 < n; i0 += per) {
+        const int k = std::min(per, n - i0);
+        if (!enc_launch(st, ws, L, T, k, srcs + i0, w, h, comps, wbytes, out + (uint64_t)i0 * stride, stride, cap, eoi, hdr,
+                        nb.data(), tot.data()))
+            return false;
+        for (int i = 0; i < k; ++i) {
+            uint64_t nbytes = nb[i], stuffed = tot[i];
+            if (nbytes + 4 > wbytes) {  // the stream outgrew the words buffer: nothing was written
+                const uint64_t wb2 = (nbytes + nbytes / 4 + 4 + kStuffWg - 1) / kStuffWg * kStuffWg;
+                uint64_t nb2 = 0, tot2 = 0;
+                if (!enc_launch(st, ws, L, T, 1, srcs + i0 + i, w, h, comps, wb2, out + (uint64_t)(i0 + i) * stride, stride,
+                                cap, eoi, hdr, &nb2, &tot2))
+                    return false;
+                if (nb2 + 4 > wb2) return false;  // (cannot happen: same image, same size)
+                nbytes = nb2;
+                stuffed = tot2;
+            }
+            ws.est_bytes = std::max(ws.est_bytes, nbytes + nbytes / 4);
+            sizes[i0 + i] = hdr.n + stuffed + (eoi ? 2 : 0);
+            fits[i0 + i] = sizes[i0 + i] <= cap;
+        }
     }
-    return false;
+    return true;
 }
 
-bool encode_host_image(hipStream_t st, const EncLayout& L, const EncTables& T, int w, int h, int comps,
-                       const uint8_t* src, std::vector<uint8_t>& out);
+static HdrArg make_hdr(const std::vector<uint8_t>& head) {
+    HdrArg ha;
+    std::memcpy(ha.b, head.data(), head.size());
+    ha.n = (int)head.size();
+    return ha;
+}
+
+// Upload, encode, download: the whole file of one host image into `out` (header built on the host).
+static bool encode_host_image(hipStream_t st, const EncLayout& L, const EncTables& T, int w, int h, int comps,
+                              const uint8_t* src, std::vector<uint8_t>& out) {
+    const size_t srcb = (size_t)w * h * comps;
+    if (!srcb) {
+        out.push_back(0xFF);
+        out.push_back(0xD9);
+        return true;
+    }
+    EncWs ws;
+    uint8_t *d_src = nullptr, *d_out = nullptr;
+    HdrArg none;
+    none.n = 0;
+    bool ok = hipMalloc(&d_src, srcb) == hipSuccess && hipMemcpyAsync(d_src, src, srcb, hipMemcpyHostToDevice, st) == hipSuccess;
+    // first pass sizes the output, the second (only when it did not fit) writes it
+    uint64_t cap = srcb + 65536, size = 0;
+    bool fit = false;
+    const uint8_t* srcs[1] = {d_src};
+    ok = ok && hipMalloc(&d_out, cap) == hipSuccess && enc_batch(st, ws, L, T, 1, srcs, w, h, comps, d_out, cap, cap, false, none, &size, &fit);
+    if (ok && !fit) {
+        (void)hipFree(d_out);
+        d_out = nullptr;
+        cap = size;
+        ok = hipMalloc(&d_out, cap) == hipSuccess && enc_batch(st, ws, L, T, 1, srcs, w, h, comps, d_out, cap, cap, false, none, &size, &fit) && fit;
+    }
+    if (ok && size) {
+        const size_t h0 = out.size();
+        out.resize(h0 + size);
+        ok = hipMemcpyAsync(out.data() + h0, d_out, size, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+    }
+    if (d_src) (void)hipFree(d_src);
+    if (d_out) (void)hipFree(d_out);
+    out.push_back(0xFF);
+    out.push_back(0xD9);
+    return ok;
+}
 
 // tiny_jpeg-exact encode (quality 1..3, 4:4:4) of a host image; `out` receives the whole file.
 bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const uint8_t* src,
@@ -823,40 +1017,6 @@ bool tje_encode_gpu(hipStream_t st, int quality, int w, int h, int comps, const 
     return encode_host_image(st, make_layout(444, w), T, w, h, comps, src, out);
 }
 
-// Shared tail of the host entry points: upload, encode, download, EOI.
-bool encode_host_image(hipStream_t st, const EncLayout& L, const EncTables& T, int w, int h, int comps,
-                       const uint8_t* src, std::vector<uint8_t>& out) {
-    EncWs ws;
-    const size_t srcb = (size_t)w * h * comps;
-    uint8_t *d_src = nullptr, *d_out = nullptr;
-    bool ok = true;
-    uint64_t n = 0;
-    if (srcb) {
-        ok = hipMalloc(&d_src, srcb) == hipSuccess &&
-             hipMemcpyAsync(d_src, src, srcb, hipMemcpyHostToDevice, st) == hipSuccess;
-        // first pass sizes the output, the second (only when it did not fit) writes it
-        uint64_t cap = srcb + 65536;
-        ok = ok && hipMalloc(&d_out, cap) == hipSuccess && encode_entropy(st, ws, L, T, d_src, w, h, comps, d_out, cap, &n);
-        if (ok && n > cap) {
-            (void)hipFree(d_out);
-            d_out = nullptr;
-            cap = n;
-            ok = hipMalloc(&d_out, cap) == hipSuccess && encode_entropy(st, ws, L, T, d_src, w, h, comps, d_out, cap, &n);
-        }
-        if (ok && n) {
-            const size_t h0 = out.size();
-            out.resize(h0 + n);
-            ok = hipMemcpyAsync(out.data() + h0, d_out, n, hipMemcpyDeviceToHost, st) == hipSuccess &&
-                 hipStreamSynchronize(st) == hipSuccess;
-        }
-    }
-    if (d_src) (void)hipFree(d_src);
-    if (d_out) (void)hipFree(d_out);
-    out.push_back(0xFF);
-    out.push_back(0xD9);
-    return ok;
-}
-
 // C4 extension, host image -> whole file.
 bool jpeg_encode_gpu(hipStream_t st, int quality, int subsampling, int w, int h, int comps, const uint8_t* src,
                      std::vector<uint8_t>& out) {
@@ -870,105 +1030,52 @@ bool jpeg_encode_gpu(hipStream_t st, int quality, int subsampling, int w, int h,
     return encode_host_image(st, make_layout(subsampling, w), T, w, h, comps, src, out);
 }
 
+// A batch of device images, same geometry and settings: image i's whole file (header, stuffed
+// stream, EOI) -> d_out + i*stride, written only when it fits in stride bytes. Per image:
+// sizes[i] (the file's bytes, also when it did not fit) and status[i] (0 ok, 1 did not fit:
+// nothing written). Returns 0, or -1 on a HIP failure. Synchronous (one host wait per launch).
+int jpeg_encode_device_batch(hipStream_t st, EncWs* ws, int n, int quality, int subsampling, int w, int h, int comps,
+                             const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t stride, uint64_t* sizes,
+                             int32_t* status) {
+    if (n <= 0) return 0;
+    uint8_t qnl[64], qnc[64];
+    ijg_table(kLumaQ, quality, qnl);
+    ijg_table(kK2Chroma, quality, qnc);
+    EncTables T;
+    build_tables(T, qnl, qnc);
+    std::vector<uint8_t> head;
+    ext_header(head, w, h, qnl, qnc, subsampling);
+    const uint64_t hn = head.size();
+    if (hn > sizeof(HdrArg::b)) return -1;
+    if (w == 0 || h == 0) {  // no data units: header + EOI only
+        static const uint8_t eoi[2] = {0xFF, 0xD9};
+        for (int i = 0; i < n; ++i) {
+            sizes[i] = hn + 2;
+            status[i] = sizes[i] > stride ? 1 : 0;
+            uint8_t* o = d_out + (uint64_t)i * stride;
+            if (!status[i] && (hipMemcpyAsync(o, head.data(), hn, hipMemcpyHostToDevice, st) != hipSuccess ||
+                               hipMemcpyAsync(o + hn, eoi, 2, hipMemcpyHostToDevice, st) != hipSuccess))
+                return -1;
+        }
+        return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+    }
+    const HdrArg ha = make_hdr(head);
+    std::unique_ptr<bool[]> fit(new bool[n]);
+    if (!enc_batch(st, *ws, make_layout(subsampling, w), T, n, d_srcs, w, h, comps, d_out, stride, stride, true, ha, sizes,
+                   fit.get()))
+        return -1;
+    for (int i = 0; i < n; ++i) status[i] = fit[i] ? 0 : 1;
+    return 0;
+}
+
 // C4 extension, device image -> whole file in d_out (device). Returns 0 ok, 1 d_out too small
 // (*size = bytes needed), -1 HIP failure.
 int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, int w, int h, int comps,
                        const uint8_t* d_src, uint8_t* d_out, uint64_t cap, uint64_t* size) {
-    uint8_t qnl[64], qnc[64];
-    ijg_table(kLumaQ, quality, qnl);
-    ijg_table(kK2Chroma, quality, qnc);
-    EncTables T;
-    build_tables(T, qnl, qnc);
-    std::vector<uint8_t> head;
-    ext_header(head, w, h, qnl, qnc, subsampling);
-    const uint64_t hn = head.size();
-    if (hn > sizeof(HdrArg::b)) return -1;
-    HdrArg ha;
-    std::memcpy(ha.b, head.data(), hn);
-    ha.n = (int)hn;
-    if (w == 0 || h == 0) {  // no data units: header + EOI only
-        *size = hn + 2;
-        if (*size > cap) return 1;
-        static const uint8_t eoi[2] = {0xFF, 0xD9};
-        if (hipMemcpyAsync(d_out, head.data(), hn, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipMemcpyAsync(d_out + hn, eoi, 2, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return -1;
-        return 0;
-    }
-    uint64_t n = 0;
-    // the whole file (header, stuffed stream, EOI) is written on the device, only if it fits
-    if (!encode_entropy(st, *ws, make_layout(subsampling, w), T, d_src, w, h, comps, d_out + hn, cap > hn ? cap - hn : 0,
-                        &n, true, &ha))
-        return -1;
-    *size = hn + n + 2;
-    return *size > cap ? 1 : 0;
-}
-
-// A batch of device images, same geometry and settings: image i -> d_out + i*stride. Images
-// alternate between two workspaces on two streams, so image i+1's kernels are issued before the
-// host waits for image i. Per image: sizes[i] and status[i] (0 ok, 1 did not fit: nothing
-// written). Returns 0, or -1 on a HIP failure. Synchronous.
-int jpeg_encode_device_batch(hipStream_t st0, hipStream_t st1, EncWs* w0, EncWs* w1, int n, int quality,
-                             int subsampling, int w, int h, int comps, const uint8_t* const* d_srcs, uint8_t* d_out,
-                             uint64_t stride, uint64_t* sizes, int32_t* status) {
-    if (n <= 0) return 0;
-    if (w == 0 || h == 0) {
-        for (int i = 0; i < n; ++i) {
-            const int rc = jpeg_encode_device(st0, w0, quality, subsampling, w, h, comps, d_srcs[i],
-                                              d_out + (uint64_t)i * stride, stride, &sizes[i]);
-            if (rc < 0) return -1;
-            status[i] = rc;
-        }
-        return 0;
-    }
-    uint8_t qnl[64], qnc[64];
-    ijg_table(kLumaQ, quality, qnl);
-    ijg_table(kK2Chroma, quality, qnc);
-    EncTables T;
-    build_tables(T, qnl, qnc);
-    std::vector<uint8_t> head;
-    ext_header(head, w, h, qnl, qnc, subsampling);
-    const uint64_t hn = head.size();
-    if (hn > sizeof(HdrArg::b)) return -1;
-    HdrArg ha;
-    std::memcpy(ha.b, head.data(), hn);
-    ha.n = (int)hn;
-    const EncLayout L = make_layout(subsampling, w);
-    EncWs* W[2] = {w0, w1};
-    hipStream_t S[2] = {st0, st1};
-    const uint64_t cap = stride > hn ? stride - hn : 0;
-    hipEvent_t fork = nullptr;
-    if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) return -1;
-    bool ok = hipEventRecord(fork, st0) == hipSuccess && hipStreamWaitEvent(st1, fork, 0) == hipSuccess;
-    auto finish = [&](int i) {  // wait for image i; re-run its tail once if its stream outgrew the buffer
-        EncWs& ws = *W[i & 1];
-        uint64_t nn = 0;
-        int rc = enc_collect(ws, &nn);
-        if (rc == 0) {
-            rc = enc_tail(S[i & 1], ws, L, w, h, comps, d_out + (uint64_t)i * stride + hn, cap, true, &ha) ? enc_collect(ws, &nn)
-                                                                                                       : -1;
-        }
-        if (rc <= 0) return false;
-        sizes[i] = hn + nn + 2;
-        status[i] = sizes[i] > stride ? 1 : 0;
-        return true;
-    };
-    for (int i = 0; ok && i < n + 2; ++i) {
-        if (i >= 2) ok = finish(i - 2);
-        if (ok && i < n) {
-            EncWs& ws = *W[i & 1];
-            ok = enc_front(S[i & 1], ws, L, i < 2 ? &T : nullptr, d_srcs[i], w, h, comps) &&
-                 enc_tail(S[i & 1], ws, L, w, h, comps, d_out + (uint64_t)i * stride + hn, cap, true, &ha);
-        }
-    }
-    // The caller's stream (st0) resumes after both -- on the error path too: an image may still
-    // be running on st1, writing d_out and ws2, and a caller that reuses d_out on st0 must not
-    // overtake it. If the join itself cannot be recorded, wait for st1 on the host.
-    const bool joined = hipEventRecord(fork, st1) == hipSuccess && hipStreamWaitEvent(st0, fork, 0) == hipSuccess;
-    if (!joined) (void)hipStreamSynchronize(st1);
-    (void)hipEventDestroy(fork);
-    return ok && joined ? 0 : -1;
+    const uint8_t* srcs[1] = {d_src};
+    int32_t stt = 0;
+    const int rc = jpeg_encode_device_batch(st, ws, 1, quality, subsampling, w, h, comps, srcs, d_out, cap, size, &stt);
+    return rc < 0 ? -1 : stt;
 }
 
 }  // namespace icx

@@ -255,9 +255,9 @@ bool jpeg_encode_gpu(hipStream_t st, int quality, int subsampling, int w, int h,
                      std::vector<uint8_t>& out);
 int jpeg_encode_device(hipStream_t st, EncWs* ws, int quality, int subsampling, int w, int h, int comps,
                        const uint8_t* d_src, uint8_t* d_out, uint64_t cap, uint64_t* size);
-int jpeg_encode_device_batch(hipStream_t st0, hipStream_t st1, EncWs* w0, EncWs* w1, int n, int quality,
-                             int subsampling, int w, int h, int comps, const uint8_t* const* d_srcs, uint8_t* d_out,
-                             uint64_t stride, uint64_t* sizes, int32_t* status);
+int jpeg_encode_device_batch(hipStream_t st, EncWs* ws, int n, int quality, int subsampling, int w, int h, int comps,
+                             const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t stride, uint64_t* sizes,
+                             int32_t* status);
 
 // PNG encoder (icx_png.hip): png_encoder::saveToFile's colour choice and filters, GPU deflate.
 struct PngWs;

@@ -128,8 +128,9 @@ def test_ext_device_estimate_regrowth(ctx):
 
 @pytest.mark.parametrize("q,sub,w,h", [(90, 420, 640, 480), (50, 444, 333, 251), (100, 420, 1024, 768)])
 def test_ext_device_batch(ctx, q, sub, w, h):
-    """icx_jpeg_encode_device_batch (two workspaces on two streams) gives each image the oracle's
-    bytes; an image whose file exceeds the stride reports OUT_OF_MEM and leaves its slot alone."""
+    """icx_jpeg_encode_device_batch (one fused k_enc_run launch over every run of every image, one
+    stuffing pass) gives each image the oracle's bytes; an image whose file exceeds the stride
+    reports OUT_OF_MEM and leaves its slot alone."""
     import torch
     imgs = [S.rgb(300 + k, w, h, 3) for k in range(5)]
     d_src = [torch.from_numpy(px).cuda() for px in imgs]
@@ -147,4 +148,34 @@ def test_ext_device_batch(ctx, q, sub, w, h):
     st, sizes = enc.encode_device_batch(q, sub, w, h, 3, [t.data_ptr() for t in d_src], d_out.data_ptr(), small)
     assert list(st) == [icx.OUT_OF_MEM] * 5 and list(sizes) == [len(x) for x in want]
     assert bool((d_out == 0xAB).all())
+    enc.close()
+
+
+def test_ext_device_batch_regrowth_and_launch_split(ctx, monkeypatch):
+    """A batch whose words-buffer estimate comes from small flat images meets a large noisy one
+    (its stream outgrows the buffer: that image alone is encoded again), and the same batch cut
+    into launches of two images (ICX_ENC_BATCH): oracle bytes either way. The images differ in
+    content, so every launch interleaves look-back chains of different lengths."""
+    import torch
+    w, h = 512, 384
+    flat = np.zeros((h, w, 3), np.uint8)
+    flat[:, :, 0] = np.arange(w, dtype=np.uint8)[None, :]
+    imgs = [flat, S.rgb(41, w, h, 3), flat.copy(), S.rgb(42, w, h, 3), flat.copy()]
+    want = [O.jpeg_encode(100, 444, w, h, 3, px.tobytes()) for px in imgs]
+    d_src = [torch.from_numpy(np.ascontiguousarray(px)).cuda() for px in imgs]
+    stride = max(len(x) for x in want) + 64
+    enc = icx.Encoder(ctx)
+    d_flat = torch.from_numpy(flat).cuda()
+    d_out = torch.empty(stride * 5, dtype=torch.uint8, device="cuda")
+    rc, _ = enc.encode_device(100, 444, w, h, 3, d_flat.data_ptr(), d_out.data_ptr(), stride)  # small estimate
+    assert rc == icx.OK
+    for split in (None, "2"):
+        if split:
+            monkeypatch.setenv("ICX_ENC_BATCH", split)
+        d_out.fill_(0xAB)
+        st, sizes = enc.encode_device_batch(100, 444, w, h, 3, [t.data_ptr() for t in d_src], d_out.data_ptr(), stride)
+        assert list(st) == [icx.OK] * 5 and list(sizes) == [len(x) for x in want]
+        out = d_out.cpu().numpy()
+        for k in range(5):
+            assert out[k * stride: k * stride + sizes[k]].tobytes() == want[k], (split, k)
     enc.close()
