@@ -456,8 +456,10 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
     uint64_t acc = 0;
     int nacc = o0;  // the first o0 bits of the first word belong to the previous unit (zeros here)
     bool firstw = true;
-    auto put = [&](int n, uint32_t v) {
-        acc = (acc << n) | (v & ((1u << n) - 1u));
+    // A Huffman code and the amplitude bits after it go out as one piece of up to 27 bits
+    // (code << size | amplitude), so each symbol costs one append and one word check.
+    auto put = [&](int n, uint32_t v) {  // v < 2^n, n <= 27
+        acc = (acc << n) | v;
         nacc += n;
         if (nacc >= 32) {
             const uint32_t word = (uint32_t)(acc >> (nacc - 32));
@@ -468,32 +470,34 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
             nacc -= 32;
         }
     };
-    auto code = [&](uint32_t e) { put((int)(e & 255), e >> 8); };
-    int nb;
-    uint32_t vb;
-    const int diff = dc - pred;
-    if (diff) {
-        vli(diff, nb, vb);
-        code(td[nb]);
-        put(nb, vb);
-    } else {
-        code(td[0]);
+    {
+        int nb = 0;
+        uint32_t vb = 0;
+        const int diff = dc - pred;
+        if (diff) vli(diff, nb, vb);
+        const uint32_t e = td[nb];
+        put((int)(e & 255) + nb, (e >> 8) << nb | vb);
     }
     int zr = 0;
 #pragma unroll
     for (int i = 1; i < 64; ++i) {
         const int v = coef(i);
         if (v) {
-            for (int z = zr >> 4; z > 0; --z) code(ta[0xF0]);
+            if (i > 16 && zr >= 16) {  // (a run of 16+ zeros needs 16 coefficients before it)
+                const uint32_t z = ta[0xF0];
+                for (int q = zr >> 4; q > 0; --q) put((int)(z & 255), z >> 8);
+            }
+            int nb;
+            uint32_t vb;
             vli(v, nb, vb);
-            code(ta[((zr & 15) << 4) | nb]);
-            put(nb, vb);
+            const uint32_t e = ta[((zr & 15) << 4) | nb];
+            put((int)(e & 255) + nb, (e >> 8) << nb | vb);
             zr = 0;
         } else {
             ++zr;
         }
     }
-    if (!coef(63)) code(ta[0]);
+    if (!coef(63)) put((int)(ta[0] & 255), ta[0] >> 8);
     if (nacc > 0) atomicOr(wp, (uint32_t)(acc << (32 - nacc)));  // shared with the next unit
 }
 
