@@ -452,22 +452,26 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
     const uint32_t* td = U.tab[c ? 2 : 0];
     const uint32_t* ta = U.tab[c ? 3 : 1];
     uint32_t* wp = words + (int64_t)img * B.wwords + (pos >> 5);
+    uint32_t* const wp0 = wp;
     const int o0 = (int)(pos & 31);
     uint64_t acc = 0;
     int nacc = o0;  // the first o0 bits of the first word belong to the previous unit (zeros here)
-    bool firstw = true;
+    // A word shared with the previous unit (o0 != 0: the first) is kept in a register and OR-ed
+    // in at the end, so the word check stores plainly or not at all.
+    bool firstw = o0 != 0;
+    uint32_t wfirst = 0;
     // A Huffman code and the amplitude bits after it go out as one piece of up to 27 bits
     // (code << size | amplitude), so each symbol costs one append and one word check.
     auto put = [&](int n, uint32_t v) {  // v < 2^n, n <= 27
         acc = (acc << n) | v;
         nacc += n;
         if (nacc >= 32) {
-            const uint32_t word = (uint32_t)(acc >> (nacc - 32));
-            if (firstw && o0) atomicOr(wp, word);  // shared with the previous unit
-            else *wp = word;
+            nacc -= 32;
+            const uint32_t word = (uint32_t)(acc >> nacc);
+            wfirst = firstw ? word : wfirst;
+            if (!firstw) *wp = word;
             firstw = false;
             ++wp;
-            nacc -= 32;
         }
     };
     {
@@ -498,6 +502,7 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
         }
     }
     if (!coef(63)) put((int)(ta[0] & 255), ta[0] >> 8);
+    if (o0 && wp != wp0) atomicOr(wp0, wfirst);                    // shared with the previous unit
     if (nacc > 0) atomicOr(wp, (uint32_t)(acc << (32 - nacc)));  // shared with the next unit
 }
 
