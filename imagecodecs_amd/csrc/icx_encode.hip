@@ -118,6 +118,9 @@ struct RunRec {
     unsigned long long inc;   // [63] valid, [62:0] stream bits up to and including the run
 };
 constexpr unsigned long long kGValid = 1ull << 63;
+#ifndef ICX_LB_SLEEP  // s_sleep units (64 clocks) between polls of a look-back record
+#define ICX_LB_SLEEP 8
+#endif
 __device__ __forceinline__ unsigned long long g_load(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -134,7 +137,7 @@ __device__ __forceinline__ unsigned long long g_wait(const unsigned long long* p
             atomicOr(fail, 1u);
             return kGValid | ((8192ull << 28) | (8192ull << 14) | 8192ull);
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(ICX_LB_SLEEP);
     }
     return v;
 }
@@ -588,8 +591,13 @@ __global__ __launch_bounds__(256) void k_stuff_write_b(const uint32_t* __restric
         chunk_words(words + (int64_t)img * wwords, ch, nbytes, w);
         nb = (int)min<uint64_t>(kStuffChunk, nbytes - b0);
     }
+    // the workgroup's stuffed bytes are assembled in LDS at the destination's dword phase, then
+    // leave as aligned dword stores (bytes only at the two ends, shared with the neighbours)
+    __shared__ uint32_t ob[(2 * kStuffWg + 8) / 4];
+    uint8_t* obb = reinterpret_cast<uint8_t*>(ob);
     const uint32_t n = chunk_ff(w, nb);
-    uint32_t incl = n;
+    const uint32_t mine = (uint32_t)nb + n;  // this lane's output bytes
+    uint32_t incl = mine;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o);
@@ -597,16 +605,32 @@ __global__ __launch_bounds__(256) void k_stuff_write_b(const uint32_t* __restric
     }
     if (lane == 63) s[wv] = incl;
     __syncthreads();
-    if (!nb) return;
-    uint32_t before = incl - n + (base[blockIdx.x] - base[0]);
-    for (int q = 0; q < wv; ++q) before += s[q];
-    uint8_t* o = o0 + hdr.n + b0 + before;
+    uint32_t lo = incl - mine;
+    for (int q = 0; q < wv; ++q) lo += s[q];
+    const uint32_t wg_len = s[0] + s[1] + s[2] + s[3];
+    if (!wg_len) return;  // (uniform: a workgroup past the stream)
+    uint8_t* gdst = o0 + hdr.n + (uint64_t)blockIdx.x * kStuffWg + (base[blockIdx.x] - base[0]);
+    const int al = (int)(reinterpret_cast<uintptr_t>(gdst) & 3);
+    {
+        uint8_t* q = obb + al + lo;
 #pragma unroll
-    for (int i = 0; i < kStuffChunk; ++i) {
-        if (i >= nb) break;
-        const uint8_t v = (uint8_t)(w[i >> 2] >> (24 - 8 * (i & 3)));
-        *o++ = v;
-        if (v == 0xFF) *o++ = 0;  // jpeg_enc.h:634-638
+        for (int i = 0; i < kStuffChunk; ++i) {
+            if (i >= nb) break;
+            const uint8_t v = (uint8_t)(w[i >> 2] >> (24 - 8 * (i & 3)));
+            *q++ = v;
+            if (v == 0xFF) *q++ = 0;  // jpeg_enc.h:634-638
+        }
+    }
+    __syncthreads();
+    uint32_t* gw = reinterpret_cast<uint32_t*>(gdst - al);
+    const int end = al + (int)wg_len, nd = (end + 3) >> 2;
+    for (int d = t; d < nd; d += 256) {
+        const int b0d = 4 * d;
+        if (b0d >= al && b0d + 4 <= end) {
+            gw[d] = ob[d];
+        } else {
+            for (int j = max(b0d, al); j < min(b0d + 4, end); ++j) (gdst - al)[j] = obb[j];
+        }
     }
 }
 
