@@ -162,13 +162,17 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
                                                  RunRec* __restrict__ recs, unsigned* __restrict__ ticket,  // [0] ticket, [1] look-back expired
                                                  uint32_t* __restrict__ words, uint64_t* __restrict__ info) {
     // the run's samples (4:4:4: Y|Cb|Cr, 8 x 512 each; 4:2:0: Y 16 x 512 | Cb|Cr 8 x 256), then
-    // (once every lane holds its unit) the code tables, code << 8 | length
+    // (once every lane holds its unit) the code tables and each unit's AC codes
+    constexpr int kSlotW = 58;  // words per unit: 63 AC codes of at most 16 + 11 bits < 58 x 32
     __shared__ union {
         float S[3 * 8 * kRunPx];
-        uint32_t tab[4][256];
+        struct {
+            uint32_t slot[192][kSlotW];  // a unit's AC codes, MSB first
+            uint32_t tab[4][256];        // code << 8 | length
+        } E;
     } U;
+    static_assert(sizeof(U.E) <= sizeof(U.S), "the codes fit the samples' LDS");
     __shared__ float pq[2][64];
-    __shared__ uint8_t aclen[2][256];
     __shared__ uint8_t dcl[2][16];
     __shared__ int32_t dcs[256];
     __shared__ uint32_t wsum[4];
@@ -179,8 +183,6 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (t == 0) s_tk = (int)atomicAdd(ticket, 1u);
     if (t < 128) pq[t >> 6][t & 63] = T->pq[t >> 6][t & 63];
-    aclen[0][t] = T->len[1][t];
-    aclen[1][t] = T->len[3][t];
     if (t < 32) dcl[t >> 4][t & 15] = (t & 15) < 12 ? T->len[(t >> 4) ? 2 : 0][t & 15] : 0;
     __syncthreads();
     // (the grid is exactly one workgroup per run of the batch; the ticket is made wave-uniform so
@@ -319,7 +321,8 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
             f[8 * r + 4] = hi.x; f[8 * r + 5] = hi.y; f[8 * r + 6] = hi.z; f[8 * r + 7] = hi.w;
         }
     }
-    __syncthreads();  // every lane holds its samples: the code tables take the samples' LDS (below)
+    __syncthreads();  // every lane holds its samples: the code tables and AC codes take their LDS
+    for (int i = t; i < 4 * 256; i += 256) U.E.tab[i >> 8][i & 255] = (uint32_t)T->code[i >> 8][i & 255] << 8 | T->len[i >> 8][i & 255];
 #pragma unroll
     for (int r = 0; r < 8; ++r) fdct8<1>(f + 8 * r);
 #pragma unroll
@@ -339,49 +342,80 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
 #pragma unroll
         for (int q = 0; q < 32; ++q) cw[q] = ((uint32_t)o[2 * q] & 0xFFFFu) | ((uint32_t)o[2 * q + 1] << 16);
     }
-    // (the whole block is quantised before the length loop reads it, and stays 32 packed
-    // registers until the emit: left alone, the compiler interleaves the FDCT with that loop and
-    // keeps the unpacked coefficients alive across the look-back, 250+ VGPRs)
+    // (the whole block is quantised before the code loop reads it: left alone, the compiler
+    // interleaves the FDCT with that loop and keeps the unpacked coefficients alive, 250+ VGPRs)
 #pragma unroll
     for (int q = 0; q < 32; ++q) asm volatile("" : "+v"(cw[q]));
     auto coef = [&](int i) { return (int)(int16_t)(cw[i >> 1] >> (16 * (i & 1))); };
-    // AC codes (jpeg_enc.h:851-887): a ZRL per 16 zeros before a nonzero coefficient, (run, size)
-    // symbol + amplitude bits, EOB unless coefficient 63 is nonzero
-    uint32_t bits = 0;
-    {
-        const uint8_t* al = aclen[c ? 1 : 0];
+    const int dc = coef(0);
+    dcs[t] = act ? dc : 0;
+    __syncthreads();  // code tables and DCs in LDS
+    // 3. the unit's AC codes into its LDS slot (jpeg_enc.h:851-887): a ZRL per 16 zeros before a
+    // nonzero coefficient, then the (run, size) code and the amplitude bits as one piece of up to
+    // 27 bits (code << size | amplitude), EOB unless coefficient 63 is nonzero. Its bit count is
+    // the unit's AC length, before any offset is known.
+    uint32_t bits_ac = 0;
+    uint32_t* const sl = U.E.slot[act ? t : 0];
+    if (act) {
+        const uint32_t* ta = U.E.tab[c ? 3 : 1];
+        uint64_t acc = 0;
+        int nacc = 0, widx = 0;
+        auto put = [&](int n, uint32_t v) {  // v < 2^n, n <= 27
+            acc = (acc << n) | v;
+            nacc += n;
+            if (nacc >= 32) {
+                nacc -= 32;
+                sl[widx++] = (uint32_t)(acc >> nacc);
+            }
+        };
         int zr = 0;
 #pragma unroll
         for (int i = 1; i < 64; ++i) {
             const int v = coef(i);
             if (v) {
-                const int mag = v < 0 ? -v : v, nb = 32 - __clz(mag);
-                bits += (uint32_t)((zr >> 4) * al[0xF0] + al[((zr & 15) << 4) | nb] + nb);
+                if (i > 16 && zr >= 16) {  // (a run of 16+ zeros needs 16 coefficients before it)
+                    const uint32_t z = ta[0xF0];
+                    for (int q = zr >> 4; q > 0; --q) put((int)(z & 255), z >> 8);
+                }
+                int nb;
+                uint32_t vb;
+                vli(v, nb, vb);
+                const uint32_t e = ta[((zr & 15) << 4) | nb];
+                put((int)(e & 255) + nb, (e >> 8) << nb | vb);
                 zr = 0;
             } else {
                 ++zr;
             }
         }
-        if (!coef(63)) bits += al[0];
+        if (!coef(63)) put((int)(ta[0] & 255), ta[0] >> 8);
+        if (nacc) sl[widx] = (uint32_t)(acc << (32 - nacc));
+        bits_ac = (uint32_t)widx * 32 + (uint32_t)nacc;
     }
-    const int dc = coef(0);
-    dcs[t] = act ? dc : 0;
-    for (int i = t; i < 4 * 256; i += 256) U.tab[i >> 8][i & 255] = (uint32_t)T->code[i >> 8][i & 255] << 8 | T->len[i >> 8][i & 255];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) asm volatile("" : "+v"(cw[q]));
-    __syncthreads();
-    // 3. DC codes of the units whose predecessor is in the run (:834: the predictor never resets)
+    // 4. the DC code (:834-849: the predictor never resets) as one piece, once its predictor is
+    // known: the previous unit of its component in the run, or (the run's first units) the last
+    // DC of the run before, from the look-back
+    const uint32_t* td = U.E.tab[c ? 2 : 0];
+    auto dc_piece = [&](int pred, int& n, uint32_t& v) {
+        int nb = 0;
+        uint32_t vb = 0;
+        const int diff = dc - pred;
+        if (diff) vli(diff, nb, vb);
+        const uint32_t e = td[nb];
+        n = (int)(e & 255) + nb;
+        v = (e >> 8) << nb | vb;
+    };
     const bool first = L.prevk[k] < 0 && ml == 0;  // the run's first unit of its component
     const int pt = L.prevk[k] >= 0 ? ml * L.upm + L.prevk[k] : (ml - 1) * L.upm + L.lastk[c];
-    int pred = first ? 0 : dcs[pt];
-    if (act && !first) bits += (uint32_t)dc_bits(dcl, c, dc - pred);
-    if (!act) bits = 0;
+    int dcn = 0;
+    uint32_t dcv = 0;
+    if (act && !first) dc_piece(dcs[pt], dcn, dcv);
+    uint32_t bits = act ? bits_ac + (uint32_t)dcn : 0u;  // (first units: AC only so far)
     {
-        const uint32_t s = wave_sum32(bits);  // (first units: AC only so far)
-        if (lane == 0) wsum[wv] = s;
+        const uint32_t sa = wave_sum32(bits);
+        if (lane == 0) wsum[wv] = sa;
     }
     __syncthreads();
-    // 4. look-back (wave 0): the run's A, first and last DCs go out first
+    // 5. look-back (wave 0): the run's A, first and last DCs go out first
     if (wv == 0) {
         const uint32_t A = wsum[0] + wsum[1] + wsum[2] + wsum[3];
         unsigned long long F = 0, Lr = 0;
@@ -434,11 +468,11 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
         }
     }
     __syncthreads();
-    if (first) {
-        pred = s_lprev[c];
-        if (act) bits += (uint32_t)dc_bits(dcl, c, dc - pred);
+    if (act && first) {
+        dc_piece(s_lprev[c], dcn, dcv);
+        bits += (uint32_t)dcn;
     }
-    // 5. block exclusive scan of the unit lengths -> bit offsets
+    // 6. block exclusive scan of the unit lengths -> bit offsets
     uint32_t incl = bits;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -452,8 +486,7 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
     const uint64_t pos = s_excl + before;
     const uint64_t cap_bits = B.wwords * 32;
     if (!act || pos + bits + 32 > cap_bits) return;  // past the words buffer: the host runs it again
-    const uint32_t* td = U.tab[c ? 2 : 0];
-    const uint32_t* ta = U.tab[c ? 3 : 1];
+    // 7. the unit's DC piece and its AC codes at its bit offset (jpeg_enc.h:613-643)
     uint32_t* wp = words + (int64_t)img * B.wwords + (pos >> 5);
     uint32_t* const wp0 = wp;
     const int o0 = (int)(pos & 31);
@@ -463,9 +496,7 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
     // in at the end, so the word check stores plainly or not at all.
     bool firstw = o0 != 0;
     uint32_t wfirst = 0;
-    // A Huffman code and the amplitude bits after it go out as one piece of up to 27 bits
-    // (code << size | amplitude), so each symbol costs one append and one word check.
-    auto put = [&](int n, uint32_t v) {  // v < 2^n, n <= 27
+    auto put = [&](int n, uint32_t v) {  // v < 2^n, n <= 32
         acc = (acc << n) | v;
         nacc += n;
         if (nacc >= 32) {
@@ -477,34 +508,10 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
             ++wp;
         }
     };
-    {
-        int nb = 0;
-        uint32_t vb = 0;
-        const int diff = dc - pred;
-        if (diff) vli(diff, nb, vb);
-        const uint32_t e = td[nb];
-        put((int)(e & 255) + nb, (e >> 8) << nb | vb);
-    }
-    int zr = 0;
-#pragma unroll
-    for (int i = 1; i < 64; ++i) {
-        const int v = coef(i);
-        if (v) {
-            if (i > 16 && zr >= 16) {  // (a run of 16+ zeros needs 16 coefficients before it)
-                const uint32_t z = ta[0xF0];
-                for (int q = zr >> 4; q > 0; --q) put((int)(z & 255), z >> 8);
-            }
-            int nb;
-            uint32_t vb;
-            vli(v, nb, vb);
-            const uint32_t e = ta[((zr & 15) << 4) | nb];
-            put((int)(e & 255) + nb, (e >> 8) << nb | vb);
-            zr = 0;
-        } else {
-            ++zr;
-        }
-    }
-    if (!coef(63)) put((int)(ta[0] & 255), ta[0] >> 8);
+    put(dcn, dcv);
+    const int nfull = (int)(bits_ac >> 5), rem = (int)(bits_ac & 31);
+    for (int q = 0; q < nfull; ++q) put(32, sl[q]);
+    if (rem) put(rem, sl[nfull] >> (32 - rem));
     if (o0 && wp != wp0) atomicOr(wp0, wfirst);                    // shared with the previous unit
     if (nacc > 0) atomicOr(wp, (uint32_t)(acc << (32 - nacc)));  // shared with the next unit
 }
