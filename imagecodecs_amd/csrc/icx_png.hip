@@ -1204,19 +1204,29 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
     }
     if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
 }
+// The file's layout once the deflate stream's length is known, on the device (k_png_size): the
+// rest of the encode reads it there, so no host read-back sits between the deflate and the file.
+struct PngTail {
+    unsigned long long dbytes;  // deflate stream bytes (zero-padded to a byte)
+    unsigned long long zlen;    // zlib stream: 2 + dbytes + 4 (Adler-32)
+    unsigned long long total;   // file bytes
+    unsigned long long fits;    // total <= cap: only then is anything written to the output
+};
+__device__ __forceinline__ bool png_fits(const PngTail* t) { return t->fits != 0; }
+
 __global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint16_t* __restrict__ tok,
                                                   const uint32_t* __restrict__ ntok, const uint32_t* __restrict__ seam,
                                                   const uint16_t* __restrict__ hbuf, const BlockCodes* __restrict__ bc,
                                                   const uint32_t* __restrict__ plan,
                                                   const unsigned long long* __restrict__ off,
                                                   const unsigned long long* __restrict__ bits, uint32_t* __restrict__ out,
-                                                  unsigned long long base_bits) {
+                                                  unsigned long long base_bits, const struct PngTail* __restrict__ tl) {
     __shared__ uint32_t img[4][kEmitWords];
     __shared__ BlockCodes B;  // the four waves' segments share one block
     stage_codes(bc, B);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t seg = (int64_t)blockIdx.x * 4 + wave;
-    if (seg >= nseg) return;  // wave-uniform; no block barriers below
+    if (seg >= nseg || !png_fits(tl)) return;  // wave-uniform; no block barriers below
     const uint32_t skip = seam[4 * seg + 1], nh = seam[4 * seg + 2];
     const uint16_t* T = tok + seg * kSlots + skip;
     const uint16_t* Hd = hbuf + seg * kHead;
@@ -1253,8 +1263,8 @@ __device__ __forceinline__ uint32_t crc_table(uint32_t i) {
 // with zeros in front): raw(range) = sum_r raw(seg_r) * X^r over r = segments after seg_r,
 // X = x^(8 kCrcSeg) mod P. One lane per segment (slicing-by-4 tables in LDS, dword loads);
 // k_png_crc_reduce folds 256 consecutive r at a time (X -> X^256 per pass).
-__global__ __launch_bounds__(256) void k_png_crc_seg(const uint8_t* __restrict__ p, int64_t n, int64_t nseg,
-                                                     uint32_t* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_png_crc_seg(const uint8_t* __restrict__ p, const PngTail* __restrict__ tl,
+                                                     int64_t nseg, uint32_t* __restrict__ part) {
     __shared__ uint32_t tab[4][256];
     uint32_t t = crc_table(threadIdx.x);
     tab[0][threadIdx.x] = t;
@@ -1267,10 +1277,14 @@ __global__ __launch_bounds__(256) void k_png_crc_seg(const uint8_t* __restrict__
     __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;  // segments after this one
     if (r >= nseg) return;
+    // (nseg covers the largest stream that fits; segments before the real one's start are 0)
+    const int64_t n = png_fits(tl) ? (int64_t)tl->zlen + 4 : 0;  // "IDAT" + the zlib stream
     const int64_t b = n - r * kCrcSeg, a = max((int64_t)0, b - kCrcSeg);
     uint32_t c = 0;
     int64_t i = a;
-    for (; i < b && (reinterpret_cast<uintptr_t>(p + i) & 3); ++i) c = tab[0][(c ^ p[i]) & 255] ^ (c >> 8);
+    // (the range's first 4 bytes enter complemented: that is the 0xFFFFFFFF register start)
+    for (; i < b && (i < 4 || (reinterpret_cast<uintptr_t>(p + i) & 3)); ++i)
+        c = tab[0][(c ^ (i < 4 ? (uint8_t)~p[i] : p[i])) & 255] ^ (c >> 8);
     for (; i + 4 <= b; i += 4) {
         c ^= *reinterpret_cast<const uint32_t*>(p + i);
         c = tab[3][c & 255] ^ tab[2][(c >> 8) & 255] ^ tab[1][(c >> 16) & 255] ^ tab[0][c >> 24];
@@ -1345,6 +1359,66 @@ __global__ void k_png_adler(const uint32_t* __restrict__ adl, int64_t nseg, uint
     }
 }
 
+// ---- the file's tail on the device (png_encoder.cpp:1888-1952 zlib, :2277 chunk CRC) -------
+__device__ __forceinline__ void be32_dev(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24);
+    p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);
+    p[3] = (uint8_t)v;
+}
+// Stream length from the last segment's bit offset -> the file layout (one thread).
+__global__ void k_png_size(const unsigned long long* __restrict__ off, const unsigned long long* __restrict__ bits,
+                           int64_t nseg, unsigned long long data_at, unsigned long long cap, PngTail* __restrict__ tl) {
+    const unsigned long long dbytes = (off[nseg - 1] + bits[nseg - 1] + 7) / 8;  // zero-padded to a byte
+    const unsigned long long zlen = 2 + dbytes + 4;
+    const unsigned long long total = data_at + zlen + 4 + 12;  // + IDAT CRC + IEND chunk
+    tl->dbytes = dbytes;
+    tl->zlen = zlen;
+    tl->total = total;
+    tl->fits = total <= cap ? 1ull : 0ull;
+}
+// Zeroes the words k_png_emit ORs into (from the 4-aligned word before the deflate data to one
+// word past it), when the file fits, with 16-byte stores over that range widened to 16-byte
+// bounds: the widening stays inside the file (the zlib header before it and the Adler-32, CRC
+// and IEND after it are written afterwards).
+__global__ __launch_bounds__(256) void k_png_zero(uint32_t* __restrict__ w, unsigned long long mis,
+                                                  const PngTail* __restrict__ tl) {
+    if (!png_fits(tl)) return;
+    const unsigned long long nb = ((tl->dbytes + mis + 3) & ~3ull) + 4;  // bytes from w
+    const uintptr_t a = reinterpret_cast<uintptr_t>(w), a16 = a & ~(uintptr_t)15, e16 = (a + nb + 15) & ~(uintptr_t)15;
+    uint4* q = reinterpret_cast<uint4*>(a16);
+    const unsigned long long n16 = (e16 - a16) / 16;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (unsigned long long)gridDim.x * 256)
+        q[i] = make_uint4(0, 0, 0, 0);
+}
+// After the emit: the header bytes (signature .. IDAT type + zlib header 78 01, built on the host
+// and staged in device memory), the IDAT length and the Adler-32 (s1 = 1 + sum of bytes,
+// s2 = N + the weighted sum, both mod 65521; the segment sums are in ad[0..1]).
+__global__ __launch_bounds__(256) void k_png_head(uint8_t* __restrict__ out, const uint8_t* __restrict__ pre, int npre,
+                                                  unsigned long long idat_at, unsigned long long dstart,
+                                                  const uint32_t* __restrict__ ad, long long N,
+                                                  const PngTail* __restrict__ tl) {
+    if (!png_fits(tl)) return;
+    for (int i = threadIdx.x; i < npre; i += 256) out[i] = pre[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        be32_dev(out + idat_at, (uint32_t)tl->zlen);
+        const uint32_t s1 = (1 + ad[0]) % kAdlerMod, s2 = (uint32_t)(((unsigned long long)N + ad[1]) % kAdlerMod);
+        be32_dev(out + dstart + tl->dbytes, s2 << 16 | s1);
+    }
+}
+// The IDAT chunk's CRC-32 (k_png_crc_seg's raw CRC over "IDAT" and the zlib stream with the
+// first 4 bytes complemented = the standard register start; the final complement here) and the
+// IEND chunk.
+__global__ void k_png_tail(uint8_t* __restrict__ out, unsigned long long data_at, const uint32_t* __restrict__ crc_sum,
+                           const PngTail* __restrict__ tl) {
+    if (!png_fits(tl)) return;
+    uint8_t* t = out + data_at + tl->zlen;
+    be32_dev(t, ~crc_sum[0]);
+    const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+    for (int i = 0; i < 12; ++i) t[4 + i] = iend[i];
+}
+
 }  // namespace png
 
 // =============================================================================== host side
@@ -1371,18 +1445,30 @@ struct PngWs {
     void* tmp = nullptr;
     size_t tmp_cap = 0;
     struct PngHost* host = nullptr;  // pinned read-back buffer (PngJob)
-    hipEvent_t done = nullptr;       // a job's phase event
-    // per-stage HIP events (icx_png_encoder_stage_times): stage i spans ev[2i] .. ev[2i+1];
-    // ms[] accumulates over calls until read
+    png::PngTail* tl = nullptr;      // device: the file layout (k_png_size)
+    uint8_t* predev = nullptr;       // device copy of the header bytes (k_png_head)
+    hipEvent_t done = nullptr;       // a job's statistics event
+    // per-stage HIP events (icx_png_encoder_stage_times): stage i spans ev[s][2i] .. ev[s][2i+1],
+    // two sets used by alternate images, so one image's times are read once the next image's
+    // statistics are in (its kernels are done by then); ms[] accumulates until read
     static constexpr int kStages = 6;
-    hipEvent_t ev[2 * kStages] = {};
+    hipEvent_t ev[2][2 * kStages] = {};
+    int evset = 0;          // the set the next image records into
+    bool ev_pending = false;  // the other set holds an image's events not yet read
     float ms[kStages] = {};
+    void read_times(int set) {
+        for (int i = 0; i < kStages; ++i) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, ev[set][2 * i], ev[set][2 * i + 1]) == hipSuccess) ms[i] += t;
+        }
+    }
     ~PngWs() {
-        for (hipEvent_t e : ev)
-            if (e) (void)hipEventDestroy(e);
+        for (auto& set : ev)
+            for (hipEvent_t e : set)
+                if (e) (void)hipEventDestroy(e);
         if (done) (void)hipEventDestroy(done);
         if (host) (void)hipHostFree(host);
-        for (void* p : {(void*)st, (void*)set_key, (void*)set_idx, (void*)mode, (void*)conv, (void*)filt, (void*)tok,
+        for (void* p : {(void*)tl, (void*)predev, (void*)st, (void*)set_key, (void*)set_idx, (void*)mode, (void*)conv, (void*)filt, (void*)tok,
                         (void*)ntok, (void*)hist, (void*)adl, (void*)crc, (void*)small, (void*)bc, (void*)bits,
                         (void*)off, (void*)seghist, (void*)segx, (void*)seam, (void*)head, (void*)plan, (void*)blksym, tmp})
             if (p) (void)hipFree(p);
@@ -1390,12 +1476,17 @@ struct PngWs {
 };
 PngWs* png_ws_create() {
     PngWs* ws = new PngWs();
-    for (hipEvent_t& e : ws->ev)
-        if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+    for (auto& set : ws->ev)
+        for (hipEvent_t& e : set)
+            if (hipEventCreate(&e) != hipSuccess) e = nullptr;
     return ws;
 }
 static const char* const kPngStageNames[PngWs::kStages] = {"stats", "filter", "lz77", "huff", "emit", "crc"};
 int png_ws_stage_times(PngWs* ws, const char** names, float* ms, int cap) {
+    if (ws->ev_pending && hipEventQuery(ws->ev[ws->evset ^ 1][2 * PngWs::kStages - 1]) == hipSuccess) {
+        ws->read_times(ws->evset ^ 1);  // (the last image encoded)
+        ws->ev_pending = false;
+    }
     const int k = cap < PngWs::kStages ? cap : PngWs::kStages;
     for (int i = 0; i < k; ++i) {
         if (names) names[i] = kPngStageNames[i];
@@ -1456,47 +1547,44 @@ static void chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data
 // are asynchronous and the host waits on an event, not on the stream).
 struct PngHost {
     Stats S;
-    unsigned long long last_off, last_bits;
-    uint32_t ad[2];
-    uint32_t crc_sum;
     uint8_t pre[2048];  // signature + IHDR / PLTE / tRNS + IDAT header + zlib header
-    uint8_t adl[4], tail[16];
 };
 
-// One image's encode as three issue phases with a host read after each (png_encode_device runs
-// them back to back; png_encode_device_batch interleaves two images on two workspaces and
-// streams, so one image's kernels run while the host waits for the other's results):
-//   A  colour statistics                                          -> Stats
-//   B  (host: colour mode, palette, header) convert, filter, LZ77, Huffman, bit offsets, Adler
-//                                                                 -> stream length, Adler sums
-//   C  (host: file layout) emit, header / Adler bytes, CRC-32      -> CRC; the tail is written
+// One image's encode as two issue phases with one host read between them (png_encode_device
+// runs them back to back; png_encode_device_batch keeps several images in flight on their own
+// workspaces and streams, so one image's kernels run while the host reads another's statistics):
+//   A  colour statistics                                                        -> Stats (host)
+//   B  (host: colour mode, palette, header bytes) convert, filter, LZ77, Huffman, bit offsets;
+//      then on the device: the file layout (k_png_size), emit, header / IDAT length / Adler-32
+//      (k_png_head), the IDAT CRC-32 and IEND (k_png_tail) -- written only when the file fits;
+//      the layout goes to `out_tl` (pinned) with the image's other work, read after the stream
 struct PngJob {
     PngWs* ws = nullptr;
     PngHost* hb = nullptr;
+    png::PngTail* out_tl = nullptr;  // pinned: where the image's layout lands
     hipStream_t st = nullptr;
-    hipEvent_t ev = nullptr;  // recorded after each phase's read-back
+    hipEvent_t ev = nullptr;  // recorded after phase A's read-back
     int w = 0, h = 0, d = 0;
     const uint8_t* d_src = nullptr;
     uint8_t* d_out = nullptr;
-    uint64_t cap = 0, size = 0;
+    uint64_t cap = 0;
     Mode M{};
     std::vector<uint8_t> head;
     int64_t N = 0, nseg = 0, nblk = 0;
     unsigned gwave = 0;
-    uint64_t zlen = 0, data_at = 0, dstart = 0, dbytes = 0;
     bool timed = false;
+    int set = 0;
     void mark(int i) {  // event i: stage i/2 begins (even) or ends (odd)
-        if (timed) (void)hipEventRecord(ws->ev[i], st);
+        if (timed) (void)hipEventRecord(ws->ev[set][i], st);
     }
     int issue_a();
-    int issue_b();  // after ev of A
-    int issue_c();  // after ev of B; 1: d_out too small (size = bytes needed)
-    int finish();   // after ev of C
+    int issue_b();  // after ev of A: everything else, no further host read
 };
 
 int PngJob::issue_a() {
     const int64_t np = (int64_t)w * h;
-    timed = ws->ev[2 * PngWs::kStages - 1] != nullptr;
+    set = ws->evset;
+    timed = ws->ev[set][2 * PngWs::kStages - 1] != nullptr;
     size_t c1 = ws->st ? sizeof(Stats) : 0, c2 = ws->set_key ? kSetSlots * 8 : 0, c3 = c2, c4 = ws->mode ? sizeof(Mode) : 0;
     if (!pgrow(ws->st, sizeof(Stats), c1) || !pgrow(ws->set_key, kSetSlots * 8, c2) ||
         !pgrow(ws->set_idx, kSetSlots * 8, c3) || !pgrow(ws->mode, sizeof(Mode), c4))
@@ -1520,6 +1608,10 @@ int PngJob::issue_a() {
 
 int PngJob::issue_b() {
     const int64_t np = (int64_t)w * h;
+    if (ws->ev_pending) {  // the previous image on this workspace ran before this one's statistics
+        ws->read_times(set ^ 1);
+        ws->ev_pending = false;
+    }
     const int gs = (int)std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 4096));
     Stats S = hb->S;
     uint32_t kr = 0, kg = 0, kb = 0;
@@ -1676,50 +1768,40 @@ int PngJob::issue_b() {
     PNG_HIP(hipcub::DeviceScan::ExclusiveSum(ws->tmp, tb, ws->bits, ws->off, (int)nseg, st));
     hipLaunchKernelGGL(k_png_adler, dim3(1), dim3(256), 0, st, ws->adl, nseg, ws->small);
     mark(7);
-    PNG_HIP(hipMemcpyAsync(&hb->last_off, ws->off + nseg - 1, 8, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipMemcpyAsync(&hb->last_bits, ws->bits + nseg - 1, 8, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipMemcpyAsync(hb->ad, ws->small, 8, hipMemcpyDeviceToHost, st));
-    PNG_HIP(hipEventRecord(ev, st));
-    return 0;
-}
-
-int PngJob::issue_c() {
-    dbytes = (hb->last_off + hb->last_bits + 7) / 8;  // deflate stream, zero-padded
-    zlen = 2 + dbytes + 4;
+    // ---- P5: the file (png_encoder.cpp:1888-1952, 2277), laid out on the device
+    size_t c13 = ws->tl ? sizeof(png::PngTail) : 0, c14 = ws->predev ? sizeof hb->pre : 0;
+    if (!pgrow(ws->tl, sizeof(png::PngTail), c13) || !pgrow(ws->predev, sizeof hb->pre, c14)) return -1;
     const uint64_t idat_at = head.size();  // IDAT chunk header position
-    data_at = idat_at + 8;                 // zlib stream position
-    const uint64_t total = data_at + zlen + 4 + 12;
-    size = total;
-    if (total > cap) return 1;
-    // The deflate bits go to a 4-byte aligned word view of d_out starting at data_at + 2
-    // rounded down -- aligned as an address, since a batch slot may start anywhere (k_png_emit's
-    // atomics on the words two segments share need it) -- and the few bytes before it (zlib
-    // header) are rewritten afterwards.
-    dstart = data_at + 2;
+    const uint64_t data_at = idat_at + 8;  // zlib stream position
+    const uint64_t dstart = data_at + 2;   // deflate data
+    hipLaunchKernelGGL(k_png_size, dim3(1), dim3(1), 0, st, ws->off, ws->bits, nseg, (unsigned long long)data_at,
+                       (unsigned long long)cap, ws->tl);
+    // The deflate bits go to a 4-byte aligned word view of d_out starting at dstart rounded down
+    // -- aligned as an address, since a batch slot may start anywhere (k_png_emit's atomics on the
+    // words two segments share need it) -- and the few bytes before it (zlib header) are
+    // rewritten afterwards.
     const uint64_t mis = (reinterpret_cast<uintptr_t>(d_out) + dstart) & 3u;
-    const uint64_t wbase = dstart - mis;
-    const unsigned long long base_bits = mis * 8;
-    PNG_HIP(hipMemsetAsync(d_out + wbase, 0, ((dbytes + mis + 3) & ~3ull) + 4, st));
+    uint32_t* wv = reinterpret_cast<uint32_t*>(d_out + dstart - mis);
     mark(8);
-    hipLaunchKernelGGL(k_png_emit, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->seam, ws->head, ws->bc, ws->plan, ws->off, ws->bits,
-                       reinterpret_cast<uint32_t*>(d_out + wbase), base_bits);
+    hipLaunchKernelGGL(k_png_zero, dim3(1024), dim3(256), 0, st, wv, (unsigned long long)mis, ws->tl);
+    hipLaunchKernelGGL(k_png_emit, dim3(gwave), dim3(256), 0, st, nseg, ws->tok, ws->ntok, ws->seam, ws->head, ws->bc,
+                       ws->plan, ws->off, ws->bits, wv, (unsigned long long)(mis * 8), ws->tl);
     mark(9);
-    // signature + IHDR/PLTE/tRNS + IDAT length/type + zlib header (78 01, :1932-1941)
+    // signature + IHDR/PLTE/tRNS + IDAT length (k_png_head) / type + zlib header (78 01, :1932-1941)
     std::vector<uint8_t> pre = head;
-    uint8_t ih[8];
-    be32(ih, (uint32_t)zlen);
-    std::memcpy(ih + 4, "IDAT", 4);
+    const uint8_t ih[8] = {0, 0, 0, 0, 'I', 'D', 'A', 'T'};
     pre.insert(pre.end(), ih, ih + 8);
     pre.push_back(0x78);
     pre.push_back(0x01);
     if (pre.size() > sizeof hb->pre) return -1;
     std::memcpy(hb->pre, pre.data(), pre.size());
-    PNG_HIP(hipMemcpyAsync(d_out, hb->pre, pre.size(), hipMemcpyHostToDevice, st));
-    const uint32_t s1 = (1 + hb->ad[0]) % kAdlerMod, s2 = (uint32_t)(((uint64_t)N + hb->ad[1]) % kAdlerMod);
-    be32(hb->adl, s2 << 16 | s1);
-    PNG_HIP(hipMemcpyAsync(d_out + dstart + dbytes, hb->adl, 4, hipMemcpyHostToDevice, st));
-    // CRC-32 over "IDAT" + zlib stream: segment CRCs, folded 256:1 per pass into ws->crc
-    const int64_t ncs = (int64_t)((zlen + kCrcSeg - 1) / kCrcSeg);
+    PNG_HIP(hipMemcpyAsync(ws->predev, hb->pre, pre.size(), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_png_head, dim3(1), dim3(256), 0, st, d_out, ws->predev, (int)pre.size(),
+                       (unsigned long long)idat_at, (unsigned long long)dstart, ws->small, (long long)N, ws->tl);
+    // CRC-32 over "IDAT" + zlib stream: segment CRCs aligned to the stream's end (the device
+    // knows its length; the grid covers the longest stream that fits), folded 256:1 per pass
+    const uint64_t zmax = cap > data_at + 16 ? cap - data_at - 16 + 4 : 4;  // ("IDAT" + stream)
+    const int64_t ncs = std::max<int64_t>(1, (int64_t)((zmax + kCrcSeg - 1) / kCrcSeg));
     size_t c12 = ws->crc_cap;
     const size_t crc_need = (size_t)(ncs + (ncs + 255) / 256 + 64) * 4;
     if (crc_need > ws->crc_cap || !ws->crc) {
@@ -1727,8 +1809,8 @@ int PngJob::issue_c() {
         ws->crc_cap = crc_need;
     }
     mark(10);
-    hipLaunchKernelGGL(k_png_crc_seg, dim3((unsigned)((ncs + 255) / 256)), dim3(256), 0, st, d_out + data_at,
-                       (int64_t)zlen, ncs, ws->crc);
+    hipLaunchKernelGGL(k_png_crc_seg, dim3((unsigned)((ncs + 255) / 256)), dim3(256), 0, st, d_out + idat_at + 4,
+                       ws->tl, ncs, ws->crc);
     uint32_t X = x8n(kCrcSeg);
     uint32_t* cur = ws->crc;
     int64_t m = ncs;
@@ -1740,40 +1822,19 @@ int PngJob::issue_c() {
         cur = nxt;
         m = nb;
     }
+    hipLaunchKernelGGL(k_png_tail, dim3(1), dim3(1), 0, st, d_out, (unsigned long long)data_at, cur, ws->tl);
     mark(11);
-    PNG_HIP(hipMemcpyAsync(&hb->crc_sum, cur, 4, hipMemcpyDeviceToHost, st));
+    PNG_HIP(hipMemcpyAsync(out_tl, ws->tl, sizeof(png::PngTail), hipMemcpyDeviceToHost, st));
     PNG_HIP(hipGetLastError());
-    PNG_HIP(hipEventRecord(ev, st));
-    return 0;
-}
-
-int PngJob::finish() {
-    uint32_t init_raw;  // raw CRC of a 0xFFFFFFFF-initialised register over "IDAT"
-    {
-        uint32_t c = 0xFFFFFFFFu;
-        const uint8_t t4[4] = {'I', 'D', 'A', 'T'};
-        for (int i = 0; i < 4; ++i) {
-            c ^= t4[i];
-            for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-        }
-        init_raw = c;
+    if (timed) {
+        ws->ev_pending = true;
+        ws->evset = set ^ 1;
     }
-    const uint32_t craw = multmodp(init_raw, x8n(zlen)) ^ hb->crc_sum;  // the "IDAT" prefix shifted over the range
-    be32(hb->tail, ~craw);
-    const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
-    std::memcpy(hb->tail + 4, iend, 12);
-    PNG_HIP(hipMemcpyAsync(d_out + data_at + zlen, hb->tail, 16, hipMemcpyHostToDevice, st));
-    PNG_HIP(hipGetLastError());
-    if (timed)
-        for (int i = 0; i < PngWs::kStages; ++i) {
-            float t = 0.f;
-            if (hipEventElapsedTime(&t, ws->ev[2 * i], ws->ev[2 * i + 1]) == hipSuccess) ws->ms[i] += t;
-        }
     return 0;
 }
 
 static bool png_job_init(PngJob& j, PngWs* ws, hipStream_t st, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
-                         uint64_t cap) {
+                         uint64_t cap, png::PngTail* out_tl) {
     if (!ws->host && hipHostMalloc(reinterpret_cast<void**>(&ws->host), sizeof(PngHost)) != hipSuccess) return false;
     if (!ws->done && hipEventCreateWithFlags(&ws->done, hipEventDisableTiming) != hipSuccess) return false;
     j.ws = ws;
@@ -1786,6 +1847,7 @@ static bool png_job_init(PngJob& j, PngWs* ws, hipStream_t st, int w, int h, int
     j.d_src = d_src;
     j.d_out = d_out;
     j.cap = cap;
+    j.out_tl = out_tl;
     return true;
 }
 
@@ -1793,62 +1855,62 @@ static bool png_job_init(PngJob& j, PngWs* ws, hipStream_t st, int w, int h, int
 // d_out. Returns 0 ok, 1 d_out too small (*size = bytes needed), -1 HIP failure.
 int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
                       uint64_t cap, uint64_t* size) {
+    png::PngTail* tl = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&tl), sizeof *tl) != hipSuccess) return -1;
     PngJob j;
-    if (!png_job_init(j, ws, st, w, h, d, d_src, d_out, cap)) return -1;
-    int rc = j.issue_a();
+    int rc = png_job_init(j, ws, st, w, h, d, d_src, d_out, cap, tl) ? j.issue_a() : -1;
     if (rc == 0) rc = hipEventSynchronize(j.ev) == hipSuccess ? j.issue_b() : -1;
-    if (rc == 0) rc = hipEventSynchronize(j.ev) == hipSuccess ? j.issue_c() : -1;
-    *size = j.size;
-    if (rc != 0) return rc;
-    if (hipEventSynchronize(j.ev) != hipSuccess || j.finish() != 0) return -1;
-    return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+    if (rc == 0) rc = hipStreamSynchronize(st) == hipSuccess ? (tl->fits ? 0 : 1) : -1;
+    *size = rc >= 0 ? tl->total : 0;
+    (void)hipHostFree(tl);
+    return rc;
 }
 
 // n images of w x h x d at d_srcs[i] into d_out + i * stride (sizes[i], status[i]: 0 ok, 1 the
-// slot is too small, -1 failure). k jobs in flight on (ws[j], st[j]): each phase of one image is
-// issued while the host waits for another's read-back, so the images' kernel chains share the GPU
-// and the host waits overlap GPU work. Returns -1 on a HIP failure.
+// slot is too small: nothing written, -1 failure). k jobs in flight on (ws[j], st[j]): the host
+// reads one image's colour statistics (the only read-back per image) while the others' kernels
+// run; every size is read once, after the last image. Returns -1 on a HIP failure.
 int png_encode_device_batch(int k, hipStream_t* sts, PngWs** wss, int n, int w, int h, int d,
                             const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t stride, uint64_t* sizes,
                             int32_t* status) {
+    png::PngTail* tl = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&tl), sizeof(png::PngTail) * std::max(n, 1)) != hipSuccess) return -1;
     std::vector<PngJob> job(k);
-    std::vector<int> img(k, -1), phase(k, 0);
-    int next = 0, fail = 0, live = 0;
+    std::vector<int> img(k, -1);
+    std::vector<int32_t> rc(std::max(n, 1), 0);
+    int next = 0, live = 0;
     auto start = [&](int j) {
         img[j] = -1;
         if (next >= n) return;
         img[j] = next++;
-        phase[j] = 0;
         job[j] = PngJob{};
-        if (!png_job_init(job[j], wss[j], sts[j], w, h, d, d_srcs[img[j]], d_out + (uint64_t)img[j] * stride, stride) ||
+        if (!png_job_init(job[j], wss[j], sts[j], w, h, d, d_srcs[img[j]], d_out + (uint64_t)img[j] * stride, stride,
+                          tl + img[j]) ||
             job[j].issue_a() != 0) {
-            status[img[j]] = -1;
-            fail = 1;
+            rc[img[j]] = -1;
             img[j] = -1;
         }
     };
     for (int j = 0; j < k; ++j) start(j);
     for (int j = 0; j < k; ++j) live += img[j] >= 0;
-    for (int j = 0; live > 0; j = (j + 1) % k) {  // round robin: wait for one job, advance it
+    // round robin over the jobs: wait for one job's statistics, issue the rest of its image and
+    // its next image's statistics (measured a little faster than taking whichever is ready first)
+    for (int j = 0; live > 0; j = (j + 1) % k) {
         if (img[j] < 0) continue;
         PngJob& J = job[j];
-        int rc = hipEventSynchronize(J.ev) == hipSuccess ? 0 : -1;
-        if (rc == 0) rc = phase[j] == 0 ? J.issue_b() : phase[j] == 1 ? J.issue_c() : J.finish();
-        if (rc != 0 || phase[j] == 2) {
-            sizes[img[j]] = J.size;
-            status[img[j]] = rc;
-            if (rc < 0) fail = 1;
-            start(j);
-            if (img[j] < 0) --live;
-        } else {
-            ++phase[j];
-        }
+        if (hipEventSynchronize(J.ev) != hipSuccess || J.issue_b() != 0) rc[img[j]] = -1;
+        start(j);
+        if (img[j] < 0) --live;
     }
     // per-image failures are in status[] (-1); the call fails only when a stream itself did
     bool stream_fail = false;
     for (int j = 0; j < k; ++j)
         if (hipStreamSynchronize(sts[j]) != hipSuccess) stream_fail = true;
-    (void)fail;
+    for (int i = 0; i < n; ++i) {
+        sizes[i] = rc[i] < 0 || stream_fail ? 0 : tl[i].total;
+        status[i] = rc[i] < 0 ? -1 : (tl[i].fits ? 0 : 1);
+    }
+    (void)hipHostFree(tl);
     return stream_fail ? -1 : 0;
 }
 

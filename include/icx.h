@@ -231,10 +231,13 @@ int icx_png_encode_device(icx_png_encoder* enc, int width, int height, int d, co
 /* n images (width x height x d each, at d_srcs[i] on the context's device) into d_out + i *
  * out_stride; out_sizes[i] = file size (or the bytes needed), status[i] = ICX_OK, ICX_OUT_OF_MEM
  * (the slot is too small) or ICX_INTERNAL_ERR (that image's own job failed: every other image still
- * gets its status and size). Returns ICX_INTERNAL_ERR only when a stream failed. The batch form of png_encoder::saveToFile for device-resident images:
- * several images in flight (ICX_PNG_INFLIGHT, default 8), each on its own workspace and stream,
- * so some images' kernels run while the host reads back another's (colour statistics, stream
- * length, CRC). Returns when every file is written. */
+ * gets its status and size). Returns ICX_INTERNAL_ERR only when a stream failed. The batch form
+ * of png_encoder::saveToFile for device-resident images: several images in flight
+ * (ICX_PNG_INFLIGHT, default 8), each on its own workspace and stream. The host reads back one
+ * thing per image, its colour statistics (the colour mode and palette are chosen on the host);
+ * the file layout, IDAT length, Adler-32, CRC-32 and IEND are computed and written on the device,
+ * and every image's size is read once, after the last image. Returns when every file is
+ * written. */
 int icx_png_encode_device_batch(icx_png_encoder* enc, int n, int width, int height, int d,
                                 const uint8_t* const* d_srcs, uint8_t* d_out, uint64_t out_stride,
                                 uint64_t* out_sizes, int32_t* status, void* hip_stream);
