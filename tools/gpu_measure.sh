@@ -11,5 +11,5 @@ echo "bench: $(cut -c1-200 $O/bench.json)"
 # same command without the CPU-baseline leg (its fork pool does not survive the profiler's preload)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- python3 "$R/bench.py" $ARGS --no-cpu --no-pcie > "$O/bench_rocprof.json" 2> "$O/rocprof.err"
 echo "rocprof done"
-timeout -k 10 1200 python3 "$R/tools/pmc_traffic.py" run --out "$O/traffic.json" > "$O/pmc.log" 2>&1
+timeout -k 10 1200 python3 "$R/tools/pmc_traffic.py" run --out "$O/traffic.json" --pipeline-out "$O/pipeline_traffic.json" > "$O/pmc.log" 2>&1
 echo "pmc: $(tail -1 $O/pmc.log | cut -c1-300)"
