@@ -1014,7 +1014,10 @@ int icx_exr_decode_device_batch(icx_ctx* ctx, int n, const uint8_t* const* data,
     if (n < 0 || (n > 0 && (!data || !d_data || !sizes || !d_out || !out_floats || !codes || !widths || !heights)))
         return ICX_EXR_INVALID_ARGUMENT;
     for (int i = 0; i < n; ++i)
-        if (!data[i] || !d_data[i] || !d_out[i]) return ICX_EXR_INVALID_ARGUMENT;
+        if (!data[i] || !d_data[i] || !d_out[i] || (reinterpret_cast<uintptr_t>(d_data[i]) & 15)) {
+            ctx->err = "icx_exr_decode_device_batch: d_data[i] must be non-null and 16-byte aligned";
+            return ICX_EXR_INVALID_ARGUMENT;
+        }
     if (n == 0) return ICX_EXR_SUCCESS;
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_EXR_INTERNAL_ERR);
     const RoctxRange range("icx_exr_decode_device_batch");
@@ -1039,7 +1042,10 @@ int icx_exr_decode_device(icx_ctx* ctx, const uint8_t* data, const uint8_t* d_da
     if (w) *w = 0;
     if (h) *h = 0;
     if (!ctx) return ICX_EXR_INTERNAL_ERR;
-    if (!data || !d_data || !d_out) return ICX_EXR_INVALID_ARGUMENT;
+    if (!data || !d_data || !d_out || (reinterpret_cast<uintptr_t>(d_data) & 15)) {
+        ctx->err = "icx_exr_decode_device: d_data must be non-null and 16-byte aligned";
+        return ICX_EXR_INVALID_ARGUMENT;
+    }
     ICX_HIP(ctx, hipSetDevice(ctx->device), ICX_EXR_INTERNAL_ERR);
     const RoctxRange range("icx_exr_decode_device");
     int ww = 0, hh = 0;

@@ -947,16 +947,22 @@ struct BitW {
 // of b's deflate block. One workgroup; thread 0 groups greedily over the base blocks' symbol
 // counts (k_png_lz77's, before the seams move a few tokens: the grouping only needs their size).
 constexpr uint32_t kBlockTokens = 16384;
+// Counts staged in LDS when they fit (kPlanLds base blocks = 4 GiB of filtered bytes); past that
+// the one walking thread reads them from global memory (slower, still exact).
+constexpr int64_t kPlanLds = 16384;
 __global__ __launch_bounds__(256) void k_png_blockplan(const uint32_t* __restrict__ blksym, int64_t nblk,
-                                                       uint32_t* __restrict__ plan) {
-    extern __shared__ uint32_t cnt[];  // nblk symbol counts (host caps nblk for the LDS size)
-    for (int64_t b = threadIdx.x; b < nblk; b += 256) cnt[b] = blksym[b];
+                                                       uint32_t* __restrict__ plan, int64_t lds_max) {
+    extern __shared__ uint32_t cnt[];  // min(nblk, lds_max) symbol counts
+    const bool lds = nblk <= lds_max;
+    if (lds)
+        for (int64_t b = threadIdx.x; b < nblk; b += 256) cnt[b] = blksym[b];
     __syncthreads();
     if (threadIdx.x != 0) return;
     int64_t first = 0;
     uint32_t acc = 0;
     for (int64_t b = 0; b <= nblk; ++b) {
-        if (b == nblk || (acc && acc + cnt[b] > kBlockTokens)) {
+        const uint32_t cb = b < nblk ? (lds ? cnt[b] : blksym[b]) : 0u;
+        if (b == nblk || (acc && acc + cb > kBlockTokens)) {
             for (int64_t k = first; k < b; ++k) {
                 plan[2 * k] = (uint32_t)first;
                 plan[2 * k + 1] = (uint32_t)(b - 1);
@@ -964,7 +970,7 @@ __global__ __launch_bounds__(256) void k_png_blockplan(const uint32_t* __restric
             first = b;
             acc = 0;
         }
-        if (b < nblk) acc += cnt[b];
+        acc += cb;
     }
 }
 
@@ -1748,7 +1754,6 @@ int PngJob::issue_b() {
         !pgrow(ws->head, (size_t)nseg * kHead * 2, ws->head_cap) || !pgrow(ws->plan, (size_t)nblk * 8, ws->plan_cap) ||
         !pgrow(ws->blksym, (size_t)nblk * 4, ws->blksym_cap))
         return -1;
-    if (nblk > 16384) return -1;  // k_png_blockplan's LDS (64 KiB): images up to 4 GiB of filtered bytes
     hipLaunchKernelGGL(k_png_lz77, dim3((unsigned)nblk), dim3(256), 0, st, ws->filt, N, nseg, 1 + M.lb, M.bw, ws->tok,
                        ws->ntok, ws->hist, ws->adl, ws->seghist, ws->segx, ws->seam, ws->blksym);
     gwave = (unsigned)((nseg + 3) / 4);  // one wave per segment
@@ -1758,7 +1763,11 @@ int PngJob::issue_b() {
                        ws->tok, ws->ntok, ws->seam, ws->head, ws->seghist, ws->segx, ws->hist);
     mark(5);
     mark(6);
-    hipLaunchKernelGGL(k_png_blockplan, dim3(1), dim3(256), (size_t)nblk * 4, st, ws->blksym, nblk, ws->plan);
+    // (ICX_PNG_PLAN_LDS lowers the LDS limit so tests reach the global-memory walk)
+    const char* pl = std::getenv("ICX_PNG_PLAN_LDS");
+    const int64_t lds_max = pl ? std::max<int64_t>(0, std::min<int64_t>(kPlanLds, std::atoll(pl))) : kPlanLds;
+    hipLaunchKernelGGL(k_png_blockplan, dim3(1), dim3(256), (size_t)std::max<int64_t>(1, std::min<int64_t>(nblk, lds_max)) * 4,
+                       st, ws->blksym, nblk, ws->plan, lds_max);
     hipLaunchKernelGGL(k_png_huff, dim3((unsigned)nblk), dim3(64), 0, st, ws->hist, nblk, ws->plan, ws->bc);
     hipLaunchKernelGGL(k_png_segbits, dim3(gwave), dim3(256), 0, st, nseg, ws->seghist, ws->segx, ws->bc, ws->plan,
                        ws->bits);

@@ -314,7 +314,9 @@ int icx_exr_probe(const uint8_t* data, size_t size, int* width, int* height);
 int icx_exr_decode(icx_ctx* ctx, const uint8_t* data, size_t size, float** out_rgba, int* width, int* height);
 /* The same read with the file already resident on the device (batch pipelines, benchmarks): the
  * header and offset table are planned from the host copy `data`; the kernels read the device copy
- * `d_data` (the same `size` bytes followed by 16 zero bytes) and write width*height*4 floats to
+ * `d_data` (the same `size` bytes followed by 16 zero bytes; 16-byte aligned, since the chunk
+ * readers load 16-byte words: a misaligned pointer is ICX_EXR_INVALID_ARGUMENT) and write
+ * width*height*4 floats to
  * `d_out` (room for `out_floats`; too little -> ICX_EXR_INTERNAL_ERR). Synchronises with the
  * context's stream; returns an icx_exr_result. */
 int icx_exr_decode_device(icx_ctx* ctx, const uint8_t* data, const uint8_t* d_data, size_t size, float* d_out,

@@ -143,6 +143,10 @@ def test_exr_decode_device_matches_host_entry(ctx):
     d_out = torch.zeros(w * h * 4, dtype=torch.float32, device=dev)
     with pytest.raises(icx.ICXError):
         ctx.exr_decode_device(data, d_file.data_ptr(), d_out.data_ptr(), w * h * 4 - 1)
+    # the chunk readers load 16-byte words, so a misaligned device copy is refused
+    d_odd = torch.zeros(len(data) + 17, dtype=torch.uint8, device=dev)
+    d_odd[1:1 + len(data)] = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
+    assert ctx.exr_decode_device(data, d_odd.data_ptr() + 1, d_out.data_ptr(), w * h * 4)[0] == icx.EXR_INVALID_ARGUMENT
 
 
 def test_exr_decode_device_batch_matches_single(ctx):

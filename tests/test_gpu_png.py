@@ -101,6 +101,17 @@ def test_png_large_rgba_and_size(ctx):
     assert len(png) <= 1.05 * len(ref), (len(png), len(ref))
 
 
+def test_png_block_plan_without_lds(ctx, monkeypatch):
+    """the deflate block grouping reads its counts from global memory when they do
+    not fit its LDS (more than 4 GiB of filtered bytes) instead of failing; forced here with
+    ICX_PNG_PLAN_LDS=0 on an image of several base blocks: the same file bytes."""
+    w = h = 1024
+    px = P.synth_rgba(7, w, h)
+    want = ctx.png_encode(w, h, 4, px.tobytes())
+    monkeypatch.setenv("ICX_PNG_PLAN_LDS", "0")
+    assert ctx.png_encode(w, h, 4, px.tobytes()) == want
+
+
 def test_png_device_api(ctx):
     import torch
     w, h = 640, 480
