@@ -1284,6 +1284,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         uint32_t ul = 0;  // exit: bits read and block-in-MCU there
         int bl = 0;
         int32_t left = Sst, nxt = sbase;  // slots left in the current run (static, then chunks), the next one
+        bool rec_on = true;  // some live lane of the wave still records MCU starts (wave-uniform)
         (void)kFar;
         // 2. store every block from g0 on
         if (wave_any(live)) do {
@@ -1297,17 +1298,21 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             asm volatile("" : "+v"(ul), "+v"(bl));
             live = live && !leave;
             const bool own_bs = live && bs;
-            if (wave_any(own_bs && b == 0 && nrec < kRecGw)) {  // MCU start: a splice point for the count lane
-                if (own_bs && b == 0 && nrec < kRecGw) {
-                    RecState e;
-                    e.rel = u - pre;
-                    e.b = 0;
-                    e.cnt = k;
-                    e.ds[0] = ds0;
-                    e.ds[1] = ds1;
-                    e.ds[2] = ds2;
-                    R[nrec] = e;
-                    ++nrec;
+            if (rec_on) {  // (wave-uniform: skipped once every lane has its kRecGw records)
+                const bool rc = own_bs && b == 0 && nrec < kRecGw;
+                if (wave_any(rc)) {  // MCU start: a splice point for the count lane
+                    if (rc) {
+                        RecState e;
+                        e.rel = u - pre;
+                        e.b = 0;
+                        e.cnt = k;
+                        e.ds[0] = ds0;
+                        e.ds[1] = ds1;
+                        e.ds[2] = ds2;
+                        R[nrec] = e;
+                        ++nrec;
+                    }
+                    rec_on = wave_any(live && nrec < kRecGw);
                 }
             }
             const bool need = own_bs && left == 0;
