@@ -147,6 +147,7 @@ __device__ __forceinline__ int dc_bits(const uint8_t (&dcl)[2][16], int c, int d
     const int nb = mag ? 32 - __clz(mag) : 0;
     return dcl[c ? 1 : 0][nb] + nb;
 }
+typedef float f2 __attribute__((ext_vector_type(2)));  // packed FP32 (v_pk_add_f32 / v_pk_mul_f32)
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -229,23 +230,32 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
                         rw[r][d] = (uint32_t)b[4 * d] | (uint32_t)b[4 * d + 1] << 8 | (uint32_t)b[4 * d + 2] << 16 | (uint32_t)b[4 * d + 3] << 24;
                 }
             }
+            // The thread's two quads (j = 0, 1; both inside the run: wpx is a multiple of 16 and qx
+            // even) as the two halves of packed-FP32 vectors: every colour expression below is the
+            // reference's, in its order, evaluated for both quads by one v_pk instruction.
             const uint8_t* B0 = reinterpret_cast<const uint8_t*>(rw[0]);
             const uint8_t* B1 = reinterpret_cast<const uint8_t*>(rw[1]);
+            auto ld = [](const uint8_t* p, int o) { return f2{(float)p[o], (float)p[6 + o]}; };
+            // pixel (dx, dy) of both quads: bytes 3 dx (+6 for quad 1) of row dy
+            f2 Yv[2][2], Cb[2][2], Cr[2][2];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if (2 * (qx + j) >= wpx) break;
-                const uint8_t *p00 = B0 + 6 * j, *p10 = B0 + 6 * j + 3, *p01 = B1 + 6 * j, *p11 = B1 + 6 * j + 3;
-                float* Y = S + 2 * qy * kRunPx + 2 * (qx + j);
-                Y[0] = ycc(p00, 0);
-                Y[1] = ycc(p10, 0);
-                Y[kRunPx] = ycc(p01, 0);
-                Y[kRunPx + 1] = ycc(p11, 0);
+            for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
-                for (int c = 1; c < 3; ++c) {
-                    const float a = ycc(p00, c), b = ycc(p10, c), cc = ycc(p01, c), d = ycc(p11, c);
-                    S[16 * kRunPx + (c - 1) * 8 * kHalf + qy * kHalf + qx + j] = ((a + b) + (cc + d)) * 0.25f;
+                for (int dx = 0; dx < 2; ++dx) {
+                    const uint8_t* p = (dy ? B1 : B0) + 3 * dx;
+                    const f2 r = ld(p, 0), g = ld(p, 1), b = ld(p, 2);
+                    Yv[dy][dx] = f2(0.299f) * r + f2(0.587f) * g + f2(0.114f) * b - f2(128.f);
+                    Cb[dy][dx] = f2(-0.1687f) * r - f2(0.3313f) * g + f2(0.5f) * b;
+                    Cr[dy][dx] = f2(0.5f) * r - f2(0.4187f) * g - f2(0.0813f) * b;
                 }
-            }
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)  // Y: pixels x .. x + 3 of the row, one 16-byte store
+                *reinterpret_cast<float4*>(S + (2 * qy + dy) * kRunPx + 2 * qx) =
+                    make_float4(Yv[dy][0].x, Yv[dy][1].x, Yv[dy][0].y, Yv[dy][1].y);
+            const f2 mb = ((Cb[0][0] + Cb[0][1]) + (Cb[1][0] + Cb[1][1])) * f2(0.25f);
+            const f2 mr = ((Cr[0][0] + Cr[0][1]) + (Cr[1][0] + Cr[1][1])) * f2(0.25f);
+            *reinterpret_cast<f2*>(S + 16 * kRunPx + qy * kHalf + qx) = mb;
+            *reinterpret_cast<f2*>(S + 16 * kRunPx + 8 * kHalf + qy * kHalf + qx) = mr;
         }
     } else if (L.sub) {  // 2x2 quads; chroma = ((a + b) + (c + d)) * 0.25f of the per-pixel values
         for (int qd = t; qd < kHalf * 8; qd += 256) {
