@@ -42,24 +42,29 @@ struct EncLayout {
     int8_t lastk[3];         // last unit of each component in an MCU
 };
 // AAN float FDCT on 8 samples at stride S (tjei_fdct, jpeg_enc.h:667-712), in registers.
-template <int S>
-__device__ __forceinline__ void fdct8(float* p) {
-    const float t0 = p[0] + p[7 * S], t7 = p[0] - p[7 * S];
-    const float t1 = p[S] + p[6 * S], t6 = p[S] - p[6 * S];
-    const float t2 = p[2 * S] + p[5 * S], t5 = p[2 * S] - p[5 * S];
-    const float t3 = p[3 * S] + p[4 * S], t4 = p[3 * S] - p[4 * S];
-    const float e10 = t0 + t3, e13 = t0 - t3, e11 = t1 + t2, e12 = t1 - t2;
+typedef float f2 __attribute__((ext_vector_type(2)));  // packed FP32 (v_pk_add_f32 / v_pk_mul_f32)
+
+// AAN float FDCT on 8 samples at stride S (tjei_fdct, jpeg_enc.h:667-712), in registers. T is
+// float, or a packed pair of floats (two independent transforms per v_pk instruction: the same
+// operations in the same order, each rounded as the reference rounds it).
+template <int S, class T>
+__device__ __forceinline__ void fdct8(T* p) {
+    const T t0 = p[0] + p[7 * S], t7 = p[0] - p[7 * S];
+    const T t1 = p[S] + p[6 * S], t6 = p[S] - p[6 * S];
+    const T t2 = p[2 * S] + p[5 * S], t5 = p[2 * S] - p[5 * S];
+    const T t3 = p[3 * S] + p[4 * S], t4 = p[3 * S] - p[4 * S];
+    const T e10 = t0 + t3, e13 = t0 - t3, e11 = t1 + t2, e12 = t1 - t2;
     p[0] = e10 + e11;
     p[4 * S] = e10 - e11;
-    const float z1 = (e12 + e13) * ((float)0.707106781);
+    const T z1 = (e12 + e13) * T((float)0.707106781);
     p[2 * S] = e13 + z1;
     p[6 * S] = e13 - z1;
-    const float o10 = t4 + t5, o11 = t5 + t6, o12 = t6 + t7;
-    const float z5 = (o10 - o12) * ((float)0.382683433);
-    const float z2 = ((float)0.541196100) * o10 + z5;
-    const float z4 = ((float)1.306562965) * o12 + z5;
-    const float z3 = o11 * ((float)0.707106781);
-    const float z11 = t7 + z3, z13 = t7 - z3;
+    const T o10 = t4 + t5, o11 = t5 + t6, o12 = t6 + t7;
+    const T z5 = (o10 - o12) * T((float)0.382683433);
+    const T z2 = T((float)0.541196100) * o10 + z5;
+    const T z4 = T((float)1.306562965) * o12 + z5;
+    const T z3 = o11 * T((float)0.707106781);
+    const T z11 = t7 + z3, z13 = t7 - z3;
     p[5 * S] = z13 + z2;
     p[3 * S] = z13 - z2;
     p[S] = z11 + z4;
@@ -147,7 +152,6 @@ __device__ __forceinline__ int dc_bits(const uint8_t (&dcl)[2][16], int c, int d
     const int nb = mag ? 32 - __clz(mag) : 0;
     return dcl[c ? 1 : 0][nb] + nb;
 }
-typedef float f2 __attribute__((ext_vector_type(2)));  // packed FP32 (v_pk_add_f32 / v_pk_mul_f32)
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -333,22 +337,41 @@ __global__ __launch_bounds__(256) void k_enc_run(EncBatch B, EncLayout L, const 
     }
     __syncthreads();  // every lane holds its samples: the code tables and AC codes take their LDS
     for (int i = t; i < 4 * 256; i += 256) U.E.tab[i >> 8][i & 255] = (uint32_t)T->code[i >> 8][i & 255] << 8 | T->len[i >> 8][i & 255];
+    // rows in pairs (P[8k + c] = rows 2k, 2k+1 of column c), then columns in pairs (Q[4r + m] =
+    // columns 2m, 2m+1 of row r): the reference's row pass, then its column pass
+    f2 P[32], Q[32];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) fdct8<1>(f + 8 * r);
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) fdct8<8>(f + q);
+        for (int cc = 0; cc < 8; ++cc) P[8 * k + cc] = f2{f[16 * k + cc], f[16 * k + 8 + cc]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fdct8<1>(P + 8 * k);
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const f2 a = P[8 * (r >> 1) + 2 * m], b = P[8 * (r >> 1) + 2 * m + 1];
+            Q[4 * r + m] = (r & 1) ? f2{a.y, b.y} : f2{a.x, b.x};
+        }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) fdct8<4>(Q + m);
     uint32_t cw[32];  // the quantised block, zig-zag order, two coefficients per word
     {
         const float* pqc = pq[c ? 1 : 0];
         int o[64];
 #pragma unroll
-        for (int i = 0; i < 64; ++i) {  // jpeg_enc.h:806-817
-            float v = f[i];
-            v *= pqc[i];
-            v = floorf(v + 1024 + 0.5f);
-            v -= 1024;
-            o[zig_of_nat(i)] = (int)v;
-        }
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {  // jpeg_enc.h:806-817, natural indices 8r + 2m, + 1
+                f2 v = Q[4 * r + m];
+                v = v * *reinterpret_cast<const f2*>(pqc + 8 * r + 2 * m);
+                v = v + f2(1024.f);
+                v = v + f2(0.5f);
+                v = f2{floorf(v.x), floorf(v.y)};
+                v = v - f2(1024.f);
+                o[zig_of_nat(8 * r + 2 * m)] = (int)v.x;
+                o[zig_of_nat(8 * r + 2 * m + 1)] = (int)v.y;
+            }
 #pragma unroll
         for (int q = 0; q < 32; ++q) cw[q] = ((uint32_t)o[2 * q] & 0xFFFFu) | ((uint32_t)o[2 * q + 1] << 16);
     }
