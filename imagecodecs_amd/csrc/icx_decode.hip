@@ -1320,7 +1320,7 @@ __global__ __launch_bounds__(256, ICX_CONV_MINW) void k_convert_stream(const Des
                                                         int fuse) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
-    if (d.status != kOk || stream_kind(d) != K || (K == 3 && (fuse == 1 || fuse == 3) && fused420(d))) return;
+    if (d.status != kOk || stream_kind(d) != K || (K == 3 && (fuse == 1 || fuse == 3 || fuse == 5) && fused420(d))) return;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     uint8_t* o = out + (int64_t)img * out_stride;
     const StreamOut so{o, d.W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (d.W & 3) == 0};
@@ -1599,9 +1599,10 @@ __device__ __forceinline__ void load_block8(const int16_t* ac, int64_t blk, int4
 #pragma unroll
     for (int k = 0; k < 8; ++k) c[k] = nt_ld(src + k);
 }
-// rowd[2r], rowd[2r+1] = the 8 pixels of row r
-__device__ __forceinline__ void block_idct(const int4 (&c)[8], const uint32_t (&qw)[16], const int32_t* dcv,
-                                           const BlkLoc& loc, uint32_t (&rowd)[16]) {
+// Dequant of one block into R (natural order, the absolute DC at R[0][0]) and the range of its
+// values (the fast-path test of block_transform).
+__device__ __forceinline__ void block_dequant(const int4 (&c)[8], const uint32_t (&qw)[16], const int32_t* dcv,
+                                              const BlkLoc& loc, int32_t (&R)[8][8], int32_t& hi, int32_t& lo) {
     auto qt = [&](int z) { return (int32_t)((qw[z >> 2] >> (8 * (z & 3))) & 0xFFu); };
     auto coef = [&](int z) {
         const int4& w = c[z >> 3];
@@ -1609,8 +1610,8 @@ __device__ __forceinline__ void block_idct(const int4 (&c)[8], const uint32_t (&
         const uint32_t d32 = (uint32_t)(e < 2 ? w.x : e < 4 ? w.y : e < 6 ? w.z : w.w);
         return (int32_t)(int16_t)(d32 >> (16 * (e & 1)));
     };
-    int32_t R[8][8];
-    int32_t hi = 0, lo = 0;
+    hi = 0;
+    lo = 0;
 #pragma unroll
     for (int n = 1; n < 64; ++n) {
         const int z = kZigOfNatC[n];
@@ -1621,6 +1622,9 @@ __device__ __forceinline__ void block_idct(const int4 (&c)[8], const uint32_t (&
     R[0][0] = wmul(blk_dc((int16_t)c[0].x, dcv, loc), qt(0));  // the absolute DC
     hi = max(hi, R[0][0]);
     lo = min(lo, R[0][0]);
+}
+// rowd[2r], rowd[2r+1] = the 8 pixels of row r
+__device__ __forceinline__ void block_transform(int32_t (&R)[8][8], int32_t hi, int32_t lo, uint32_t (&rowd)[16]) {
     if (hi < (1 << 14) && lo > -(1 << 14)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) idct_row_full(R[i]);
@@ -1653,6 +1657,12 @@ __device__ __forceinline__ void block_idct(const int4 (&c)[8], const uint32_t (&
             for (int r = 0; r < 8; ++r) rowd[2 * r + (j >> 2)] |= (uint32_t)ob[r] << (8 * (j & 3));
         }
     }
+}
+__device__ __forceinline__ void block_idct(const int4 (&c)[8], const uint32_t (&qw)[16], const int32_t* dcv,
+                                           const BlkLoc& loc, uint32_t (&rowd)[16]) {
+    int32_t R[8][8], hi, lo;
+    block_dequant(c, qw, dcv, loc, R, hi, lo);
+    block_transform(R, hi, lo, rowd);
 }
 // Units of one plane: `ucols` units of 64 blocks per block row, `nby` block rows; unit u's lane
 // takes block column bx = (u % ucols) * 64 + lane, clamped to the row (a lane past the row's end
@@ -1716,10 +1726,11 @@ __device__ __forceinline__ void plane_units(const Desc& d, const int16_t* ac, co
 #endif
 }
 // All three planes of fused420 images: gridDim.x workgroups per image walk the luma units, then
-// the Cb and Cr units (one grid-stride sequence over the three planes' units).
+// the Cb and Cr units (one grid-stride sequence over the three planes' units); with luma == 0 only
+// the chroma planes (mode 5: k_fused420s transforms the luma).
 __global__ __launch_bounds__(256, ICX_IDCT1_MINW) void k_idct420s(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                                                    const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
-                                                                   uint8_t* __restrict__ planes, int64_t plane_cap) {
+                                                                   uint8_t* __restrict__ planes, int64_t plane_cap, int luma) {
     const int img = blockIdx.y;
     const Desc& d = desc[img];
     if (!fused420(d)) return;
@@ -1729,7 +1740,7 @@ __global__ __launch_bounds__(256, ICX_IDCT1_MINW) void k_idct420s(const Desc* __
     const uint32_t mbw = (uint32_t)d.mbw, mbh = (uint32_t)d.mbh;
     uint8_t* const slot = planes + (int64_t)img * plane_cap;
     // luma: 2 x 2 blocks per MCU (k = 2 sby + sbx), block rows 2 mbh
-    const uint32_t ynbx = 2 * mbw, yunits = ((ynbx + 63) >> 6) * (2 * mbh);
+    const uint32_t ynbx = 2 * mbw, yunits = luma ? ((ynbx + 63) >> 6) * (2 * mbh) : 0u;  // (mode 5: chroma only)
     const uint32_t cnbx = mbw, cunits = ((cnbx + 63) >> 6) * mbh;
     // The three planes' units are one sequence (luma, Cb, Cr); a wave takes units wid, wid + nw, ...
     // of it, i.e. in a plane whose units start at `base` the local units first(base), + nw, ...
@@ -1829,6 +1840,133 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
                     so.put3(y, x0, w, nb);
                 };
                 kv_rows<true>(w, c1, c2, M, f1, f2, Y0, Y1, luma, emit);
+            }
+            asm volatile("" ::: "memory");
+        }
+    }
+}
+
+// Mode 5: the luma IDCT inside the conversion with the one-lane IDCT (k_idct420s transforms only
+// the chroma planes). A wave owns a strip of 16 MCUs (256 pixels) by kFB5 MCU rows; per MCU row
+// lane l transforms luma block l & 3 of MCU mx0 + (l >> 2) -- the row's 64 blocks, one per lane
+// -- into the wave's 16 x 256 luma rows in LDS, then converts those 16 rows as k_fused420 does
+// (kv_rows: the chroma window carried in registers from the MCU row above, chroma from the planes,
+// luma from LDS). The luma plane (16.8 MB per 4096^2 image, written and read back in mode 4) never
+// goes through HBM. The next MCU row's block is loaded before this row's conversion, its map entry
+// a row earlier. No workgroup barriers.
+#ifndef ICX_FB5
+#define ICX_FB5 4
+#endif
+#ifndef ICX_FUSED5_MINW  // 3: 152 VGPRs, no spills (4 spills; measured slower)
+#define ICX_FUSED5_MINW 3
+#endif
+// (timing variants: ICX_F5_CARRY=0 sets the chroma window up again per MCU row instead of carrying
+// it through the IDCT's registers; ICX_F5_PF=0 loads a row's block at the start of its IDCT)
+#ifndef ICX_F5_CARRY
+#define ICX_F5_CARRY 1
+#endif
+#ifndef ICX_F5_PF
+#define ICX_F5_PF 1
+#endif
+#ifndef ICX_F5_QR
+#define ICX_F5_QR 0  // 1: the dequant table reloaded per MCU row (fewer SGPR spills; measured no faster)
+#endif
+constexpr int kFB5 = ICX_FB5;
+__global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
+                                                   const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
+                                                   const uint8_t* __restrict__ planes, int64_t plane_cap,
+                                                   uint8_t* __restrict__ out, uint64_t out_stride) {
+    const int img = blockIdx.y;
+    const Desc& d = desc[img];
+    if (!fused420(d)) return;
+    __shared__ __attribute__((aligned(16))) uint32_t Yl_all[4][16][64];  // per wave: 16 luma rows x 256 pixels
+    const int wave = wave_index(), lane = threadIdx.x & 63, mq = lane >> 2, k = lane & 3, sbx = k & 1, sby = k >> 1;
+    uint32_t (*Yl)[64] = Yl_all[wave];
+    const uint8_t* qp = d.q[d.c[0].tq];
+    const int W = d.W, H = d.H, mbw = d.mbw, mbh = d.mbh;
+    const uint8_t* pslot = planes + (int64_t)img * plane_cap;
+    const CPl c1{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
+    const CPl c2{pslot + comp_plane_off(d, 2), d.c[2].w, d.c[2].h, d.c[2].stride};
+    uint8_t* o = out + (int64_t)img * out_stride;
+    const StreamOut so{o, W, ((reinterpret_cast<uintptr_t>(o) & 3) == 0) && (W & 3) == 0};
+    const int nsx = (mbw + 15) >> 4, nsy = (mbh + kFB5 - 1) / kFB5, nstrip = nsx * nsy;
+    // Border lanes (lane 0 and from edge_from on, as in k_convert_stream) are k_convert_edge's: for
+    // their 4 columns this kernel writes the luma plane, which k_convert_edge reads; every other
+    // lane converts with the interior taps (compile-time: the generic taps stay out of this kernel).
+    uint8_t* const P0 = const_cast<uint8_t*>(pslot);
+    const int s0 = d.c[0].stride;
+    const int ef = edge_from(c1, c2, W);
+    const bool conv = ef > 1;  // (wave-uniform: else every lane is a border lane)
+    const uint32_t chunk0 = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    for (int strip = chunk0 * 4 + wave; strip < nstrip; strip += gridDim.x * 4) {  // wave-uniform
+        const int sy = strip / nsx, sx = strip - sy * nsx;
+        const int mx0 = sx << 4, mb0 = sy * kFB5, mb1 = min(mbh, mb0 + kFB5);
+        const int M = 64 * sx + lane, x0 = 4 * M;
+        const bool live = M >= 1 && M < ef;
+        const bool border = x0 < W && !live;
+        const int Mc = min(max(M, 1), max(ef - 1, 1));
+        const int nb = live ? min(4, W - x0) * 3 : 0;
+        // block of MCU row mby (a lane past the row's last MCU takes that MCU's block again: a
+        // harmless reload, so every load is unconditional)
+        const int mxl = min(mx0 + mq, mbw - 1);
+        auto nblk = [&](int mby) { return ((int64_t)min(mby, mb1 - 1) * mbw + mxl) * 6 + k; };
+        BlkPend p = blk_pend(d, map, nblk(mb0));
+#if ICX_F5_CARRY
+        KvWin w;
+        if (conv) kv_init<true>(w, c1, c2, Mc, true, true, 8 * mb0);
+#endif
+#if ICX_F5_PF  // the next MCU row's block loaded before this row's conversion
+        BlkLoc l = blk_resolve(d, p);
+        int4 c[8];
+        load_block8(ac, l.blk, c);
+        p = blk_pend(d, map, nblk(mb0 + 1));
+#endif
+        for (int mby = mb0; mby < mb1; ++mby) {
+            {
+#if !ICX_F5_PF
+                const BlkLoc l = blk_resolve(d, p);
+                int4 c[8];
+                load_block8(ac, l.blk, c);
+                p = blk_pend(d, map, nblk(mby + 1));
+#endif
+                // the dequant table (16 scalar registers) is loaded again per MCU row, so it does not
+                // hold SGPRs through the conversion (whose row bases spilled into VGPR lanes)
+#if ICX_F5_QR
+                asm volatile("" : "+s"(qp));
+#endif
+                uint32_t qw[16];
+                load_qw_g(qp, qw);
+                uint32_t rowd[16];
+                block_idct(c, qw, dcv, l, rowd);
+                uint2* dst = reinterpret_cast<uint2*>(&Yl[sby * 8][mq * 4 + sbx * 2]);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) dst[r * 32] = make_uint2(rowd[2 * r], rowd[2 * r + 1]);
+            }
+#if ICX_F5_PF
+            l = blk_resolve(d, p);
+            load_block8(ac, l.blk, c);
+            p = blk_pend(d, map, nblk(mby + 2));
+#endif
+            asm volatile("" ::: "memory");  // (a wave's LDS accesses execute in order)
+            const int Y0 = 16 * mby, Y1 = min(H, Y0 + 16);
+            if (border) {  // (rare: border strips only)
+                for (int y = Y0; y < Y1; ++y)
+                    *reinterpret_cast<uint32_t*>(P0 + (int64_t)y * s0 + x0) = Yl[y - Y0][lane];
+            }
+            if (conv) {
+                auto luma = [&](int y) { return Yl[y - Y0][lane]; };
+                auto emit = [&](int y, uint32_t yv, uint32_t cb, uint32_t cr) {
+                    uint32_t wo[3];
+                    ycc4_to_rgb(yv, cb, cr, wo);
+                    so.put3(y, 4 * Mc, wo, nb);
+                };
+#if !ICX_F5_CARRY
+                // the chroma window is set up again per MCU row (its rows were just read by this
+                // wave, so mostly from L2) rather than carried through the IDCT's registers
+                KvWin w;
+                kv_init<true>(w, c1, c2, Mc, true, true, Y0 >> 1);
+#endif
+                kv_rows<true>(w, c1, c2, Mc, true, true, Y0, Y1, luma, emit);
             }
             asm volatile("" ::: "memory");
         }
@@ -2103,17 +2241,18 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     static const int gwg = std::getenv("ICX_GENERIC_WG") ? std::max(8, std::atoi(std::getenv("ICX_GENERIC_WG"))) : kGenericWG;
     int gx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk + 32 * kIdctU - 1) / (32 * kIdctU), gwg / n));
     if (gx >= 8) gx &= ~7;  // XCD-aware chunk order in k_idct needs a multiple of 8
-    // 4:2:0 images (fused420): mode 2 (default) transforms their planes with the lane-pair IDCT,
-    // k_idct420y / k_idct420c, whose stores are whole 128-byte plane rows (k_idct skips them);
-    // mode 1 takes k_idct420c + k_fused420 (the luma IDCT inside the conversion; bit-exact, but
-    // slower beside the second pipeline: DESIGN.md §4); mode 0 leaves them to k_idct. ICX_FUSE420
-    // overrides the mode (tests, experiments).
-    // (any value other than 0, 1, 2 is the default: an unknown mode would leave 4:2:0 luma untransformed)
-    // Mode 4 (default): all three planes by the one-lane-per-block IDCT k_idct420s, then the
-    // stream conversion as in mode 2.
+    // 4:2:0 images (fused420), by plane mode (ICX_FUSE420 overrides it: tests, experiments; any
+    // other value is the default, since an unknown mode would leave 4:2:0 luma untransformed):
+    //   5 (default) k_idct420s transforms the chroma planes, k_fused420s the luma blocks inside
+    //     the conversion (no luma plane in HBM); k_convert_edge takes the border lanes
+    //   4 k_idct420s (one lane per block) for all three planes, then the stream conversion
+    //   3 k_back420, the whole back half without planes
+    //   2 the lane-pair IDCT k_idct420y / k_idct420c, then the stream conversion
+    //   1 k_idct420c + k_fused420 (round 2's luma IDCT inside the conversion, lane pairs)
+    //   0 the generic k_idct
     const int fuse = [] {  // (read per launch: tests switch modes within one process)
-        const int v = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 4;
-        return (v >= 0 && v <= 4) ? v : 4;
+        const int v = std::getenv("ICX_FUSE420") ? std::atoi(std::getenv("ICX_FUSE420")) : 5;
+        return (v >= 0 && v <= 5) ? v : 5;
     }();
     if (other || fuse == 0) {
         hipLaunchKernelGGL(k_idct, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes, ws.plane_cap,
@@ -2121,11 +2260,11 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
         hipLaunchKernelGGL(k_idct_any, dim3(gx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap);
     }
-    if (fuse == 4) {  // 4:2:0: 64 blocks of a block row per wave unit, luma then chroma units
-        const int64_t units = (maxblk / 6) * 6 / 64 + 3;
+    if (fuse == 4 || fuse == 5) {  // 4:2:0: 64 blocks of a block row per wave unit, luma (mode 4) then chroma units
+        const int64_t units = (maxblk / 6) * (fuse == 4 ? 6 : 2) / 64 + 3;
         const int sgx = (int)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 16384 / n)) & ~7;
         hipLaunchKernelGGL(k_idct420s, dim3(std::max(sgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map,
-                           ws.planes, ws.plane_cap);
+                           ws.planes, ws.plane_cap, fuse == 4 ? 1 : 0);
     }
     if (fuse == 1 || fuse == 2) {  // 4:2:0: chroma planes (and, mode 2, luma planes) by the lane-pair IDCT
         const int cgx = (int)std::max<int64_t>(1, std::min<int64_t>((maxblk / 6 / 16 + 31) / 32, 16384 / n)) & ~7;
@@ -2165,6 +2304,13 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
     if (fuse == 1)
         hipLaunchKernelGGL(k_fused420, dim3(fgx, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap, d_out, out_stride);
+    if (fuse == 5) {
+        const int64_t fs = ((int64_t)(ws.max_w + 255) / 256) * ((ws.max_h + 16 * kFB5 - 1) / (16 * kFB5));
+        int f5 = (int)std::max<int64_t>(1, std::min<int64_t>((fs + 3) / 4, 16384 / n));
+        if (f5 >= 8) f5 &= ~7;  // (XCD-aware strip order needs a multiple of 8)
+        hipLaunchKernelGGL(k_fused420s, dim3(f5, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
+                           ws.plane_cap, d_out, out_stride);
+    }
     if (other) {
         hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                            out_stride, fuse);

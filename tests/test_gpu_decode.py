@@ -302,13 +302,15 @@ def test_corrupt_dri_images_cost_no_sequential_time(ctx):
     b.close()
 
 
-@pytest.mark.parametrize("mode,seg", [("0", None), ("1", None), ("2", None), ("3", None), ("3", "1"), ("3", "3"), ("4", None)])
+@pytest.mark.parametrize("mode,seg", [("0", None), ("1", None), ("2", None), ("3", None), ("3", "1"), ("3", "3"), ("4", None), ("5", None)])
 def test_420_plane_modes_bit_exact(ctx, monkeypatch, mode, seg):
     """Every 4:2:0 plane mode -- 0: k_idct, 1: k_idct420c + k_fused420 (luma IDCT inside the
     conversion), 2: k_idct420y + k_idct420c, 3: k_back420 (the whole back half, no planes; with
-    1- and 3-MCU-row segments too, so most rows sit next to a segment edge), 4 (default): k_idct420s
-    (one lane per block, all three planes) -- decodes every golden and odd-sized synthetic 4:2:0
-    images exactly as the oracle."""
+    1- and 3-MCU-row segments too, so most rows sit next to a segment edge), 4: k_idct420s (one lane
+    per block, all three planes), 5 (default): k_idct420s for the chroma planes + k_fused420s (the
+    one-lane luma IDCT inside the conversion, border lanes through the luma plane and
+    k_convert_edge) -- decodes every golden and odd-sized synthetic 4:2:0 images exactly as the
+    oracle."""
     monkeypatch.setenv("ICX_FUSE420", mode)
     if seg is not None:
         monkeypatch.setenv("ICX_BSEG", seg)

@@ -59,7 +59,7 @@ def _batch_check(ctx, names, max_w, max_h):
 
 
 @pytest.mark.parametrize("gw", ["1", "0", None])
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5"])
 def test_foreign_batch_all_plane_modes(ctx, monkeypatch, mode, gw):
     """All foreign + crafted streams in one batch, under each 4:2:0 plane mode (the lane-pair IDCT
     of modes 1 and 2 meets the large-coefficient streams) and each entropy path (ICX_GW 1:
@@ -81,7 +81,7 @@ def test_crafted_big_coefficients_each_mode(ctx, monkeypatch):
     2^14 gate; its 181 products need 32 bits."""
     name = "crafted/bigac_420_zz1_q250.jpg"
     data = open(os.path.join(GOLDEN, name), "rb").read()
-    for mode in ("4", "3", "2", "1", "0"):
+    for mode in ("5", "4", "3", "2", "1", "0"):
         monkeypatch.setenv("ICX_FUSE420", mode)
         b = icx.Batch(ctx, 1, 64, 64)
         code, w, h, c, pix = b.decode_host([data])[0]
@@ -89,7 +89,7 @@ def test_crafted_big_coefficients_each_mode(ctx, monkeypatch):
         b.close()
 
 
-@pytest.mark.parametrize("mode", [None, "2", "3", "4"])
+@pytest.mark.parametrize("mode", [None, "2", "3", "4", "5"])
 def test_foreign_large_regenerated(ctx, monkeypatch, mode):
     """The large regenerated inputs (tools/foreign.LARGE): a 4096^2 q90 4:2:0 optimised-table
     photo-like image, 4:4:4 q100 at 1.3 B/px (more than one workspace slot of U: the pool),

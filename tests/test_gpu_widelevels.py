@@ -69,7 +69,7 @@ def test_wide_levels_bit_exact(ctx, sampling, w, h, cap, restart):
     b.close()
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5"])
 def test_wide_levels_420_modes(ctx, monkeypatch, mode):
     """4:2:0 back halves: generic (0), fused luma (1), lane-pair IDCT + stream convert (2),
     k_back420 (3)."""
