@@ -63,13 +63,21 @@ __global__ __launch_bounds__(64) void k_parse(int n, const uint8_t* __restrict__
 // the image's four Huffman tables in LDS and the stream's next bytes in an LDS ring, refilled a KiB
 // at a time by all 64 lanes with 16-byte loads, so the serial walk runs at LDS latency instead of
 // a dependent global load per byte and per table lookup.
+// ICX_SEQ_LDS=0 (default): the tables and the stream are read from global memory (L1/L2) instead.
+// The LDS form walks ~10% faster, but a kernel holding ~14 KB of LDS per workgroup cannot be
+// dispatched while the other pipeline's entropy kernels fill every CU's LDS, and it sits in the
+// stream before the back half even when it has nothing to do (every group, every call): at C2 it
+// waited ~0.16 ms per group for LDS it then did not use.
+#ifndef ICX_SEQ_LDS
+#define ICX_SEQ_LDS 0
+#endif
 constexpr int kSeqRing = 4096;  // 4 quarters of 1 KiB; lane 0 always has >= 2 KiB loaded ahead
 struct RingBits {                // rb_fill's byte rules (icx_jpeg.h) over the ring
     const uint8_t* ring;
     int64_t pos, end;            // next byte, stream end (relative to the aligned ring origin)
     uint32_t acc;
     int32_t nacc, err;
-    __device__ uint32_t byte() { return ring[(pos++) & (kSeqRing - 1)]; }
+    __device__ uint32_t byte() { return ring[(pos++) & (ICX_SEQ_LDS ? kSeqRing - 1 : ~(int64_t)0)]; }
     __device__ void fill(int want) {
         while (nacc < want) {
             if (pos >= end) { acc = (acc << 8) | 0xFFu; nacc += 8; continue; }
@@ -101,9 +109,18 @@ __global__ __launch_bounds__(64) void k_entropy_seq(int n, const uint8_t* __rest
     if (i >= n) return;
     Desc& d = desc[i];
     if (d.status != kPending) return;  // (uniform)
+    const int lane = threadIdx.x;
+    const uint8_t* S = data + off[i] + d.scan_off;
+    const int mis = (int)(reinterpret_cast<uintptr_t>(S) & 15);
+    const uint8_t* S0 = S - mis;
+    const int64_t end = (int64_t)(d.size - d.scan_off) + mis;
+#if !ICX_SEQ_LDS
+    const Huff* HT = d.huff;
+    RingBits b{S0, mis, end, 0u, 0, 0};  // (fill never reads at or past `end`)
+    auto refill = [&](int64_t) {};
+#else
     __shared__ Huff HT[4];
     __shared__ uint4 ring4[kSeqRing / 16];
-    const int lane = threadIdx.x;
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(d.huff);
         uint32_t* dst = reinterpret_cast<uint32_t*>(HT);
@@ -111,10 +128,6 @@ __global__ __launch_bounds__(64) void k_entropy_seq(int n, const uint8_t* __rest
     }
     // the ring holds the stream from a 16-byte aligned origin: quarter q of the ring = stream KiB qi
     // with qi % 4 == q; quarters qlo .. qlo+3 are loaded
-    const uint8_t* S = data + off[i] + d.scan_off;
-    const int mis = (int)(reinterpret_cast<uintptr_t>(S) & 15);
-    const uint8_t* S0 = S - mis;
-    const int64_t end = (int64_t)(d.size - d.scan_off) + mis;
     auto fill_quarter = [&](int64_t qi) {  // all lanes (bytes past the end read as FF, never used)
         const int64_t at = qi * 1024 + lane * 16;
         uint4 v = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -131,6 +144,13 @@ __global__ __launch_bounds__(64) void k_entropy_seq(int n, const uint8_t* __rest
     for (int q = 0; q < 4; ++q) fill_quarter(q);
     __syncthreads();
     RingBits b{reinterpret_cast<const uint8_t*>(ring4), mis, end, 0u, 0, 0};
+    auto refill = [&](int64_t pos) {
+        while (pos >= (qlo + 2) * 1024) {
+            fill_quarter(qlo + 4);
+            ++qlo;
+        }
+    };
+#endif
     int16_t* A = ac + d.acbase * 64;  // (in place: the pool region k_spec_plan gave the image)
     int32_t* D = dcv + d.acbase;
     int32_t pred[3] = {0, 0, 0};
@@ -143,10 +163,7 @@ __global__ __launch_bounds__(64) void k_entropy_seq(int n, const uint8_t* __rest
             // wave-uniform: keep >= 2 KiB loaded past lane 0's position (a block reads < 600 bytes)
             const int64_t pos = __builtin_amdgcn_readfirstlane((int)b.pos) |
                                 ((int64_t)__builtin_amdgcn_readfirstlane((int)(b.pos >> 32)) << 32);
-            while (pos >= (qlo + 2) * 1024) {
-                fill_quarter(qlo + 4);
-                ++qlo;
-            }
+            refill(pos);
             __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses stay in order)
             if (lane == 0) {
                 int sbx, sby;
