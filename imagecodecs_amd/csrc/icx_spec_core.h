@@ -80,13 +80,53 @@ ICX_HD Ustf16 ustf16(const uint8_t* R, int64_t L, int64_t a, const uint32_t (&D)
     o.end_at = -1;
     o.end_err = 0;
     const bool prev_ff = prun > 0;
-    if (a >= 0 && a + 16 <= L && !prev_ff && !has_ff(D)) {  // the common case: 16 bytes kept unchanged
-        o.kept = 16;
-        if (WRITE) {
+    if (a >= 0 && a + 16 < L && prun <= 1) {
+        // The common case, stuffing only: every FF of the chunk is followed by 00 (byte 15's by the
+        // next chunk's byte 0), and a single FF before the chunk by byte 0 = 00. Then each FF drops
+        // the byte after it (the chunk's own bytes: FFs at 0..14; byte 0 for the FF before it), and
+        // nothing ends the data. Per dword: FF bytes by a carry-free add, the byte after each by a
+        // funnel shift, one AND-OR against the FF bytes' masks, one bit count -- no byte-position
+        // masks unless bytes are dropped and written (ustf16's mask tier below computed 00 and FF
+        // position masks for every chunk).
+        uint32_t bad = prun ? (D[0] & 0xFFu) : 0u, nff = 0u, f[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) o.out[k] = D[k];
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w = D[k];
+            f[k] = ((w & 0x7F7F7F7Fu) + 0x01010101u) & w & 0x80808080u;  // bit 7 of each FF byte
+            const uint32_t nw = k < 3 ? D[k + 1] : (uint32_t)nx;
+            const uint32_t after = (uint32_t)((((uint64_t)nw << 32) | w) >> 8);  // byte i: the byte after byte i
+            bad |= after & ((f[k] << 1) - (f[k] >> 7));                          // FF bytes' masks
+            nff += (uint32_t)__builtin_popcount(k < 3 ? f[k] : f[k] & 0x7FFFFFFFu);
         }
-        return o;
+        if (bad == 0u) {
+            o.kept = 16 - (int)nff - prun;
+            if (WRITE) {
+                uint64_t q0 = (uint64_t)D[0] | ((uint64_t)D[1] << 32), q1 = (uint64_t)D[2] | ((uint64_t)D[3] << 32);
+                if (nff | (uint32_t)prun) {
+                    uint32_t ffm = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        ffm |= (((f[k] >> 7) & 1u) | ((f[k] >> 14) & 2u) | ((f[k] >> 21) & 4u) | ((f[k] >> 28) & 8u)) << (4 * k);
+                    for (uint32_t m = ((ffm << 1) | (uint32_t)prun) & 0xFFFFu; m;) {  // highest dropped byte first
+                        const int p = 31 - __builtin_clz(m);
+                        m &= ~(1u << p);
+                        const int b = 8 * (p & 7);
+                        const uint64_t keep = b ? (1ull << b) - 1ull : 0ull;  // bytes below p
+                        if (p >= 8) {
+                            q1 = (q1 & keep) | ((q1 >> 8) & ~keep);
+                        } else {
+                            q0 = (q0 & keep) | ((q0 >> 8) & ~keep) | (q1 << 56);
+                            q1 >>= 8;
+                        }
+                    }
+                }
+                o.out[0] = (uint32_t)q0;
+                o.out[1] = (uint32_t)(q0 >> 32);
+                o.out[2] = (uint32_t)q1;
+                o.out[3] = (uint32_t)(q1 >> 32);
+            }
+            return o;
+        }
     }
     // byte 0 is the marker byte of an FF before the chunk (an odd FF run ends at a-1)
     const bool carry = prev_ff && (prun < 4 ? (prun & 1) != 0 : carry_after_ff(R, a, giveup));
