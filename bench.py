@@ -33,7 +33,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # stage (icx_batch_stage_times) -> the kernel it times
-STAGE_KERNEL = {"write": "k_gw_lane", "idct": "k_idct420y+k_idct420c", "convert": "k_convert_stream",
+STAGE_KERNEL = {"write": "k_gw_lane", "idct": "k_idct420s (4:2:0 chroma planes; plane mode 5)",
+                "convert": "k_fused420s (4:2:0 luma IDCT + conversion)+k_convert_stream+k_convert_edge",
                 "unstuff": "k_ustf_count+k_ustf_scan+k_ustf_write",
                 "entropy": "k_gw_check+k_gw_count+k_gw_repair+k_gw_scan+k_gw_map",
                 "parse": "k_parse", "upsample": "k_upsample"}
