@@ -268,6 +268,14 @@ def _stuffing_corpus():
             body += pieces[int(rng.integers(0, len(pieces)))]
         tail = [b"\xff\xd9", b"\xff\xc4", b"\xff", b""][k % 4]
         files.append(head + bytes(body) + tail)
+    # dense stuffing (several FF 00 pairs per 16-byte chunk, FFs at every chunk offset including
+    # the last, whose 00 is the next chunk's first byte): ustf16's stuffing-only tier
+    for k in range(8):
+        body = bytearray()
+        while len(body) < 9000:
+            body += bytes(rng.integers(0, 255, int(rng.integers(0, 7)), dtype=np.uint8))
+            body += b"\xff\x00" if rng.random() < 0.97 else pieces[int(rng.integers(1, len(pieces)))]
+        files.append(head + bytes(body) + [b"\xff\xd9", b""][k % 2])
     return files
 
 
@@ -286,7 +294,7 @@ def test_emulated_unstuff_every_alignment():
             u, e, rst, _ = emu_unstuff(data, sh)
             assert (u, e, rst) == ref, sh
         checked += 1
-    assert checked >= 140
+    assert checked >= 148
 
 
 FOREIGN = json.load(open(os.path.join(GOLDEN, "foreign_manifest.json")))
