@@ -75,6 +75,7 @@ _SIGS = {
     "icx_jpeg_batch_decode_host": (_i32, [_vp, _i32, _vp, _vp, _vp, _u64, _vp, _vp]),
     "icx_batch_stage_times": (_i32, [_vp, _vp, _vp, _i32]),
     "icx_batch_group": (_i32, [_vp]),
+    "icx_batch_groups": (_i32, [_vp, _i32]),
     "icx_batch_path_stats": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "icx_tje_encode_with_func": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "icx_tje_encode_to_file_at_quality": (_i32, [_vp, C.c_char_p, _i32, _i32, _i32, _i32, _vp]),
@@ -580,8 +581,8 @@ class Batch:
         return int(lib().icx_batch_group(self._p))
 
     def groups_per_call(self, n: int) -> int:
-        g = max(1, self.group)
-        return (n + g - 1) // g
+        """Groups a call of n images takes (icx_batch_groups): each per-group kernel launches once per group."""
+        return int(lib().icx_batch_groups(self._p, n))
 
     def stage_times(self) -> dict:
         names = (C.c_char_p * 16)()

@@ -194,7 +194,8 @@ static int64_t ws_per_slot(GroupWs& ws, int max_w, int max_h) {
     const int64_t tiles_per_slot = ws.ucap / kTileBytes + 2;
     const int64_t lanes_per_slot = ((ws.ucap + kSubBytesSmall - 1) / kSubBytesSmall + kLanes - 1) / kLanes * kLanes + kLanes;
     // coefficient pool: kPoolPerSlot x coef_cap blocks per slot (int16 block + int32 DC escape + map entry)
-    return ws.coef_cap * kPoolPerSlotX4 / 4 * (64 * 2 + 4 + 8) + ws.plane_cap + 6 * ws.tmp_cap + (int64_t)sizeof(Desc) + ws.ucap +
+    // (the generic upsample's ping-pong planes, 6 x tmp_cap, live in the coefficient pool: ws_alloc_all)
+    return ws.coef_cap * kPoolPerSlotX4 / 4 * (64 * 2 + 4 + 8) + ws.plane_cap + (int64_t)sizeof(Desc) + ws.ucap +
            (int64_t)sizeof(StepSet) +
            tiles_per_slot * 28 + ws.rst_cap * 8 +
            lanes_per_slot * (8 + 8 + 20 + 24 + 4 + 16 + (int64_t)sizeof(RecState) * kRec + (int64_t)sizeof(GwOut) +
@@ -202,7 +203,8 @@ static int64_t ws_per_slot(GroupWs& ws, int max_w, int max_h) {
 }
 
 static void ws_free(GroupWs& ws) {
-    for (void* p : {(void*)ws.desc, (void*)ws.ac, (void*)ws.dc, (void*)ws.planes, (void*)ws.tmp, (void*)ws.spec,
+    if (ws.tmp_own && ws.tmp) (void)hipFree(ws.tmp);
+    for (void* p : {(void*)ws.desc, (void*)ws.ac, (void*)ws.dc, (void*)ws.planes, (void*)ws.spec,
                     (void*)ws.tilepre, (void*)ws.wgpre, (void*)ws.wg2pre, (void*)ws.totals, (void*)ws.tiles,
                     (void*)ws.tile_obase, (void*)ws.U, (void*)ws.X, (void*)ws.sub, (void*)ws.rst, (void*)ws.tile_rbase,
                     (void*)ws.ent, (void*)ws.stats, (void*)ws.Y, (void*)ws.rec, (void*)ws.nrec, (void*)ws.guess_cnt,
@@ -246,7 +248,17 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ICX_HIP(ctx, hipMalloc(&ws.chunk_next, (size_t)(ws.pool_cap / kGwChunk + 2) * 4), false);
     ICX_HIP(ctx, hipMalloc(&ws.pool_next, sizeof(unsigned long long)), false);
     ICX_HIP(ctx, hipMalloc(&ws.planes, (size_t)ws.plane_cap * group), false);
-    ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), false);
+    // The generic upsample's ping-pong planes (exotic samplings only: k_upsample, k_convert) share
+    // the coefficient pool's memory: launch_decode_back runs them after every kernel that reads the
+    // group's coefficients (the pool holds >= 15 x the slot's MCU-padded pixels in bytes, the planes
+    // 6 x (w + 8)(h + 8) <= 7.6 x), and the next group on this workspace writes the pool only after
+    // that, in stream order. (A separate buffer only if the pool were ever too small.)
+    if ((int64_t)(ws.pool_cap + kGwChunk) * 64 * 2 >= ws.tmp_cap * 6 * group) {
+        ws.tmp = reinterpret_cast<uint8_t*>(ws.ac);
+    } else {
+        ICX_HIP(ctx, hipMalloc(&ws.tmp, (size_t)ws.tmp_cap * 6 * group), false);
+        ws.tmp_own = true;
+    }
     ws.tiles_cap = tiles_per_slot * (group + 2);
     ws.lanes_cap = lanes_per_slot * (group + 2);
     ICX_HIP(ctx, hipMalloc(&ws.spec, sizeof(SpecImg) * group), false);
@@ -298,10 +310,13 @@ icx_batch* icx_batch_create(icx_ctx* ctx, int max_images, int max_w, int max_h, 
     if (max_images < 2) pipes = 1;
     GroupWs probe;
     const int64_t per_slot = ws_per_slot(probe, max_w, max_h);
-    if (group <= 0) {  // auto: up to 60% of the free HBM (288 GB per MI355X), at least one image
+    if (group <= 0) {  // auto: up to 80% of the free HBM (288 GB per MI355X), at least one image
+        // (C3's 512 images per GPU fit one group per pipeline at ~395 MB per 4096^2 slot: 2 groups
+        // of 256 instead of 4 of 128, C3 +3%, C3 with restart markers +12%: its interval lanes take
+        // as long for 256 images as for 128)
         size_t free_b = 0, total_b = 0;
         ICX_HIP(ctx, hipMemGetInfo(&free_b, &total_b), nullptr);
-        const int64_t budget = (int64_t)(0.6 * (double)free_b);
+        const int64_t budget = (int64_t)(0.8 * (double)free_b);
         group = (int)std::max<int64_t>(1, std::min<int64_t>(max_images, budget / per_slot));
     }
     group = std::min(group, max_images);
@@ -337,6 +352,21 @@ void icx_batch_destroy(icx_batch* b) {
     delete b;
 }
 
+// Groups a call of n images is cut into (equal-sized, see icx_jpeg_batch_decode): enough for the
+// slots, at least ICX_GROUPS, and a multiple of the pipelines when that still fits (3 groups on 2
+// pipes run the third alone; 4 smaller ones keep both busy).
+static int batch_ngroups(const icx_batch* b, int n) {
+    const int slots = b->ws[0].slots;
+    int ngroups = std::min(n, std::max((n + slots - 1) / slots, b->min_groups));
+    if (b->pipes > 1 && ngroups > 1 && ngroups % b->pipes) {
+        const int up = (ngroups + b->pipes - 1) / b->pipes * b->pipes;
+        if (up <= n) ngroups = up;
+    }
+    return ngroups;
+}
+
+int icx_batch_groups(const icx_batch* b, int n) { return b && n > 0 ? batch_ngroups(b, n) : 0; }
+
 int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_size,
                           uint8_t* d_out, uint64_t out_stride, int32_t* d_status, int32_t* d_dims, void* stream) {
     if (!b) return ICX_INTERNAL_ERR;
@@ -352,8 +382,7 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
         ICX_HIP(ctx, hipMemsetAsync(b->ws[p].stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
     // equal-sized groups (512 images on 361 slots -> 256 + 256, not 361 + 151): every kernel's
     // grid is sized by the work of its group, so a small tail group leaves the GPU half idle
-    const int slots = b->ws[0].slots;
-    const int ngroups = std::min(n, std::max((n + slots - 1) / slots, b->min_groups));
+    const int ngroups = batch_ngroups(b, n);
     const int per = (n + ngroups - 1) / ngroups;
     const int used = std::min(b->pipes, (n + per - 1) / per);
     if (used > 1) {  // the other pipes start after the caller's prior work on `st`

@@ -2294,19 +2294,10 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
         }
     }
     E(kStIdct);
-    B(kStUpsample);
-    const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, gwg / (3 * n)));
-    for (int p = 0; p < 6 && other; ++p)
-        hipLaunchKernelGGL(k_upsample, dim3(ux, n * 3), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
-                           ws.tmp_cap, p);
-    E(kStUpsample);
+    // The kernels that read the coefficients inside the conversion (4:2:0 plane modes 1, 3, 5) run
+    // before the generic upsample: its ping-pong planes (ws.tmp) live in the coefficient pool
+    // (icx_api.cpp ws_alloc_all), which is dead from here on.
     B(kStConvert);
-    const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, gwg / n));
-    const int64_t sxw = ((int64_t)(ws.max_w + 255) / 256) * ((ws.max_h + kSH - 1) / kSH) / 4 + 1;
-    const int sxg = (int)std::max<int64_t>(1, std::min<int64_t>(sxw, 16384 / n));
-    const int sxo = (int)std::max<int64_t>(1, std::min<int64_t>(sxw, gwg / n));  // the other layouts
-    hipLaunchKernelGGL(k_convert_stream<3>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
-                       out_stride, fuse);
     const int fgx = (int)std::max<int64_t>(1, std::min<int64_t>((((int64_t)(ws.max_w + 255) / 256) *
                                                                   ((ws.max_h + 16 * kFB - 1) / (16 * kFB)) + 3) / 4,
                                                                  16384 / n));
@@ -2328,6 +2319,20 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
         hipLaunchKernelGGL(k_fused420s, dim3(f5, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap, d_out, out_stride);
     }
+    E(kStConvert);
+    B(kStUpsample);
+    const int ux = (int)std::max<int64_t>(1, std::min<int64_t>((ws.tmp_cap + 255) / 256, gwg / (3 * n)));
+    for (int p = 0; p < 6 && other; ++p)
+        hipLaunchKernelGGL(k_upsample, dim3(ux, n * 3), dim3(256), 0, st, ws.desc, ws.planes, ws.tmp, ws.plane_cap,
+                           ws.tmp_cap, p);
+    E(kStUpsample);
+    B(kStConvert);
+    const int cx = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)ws.max_w * ws.max_h + 255) / 256, gwg / n));
+    const int64_t sxw = ((int64_t)(ws.max_w + 255) / 256) * ((ws.max_h + kSH - 1) / kSH) / 4 + 1;
+    const int sxg = (int)std::max<int64_t>(1, std::min<int64_t>(sxw, 16384 / n));
+    const int sxo = (int)std::max<int64_t>(1, std::min<int64_t>(sxw, gwg / n));  // the other layouts
+    hipLaunchKernelGGL(k_convert_stream<3>, dim3(sxg, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
+                       out_stride, fuse);
     if (other) {
         hipLaunchKernelGGL(k_convert_stream<0>, dim3(sxo, n), dim3(256), 0, st, ws.desc, ws.planes, ws.plane_cap, d_out,
                            out_stride, fuse);

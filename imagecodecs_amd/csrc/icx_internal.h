@@ -110,7 +110,8 @@ struct GroupWs {
     int16_t* ac = nullptr;   // [pool_cap + kGwChunk][64] coefficient pool: quantized blocks, zig-zag order
     int32_t* dc = nullptr;   // [pool_cap + kGwChunk] int32 DC of pool blocks whose cell holds kDcEscape
     uint8_t* planes = nullptr;  // [slots][plane_cap]
-    uint8_t* tmp = nullptr;     // [slots][3 comps][2 buffers][tmp_cap]
+    uint8_t* tmp = nullptr;     // [slots][3 comps][2 buffers][tmp_cap]; aliases `ac` (tmp_own == false)
+    bool tmp_own = false;       // tmp is an allocation of its own (ac too small to hold it)
     // parallel entropy decode
     int64_t ucap = 0;           // unstuffed bytes per slot on average: U is one pool of (slots + 2) * ucap
                                 // bytes, each image's stream at SpecImg::uoff (k_spec_plan), so one

@@ -110,6 +110,7 @@ int icx_jpeg_batch_decode_host(icx_batch* b, int n, const uint8_t* const* jpegs,
 
 /* Images per workspace group (each kernel of the pipeline launches once per group). */
 int icx_batch_group(const icx_batch* b); /* images per group (one pipeline's workspace) */
+int icx_batch_groups(const icx_batch* b, int n); /* groups (launches of each per-group kernel) a call of n images takes */
 
 /* Per-stage timings (ms) of the most recent batch call, measured with HIP events on the
  * stream the kernels ran on. Fills up to `cap` entries; returns the number of stages. */
