@@ -1301,7 +1301,10 @@ __device__ __forceinline__ void stream_image(const Desc& d, const uint8_t* pslot
 // edge_from on, with the generic taps (double_tap, stride-end reads). One thread per (lane,
 // kSH-row strip); a wave's 64 threads all take the generic path, so it runs with full lanes
 // instead of as a divergent tail inside k_convert_stream's waves (which cost it 4.2 of 14.6 ms).
-constexpr int kSHE = 16;  // rows per edge item (even): short strips, so the few border lanes fill the chip
+#ifndef ICX_SHE
+#define ICX_SHE 16
+#endif
+constexpr int kSHE = ICX_SHE;  // rows per edge item (even): short strips, so the few border lanes fill the chip
 template <int K>
 __global__ __launch_bounds__(256) void k_convert_edge(const Desc* __restrict__ desc, const uint8_t* __restrict__ planes,
                                                       int64_t plane_cap, uint8_t* __restrict__ out, uint64_t out_stride,
