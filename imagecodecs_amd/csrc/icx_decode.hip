@@ -1888,9 +1888,6 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
 #ifndef ICX_F5_PF
 #define ICX_F5_PF 1
 #endif
-#ifndef ICX_F5_QR
-#define ICX_F5_QR 0  // 1: the dequant table reloaded per MCU row (fewer SGPR spills; measured no faster)
-#endif
 constexpr int kFB5 = ICX_FB5;
 __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                                    const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
@@ -1902,7 +1899,10 @@ __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* 
     __shared__ __attribute__((aligned(16))) uint32_t Yl_all[4][16][64];  // per wave: 16 luma rows x 256 pixels
     const int wave = wave_index(), lane = threadIdx.x & 63, mq = lane >> 2, k = lane & 3, sbx = k & 1, sby = k >> 1;
     uint32_t (*Yl)[64] = Yl_all[wave];
-    const uint8_t* qp = d.q[d.c[0].tq];
+    uint32_t qw[16];  // (wave-uniform: scalar registers, read by SDWA)
+    load_qw_g(d.q[d.c[0].tq], qw);
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) qw[k2] = __builtin_amdgcn_readfirstlane(qw[k2]);
     const int W = d.W, H = d.H, mbw = d.mbw, mbh = d.mbh;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     const CPl c1{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
@@ -1949,13 +1949,6 @@ __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* 
                 load_block8(ac, l.blk, c);
                 p = blk_pend(d, map, nblk(mby + 1));
 #endif
-                // the dequant table (16 scalar registers) is loaded again per MCU row, so it does not
-                // hold SGPRs through the conversion (whose row bases spilled into VGPR lanes)
-#if ICX_F5_QR
-                asm volatile("" : "+s"(qp));
-#endif
-                uint32_t qw[16];
-                load_qw_g(qp, qw);
                 uint32_t rowd[16];
                 block_idct(c, qw, dcv, l, rowd);
                 uint2* dst = reinterpret_cast<uint2*>(&Yl[sby * 8][mq * 4 + sbx * 2]);
