@@ -83,6 +83,26 @@ def test_synth_large(ctx, key):
     assert sha(pix) == e["sha256"]
 
 
+@pytest.mark.parametrize("group,n", [(3, 10), (5, 9), (4, 4), (2, 7)])
+def test_batch_group_count_balanced_and_exact(ctx, group, n):
+    """A call is cut into equal groups whose count is a multiple of the two pipelines when the
+    images allow it (icx_batch_groups; 3 groups on 2 pipes would run the third alone), and every
+    cut decodes every image exactly as the oracle -- with the generic upsample's planes in the
+    coefficient pool (a 4:4:4 / 4:2:2 / 4:1:1 / gray mix beside 4:2:0 in each group)."""
+    samplings = ["420", "444", "422", "411", "gray", "440"]
+    imgs = [S.synth_jpeg(4000 + k, 40 + 17 * k, 33 + 11 * k, samplings[k % len(samplings)], 60 + 4 * k) for k in range(n)]
+    b = icx.Batch(ctx, n, 256, 256, group)
+    g = b.groups_per_call(n)
+    slots = b.group
+    assert g >= -(-n // slots)
+    if g > 1 and -(-g // 2) * 2 <= n:
+        assert g % 2 == 0, (g, slots, n)
+    for data, (code, w, h, c, pix) in zip(imgs, b.decode_host(imgs)):
+        ocode, ow, oh, on, opix = O.decode(data)
+        assert (code, w, h) == (ocode, ow, oh) and pix.tobytes() == opix
+    b.close()
+
+
 def test_batch_out_of_capacity_is_oom(ctx):
     small = S.synth_jpeg(1, 64, 64)
     big = S.synth_jpeg(2, 200, 100)
