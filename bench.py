@@ -61,14 +61,17 @@ def pipeline_traffic(workload, n, alg_bytes):
             "pipeline_traffic_source": "profiles/pipeline_traffic.json (" + tj.get("source", "PMC run") + ")"}
 
 
-def stage_kernels(w, h):
+def stage_kernels(w, h, restart=0):
     """STAGE_KERNEL for a batch of w x h images: the three-pass entropy path's kernels where the
-    library takes it (ICX_GW=0, or a workspace for images of at most GW_MIN_PIXELS)."""
+    library takes it (ICX_GW=0, or a workspace for images of at most GW_MIN_PIXELS); with restart
+    markers the write stage is the restart-interval lanes (icx_spec.hip: one lane per interval)."""
     env = os.environ.get("ICX_GW")
     gw = env != "0" if env is not None else w * h > GW_MIN_PIXELS
     k = dict(STAGE_KERNEL)
     if not gw:
         k.update(write="k_spec_write", entropy="k_spec_guess+k_spec_count+k_spec_scan")
+    if restart:
+        k.update(write="k_spec_write<256> (restart-interval lanes)")
     return k
 
 WORKLOADS = {
@@ -926,7 +929,7 @@ def main():
         achieved = alg_bytes / (stages[dom] * 1e-3) / 1e9  # = per-launch alg bytes / avg launch time
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        kname = stage_kernels(W, H).get(dom, dom)
+        kname = stage_kernels(W, H, wl.get("restart", 0)).get(dom, dom)
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             # PMC runs may group images differently (the profiler holds HBM, so fewer images fit a

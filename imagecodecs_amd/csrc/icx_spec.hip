@@ -1896,9 +1896,12 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
     if (piece == kRoundHead) return;
     // the round's tail: restart intervals (DRI) -- one write lane per interval, 256-lane workgroups
     // (the non-big three-pass launch above took them) -- and the round's end
-    if ((gw || big) && piece != kRoundTailNoDri)
+    if ((gw || big) && piece != kRoundTailNoDri) {
+        B(kStWrite);  // (the write stage's second bracket: restart-interval lanes)
         hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
                            ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
+        E(kStWrite);
+    }
     hipLaunchKernelGGL(k_spec_finish, dim3((n + 63) / 64), dim3(64), 0, st, n, ws.desc, ws.spec, ws.stats);
 }
 
