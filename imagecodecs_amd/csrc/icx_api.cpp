@@ -352,20 +352,36 @@ void icx_batch_destroy(icx_batch* b) {
     delete b;
 }
 
-// Groups a call of n images is cut into (equal-sized, see icx_jpeg_batch_decode): enough for the
-// slots, at least ICX_GROUPS, and a multiple of the pipelines when that still fits (3 groups on 2
-// pipes run the third alone; 4 smaller ones keep both busy).
-static int batch_ngroups(const icx_batch* b, int n) {
+// How a call of n images is cut (equal-sized groups, see icx_jpeg_batch_decode): *per images a
+// group (the last may hold fewer), returning the groups actually launched, ceil(n / per). Enough
+// groups for the slots and at least ICX_GROUPS; and a multiple of the pipelines where rounding the
+// count up still gives one (3 groups on 2 pipes run the third alone; 4 smaller ones keep both
+// busy) -- only then, since a rounded-up count whose `per` launches fewer groups (n = 5 on slots
+// of 2: 4 -> per 2 -> 3 groups) buys nothing.
+static int batch_split(const icx_batch* b, int n, int* per_out) {
     const int slots = b->ws[0].slots;
-    int ngroups = std::min(n, std::max((n + slots - 1) / slots, b->min_groups));
-    if (b->pipes > 1 && ngroups > 1 && ngroups % b->pipes) {
-        const int up = (ngroups + b->pipes - 1) / b->pipes * b->pipes;
-        if (up <= n) ngroups = up;
+    const int want = std::min(n, std::max((n + slots - 1) / slots, b->min_groups));
+    int per = (n + want - 1) / want;
+    int ng = (n + per - 1) / per;
+    if (b->pipes > 1 && ng > 1 && ng % b->pipes) {
+        const int up = (ng + b->pipes - 1) / b->pipes * b->pipes;
+        if (up <= n) {
+            const int per2 = (n + up - 1) / up;
+            const int ng2 = (n + per2 - 1) / per2;
+            if (ng2 % b->pipes == 0) {
+                per = per2;
+                ng = ng2;
+            }
+        }
     }
-    return ngroups;
+    *per_out = per;
+    return ng;
 }
 
-int icx_batch_groups(const icx_batch* b, int n) { return b && n > 0 ? batch_ngroups(b, n) : 0; }
+int icx_batch_groups(const icx_batch* b, int n) {
+    int per = 0;
+    return b && n > 0 ? batch_split(b, n, &per) : 0;
+}
 
 int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_size,
                           uint8_t* d_out, uint64_t out_stride, int32_t* d_status, int32_t* d_dims, void* stream) {
@@ -382,9 +398,9 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
         ICX_HIP(ctx, hipMemsetAsync(b->ws[p].stats, 0, sizeof(int32_t) * 4, st), ICX_INTERNAL_ERR);
     // equal-sized groups (512 images on 361 slots -> 256 + 256, not 361 + 151): every kernel's
     // grid is sized by the work of its group, so a small tail group leaves the GPU half idle
-    const int ngroups = batch_ngroups(b, n);
-    const int per = (n + ngroups - 1) / ngroups;
-    const int used = std::min(b->pipes, (n + per - 1) / per);
+    int per = 0;
+    const int ng = batch_split(b, n, &per);
+    const int used = std::min(b->pipes, ng);
     if (used > 1) {  // the other pipes start after the caller's prior work on `st`
         ICX_HIP(ctx, hipEventRecord(b->fork, st), ICX_INTERNAL_ERR);
         for (int p = 1; p < used; ++p) ICX_HIP(ctx, hipStreamWaitEvent(b->pst[p], b->fork, 0), ICX_INTERNAL_ERR);
@@ -404,7 +420,6 @@ int icx_jpeg_batch_decode(icx_batch* b, int n, const uint8_t* d_data, const uint
     const char* hw = std::getenv("ICX_HOST_WAIT");  // (read per call: tests vary it)
     const bool no_wait_env = hw && std::atoi(hw) == 0;
     const bool host_wait = !stagger && cap == hipStreamCaptureStatusNone && !no_wait_env;
-    const int ng = (n + per - 1) / per;
     while (stagger && (int)b->front_done.size() < ng) {
         hipEvent_t e;
         ICX_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), ICX_INTERNAL_ERR);

@@ -146,7 +146,8 @@ int icx_multi_shard(const size_t* sizes, int n, int ndev, int32_t* shard_of) {
 }
 
 // One device's shard: stage the files, decode, records, copy pixels back; its records go to
-// `records` (host gather) or stay in d.d_rec, padded to `pad` entries, for the RCCL gather.
+// `records` (the host gather; the shard reads them anyway to pick its pixel copies) and, for the
+// RCCL gather, stay in d.d_rec, padded to `pad` entries.
 static int run_shard(icx_multi* m, Dev& d, const std::vector<int>& idx, const uint8_t* const* jpegs,
                      const size_t* sizes, uint8_t* const* outs, uint64_t out_stride, icx_record* records, int pad) {
     const int n = (int)idx.size();
@@ -226,7 +227,7 @@ static int run_shard(icx_multi* m, Dev& d, const std::vector<int>& idx, const ui
             r.status = ICX_OUT_OF_MEM;
             bytes = 0;
         }
-        if (pad == 0) std::memcpy(&records[idx[k]], &r, sizeof r);
+        std::memcpy(&records[idx[k]], &r, sizeof r);  // (also with RCCL: the fallback if its gather fails)
         if (outs && outs[idx[k]] && r.status == ICX_OK && bytes)
             chk(hipMemcpyAsync(outs[idx[k]], d_out + (uint64_t)k * stride_al, std::min<uint64_t>(bytes, out_stride),
                                hipMemcpyDeviceToHost, st), "D2H pixels");
@@ -312,7 +313,19 @@ int icx_multi_decode_host(icx_multi* m, int n, const uint8_t* const* jpegs, cons
             m->err = "device " + std::to_string(m->devs[k].device) + ": " + m->devs[k].err;
             return rc[k];
         }
-    return pad ? rccl_gather(m, idx, (int)pad, out_stride, records) : ICX_OK;
+    if (!pad) return ICX_OK;
+    // The decode and the pixel copies succeeded and `records` already holds every shard's records
+    // (run_shard): a failed RCCL gather falls back to them and says why, rather than
+    // failing a call whose results are all there.
+    std::vector<icx_record> via_rccl(records, records + n);
+    if (rccl_gather(m, idx, (int)pad, out_stride, via_rccl.data()) == ICX_OK) {
+        std::memcpy(records, via_rccl.data(), sizeof(icx_record) * n);
+        m->gather_desc = "rccl";
+    } else {
+        m->gather_desc = "host (RCCL gather failed: " + m->err + ")";
+        m->err.clear();
+    }
+    return ICX_OK;
 }
 
 const char* icx_multi_gather(const icx_multi* m) { return m ? m->gather_desc.c_str() : ""; }

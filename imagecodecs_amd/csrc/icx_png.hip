@@ -1554,6 +1554,7 @@ static void chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data
 struct PngHost {
     Stats S;
     uint8_t pre[2048];  // signature + IHDR / PLTE / tRNS + IDAT header + zlib header
+    png::PngTail tl;    // png_encode_device's layout read-back (pinned with the rest: no per-call allocation)
 };
 
 // One image's encode as two issue phases with one host read between them (png_encode_device
@@ -1809,7 +1810,13 @@ int PngJob::issue_b() {
                        (unsigned long long)idat_at, (unsigned long long)dstart, ws->small, (long long)N, ws->tl);
     // CRC-32 over "IDAT" + zlib stream: segment CRCs aligned to the stream's end (the device
     // knows its length; the grid covers the longest stream that fits), folded 256:1 per pass
-    const uint64_t zmax = cap > data_at + 16 ? cap - data_at - 16 + 4 : 4;  // ("IDAT" + stream)
+    // (bounded by the longest stream this image can produce -- at most 16 bits per filtered byte
+    // (a length-3 match with 15-bit codes and 5 + 13 extra bits), plus every block's dynamic
+    // header (< 600 bytes: 17 + 19 x 3 bits + 316 code lengths of at most 7 + 7 bits) and EOB,
+    // and the zlib framing -- not by the caller's capacity, which may be far larger)
+    const uint64_t zworst = 2 + 2 * (uint64_t)N + (uint64_t)nblk * 1024 + 1024;
+    const uint64_t zcap = cap > data_at + 16 ? cap - data_at - 16 : 0;
+    const uint64_t zmax = std::min(zcap, zworst) + 4;  // ("IDAT" + stream)
     const int64_t ncs = std::max<int64_t>(1, (int64_t)((zmax + kCrcSeg - 1) / kCrcSeg));
     size_t c12 = ws->crc_cap;
     const size_t crc_need = (size_t)(ncs + (ncs + 255) / 256 + 64) * 4;
@@ -1864,14 +1871,19 @@ static bool png_job_init(PngJob& j, PngWs* ws, hipStream_t st, int w, int h, int
 // d_out. Returns 0 ok, 1 d_out too small (*size = bytes needed), -1 HIP failure.
 int png_encode_device(hipStream_t st, PngWs* ws, int w, int h, int d, const uint8_t* d_src, uint8_t* d_out,
                       uint64_t cap, uint64_t* size) {
-    png::PngTail* tl = nullptr;
-    if (hipHostMalloc(reinterpret_cast<void**>(&tl), sizeof *tl) != hipSuccess) return -1;
+    // (the layout lands in the workspace's pinned PngHost: no per-call pinned allocation, whose
+    // hipHostFree would synchronise the device)
     PngJob j;
-    int rc = png_job_init(j, ws, st, w, h, d, d_src, d_out, cap, tl) ? j.issue_a() : -1;
+    int rc = png_job_init(j, ws, st, w, h, d, d_src, d_out, cap, nullptr) ? 0 : -1;
+    png::PngTail* tl = rc == 0 ? &ws->host->tl : nullptr;
+    if (rc == 0) {
+        *tl = png::PngTail{};
+        j.out_tl = tl;
+        rc = j.issue_a();
+    }
     if (rc == 0) rc = hipEventSynchronize(j.ev) == hipSuccess ? j.issue_b() : -1;
     if (rc == 0) rc = hipStreamSynchronize(st) == hipSuccess ? (tl->fits ? 0 : 1) : -1;
     *size = rc >= 0 ? tl->total : 0;
-    (void)hipHostFree(tl);
     return rc;
 }
 
@@ -1884,9 +1896,12 @@ int png_encode_device_batch(int k, hipStream_t* sts, PngWs** wss, int n, int w, 
                             int32_t* status) {
     png::PngTail* tl = nullptr;
     if (hipHostMalloc(reinterpret_cast<void**>(&tl), sizeof(png::PngTail) * std::max(n, 1)) != hipSuccess) return -1;
+    std::memset(tl, 0, sizeof(png::PngTail) * std::max(n, 1));
     std::vector<PngJob> job(k);
     std::vector<int> img(k, -1);
-    std::vector<int32_t> rc(std::max(n, 1), 0);
+    // -1 until the image's whole work is issued (an image no job reached, or whose issue failed,
+    // reports -1, never a stale layout)
+    std::vector<int32_t> rc(std::max(n, 1), -1);
     int next = 0, live = 0;
     auto start = [&](int j) {
         img[j] = -1;
@@ -1907,7 +1922,7 @@ int png_encode_device_batch(int k, hipStream_t* sts, PngWs** wss, int n, int w, 
     for (int j = 0; live > 0; j = (j + 1) % k) {
         if (img[j] < 0) continue;
         PngJob& J = job[j];
-        if (hipEventSynchronize(J.ev) != hipSuccess || J.issue_b() != 0) rc[img[j]] = -1;
+        rc[img[j]] = hipEventSynchronize(J.ev) != hipSuccess || J.issue_b() != 0 ? -1 : 0;
         start(j);
         if (img[j] < 0) --live;
     }
@@ -1916,8 +1931,9 @@ int png_encode_device_batch(int k, hipStream_t* sts, PngWs** wss, int n, int w, 
     for (int j = 0; j < k; ++j)
         if (hipStreamSynchronize(sts[j]) != hipSuccess) stream_fail = true;
     for (int i = 0; i < n; ++i) {
-        sizes[i] = rc[i] < 0 || stream_fail ? 0 : tl[i].total;
-        status[i] = rc[i] < 0 ? -1 : (tl[i].fits ? 0 : 1);
+        const bool bad = rc[i] < 0 || stream_fail;
+        sizes[i] = bad ? 0 : tl[i].total;
+        status[i] = bad ? -1 : (tl[i].fits ? 0 : 1);
     }
     (void)hipHostFree(tl);
     return stream_fail ? -1 : 0;

@@ -76,7 +76,7 @@ void icx_free(void* p);
 typedef struct icx_batch icx_batch;
 
 /* Workspace for up to `max_images` images per call, each at most max_width x max_height
- * (any sampling NanoJPEG accepts). At most `group` images (0 = auto: 60% of free HBM) are in
+ * (any sampling NanoJPEG accepts). At most `group` images (0 = auto: 80% of free HBM) are in
  * flight at once, split over up to two decode pipelines (a workspace and a HIP stream each;
  * env ICX_PIPES=1 keeps one): consecutive groups alternate between the pipelines so their
  * kernels overlap, and the call's stream waits for both. Returns NULL on allocation failure. */

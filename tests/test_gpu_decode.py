@@ -83,20 +83,37 @@ def test_synth_large(ctx, key):
     assert sha(pix) == e["sha256"]
 
 
-@pytest.mark.parametrize("group,n", [(3, 10), (5, 9), (4, 4), (2, 7)])
+def _expected_groups(n, slots, pipes=2):
+    """icx_api.cpp batch_split: the groups a call launches (ceil(n / per))."""
+    want = min(n, -(-n // slots))
+    per = -(-n // want)
+    ng = -(-n // per)
+    if pipes > 1 and ng > 1 and ng % pipes:
+        up = -(-ng // pipes) * pipes
+        if up <= n:
+            per2 = -(-n // up)
+            if -(-n // per2) % pipes == 0:
+                per, ng = per2, -(-n // per2)
+    return ng, per
+
+
+@pytest.mark.parametrize("group,n", [(3, 10), (5, 9), (4, 4), (2, 7), (2, 5), (6, 7)])
 def test_batch_group_count_balanced_and_exact(ctx, group, n):
-    """A call is cut into equal groups whose count is a multiple of the two pipelines when the
-    images allow it (icx_batch_groups; 3 groups on 2 pipes would run the third alone), and every
-    cut decodes every image exactly as the oracle -- with the generic upsample's planes in the
-    coefficient pool (a 4:4:4 / 4:2:2 / 4:1:1 / gray mix beside 4:2:0 in each group)."""
+    """A call is cut into equal groups; icx_batch_groups reports exactly the groups launched
+    ((group 2, n 5) used to report 4 for 3 launched), a multiple of the two pipelines
+    when rounding the count up still yields one ((6, 7): 3 -> 4 groups of 2; 3 groups on 2 pipes
+    would run the third alone), and every cut decodes every image exactly as the oracle -- with
+    the generic upsample's planes in the coefficient pool (a 4:4:4 / 4:2:2 / 4:1:1 / gray mix
+    beside 4:2:0 in each group)."""
     samplings = ["420", "444", "422", "411", "gray", "440"]
     imgs = [S.synth_jpeg(4000 + k, 40 + 17 * k, 33 + 11 * k, samplings[k % len(samplings)], 60 + 4 * k) for k in range(n)]
     b = icx.Batch(ctx, n, 256, 256, group)
     g = b.groups_per_call(n)
     slots = b.group
-    assert g >= -(-n // slots)
-    if g > 1 and -(-g // 2) * 2 <= n:
-        assert g % 2 == 0, (g, slots, n)
+    eg, per = _expected_groups(n, slots)
+    assert g == eg and per <= slots and -(-n // per) == g, (g, eg, per, slots, n)
+    if (group, n) == (6, 7):
+        assert g == 4
     for data, (code, w, h, c, pix) in zip(imgs, b.decode_host(imgs)):
         ocode, ow, oh, on, opix = O.decode(data)
         assert (code, w, h) == (ocode, ow, oh) and pix.tobytes() == opix
