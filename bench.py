@@ -745,6 +745,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive sub-batch (decode workloads)")
     ap.add_argument("--png-single", action="store_true", help="C5: one encode call per image (no batch entry)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="decode workloads: steps in flight (0 = the workload's default); step k runs on batch "
+                         "k %% M with its own stream and output buffers, so one step's back half overlaps the "
+                         "next step's front half")
     args = ap.parse_args()
 
     # --gpus N: one rank per GPU. Without a launcher (WORLD_SIZE unset) the bench starts
@@ -816,18 +820,33 @@ def main():
     d_off = torch.from_numpy(offs).to(dev)
     d_sz = torch.from_numpy(sizes).to(dev)
     stride = W * H * 3
-    d_out = torch.empty(n * stride, dtype=torch.uint8, device=dev)
-    d_st = torch.empty(n, dtype=torch.int32, device=dev)
-    d_dims = torch.empty((n, 3), dtype=torch.int32, device=dev)
+    # Steps in flight (--inflight M): M batches (each its own workspace groups, pipelines and
+    # streams), M output sets, step k on set k % M. A batch call returns once its groups are
+    # planned and enqueued, so step k + 1's front half (parse, unstuff, entropy) runs while step k's
+    # back half (IDCT, convert) still does: a data loader decoding batch after batch. Every step
+    # still decodes all n images into its own buffers; the timed region ends when every stream is
+    # done. The batches share the HBM budget: the auto group size takes 80% of free HBM for one
+    # batch, so a workload whose workspaces are large gives M > 1 an explicit group per batch
+    # (--group, or the workload's inflight_group).
+    M = max(1, args.inflight or wl.get("inflight", 1))
+    d_out = [torch.empty(n * stride, dtype=torch.uint8, device=dev) for _ in range(M)]
+    d_st = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(M)]
+    d_dims = [torch.empty((n, 3), dtype=torch.int32, device=dev) for _ in range(M)]
 
     ctx = icx.Context(local)
-    batch = icx.Batch(ctx, n, W, H, args.group)
+    group = args.group or (wl.get("inflight_group", 0) if M > 1 else 0)
+    batches = [icx.Batch(ctx, n, W, H, group) for _ in range(M)]
+    batch = batches[0]
     stream = torch.cuda.current_stream(dev)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(M - 1)]
+    seq = [0]
 
     def step():  # no collective inside the timed loop: the records gather after it is the only one
-        batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out.data_ptr(), stride,
-                            d_st.data_ptr(), d_dims.data_ptr(), stream.cuda_stream)
-        return d_st
+        k = seq[0] % M
+        seq[0] += 1
+        batches[k].decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out[k].data_ptr(), stride,
+                                 d_st[k].data_ptr(), d_dims[k].data_ptr(), streams[k].cuda_stream)
+        return k
 
     for _ in range(args.warmup):
         step()
@@ -836,9 +855,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    last = d_st
     for _ in range(args.steps):
-        last = step()
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -846,6 +864,8 @@ def main():
     elapsed = time.perf_counter() - t0
     stages = batch.stage_times()  # HIP events on this stream, last step
     paths = batch.path_stats()
+    # (outputs of the last step on set 0: every set decodes the same images)
+    d_out, d_st, d_dims, last = d_out[0], d_st[0], d_dims[0], d_st[0]
 
     # Final gather: every rank's per-image records {status, w, h, ncomp,
     # checksum64}, computed on its device (icx_jpeg_records) from the last step's outputs,
@@ -963,6 +983,7 @@ def main():
         "cpu_baseline": cpu,
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
         "entropy_paths": paths,
+        "inflight": {"steps_in_flight": M, "group": group or "auto", "groups_per_call": batch.groups_per_call(n)},
         "records": records,
         "pcie_inclusive": pcie,
         "gen_seconds": round(gen_s, 1),

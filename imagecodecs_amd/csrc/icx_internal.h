@@ -68,7 +68,9 @@ struct LaneEntry { int64_t G; int32_t p0, p1, p2, pad; };
 // blocks per lane), chained through GroupWs::chunk_next.
 constexpr int kGwChunk = 32;
 constexpr int kRecGw = kRec;    // MCU starts a guess-write lane records (the count lanes splice at the first
-                                // they reach; a lane that cannot splice is count-decoded whole)
+                                // they reach; a lane that cannot splice is count-decoded whole). (8 was
+                                // tried in round 6: k_gw_lane -1%, but k_gw_count 0.64 -> 1.65 ms per 256
+                                // images -- a few lanes of the C3 pool splice past record 7)
 constexpr int64_t kGwMinPixels = 2048 * 2048;  // workspaces for larger images take the guess-write path
 constexpr int kGwMaxWalk = 64;  // lanes a repair walk may re-derive before the image goes sequential
 struct GwOut {

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "icx_spec_core.h"
 
@@ -1198,7 +1199,13 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 #ifndef ICX_GW_MINW  // (timing experiments: waves per SIMD k_gw_lane is compiled for)
 #define ICX_GW_MINW 1
 #endif
-template <int NL>
+// CHK: the instance for images whose data ends in a syntax error (SpecImg::errpos set): every
+// lookup tests NanoJPEG's error-byte bounds (ErrBounds). A stream that ends in FF D9 -- every valid
+// one -- takes the instance without them (round 6: -4 VALU a lookup). Both are launched; each
+// skips the other's images before staging any table. (One kernel with both loops behind a
+// uniform branch took 117 VGPRs instead of 95 / 98, and in the two-pipeline step the back half's
+// kernels then no longer fit beside it on a SIMD.)
+template <int NL, bool CHK>
 __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                 const int32_t* __restrict__ wpre, const int32_t* __restrict__ totals,
                                                 const StepSet* __restrict__ steps, const uint8_t* __restrict__ U,
@@ -1236,9 +1243,12 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
     int4* A = reinterpret_cast<int4*>(ac);
     const int32_t scratch = (int32_t)pool_cap;  // (a lane the pool could not hold writes here)
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
+        {  // uniform per workgroup; tested before the tables are staged
+            const SpecImg& s0 = spec[find_image(wpre, n, wg)];
+            if (s0.mode != 1 || (s0.errpos != INT64_MAX) != CHK) continue;
+        }
         const int i = wg_image_setup(wpre, n, wg, cur, T, steps);
         SpecImg& s = spec[i];
-        if (s.mode != 1) continue;  // uniform per workgroup
         __syncthreads();  // (the previous item's slots are done with)
 #ifdef ICX_EXP_GW8
         stage_tab(L.st, steps[i].scan11);
@@ -1277,10 +1287,17 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         const int32_t Sst = s.gw_S;
         const int32_t sbase = (int32_t)(desc[i].acbase + j * Sst);
         RecState* R = rec + f * kRec;
-        int ci = 0, nrec = 0;
+        int nrec = 0;
         bool live = act;  // storing; false from the exit on (and for lanes past the image's last)
         int32_t k = 0, err = INT32_MAX, chunk = -1, chunk0 = -1, over = 0, addr = 0;
-        int32_t ds0 = 0, ds1 = 0, ds2 = 0;
+        // Lane-local DC sums rotated with the current block's component: dc0 is the sum of block
+        // b's component, dc1 / dc2 those of the next two in MCU order. An MCU runs through the
+        // components in order (0 .. 0, 1 .. 1, 2 .. 2, then block 0 again), so a block end whose
+        // next block has another component rotates them by one, and a DC code reads and updates
+        // dc0 alone (round 6: 2 compares, 2 selects and 3 predicated updates per lookup became 1
+        // bit test and 4 selects). At an MCU start (b == 0, component 0) they are ds[0..2].
+        int32_t dc0 = 0, dc1 = 0, dc2 = 0;
+        const uint32_t chgm = S.chg_mask();
         uint32_t ul = 0;  // exit: bits read and block-in-MCU there
         int bl = 0;
         int32_t left = Sst, nxt = sbase;  // slots left in the current run (static, then chunks), the next one
@@ -1306,9 +1323,9 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                         e.rel = u - pre;
                         e.b = 0;
                         e.cnt = k;
-                        e.ds[0] = ds0;
-                        e.ds[1] = ds1;
-                        e.ds[2] = ds2;
+                        e.ds[0] = dc0;  // (b == 0: the rotation is at component 0)
+                        e.ds[1] = dc1;
+                        e.ds[2] = dc2;
                         R[nrec] = e;
                         ++nrec;
                     }
@@ -1335,17 +1352,15 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             addr = own_bs ? nxt : addr;
             nxt += own_bs && !over ? 1 : 0;
             left -= own_bs ? 1 : 0;
-            ci = bs ? S.comp(b) : ci;
             // one lookup (every lane: the reader moves on idle lanes too, see k_spec_write)
             const uint32_t u0 = r.used;
-            const WriteOut o = write_step(r, T, H, S, b, z, eb.near(u0));
-            const bool fail = eb.fail(u0, o.err, r.used);
+            const int bcur = b;
+            const WriteOut o = write_step(r, T, H, S, b, z, CHK ? eb.near(u0) : false);
+            const bool fail = CHK ? eb.fail(u0, o.err, r.used) : o.err;
             err = live && fail && err == INT32_MAX ? k : err;
             const bool owndc = own_bs;
-            const int32_t pc = wadd(ci == 0 ? ds0 : (ci == 1 ? ds1 : ds2), o.v1);
-            ds0 = owndc && ci == 0 ? pc : ds0;
-            ds1 = owndc && ci == 1 ? pc : ds1;
-            ds2 = owndc && ci == 2 ? pc : ds2;
+            const int32_t pc = wadd(dc0, o.v1);
+            dc0 = owndc ? pc : dc0;
             const int32_t cell = dc_cell(pc);
             if (owndc && cell == kDcEscape) dcv[addr] = pc;  // lane-local DC outside int16 (rare)
             // (v1 is 0 for EOB and invalid codes; an invalid DC code is a decode error, so that
@@ -1354,6 +1369,13 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             sv[slot_cell(threadIdx.x, o.n1)] = (Cell)(bs ? cell : o.v1);
             const bool done = live && z == 0;
             k += done ? 1 : 0;
+            {  // the block ended: the next block's component (frozen once the lane left)
+                const bool rot = done && ((chgm >> bcur) & 1u) != 0u;
+                const int32_t t0 = dc0;
+                dc0 = rot ? dc1 : dc0;
+                dc1 = rot ? dc2 : dc1;
+                dc2 = rot ? t0 : dc2;
+            }
             const uint64_t m = wave_ballot(done);
             if (m) {  // wave-uniform: flush the completed blocks, 8 per round
                 if (done) {
@@ -1388,9 +1410,12 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             GwOut g;
             g.g0 = g0;
             g.k = k;
-            g.ds[0] = ds0;
-            g.ds[1] = ds1;
-            g.ds[2] = ds2;
+            {  // un-rotate: at the exit the rotation is at block bl's component
+                const int c = S.comp(bl);
+                g.ds[c] = dc0;
+                g.ds[c == 2 ? 0 : c + 1] = dc1;
+                g.ds[c == 0 ? 2 : c - 1] = dc2;
+            }
             g.err = err;
             g.chunk0 = chunk0;
             g.nrec = nrec;
@@ -1843,9 +1868,15 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
         // Guess-write path (default; ICX_GW=0: guess, count, write)
         if (gw) {
             B(kStWrite);
-            hipLaunchKernelGGL(k_gw_lane<kWriteLanesBig>, dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec, ws.wg2pre,
-                               ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.X, ws.gw,
-                               ws.rec, lead);
+            hipLaunchKernelGGL((k_gw_lane<kWriteLanesBig, false>), dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec,
+                               ws.wg2pre, ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap,
+                               ws.X, ws.gw, ws.rec, lead);
+            // (the CHK instance on a small grid: it usually finds no image of its own, and 2048
+            // empty workgroups of 80 KB of LDS each waited ~0.5 ms for LDS beside the other pipeline)
+            hipLaunchKernelGGL((k_gw_lane<kWriteLanesBig, true>), dim3(std::min(g, 128)), dim3(kWriteLanesBig), 0, st, n,
+                               ws.desc, ws.spec,
+                               ws.wg2pre, ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap,
+                               ws.X, ws.gw, ws.rec, lead);
             E(kStWrite);
             B(kStEntropy);
             hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,

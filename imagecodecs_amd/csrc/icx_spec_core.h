@@ -236,6 +236,12 @@ struct Sel {
     uint32_t comps;
     uint64_t tabs;
     ICX_HD int comp(int b) const { return (int)((comps >> (2 * b)) & 3u); }
+    // bit b: block (b + 1) mod bpm belongs to another component than block b
+    ICX_HD uint32_t chg_mask() const {
+        uint32_t m = 0;
+        for (int b = 0; b < bpm && b < 16; ++b) m |= (uint32_t)(comp(b) != comp(b + 1 == bpm ? 0 : b + 1)) << b;
+        return m;
+    }
     ICX_HD int tab(int b, bool dc) const { return (int)((tabs >> (4 * b + (dc ? 0 : 2))) & 3u); }
 };
 ICX_HD Sel make_sel(const Desc& d) {

@@ -421,8 +421,18 @@ static uint64_t emu_gw_lane(const uint8_t* U, int64_t ulen, const WriteTab& TW, 
 }
 
 static int64_t g_gw_stats[8];  // lanes, synced at start, count lanes, spliced, repaired, overflow chunks, pool used
+// count lanes by the guess record they spliced at (m = 0 .. kRec-1); [kRec]: never spliced, whole
+// lane decoded (m = -1); [kRec + 1]: other (accumulated over calls; emu_gw_splice_hist reads it)
+static int64_t g_gw_splice_hist[kRec + 2];
 
 extern "C" {
+
+void emu_gw_splice_hist(int64_t* out /*[kRec + 2]*/, int reset) {
+    for (int k = 0; k < kRec + 2; ++k) {
+        out[k] = g_gw_splice_hist[k];
+        if (reset) g_gw_splice_hist[k] = 0;
+    }
+}
 
 // The guess-write path end to end on the CPU. Returns like emu_spec_decode; static_frac scales
 // the static slots per lane (k_spec_plan's kGwStaticSlack; small values force overflow chunks).
@@ -489,6 +499,7 @@ int emu_gw_decode(const uint8_t* file, int64_t size, int sub_bytes, int64_t lead
         ++counted;
         if (!count_lane(j, entry)) return 1;
         spliced += c[j].m >= 0;
+        ++g_gw_splice_hist[c[j].m >= 0 ? std::min<int>(c[j].m, kRec - 1) : kRec + (c[j].m == -1 ? 0 : 1)];
         if (c[j].m < 0 && j + 1 < nsub && Y[j] != X[j]) queue.push_back(j);
     }
     // ---- k_gw_repair: an unspliced count lane whose exit differs re-derives the next lanes
