@@ -360,20 +360,31 @@ constexpr uint8_t kZigOfNatC[64] = {
 // Full row / column formulas (no shortcuts): 24-bit multiplies of the inputs and their pairwise
 // sums (below 2^23 on the fast path), 32-bit multiplies for the last butterfly's 181 products,
 // whose operands x4 +- x5 are not (a dequantized AC of 2500 puts 8.5M there).
+// The three rotations as packed 16-bit dot products (round 6): over the integers
+// W7(x4 + x5) + (W1 - W7)x4 = W1 x4 + W7 x5 and W7(x4 + x5) - (W1 + W7)x5 = W7 x4 - W1 x5 (likewise
+// for (x6, x7) and (x2, x3)), with no rounding between, so one v_dot2_i32_i16 of the packed pair
+// gives each output exactly. The inputs are dequantized coefficients, below 2^14 on this path
+// (block_transform's vote), so the pairs pack into int16 and no sum leaves int32 (< 2^27).
+// (v_dot2_i32_i16 written out: the builtin became the VOP2 v_dot2c, whose accumulator is its
+// destination, plus a v_mov of the zero into it -- more issue cycles than the multiplies it replaced)
+__device__ __forceinline__ uint32_t pk16(int32_t lo, int32_t hi) {  // (lo, hi) low halves, one v_perm
+    return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+__device__ __forceinline__ int32_t rdot2(uint32_t a, uint32_t w, int32_t zero) {
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(w), "v"(zero));
+    return r;
+}
+constexpr uint32_t kw16(int lo, int hi) { return ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16); }
 __device__ __forceinline__ void idct_row_full(int32_t (&r)[8]) {
-    int32_t x0 = (r[0] << 11) + 128, x1 = r[4] << 11, x2 = r[6], x3 = r[2];
-    int32_t x4 = r[1], x5 = r[7], x6 = r[5], x7 = r[3], x8;
-    x8 = m24(kW7, x4 + x5);
-    x4 = x8 + m24(kW1 - kW7, x4);
-    x5 = x8 - m24(kW1 + kW7, x5);
-    x8 = m24(kW3, x6 + x7);
-    x6 = x8 - m24(kW3 - kW5, x6);
-    x7 = x8 - m24(kW3 + kW5, x7);
-    x8 = x0 + x1;
+    const int32_t z = __builtin_amdgcn_readfirstlane(0);  // (a zero accumulator the compiler keeps in a register)
+    const uint32_t p17 = pk16(r[1], r[7]), p53 = pk16(r[5], r[3]), p26 = pk16(r[2], r[6]);
+    int32_t x0 = (r[0] << 11) + 128, x1 = r[4] << 11;
+    int32_t x4 = rdot2(p17, kw16(kW1, kW7), z), x5 = rdot2(p17, kw16(kW7, -kW1), z);  // W1 r1 + W7 r7, W7 r1 - W1 r7
+    int32_t x6 = rdot2(p53, kw16(kW5, kW3), z), x7 = rdot2(p53, kw16(kW3, -kW5), z);  // W5 r5 + W3 r3, W3 r5 - W5 r3
+    int32_t x3 = rdot2(p26, kw16(kW2, kW6), z), x2 = rdot2(p26, kw16(kW6, -kW2), z);  // W2 r2 + W6 r6, W6 r2 - W2 r6
+    int32_t x8 = x0 + x1;
     x0 -= x1;
-    x1 = m24(kW6, x3 + x2);
-    x2 = x1 - m24(kW2 + kW6, x2);
-    x3 = x1 + m24(kW2 - kW6, x3);
     x1 = x4 + x6;
     x4 -= x6;
     x6 = x5 + x7;
