@@ -39,6 +39,7 @@ STAGE_KERNEL = {"write": "k_gw_lane", "idct": "k_idct420s (4:2:0 chroma planes; 
                 "entropy": "k_gw_check+k_gw_count+k_gw_repair+k_gw_scan+k_gw_map",
                 "parse": "k_parse", "upsample": "k_upsample"}
 GW_MIN_PIXELS = 2048 * 2048  # icx_internal.h kGwMinPixels: larger workspaces take the guess-write path
+DRI_GW_MIN = 4096  # icx_internal.h kDriGwMin: restart intervals from this many bytes take guess-write lanes
 
 
 def coef_cell_bytes():
@@ -61,17 +62,24 @@ def pipeline_traffic(workload, n, alg_bytes):
             "pipeline_traffic_source": "profiles/pipeline_traffic.json (" + tj.get("source", "PMC run") + ")"}
 
 
-def stage_kernels(w, h, restart=0):
+def stage_kernels(w, h, restart=0, interval_bytes=0):
     """STAGE_KERNEL for a batch of w x h images: the three-pass entropy path's kernels where the
     library takes it (ICX_GW=0, or a workspace for images of at most GW_MIN_PIXELS); with restart
-    markers the write stage is the restart-interval lanes (icx_spec.hip: one lane per interval)."""
+    markers the write stage is the restart-interval lanes (icx_spec.hip: one lane per interval),
+    unless the guess-write path cuts the intervals into lanes (k_spec_plan: intervals averaging
+    DRI_GW_MIN compressed bytes or more; ICX_DRI_GW=0 never, 1 from 512)."""
     env = os.environ.get("ICX_GW")
     gw = env != "0" if env is not None else w * h > GW_MIN_PIXELS
     k = dict(STAGE_KERNEL)
     if not gw:
         k.update(write="k_spec_write", entropy="k_spec_guess+k_spec_count+k_spec_scan")
     if restart:
-        k.update(write="k_spec_write<256> (restart-interval lanes)")
+        denv = os.environ.get("ICX_DRI_GW")
+        dmin = (512 if denv != "0" else None) if denv is not None else DRI_GW_MIN
+        if gw and dmin is not None and interval_bytes >= dmin:
+            k.update(write="k_gw_lane (interval-aligned lanes)+k_spec_write<256> (fallbacks)")
+        else:
+            k.update(write="k_spec_write<256> (restart-interval lanes)")
     return k
 
 WORKLOADS = {
@@ -949,7 +957,12 @@ def main():
         achieved = alg_bytes / (stages[dom] * 1e-3) / 1e9  # = per-launch alg bytes / avg launch time
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        kname = stage_kernels(W, H, wl.get("restart", 0)).get(dom, dom)
+        rst = wl.get("restart", 0)
+        ibytes = 0
+        if rst:  # average compressed bytes per restart interval (interval_bytes: the scan's share)
+            mcus = -(-W // 16) * -(-H // 16) if wl["sampling"] == "420" else -(-W // 8) * -(-H // 8)
+            ibytes = sum(len(p) for p in pool) / len(pool) / -(-mcus // rst)
+        kname = stage_kernels(W, H, rst, ibytes).get(dom, dom)
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             # PMC runs may group images differently (the profiler holds HBM, so fewer images fit a

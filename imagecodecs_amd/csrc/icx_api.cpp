@@ -285,8 +285,8 @@ static bool ws_alloc_all(icx_ctx* ctx, GroupWs& ws, int group, int max_w, int ma
     ICX_HIP(ctx, hipMalloc(&ws.gw, sizeof(GwOut) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.crec, sizeof(GcRec) * ws.lanes_cap), false);
     ICX_HIP(ctx, hipMalloc(&ws.clist, sizeof(int2) * ws.lanes_cap), false);
-    ICX_HIP(ctx, hipHostMalloc(&ws.h_defer, 2 * sizeof(int32_t), hipHostMallocDefault), false);
-    ws.h_defer[0] = ws.h_defer[1] = 0;
+    ICX_HIP(ctx, hipHostMalloc(&ws.h_defer, 3 * sizeof(int32_t), hipHostMallocDefault), false);
+    ws.h_defer[0] = ws.h_defer[1] = ws.h_defer[2] = 0;
     ICX_HIP(ctx, hipHostMalloc(&ws.h_layout, sizeof(int32_t), hipHostMallocDefault), false);
     *ws.h_layout = 1;
     ICX_HIP(ctx, hipEventCreateWithFlags(&ws.ev_defer, hipEventDisableTiming), false);

@@ -38,7 +38,7 @@ struct SpecImg {
     int32_t nwg, wg_base;  // 256-lane decode groups; the image's first lane record / 256 (subsequence
                            // images only: a flat numbering over the batch group's lane records)
     int32_t nsub, nrepair;   // lanes; unsynchronised lanes queued for repair
-    int32_t nint, nrst;      // DRI (mode 3): restart intervals; restart markers found in U
+    int32_t nint, nrst;      // DRI (modes 3, and 1 with kint): restart intervals; restart markers found in U
     int32_t sub_bytes;       // unstuffed bytes per decode lane (mode 1)
     int32_t gw_S;            // guess-write static pool slots per lane (mode 1)
     int64_t scan_len;      // raw entropy-coded bytes (file end - scan start)
@@ -50,7 +50,9 @@ struct SpecImg {
     int32_t dri_first;     // DRI: 2 j + (kind == kDriElsewhere) of the first interval j not ending
                            // at its marker (dri_end_kind; atomicMin, INT32_MAX: none)
     int64_t tail_G, tail_n;  // guess-write: the lanes' blocks end at block tail_G, tail_n before the
-    int32_t tail_p[3], pad3_;// frame's last (k_gw_tail reads on into the padding; DC predictors there)
+    int32_t tail_p[3];       // frame's last (k_gw_tail reads on into the padding; DC predictors there)
+    int32_t kint;            // guess-write over restart intervals (mode 1, DRI): lanes per interval
+                             // (lane j in interval j / kint, icx_spec_core.h lane_span); 0 otherwise
 };
 struct TileRec { int32_t kept, end_err; int64_t end_at; int32_t nrst, pad_; };
 struct SubRec { int32_t cnt, ds0, ds1, ds2; int32_t mism; };
@@ -73,6 +75,10 @@ constexpr int kRecGw = kRec;    // MCU starts a guess-write lane records (the co
                                 // images -- a few lanes of the C3 pool splice past record 7)
 constexpr int64_t kGwMinPixels = 2048 * 2048;  // workspaces for larger images take the guess-write path
 constexpr int kGwMaxWalk = 64;  // lanes a repair walk may re-derive before the image goes sequential
+// Restart intervals on the guess-write path (round 6): an image whose intervals average at least
+// kDriGwMin unstuffed bytes (ICX_DRI_GW: 0 never, 1 from kSubBytesSmall) has each interval cut into
+// kint lanes of at most kSubBytes instead of one serial lane per interval (mode 3).
+constexpr int kDriGwMin = 4096;
 struct GwOut {
     uint64_t g0;     // first block start at or after the lane's start: pack_state(pos, b, 0)
     int32_t k;       // blocks the lane stored (slots 0 .. k-1)
@@ -150,7 +156,8 @@ struct GroupWs {
     GwOut* gw = nullptr;               // [lanes_cap]
     GcRec* crec = nullptr;             // [lanes_cap]
     int2* clist = nullptr;             // [lanes_cap] per image, in its lane-record range: (image, lane) to count-decode
-    int32_t* h_defer = nullptr;        // pinned [2]: images the last k_spec_plan deferred, and gave restart-interval lanes
+    int32_t* h_defer = nullptr;        // pinned [3]: images the last k_spec_plan deferred, gave restart-interval lanes, gave
+                                       // interval-aligned guess-write lanes
     int32_t* h_layout = nullptr;       // pinned: the group has an image outside the fused 4:2:0 layout (k_parse)
     hipEvent_t ev_defer = nullptr;     // after round 0's k_spec_plan
 };
@@ -231,8 +238,10 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
 void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
                          StageHook* hook, int part = kFrontAll);
 // piece: kRoundAll the whole round; kRoundHead up to its restart-interval write; kRoundTail that
-// write and the round's end; kRoundTailNoDri the end alone (no image got restart-interval lanes).
-enum { kRoundAll = 0, kRoundHead = 1, kRoundTail = 2, kRoundTailNoDri = 3 };
+// write and the round's end; kRoundTailNoDri the end alone (no image got restart-interval lanes);
+// kRoundTailGw that write on a small grid (only guess-write DRI images, whose lanes fall back to it
+// when they cannot decide the image).
+enum { kRoundAll = 0, kRoundHead = 1, kRoundTail = 2, kRoundTailNoDri = 3, kRoundTailGw = 4 };
 void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const uint64_t* d_off, hipStream_t st,
                        StageHook* hook, int round, int last, int piece = kRoundAll);
 

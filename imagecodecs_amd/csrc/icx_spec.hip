@@ -53,7 +53,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                                                     int32_t* __restrict__ wg2pre, int32_t* __restrict__ totals,
                                                     int64_t upool, int64_t lanes_cap, int sub_bytes, int64_t pool_cap,
                                                     unsigned long long* __restrict__ pool_next, int gw, int round,
-                                                    int last_round, int32_t* __restrict__ defer_out) {
+                                                    int last_round, int32_t* __restrict__ defer_out, int dri_min) {
     __shared__ int sh[1024];
     __shared__ int last[7];
     if (round > 0) {  // a later round with nothing deferred plans nothing, at once
@@ -63,12 +63,12 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             if (threadIdx.x == 0) {
                 totals[0] = totals[1] = totals[2] = 0;
                 tilepre[n] = wgpre[n] = wg2pre[n] = 0;
-                if (defer_out) defer_out[0] = defer_out[1] = 0;
+                if (defer_out) defer_out[0] = defer_out[1] = defer_out[2] = 0;
             }
             return;
         }
     }
-    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0, carry_a = 0, carry_d = 0, carry_i = 0;
+    int carry_t = 0, carry_w = 0, carry_w2 = 0, carry_u = 0, carry_c = 0, carry_r = 0, carry_a = 0, carry_d = 0, carry_i = 0, carry_k = 0;
     const int64_t pool_units = upool >> 12, wg_cap = lanes_cap / kLanes;
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
         const int i = i0 + threadIdx.x;
@@ -82,8 +82,8 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         const bool mine = i < n && (round == 0 || spec[i].mode == 4);
         const bool cand = mine && desc[i].status == kPending && desc[i].nc >= 1 && desc[i].bpm <= kSpecMaxBpm &&
                           scan_len > 0 && scan_len < ((int64_t)1 << 40);
-        int nt = 0, nw = 0, nw2 = 0, nu = 0;
-        int64_t sb = kSubBytes, nsub = 0;
+        int nt = 0, nw = 0, nw2 = 0, nu = 0, kint = 0;
+        int64_t sb = kSubBytes, nsub = 0, nlanes = 0;
         if (cand) {
             const Desc& d = desc[i];
             nu = (int)min<int64_t>((scan_len + 64 + 4095) >> 12, INT32_MAX / 4);
@@ -102,14 +102,22 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
                 sb = min<int64_t>(smax, max<int64_t>(kSubBytesSmall, (sb + 15) & ~15));
             }
             nsub = d.restart == 0 ? (scan_len + sb - 1) / sb : (nmcu + d.restart - 1) / d.restart;
-            nw = (int)min<int64_t>((nsub + kLanes - 1) / kLanes, INT32_MAX / 4);
-            nw2 = (int)((nsub + kWriteLanesBig - 1) / kWriteLanesBig);
+            // restart intervals on the guess-write path: long intervals, every MCU >= 8 bits
+            // (lane_span), cut into kint lanes of at most kSubBytes
+            if (d.restart != 0 && gw && dri_min > 0 && scan_len / nsub >= dri_min && min_mcu_bits(d) >= 8) {
+                const int64_t avg = scan_len / nsub;
+                kint = (int)min<int64_t>(64, max<int64_t>(2, (avg + kSubBytes - 1) / kSubBytes));
+                sb = (avg + kint - 1) / kint;
+            }
+            nlanes = kint ? nsub * kint : nsub;
+            nw = (int)min<int64_t>((nlanes + kLanes - 1) / kLanes, INT32_MAX / 4);
+            nw2 = (int)((nlanes + kWriteLanesBig - 1) / kWriteLanesBig);
         }
         // Capacity: an image whose U units or lane records would pass the workspace's goes to
         // the sequential kernel. Only subsequence lanes have records (X, rec, sub, ent: a DRI
         // interval lane needs none), numbered apart from the workgroups. The prefixes count
         // every candidate, so they bound what the images taken below use.
-        const int nwc = cand && desc[i].restart == 0 ? nw : 0;
+        const int nwc = cand && (desc[i].restart == 0 || kint) ? nw : 0;
         const int eu = block_exclusive_scan(nu, sh);
         const int ec = block_exclusive_scan(nwc, sh);
         const bool ok = cand && (int64_t)carry_u + eu + nu <= pool_units && (int64_t)carry_c + ec + nwc <= wg_cap;
@@ -124,16 +132,16 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         // (round 0 reserves every image's region, a deferred candidate's as for the guess-write
         // path, so the image keeps it in a later round)
         const int64_t tb = i < n && desc[i].status == kPending ? (int64_t)desc[i].mbw * desc[i].mbh * desc[i].bpm : 0;
-        const bool gwr = gw && cand && desc[i].restart == 0, gwi = gwr && ok;
-        const int32_t gS = gwr ? (int32_t)((tb * 11 / 10 + nsub - 1) / nsub + 1) : 0;
-        const int64_t region = gwr ? nsub * gS : tb;
+        const bool gwr = gw && cand && (desc[i].restart == 0 || kint), gwi = gwr && ok;
+        const int32_t gS = gwr ? (int32_t)((tb * 11 / 10 + nlanes - 1) / nlanes + 1) : 0;
+        const int64_t region = gwr ? nlanes * gS : tb;
         const int na = round ? 0 : (int)min<int64_t>((region + kGwChunk - 1) / kGwChunk, INT32_MAX / 4);
         const int ea = block_exclusive_scan(na, sh);
         if (threadIdx.x == blockDim.x - 1) last[6] = ea + na;
         if (mine) {
             const Desc& d = desc[i];
             SpecImg& s = spec[i];
-            s.mode = ok ? (d.restart == 0 ? 1 : 3) : (cand && !last_round ? 4 : 0);
+            s.mode = ok ? (d.restart == 0 || kint ? 1 : 3) : (cand && !last_round ? 4 : 0);
             s.err = 0;
             s.nrepair = 0;
             s.ncount = 0;
@@ -144,7 +152,8 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             s.ulen = 0;
             s.scan_len = ok ? scan_len : 0;
             s.total_blocks = ok ? (int64_t)d.mbw * d.mbh * d.bpm : 0;
-            s.nint = ok && s.mode == 3 ? (int32_t)nsub : 0;
+            s.nint = ok && (s.mode == 3 || kint) ? (int32_t)nsub : 0;
+            s.kint = ok ? kint : 0;
             s.ntiles = nt;
             s.nwg = nw;
             s.gw_S = gS;
@@ -159,7 +168,8 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
             }
         }
         carry_d += __syncthreads_count(mine && !ok && cand && !last_round);  // deferred to the next round
-        carry_i += __syncthreads_count(ok && desc[i].restart != 0);        // restart-interval lanes (mode 3)
+        carry_i += __syncthreads_count(ok && desc[i].restart != 0 && !kint);  // restart-interval lanes (mode 3)
+        carry_k += __syncthreads_count(ok && kint);                         // interval-aligned guess-write lanes
         const int et = block_exclusive_scan(nt, sh);
         const int ew = block_exclusive_scan(nw, sh);
         const int ew2 = block_exclusive_scan(nw2, sh);
@@ -196,6 +206,7 @@ __global__ __launch_bounds__(1024) void k_spec_plan(int n, const uint8_t* __rest
         if (defer_out) {
             defer_out[0] = carry_d;
             defer_out[1] = carry_i;
+            defer_out[2] = carry_k;
         }
     }
 }
@@ -424,7 +435,7 @@ __global__ __launch_bounds__(256) void k_ustf_scan(int n, SpecImg* __restrict__ 
         s.nrst = rcarry;
         s.errpos = (fe != INT32_MAX && tiles[s.tile_base + fe].end_err) ? carry : INT64_MAX;
         const int64_t nsub = carry > 0 ? (carry + s.sub_bytes - 1) / s.sub_bytes : 1;
-        s.nsub = s.mode == 3 ? s.nint : (int32_t)nsub;
+        s.nsub = s.mode == 3 ? s.nint : (s.kint > 0 ? s.nint * s.kint : (int32_t)nsub);
     }
 }
 
@@ -764,7 +775,7 @@ __global__ __launch_bounds__(256) void k_ustf_one(int n, const uint8_t* __restri
                     s.nrst = (int32_t)ir;
                     s.errpos = own_end && end_err ? ulen : INT64_MAX;
                     const int64_t nsub = ulen > 0 ? (ulen + s.sub_bytes - 1) / s.sub_bytes : 1;
-                    s.nsub = s.mode == 3 ? s.nint : (int32_t)nsub;
+                    s.nsub = s.mode == 3 ? s.nint : (s.kint > 0 ? s.nint * s.kint : (int32_t)nsub);
                 }
             }
         }
@@ -1212,7 +1223,8 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                                                 int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                 int32_t* __restrict__ chunk_next, unsigned long long* __restrict__ pool_next,
                                                 int64_t pool_cap, uint64_t* __restrict__ X, GwOut* __restrict__ gwo,
-                                                RecState* __restrict__ rec, int lead) {
+                                                RecState* __restrict__ rec, int lead, const int64_t* __restrict__ rst,
+                                                int64_t rst_cap) {
     __shared__ WriteTab T;
 #ifdef ICX_EXP_GW8  // timing experiment only: 64-byte int8 slots (values truncated), 11-bit lead tables
     constexpr int kSQ = 4;  // 16-byte quarters per slot
@@ -1261,10 +1273,13 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         const Huff* H = desc[i].huff;
         const bool act = j < s.nsub;
         const int64_t f = (int64_t)s.wg_base * kLanes + (act ? j : 0);
-        const int64_t sb = (int64_t)s.sub_bytes * 8;
-        const int64_t start = j * sb, end = j == s.nsub - 1 ? s.ulen * 8 : (j + 1) * sb;
-        const int64_t ld = j == 0 ? 0 : (lead >= 0 ? lead : min(kGuessLead, s.sub_bytes * 2));
-        const int64_t s0 = act && start - ld > 0 ? start - ld : 0;
+        // (restart intervals: lane_span cuts each interval into s.kint lanes)
+        const LaneSpan ls = lane_span(act ? j : 0, s.nsub, s.sub_bytes, s.ulen, s.kint, s.nint, rst + (int64_t)i * rst_cap,
+                                      min<int64_t>(s.nrst, rst_cap));
+        const int64_t start = ls.start, end = ls.end;
+        const int64_t ld = ls.first ? 0 : (lead >= 0 ? lead : min(kGuessLead, s.sub_bytes * 2));
+        const int64_t s0 = act ? max(start - ld, ls.floor) : 0;
+        const int bmax = ls.bmax;  // (255, or 0 for an interval's last lane: it exits at an MCU start)
         const uint32_t kFar = 1u << 30;
         const uint32_t pre = act ? (uint32_t)(start - s0) : 0u, span = act ? (uint32_t)(end - s0) : 0u;
         Reader r;
@@ -1307,7 +1322,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         if (wave_any(live)) do {
             const bool bs = z == 0;
             const uint32_t u = r.used;
-            const bool leave = live && bs && u >= span;
+            const bool leave = live && bs && u >= span && b <= bmax;
             ul = leave ? u : ul;
             bl = leave ? b : bl;
             // (here, not sunk to the latch: there they keep the old b / used alive past their
@@ -1431,7 +1446,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
 __global__ __launch_bounds__(256) void k_gw_check(int n, SpecImg* __restrict__ spec, const int32_t* __restrict__ wpre,
                                                   const int32_t* __restrict__ totals, const uint64_t* __restrict__ X,
                                                   const GwOut* __restrict__ gwo, GcRec* __restrict__ crec,
-                                                  int2* __restrict__ clist) {
+                                                  int2* __restrict__ clist, const int64_t* __restrict__ rst, int64_t rst_cap) {
     const int total = totals[1];
     for (int wg = blockIdx.x; wg < total; wg += gridDim.x) {
         const int i = find_image(wpre, n, wg);
@@ -1440,7 +1455,10 @@ __global__ __launch_bounds__(256) void k_gw_check(int n, SpecImg* __restrict__ s
         const int64_t j = (int64_t)(wg - wpre[i]) * kLanes + threadIdx.x;
         if (j >= s.nsub) continue;
         const int64_t f = (int64_t)s.wg_base * kLanes + j;
-        const uint64_t entry = j == 0 ? pack_state(0, 0, 0) : X[f - 1];
+        // (an image's first lane, and a restart interval's: NanoJPEG's state is known there)
+        const LaneSpan ls = lane_span(j, s.nsub, s.sub_bytes, s.ulen, s.kint, s.nint, rst + (int64_t)i * rst_cap,
+                                      min<int64_t>(s.nrst, rst_cap));
+        const uint64_t entry = ls.first ? pack_state(ls.start, 0, 0) : X[f - 1];
         GcRec c;
         c.chunk0 = -1;
         c.pad_ = 0;
@@ -1489,20 +1507,29 @@ struct ChainSink {
     }
 };
 
+// A restart-interval image on the guess-write path that its lanes cannot decide exactly (k_gw_scan,
+// k_gw_repair): the interval lanes (mode 3) decide it, in place (k_spec_finish clears Desc::mapped).
+__device__ __forceinline__ void dri_gw_fallback(SpecImg& s) {
+    s.mode = 3;
+    s.nsub = s.nint;
+    s.err = 0;
+    s.dri_first = INT32_MAX;
+    s.tail_n = 0;
+}
+
 // One count lane (k_gw_count, k_gw_repair): from the true entry to the splice with the guess lane
 // (or its whole range), storing those blocks; *exit = its own exit when it did not splice.
 __device__ void gw_count_lane(const Desc& d, const SpecImg& s, const StepSet& SS, const uint8_t* U, int64_t j, int64_t f,
                               uint64_t entry, const GwOut& g, const RecState* rec, int16_t* ac, int32_t* dcv,
                               int32_t* chunk_next, unsigned long long* pool_next, int64_t pool_cap, GcRec* crec,
-                              uint64_t* exit, int32_t* give_up) {
+                              uint64_t* exit, int32_t* give_up, const int64_t* RS, int64_t nrst) {
     const Sel S = make_sel(d);
-    const int64_t sb = (int64_t)s.sub_bytes * 8;
-    const int64_t start = j * sb, end = j == s.nsub - 1 ? s.ulen * 8 : (j + 1) * sb;
+    const LaneSpan ls = lane_span(j, s.nsub, s.sub_bytes, s.ulen, s.kint, s.nint, RS, nrst);
     ChainSink sink{ac, dcv, chunk_next, pool_next, pool_cap, -1, -1, 0};
     GcRec c;
     c.pad_ = 0;
-    c.c = gc_walk(U + s.uoff, s.ulen, SS.write, d.huff, S, entry, start, end, rec, g.nrec,
-                  s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, sink, c.cds, &c.m, exit, &c.err);
+    c.c = gc_walk(U + s.uoff, s.ulen, SS.write, d.huff, S, entry, ls.start, ls.end, rec, g.nrec,
+                  s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8, sink, c.cds, &c.m, exit, &c.err, ls.bmax);
     c.chunk0 = sink.chunk0;
     if (c.m == -3) *give_up = 1;  // the pool ran out
     crec[f] = c;
@@ -1517,7 +1544,8 @@ __global__ __launch_bounds__(512) void k_gw_count(int n, const Desc* __restrict_
                                                   int32_t* __restrict__ dcv, int32_t* __restrict__ chunk_next,
                                                   unsigned long long* __restrict__ pool_next, int64_t pool_cap,
                                                   GcRec* __restrict__ crec, uint64_t* __restrict__ Y,
-                                                  const int2* __restrict__ clist, int32_t* __restrict__ repair) {
+                                                  const int2* __restrict__ clist, int32_t* __restrict__ repair,
+                                                  const int64_t* __restrict__ rst, int64_t rst_cap) {
     __shared__ StepSet SS;
     const int i = blockIdx.x;
     if (i >= n) return;
@@ -1533,10 +1561,12 @@ __global__ __launch_bounds__(512) void k_gw_count(int n, const Desc* __restrict_
         uint64_t ex = 0;
         int32_t give_up = 0;
         gw_count_lane(desc[i], s, SS, U, j, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, chunk_next, pool_next, pool_cap,
-                      crec, &ex, &give_up);
+                      crec, &ex, &give_up, rst + (int64_t)i * rst_cap, min<int64_t>(s.nrst, rst_cap));
         if (give_up) atomicOr(&s.err, kSpecGiveUp);
         Y[f] = ex;
-        if (crec[f].m < 0 && j + 1 < s.nsub && ex != X[f]) {  // no splice, another exit: repair walk
+        // no splice, another exit: repair walk (not into the next restart interval: its first lane
+        // starts in a known state)
+        if (crec[f].m < 0 && j + 1 < s.nsub && ex != X[f] && !(s.kint > 0 && (j + 1) % s.kint == 0)) {
             const int r = atomicAdd(&s.nrepair, 1);
             if (r < kMaxRepair) repair[(int64_t)i * kMaxRepair + r] = (int32_t)j;
         }
@@ -1551,12 +1581,20 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
                                                   const GwOut* __restrict__ gwo, const RecState* __restrict__ rec,
                                                   int16_t* __restrict__ ac, int32_t* __restrict__ dcv,
                                                   int32_t* __restrict__ chunk_next, unsigned long long* __restrict__ pool_next,
-                                                  int64_t pool_cap, GcRec* __restrict__ crec, int32_t* __restrict__ repair) {
+                                                  int64_t pool_cap, GcRec* __restrict__ crec, int32_t* __restrict__ repair,
+                                                  const int64_t* __restrict__ rst, int64_t rst_cap) {
     const int i = blockIdx.x;
     if (i >= n || threadIdx.x != 0) return;
     SpecImg& s = spec[i];
     if (s.mode != 1 || s.nrepair == 0) return;
-    if (s.nrepair > kMaxRepair) { s.mode = 2; return; }
+    const int64_t* RS = rst + (int64_t)i * rst_cap;
+    const int64_t nrst = min<int64_t>(s.nrst, rst_cap);
+    // (too long a walk: the sequential kernel; with restart intervals, their lanes -- mode 3)
+    auto give_up_walk = [&] {
+        if (s.kint > 0) dri_gw_fallback(s);
+        else s.mode = 2;
+    };
+    if (s.nrepair > kMaxRepair) { give_up_walk(); return; }
     int32_t* q = repair + (int64_t)i * kMaxRepair;
     const int nq = s.nrepair;
     for (int a = 1; a < nq; ++a) {  // insertion sort (short list)
@@ -1573,7 +1611,8 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
         X[base + j] = Y[base + j];
         int64_t k = j + 1;
         for (int steps_ = 0; k < s.nsub; ++k, ++steps_) {
-            if (steps_ >= kGwMaxWalk) { s.mode = 2; return; }
+            if (s.kint > 0 && k % s.kint == 0) break;  // a restart interval's first lane: synchronised
+            if (steps_ >= kGwMaxWalk) { give_up_walk(); return; }
             const int64_t f = base + k;
             if (gwo[f].g0 == X[f - 1]) {
                 GcRec c;
@@ -1584,8 +1623,8 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
             uint64_t ex = 0;
             int32_t give_up = 0;
             gw_count_lane(desc[i], s, steps[i], U, k, f, X[f - 1], gwo[f], rec + f * kRec, ac, dcv, chunk_next, pool_next,
-                          pool_cap, crec, &ex, &give_up);
-            if (give_up) { s.mode = 2; return; }
+                          pool_cap, crec, &ex, &give_up, RS, nrst);
+            if (give_up) { give_up_walk(); return; }
             if (crec[f].m >= 0 || k + 1 == s.nsub || ex == X[f]) break;
             X[f] = ex;
         }
@@ -1599,7 +1638,10 @@ __global__ __launch_bounds__(64) void k_gw_repair(int n, const Desc* __restrict_
 // exhausted pool send the image to the sequential kernel.
 __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc, SpecImg* __restrict__ spec,
                                                  const GwOut* __restrict__ gwo, const GcRec* __restrict__ crec,
-                                                 const RecState* __restrict__ rec, LaneEntry* __restrict__ ent) {
+                                                 const RecState* __restrict__ rec, LaneEntry* __restrict__ ent,
+                                                 const uint64_t* __restrict__ X, const uint64_t* __restrict__ Y,
+                                                 const uint8_t* __restrict__ U, const int64_t* __restrict__ rst,
+                                                 int64_t rst_cap) {
     __shared__ int sh[256];
     __shared__ int s_cnt, s_d0, s_d1, s_d2;
     __shared__ int s_bad;
@@ -1607,6 +1649,61 @@ __global__ __launch_bounds__(256) void k_gw_scan(int n, Desc* __restrict__ desc,
     if (i >= n) return;
     SpecImg& s = spec[i];
     if (s.mode != 1) return;
+    if (s.kint > 0) {
+        // Restart intervals (round 6): no scan across intervals -- interval m's first block is
+        // m R bpm and its DC predictors start at 0 -- one thread per interval chains its kint
+        // lanes. The result is NanoJPEG's exactly when every interval holds R MCUs ending at an MCU
+        // start in the byte before marker m, which is the expected FF D0+(m&7) at its recorded
+        // place (dri_end_kind: exact), with no decode error on the true path, and the last interval
+        // reaches the frame's last block. Anything else (corrupt or truncated data, missing
+        // markers, an exhausted pool) goes to the interval lanes (mode 3), which decide it.
+        const int64_t K = s.kint, nint = s.nint, base = (int64_t)s.wg_base * kLanes;
+        const int64_t iblk = (int64_t)desc[i].restart * desc[i].bpm;
+        const int64_t* RS = rst + (int64_t)i * rst_cap;
+        const int64_t nrst = min<int64_t>(s.nrst, rst_cap);
+        if (threadIdx.x == 0) s_bad = (s.err & kSpecGiveUp) != 0 || nrst < nint - 1;
+        __syncthreads();
+        const bool give_up = s_bad != 0;
+        for (int64_t m = threadIdx.x; m < nint && !give_up; m += blockDim.x) {
+            const int64_t G0 = m * iblk;
+            int32_t cnt = 0, p0 = 0, p1 = 0, p2 = 0;
+            bool bad = false;
+            for (int64_t ii = 0; ii < K; ++ii) {
+                const int64_t f = base + m * K + ii;
+                const GwOut g = gwo[f];
+                const GcRec c = crec[f];
+                int32_t d[3];
+                const int32_t nb = gw_lane_total(g, c, rec + f * kRec, d);
+                const int32_t e = gw_lane_err(g, c, rec + f * kRec);
+                LaneEntry le;
+                le.G = G0 + cnt;
+                le.p0 = p0;
+                le.p1 = p1;
+                le.p2 = p2;
+                le.pad = nb;
+                ent[f] = le;
+                if (e != INT32_MAX && le.G + e < s.total_blocks) bad = true;
+                cnt += nb;
+                p0 = wadd(p0, d[0]);
+                p1 = wadd(p1, d[1]);
+                p2 = wadd(p2, d[2]);
+                if (ii == K - 1 && m + 1 < nint) {  // the interval's end, where NanoJPEG reads marker m
+                    const uint64_t ex = c.m == -1 ? Y[f] : X[f];
+                    const int64_t em = RS[m] >> 3, p = st_pos(ex);
+                    if (st_b(ex) != 0 || p < em * 8 - 7 || p > em * 8) bad = true;
+                    if (dri_end_kind(U + s.uoff, s.ulen, s.errpos, em, m, RS[m]) != kDriExact) bad = true;
+                }
+            }
+            if (m + 1 < nint ? cnt != iblk : cnt < s.total_blocks - G0) bad = true;
+            if (bad) atomicOr(&s_bad, 1);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s.tail_n = 0;
+            if (s_bad) dri_gw_fallback(s);
+        }
+        return;
+    }
     if (s.err & kSpecGiveUp) {
         if (threadIdx.x == 0) { s.mode = 2; desc[i].mapped = 0; }
         return;
@@ -1809,7 +1906,7 @@ void launch_spec_entropy(const GroupWs& ws, int n, const uint8_t* d_data, const 
     if (part == kFrontRest) {  // round 0's tail: the restart-interval write only if its plan gave DRI lanes
         const bool known = hipEventSynchronize(ws.ev_defer) == hipSuccess;
         launch_spec_round(ws, n, d_data, d_off, st, hook, 0, rounds == 1,
-                          known && ws.h_defer[1] == 0 ? kRoundTailNoDri : kRoundTail);
+                          !known || ws.h_defer[1] != 0 ? kRoundTail : ws.h_defer[2] != 0 ? kRoundTailGw : kRoundTailNoDri);
         if (!known) return;
     }
     for (int r = part == kFrontRest ? 1 : 0; r < rounds; ++r) {
@@ -1841,10 +1938,15 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
     const char* gw_env = std::getenv("ICX_GW");
     const int gw = gw_env ? (std::atoi(gw_env) != 0) : ((int64_t)ws.max_w * ws.max_h > kGwMinPixels ? 1 : 0);
     const bool big = !gw && (std::getenv("ICX_BIG_WG") ? std::atoi(std::getenv("ICX_BIG_WG")) != 0 : true);
+    // restart intervals on the guess-write path (ICX_DRI_GW: 0 never, 1 from kSubBytesSmall bytes per
+    // interval; read per launch: tests run both paths)
+    const char* dri_env = std::getenv("ICX_DRI_GW");
+    const int dri_min = dri_env ? (std::atoi(dri_env) != 0 ? kSubBytesSmall : 0) : kDriGwMin;
     if (piece == kRoundAll || piece == kRoundHead) {
         B(kStUnstuff);
         hipLaunchKernelGGL(k_spec_plan, dim3(1), dim3(1024), 0, st, n, d_data, d_off, ws.desc, ws.spec, ws.tilepre, ws.wgpre, ws.wg2pre,
-                           ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw, round, last, ws.h_defer);
+                           ws.totals, ws.upool, ws.lanes_cap, sub_env, ws.pool_cap, ws.pool_next, gw, round, last, ws.h_defer,
+                           dri_min);
         (void)hipEventRecord(ws.ev_defer, st);
         if (round == 0)  // (an image's tables serve every round)
             hipLaunchKernelGGL(k_step_tabs, dim3(n), dim3(256), 0, st, n, ws.desc, ws.steps);
@@ -1870,22 +1972,25 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
             B(kStWrite);
             hipLaunchKernelGGL((k_gw_lane<kWriteLanesBig, false>), dim3(g), dim3(kWriteLanesBig), 0, st, n, ws.desc, ws.spec,
                                ws.wg2pre, ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap,
-                               ws.X, ws.gw, ws.rec, lead);
+                               ws.X, ws.gw, ws.rec, lead, ws.rst, ws.rst_cap);
             // (the CHK instance on a small grid: it usually finds no image of its own, and 2048
             // empty workgroups of 80 KB of LDS each waited ~0.5 ms for LDS beside the other pipeline)
             hipLaunchKernelGGL((k_gw_lane<kWriteLanesBig, true>), dim3(std::min(g, 128)), dim3(kWriteLanesBig), 0, st, n,
                                ws.desc, ws.spec,
                                ws.wg2pre, ws.totals, ws.steps, ws.U, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap,
-                               ws.X, ws.gw, ws.rec, lead);
+                               ws.X, ws.gw, ws.rec, lead, ws.rst, ws.rst_cap);
             E(kStWrite);
             B(kStEntropy);
             hipLaunchKernelGGL(k_gw_check, dim3(g), dim3(kLanes), 0, st, n, ws.spec, ws.wgpre, ws.totals, ws.X, ws.gw, ws.crec,
-                               ws.clist);
+                               ws.clist, ws.rst, ws.rst_cap);
             hipLaunchKernelGGL(k_gw_count, dim3(n), dim3(512), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.gw, ws.rec,
-                               ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair);
+                               ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.Y, ws.clist, ws.repair,
+                               ws.rst, ws.rst_cap);
             hipLaunchKernelGGL(k_gw_repair, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.gw,
-                               ws.rec, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.repair);
-            hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent);
+                               ws.rec, ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.crec, ws.repair, ws.rst,
+                               ws.rst_cap);
+            hipLaunchKernelGGL(k_gw_scan, dim3(n), dim3(256), 0, st, n, ws.desc, ws.spec, ws.gw, ws.crec, ws.rec, ws.ent, ws.X,
+                               ws.Y, ws.U, ws.rst, ws.rst_cap);
             hipLaunchKernelGGL(k_gw_tail, dim3(n), dim3(64), 0, st, n, ws.desc, ws.spec, ws.steps, ws.U, ws.X, ws.Y, ws.crec,
                                ws.ac, ws.dc, ws.chunk_next, ws.pool_next, ws.pool_cap, ws.map);
             hipLaunchKernelGGL(k_gw_map, dim3(g), dim3(kLanes), 0, st, n, ws.desc, ws.spec, ws.wgpre, ws.totals, ws.gw, ws.crec,
@@ -1929,7 +2034,10 @@ void launch_spec_round(const GroupWs& ws, int n, const uint8_t* d_data, const ui
     // (the non-big three-pass launch above took them) -- and the round's end
     if ((gw || big) && piece != kRoundTailNoDri) {
         B(kStWrite);  // (the write stage's second bracket: restart-interval lanes)
-        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(g), dim3(kLanes), 0, st, 3, n, ws.desc, ws.spec, ws.wgpre,
+        // (kRoundTailGw: only fallbacks of guess-write DRI images, rare; 2048 empty workgroups of
+        // 48 KB of LDS would cost as much as the CHK instance's did)
+        hipLaunchKernelGGL(k_spec_write<kLanes>, dim3(piece == kRoundTailGw ? std::min(g, 128) : g), dim3(kLanes), 0, st, 3,
+                           n, ws.desc, ws.spec, ws.wgpre,
                            ws.totals, ws.steps, ws.U, ws.X, ws.ent, ws.ac, ws.dc, ws.rst, ws.rst_cap);
         E(kStWrite);
     }

@@ -656,17 +656,92 @@ struct ErrBounds {
     }
 };
 
+// The fewest bits any MCU of the frame can take on a valid stream: per block the shortest DC code
+// plus its magnitude bits, plus the AC table's EOB code (a block without EOB holds 63 AC symbols).
+// Restart intervals go to the guess-write path only when this is at least 8 (lane_span's exit rule).
+ICX_HD int huff_count(const Huff& t, int L) { return (int)((t.bound[L] - t.bound[L - 1]) >> (16 - L)); }
+ICX_HD int min_mcu_bits(const Desc& d) {
+    int bits = 0;
+    for (int b = 0; b < d.bpm && b < kSpecMaxBpm; ++b) {
+        int sbx, sby;
+        const int ci = mcu_block_comp(d, b, sbx, sby);
+        const Huff& hd = d.huff[d.c[ci].dc_tab & 3];
+        const Huff& ha = d.huff[d.c[ci].ac_tab & 3];
+        int mdc = 64, eob = 63;
+        for (int L = 1; L <= 16; ++L) {
+            const int n = huff_count(hd, L), na = huff_count(ha, L);
+            for (int q = 0; q < n; ++q) {
+                const int v = L + (hd.sym[hd.first[L] + q] & 15);
+                mdc = v < mdc ? v : mdc;
+            }
+            for (int q = 0; q < na; ++q)
+                if (ha.sym[ha.first[L] + q] == 0 && L < eob) eob = L;
+        }
+        bits += mdc + eob;
+    }
+    return bits;
+}
+
+// Lane j's range in U bits and how it ends.
+//  * kint == 0 (no restart markers): lanes of sub_bytes, the last to the end of the data; a lane
+//    exits at its first block start at or after `end`.
+//  * kint > 0 (guess-write over restart intervals): interval m = j / kint runs from the byte after
+//    marker m-1 (RS[m-1] >> 3, plus its 2 bytes; byte 0 for m = 0) to marker m (RS[m] >> 3; the last
+//    interval to ulen), cut into kint lanes. The interval's first lane starts where NanoJPEG does
+//    after the marker (byte-aligned, b = 0, DC predictors 0: synchronised by construction); the
+//    others' lead stops at that point (`floor`). NanoJPEG's R MCUs end in the byte before the marker
+//    (jpeg_dec.h:707-715 byte-aligns there), and an MCU takes at least 8 bits (k_spec_plan only sends
+//    such images here), so the true path's first MCU start at or past bit 8 em - 7 is the
+//    interval's end: the interval's last lane exits at the first block start at or after `end`
+//    whose block-in-MCU is at most `bmax` (0: an MCU start). Missing markers give degenerate but
+//    bounded ranges; k_gw_scan then sends the image to the interval lanes (mode 3).
+struct LaneSpan {
+    int64_t start, end;  // bits
+    int64_t floor;       // a lead starts no earlier
+    int bmax;            // the exit's block-in-MCU is at most this
+    bool first;          // starts in a known state (b = 0, predictors 0)
+};
+ICX_HD LaneSpan lane_span(int64_t j, int64_t nsub, int64_t sub_bytes, int64_t ulen, int kint, int64_t nint,
+                          const int64_t* RS, int64_t nrst) {
+    LaneSpan L;
+    if (kint <= 0) {
+        L.start = j * sub_bytes * 8;
+        L.end = j == nsub - 1 ? ulen * 8 : (j + 1) * sub_bytes * 8;
+        L.floor = 0;
+        L.bmax = 255;
+        L.first = j == 0;
+        return L;
+    }
+    const int64_t m = j / kint, ii = j - m * kint;
+    auto at = [&](int64_t k) { return k < nrst ? (RS[k] >> 3) : ulen; };  // marker k's byte (missing: the end)
+    const int64_t sm = m == 0 ? 0 : (at(m - 1) + 2 < ulen ? at(m - 1) + 2 : ulen);
+    const int64_t em = m + 1 < nint ? (at(m) > sm ? at(m) : sm) : ulen;
+    const int64_t len = em - sm, sub = (len + kint - 1) / kint > 0 ? (len + kint - 1) / kint : 1;
+    const int64_t st = sm + ii * sub < em ? sm + ii * sub : em;
+    L.start = st * 8;
+    L.floor = sm * 8;
+    L.first = ii == 0;
+    if (ii == kint - 1 && m + 1 < nint) {
+        L.end = em * 8 - 7 > L.start ? em * 8 - 7 : L.start;
+        L.bmax = 0;
+    } else {
+        L.end = (ii == kint - 1 ? em : (sm + (ii + 1) * sub < em ? sm + (ii + 1) * sub : em)) * 8;
+        L.bmax = 255;
+    }
+    return L;
+}
+
 // Count lane (write tables): from the true entry (a block start), store every block through
 // `sink` until the first MCU start the guess lane recorded (*m = its index: from there on the guess
 // lane's blocks are the true ones) or -- no such state -- the first block start at or after `end`
-// (*m = -1, *exit = that state). sink.begin(t) readies block t (false: no pool left, the walk
+// whose block-in-MCU is at most bmax (lane_span; *m = -1, *exit = that state). sink.begin(t) readies block t (false: no pool left, the walk
 // stops with *m = -3), sink.cell(t, zz, v) stores a coefficient, sink.dc(t, v) the block's
 // lane-local DC, cumulative from the entry. Returns the blocks stored, *cds their DC sums, *err
 // the first block whose decode failed (INT32_MAX: none; error semantics as k_spec_write's).
 template <class Sink>
 ICX_HD int32_t gc_walk(const uint8_t* U, int64_t ulen, const WriteTab& TW, const Huff* H, const Sel& S, uint64_t entry,
                        int64_t start, int64_t end, const RecState* rec, int nrec, int64_t errbits, Sink& sink,
-                       int32_t* cds, int* m, uint64_t* exit, int32_t* err) {
+                       int32_t* cds, int* m, uint64_t* exit, int32_t* err, int bmax = 255) {
     Reader r;
     r.init(U, ulen, st_pos(entry));
     ErrBounds eb;
@@ -683,7 +758,7 @@ ICX_HD int32_t gc_walk(const uint8_t* U, int64_t ulen, const WriteTab& TW, const
                 while (mi < nrec && (int64_t)rec[mi].rel < p - start) ++mi;
                 if (mi < nrec && (int64_t)rec[mi].rel == p - start) { *m = mi; return t; }
             }
-            if (p >= end) { *m = -1; *exit = pack_state(p, b, 0); return t; }
+            if (p >= end && b <= bmax) { *m = -1; *exit = pack_state(p, b, 0); return t; }
             ci = S.comp(b);
             if (!sink.begin(t)) { *m = -3; return t; }
         }

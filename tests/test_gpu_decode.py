@@ -285,6 +285,52 @@ def test_dri_corrupt_markers_decided_in_parallel(ctx):
     b.close()
 
 
+@pytest.mark.parametrize("gw_env", ["1", "0"])
+def test_dri_guess_write_lanes_bit_exact(ctx, monkeypatch, gw_env):
+    """Restart intervals on the guess-write path (ICX_GW=1 with ICX_DRI_GW=1: intervals from 512
+    unstuffed bytes, cut into interval-aligned lanes, k_spec_plan/lane_span): long and short
+    intervals, one batch, every sampling -- bit-exact against the oracle, all on the parallel path.
+    ICX_DRI_GW=0 runs the same batch on the interval lanes alone."""
+    monkeypatch.setenv("ICX_GW", "1")
+    monkeypatch.setenv("ICX_DRI_GW", gw_env)
+    specs = [(1024, 768, "420", 64), (1000, 1000, "420", 1000), (640, 487, "444", 64), (800, 600, "422", 50),
+             (777, 555, "gray", 97), (1024, 1024, "420", 7), (512, 512, "420", 1), (1023, 999, "444", 300)]
+    jpegs = [S.synth_jpeg(4400 + k, w, h, smp, 60 + 5 * k, r) for k, (w, h, smp, r) in enumerate(specs)]
+    b = icx.Batch(ctx, len(jpegs), 1024, 1024)
+    res = b.decode_host(jpegs)
+    stats = b.path_stats()
+    assert stats == {"parallel": len(jpegs), "fallback": 0, "sequential": 0}, stats
+    for j, (code, w, h, n, pix) in zip(jpegs, res):
+        ocode, ow, oh, on, opix = O.decode(j)
+        assert code == ocode == 0 and (w, h, n) == (ow, oh, on)
+        assert pix.tobytes() == opix
+    b.close()
+
+
+def test_dri_guess_write_corrupt_markers(ctx, monkeypatch):
+    """Corrupt restart markers, flipped data and truncation on the guess-write DRI lanes: an image
+    its lanes cannot decide exactly falls back to the interval lanes (dri_gw_fallback), which give
+    NanoJPEG's status; the ones that stay OK match the oracle byte for byte. Nothing goes to the
+    sequential kernel."""
+    monkeypatch.setenv("ICX_GW", "1")
+    monkeypatch.setenv("ICX_DRI_GW", "1")
+    rng = np.random.default_rng(43)
+    cases = []
+    for seed, (w, h, smp, r) in enumerate([(640, 480, "420", 40), (640, 480, "444", 80), (640, 480, "gray", 40),
+                                           (512, 512, "422", 64)]):
+        cases += dri_corruptions(S.synth_jpeg(4500 + seed, w, h, smp, 85, r), rng, 24)
+    b = icx.Batch(ctx, len(cases), 640, 512)
+    res = b.decode_host(cases)
+    stats = b.path_stats()
+    assert stats["sequential"] == 0, stats
+    for j, (code, w, h, n, pix) in zip(cases, res):
+        ocode, _, _, _, opix = O.decode(j)
+        assert code == ocode
+        if code == 0:
+            assert pix.tobytes() == opix
+    b.close()
+
+
 def test_dri_marker_read_elsewhere_falls_back_exactly(ctx):
     """FF D0+(j&7) at interval j's end that is stuffed data, not marker j: NanoJPEG resumes there,
     where no lane started, so that image alone goes to the sequential kernel -- with NanoJPEG's
