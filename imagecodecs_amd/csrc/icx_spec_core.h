@@ -661,23 +661,28 @@ struct ErrBounds {
 // Restart intervals go to the guess-write path only when this is at least 8 (lane_span's exit rule).
 ICX_HD int huff_count(const Huff& t, int L) { return (int)((t.bound[L] - t.bound[L - 1]) >> (16 - L)); }
 ICX_HD int min_mcu_bits(const Desc& d) {
-    int bits = 0;
+    // (per Huffman table once: the shortest DC code + its category's bits, the EOB code's length)
+    int tmin[8], done = 0, bits = 0;
     for (int b = 0; b < d.bpm && b < kSpecMaxBpm; ++b) {
         int sbx, sby;
         const int ci = mcu_block_comp(d, b, sbx, sby);
-        const Huff& hd = d.huff[d.c[ci].dc_tab & 3];
-        const Huff& ha = d.huff[d.c[ci].ac_tab & 3];
-        int mdc = 64, eob = 63;
-        for (int L = 1; L <= 16; ++L) {
-            const int n = huff_count(hd, L), na = huff_count(ha, L);
-            for (int q = 0; q < n; ++q) {
-                const int v = L + (hd.sym[hd.first[L] + q] & 15);
-                mdc = v < mdc ? v : mdc;
+        const int td = d.c[ci].dc_tab & 3, ta = 4 + (d.c[ci].ac_tab & 3);
+        for (int t : {td, ta}) {
+            if (done >> t & 1) continue;
+            const Huff& h = d.huff[t & 3];
+            int m = 64;
+            for (int L = 1; L <= 16 && L < m; ++L) {
+                const int n = huff_count(h, L);
+                for (int q = 0; q < n; ++q) {
+                    const int sym = h.sym[h.first[L] + q];
+                    const int v = t < 4 ? L + (sym & 15) : (sym == 0 ? L : 64);
+                    m = v < m ? v : m;
+                }
             }
-            for (int q = 0; q < na; ++q)
-                if (ha.sym[ha.first[L] + q] == 0 && L < eob) eob = L;
+            tmin[t] = m;
+            done |= 1 << t;
         }
-        bits += mdc + eob;
+        bits += tmin[td] + tmin[ta];
     }
     return bits;
 }
