@@ -1899,6 +1899,9 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
 #ifndef ICX_F5_PF
 #define ICX_F5_PF 1
 #endif
+#ifndef ICX_F5_QV  // 1: the quantisation table in VGPRs (168 VGPRs, no v_readlane): C3 -1.1%
+#define ICX_F5_QV 0
+#endif
 constexpr int kFB5 = ICX_FB5;
 __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                                    const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
@@ -1910,10 +1913,15 @@ __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* 
     __shared__ __attribute__((aligned(16))) uint32_t Yl_all[4][16][64];  // per wave: 16 luma rows x 256 pixels
     const int wave = wave_index(), lane = threadIdx.x & 63, mq = lane >> 2, k = lane & 3, sbx = k & 1, sby = k >> 1;
     uint32_t (*Yl)[64] = Yl_all[wave];
-    uint32_t qw[16];  // (wave-uniform: scalar registers, read by SDWA)
+    uint32_t qw[16];
     load_qw_g(d.q[d.c[0].tq], qw);
+#if ICX_F5_QV  // in vector registers, read by SDWA (in scalar registers they were spilled to VGPR lanes: 63 v_readlane per block)
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) asm volatile("" : "+v"(qw[k2]));
+#else
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) qw[k2] = __builtin_amdgcn_readfirstlane(qw[k2]);
+#endif
     const int W = d.W, H = d.H, mbw = d.mbw, mbh = d.mbh;
     const uint8_t* pslot = planes + (int64_t)img * plane_cap;
     const CPl c1{pslot + comp_plane_off(d, 1), d.c[1].w, d.c[1].h, d.c[1].stride};
@@ -2285,8 +2293,11 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
                            ws.plane_cap);
     }
     if (fuse == 4 || fuse == 5) {  // 4:2:0: 64 blocks of a block row per wave unit, luma (mode 4) then chroma units
+        // (units per wave: ICX_IDCT1_UPW, at least; small images' waves otherwise take one unit
+        // each and its dependent map -> block -> store latency alone)
+        static const int upw = std::getenv("ICX_IDCT1_UPW") ? std::max(1, std::atoi(std::getenv("ICX_IDCT1_UPW"))) : 1;
         const int64_t units = (maxblk / 6) * (fuse == 4 ? 6 : 2) / 64 + 3;
-        const int sgx = (int)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 16384 / n)) & ~7;
+        const int sgx = (int)std::max<int64_t>(1, std::min<int64_t>((units + 4 * upw - 1) / (4 * upw), 16384 / n)) & ~7;
         hipLaunchKernelGGL(k_idct420s, dim3(std::max(sgx, 8), n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map,
                            ws.planes, ws.plane_cap, fuse == 4 ? 1 : 0);
     }
@@ -2321,7 +2332,8 @@ void launch_decode_back(const GroupWs& ws, int n, uint8_t* d_out, uint64_t out_s
                            ws.plane_cap, d_out, out_stride);
     if (fuse == 5) {
         const int64_t fs = ((int64_t)(ws.max_w + 255) / 256) * ((ws.max_h + 16 * kFB5 - 1) / (16 * kFB5));
-        int f5 = (int)std::max<int64_t>(1, std::min<int64_t>((fs + 3) / 4, 16384 / n));
+        static const int spw = std::getenv("ICX_F5_SPW") ? std::max(1, std::atoi(std::getenv("ICX_F5_SPW"))) : 1;
+        int f5 = (int)std::max<int64_t>(1, std::min<int64_t>((fs + 4 * spw - 1) / (4 * spw), 16384 / n));
         if (f5 >= 8) f5 &= ~7;  // (XCD-aware strip order needs a multiple of 8)
         hipLaunchKernelGGL(k_fused420s, dim3(f5, n), dim3(256), 0, st, ws.desc, ws.ac, ws.dc, ws.map, ws.planes,
                            ws.plane_cap, d_out, out_stride);

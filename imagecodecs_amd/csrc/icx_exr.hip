@@ -32,18 +32,302 @@
 
 namespace icx {
 
+// ------------------------------------------------------------ the wave's inflate (round 6)
+// exr_inflate (icx_exr_core.h) with the same decisions, error checks and result, laid out for one
+// wave whose decoder state is wave-uniform (SGPRs), without the per-byte memory round trips that
+// bounded round 5's version (~860 cycles per output byte: a chunk of 256 KiB took ~90 ms):
+//  * input: a 512-byte window in registers (one dword per lane of [wb, wb+256) and of the next
+//    256 bytes, loaded 256 bytes ahead); a refill is two v_readlane and a funnel shift, not four
+//    dependent byte loads from HBM.
+//  * output: bytes go to the W-byte LDS ring only; every 4 KiB completed the wave copies them to
+//    the chunk's scratch with 16-byte stores.
+//  * matches: the wave copies all bytes of a match at once, lane k byte k (64 per round), from the
+//    ring (distance + length <= W) or from the flushed output (farther back); byte k's source is
+//    out - dist + (k mod dist), a byte from before the match, so a repeat (dist < length) needs no
+//    ordering between lanes.
+//  * Adler-32 over the output afterwards, by the wave in parallel (in round 5 four dependent adds
+//    and a counter per output byte).
+// Input bytes past the chunk read as 0 and are counted (`over`), as BitIn does.
+// 32-bit positions (a chunk and its output below 1 GiB; larger ones take exr_inflate).
+struct InW {
+    const uint8_t* A;    // the chunk's bytes rounded down to 4
+    uint32_t n, e;       // bytes; e = n + mis, the end relative to A
+    uint32_t wb;         // window start relative to A (multiple of 256)
+    uint32_t cur, nxt;   // this lane's dword of [wb, wb + 256) and [wb + 256, wb + 512)
+    uint32_t pos;        // next byte (relative to the chunk) into buf
+    uint32_t mis;
+    uint64_t buf;        // LSB-first bit buffer
+    int cnt;
+    uint32_t over;
+    __device__ __forceinline__ uint32_t ld(uint32_t base) const {  // dword lane of [base, base + 256) (relative to A)
+        const uint32_t a = base + 4u * __lane_id();
+        if (a + 4u <= e) return *reinterpret_cast<const uint32_t*>(A + a);
+        uint32_t v = 0;
+        for (uint32_t j = 0; j < 4; ++j)
+            if (a + j < e) v |= (uint32_t)A[a + j] << (8 * j);
+        return v;
+    }
+    __device__ __forceinline__ void init(const uint8_t* src, uint32_t nb) {
+        mis = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3u);
+        A = src - mis;
+        n = nb;
+        e = nb + mis;
+        wb = 0;
+        cur = ld(0);
+        nxt = ld(256);
+        pos = 0;
+        buf = 0;
+        cnt = 0;
+        over = 0;
+    }
+    __device__ __forceinline__ void fill(int k) {  // k <= 32
+        if (cnt >= k) return;
+        const uint32_t p = pos + mis;
+        while (p >= wb + 256u) {  // (wave-uniform) the next window; its successor's load goes out now
+            cur = nxt;
+            wb += 256u;
+            nxt = ld(wb + 256u);
+        }
+        const uint32_t o = p - wb, i0 = o >> 2;
+        const uint32_t v0 = __builtin_amdgcn_readlane(cur, i0);
+        const uint32_t v1 = i0 == 63u ? __builtin_amdgcn_readlane(nxt, 0) : __builtin_amdgcn_readlane(cur, i0 + 1u);
+        const uint32_t w = __builtin_amdgcn_alignbyte(v1, v0, o & 3u);
+        if (pos + 4u > n) over += 8u * (pos + 4u - max(pos, n));  // (bytes at or past n read as 0: ld does not load them)
+        buf |= (uint64_t)w << cnt;
+        pos += 4u;
+        cnt += 32;
+    }
+    __device__ __forceinline__ uint32_t bits(int k) {  // k <= 24
+        fill(k);
+        const uint32_t v = (uint32_t)buf & ((1u << k) - 1u);
+        buf >>= k;
+        cnt -= k;
+        return v;
+    }
+    __device__ __forceinline__ bool past_end() const { return over > (uint32_t)cnt; }
+};
+// inf_decode for the wave: a code longer than kInfFast bits is found from the per-length limits
+// (the six reads are independent: one LDS round trip, where inf_decode's walk read the counts one
+// dependent length at a time). The same symbol or -1 as inf_decode.
+__device__ __forceinline__ int inf_decode_w(InW& in, const InfTab& h) {
+    in.fill(16);
+    const uint32_t e = exr_uni(h.fast[(uint32_t)in.buf & ((1u << kInfFast) - 1u)]);
+    if (e) {
+        in.buf >>= e & 15u;
+        in.cnt -= (int)(e & 15u);
+        return (int)(e >> 4);
+    }
+    // the next 15 stream bits, the first as the most significant (a canonical code's bit order)
+    const uint32_t r = __builtin_bitreverse32((uint32_t)in.buf) >> 17;
+    uint32_t lim[16];
+#pragma unroll
+    for (int l = kInfFast + 1; l <= 15; ++l) lim[l] = exr_uni(h.lim[l]);
+#pragma unroll
+    for (int l = kInfFast + 1; l <= 15; ++l) {
+        const uint32_t c = r >> (15 - l);
+        if (c < lim[l]) {  // (no shorter code matched: c >= the length's first code)
+            in.buf >>= l;
+            in.cnt -= l;
+            return (int)exr_uni(h.sym[(int)exr_uni((uint32_t)(int32_t)h.off[l]) + (int)c]);
+        }
+    }
+    return -1;
+}
+static_assert(kInfFast == 9, "inf_decode_w starts the long codes at 10 bits");
+
+// RFC 1951 length / distance bases and extra bits by arithmetic (Deflate's tables, without a
+// memory load whose wait would also wait for the flushes' stores)
+__device__ __forceinline__ uint32_t len_ext(uint32_t li) { return li < 8u || li == 28u ? 0u : (li - 4u) >> 2; }
+__device__ __forceinline__ uint32_t len_base(uint32_t li) {
+    return li < 8u ? 3u + li : li == 28u ? 258u : ((4u + ((li - 4u) & 3u)) << len_ext(li)) + 3u;
+}
+__device__ __forceinline__ uint32_t dist_ext(uint32_t di) { return di < 4u ? 0u : (di - 2u) >> 1; }
+__device__ __forceinline__ uint32_t dist_base(uint32_t di) { return di < 4u ? 1u + di : ((2u + (di & 1u)) << dist_ext(di)) + 1u; }
+
+template <int W>
+__device__ __forceinline__ bool exr_inflate_wave(const uint8_t* src, int64_t n64, uint8_t* dst, int64_t cap64, int64_t* produced, InfState& st,
+                                 uint8_t* ring) {
+    static_assert(W >= 1024 && (W & (W - 1)) == 0, "a power-of-two ring of at least 1 KiB");
+    *produced = 0;
+    if (n64 < 2) return false;
+    if (n64 >= (int64_t)1 << 30 || cap64 >= (int64_t)1 << 30) return exr_inflate<W>(src, n64, dst, cap64, produced, st, ring);
+    const uint32_t n = (uint32_t)n64, cap = (uint32_t)cap64;
+    const uint32_t lane = __lane_id();
+    const uint32_t cmf = exr_uni(src[0]), flg = exr_uni(src[1]);
+    if ((cmf * 256u + flg) % 31u != 0 || (flg & 32u) || (cmf & 15u) != 8) return false;
+    InW in;
+    in.init(src, n);
+    (void)in.bits(16);  // (the two header bytes)
+    uint32_t out = 0, fl = 0;  // bytes out; bytes copied to dst (multiple of 256 until the end)
+    // (output past cap fails the chunk; it is found here, before any byte past cap is stored, and at
+    // the end -- the same result as exr_inflate's test per byte)
+    bool over_cap = false;
+    // kFlush bytes from fl, 16 per lane and store (wave-uniform; readfirstlane keeps fl a scalar).
+    // Large, so that the input window's loads seldom wait behind flush stores (one vmcnt counts both).
+    constexpr uint32_t kFlush = 4096;
+    static_assert(W >= 4 * (int)kFlush, "unflushed bytes and the near-match window fit the ring");
+    auto flush1 = [&]() {
+        over_cap = over_cap || fl + kFlush > cap;
+        if (over_cap) return;
+#pragma unroll
+        for (uint32_t q = 0; q < kFlush / 1024u; ++q) {
+            const uint32_t o = fl + 1024u * q + 16u * lane;
+            const uint4 v = *reinterpret_cast<const uint4*>(ring + (o & (W - 1)));
+            *reinterpret_cast<uint4*>(dst + o) = v;
+        }
+        fl = exr_uni(fl + kFlush);
+    };
+    auto flush = [&]() {  // (a literal or a match completes at most one block)
+        if (out - fl >= kFlush) flush1();
+    };
+    auto lit = [&](uint32_t b) {
+        if (lane == 0) ring[out & (W - 1)] = (uint8_t)b;
+        out = exr_uni(out + 1u);
+        if (out - fl >= kFlush) flush1();
+    };
+    int last = 0;
+    while (!last) {
+        last = (int)in.bits(1);
+        const uint32_t type = in.bits(2);
+        if (type == 0) {  // stored
+            in.bits(in.cnt & 7);
+            const uint32_t len = in.bits(16), nlen = in.bits(16);
+            if (in.past_end() || (len ^ 0xFFFFu) != nlen) return false;
+            if (out + len > cap) return false;
+            for (uint32_t k = 0; k < len; ++k) {
+                const uint32_t b = in.bits(8);
+                if (in.past_end()) return false;
+                lit(b);
+            }
+            continue;
+        }
+        if (type == 3) return false;
+        if (type == 1) {  // fixed codes
+            for (int s = 0; s < 288; ++s) st.len[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+            (void)inf_build(st.lit, st.len, 288);
+            for (int s = 0; s < 32; ++s) st.len[s] = 5;
+            (void)inf_build(st.dist, st.len, 32);
+        } else {  // dynamic codes
+            const int nlen = (int)in.bits(5) + 257, ndist = (int)in.bits(5) + 1, ncode = (int)in.bits(4) + 4;
+            if (nlen > 286 || ndist > 30) return false;
+            for (int k = 0; k < 19; ++k) st.len[Deflate::kClOrder[k]] = k < ncode ? (uint8_t)in.bits(3) : 0;
+            if (in.past_end() || !inf_build(st.lit, st.len, 19)) return false;
+            int k = 0;
+            while (k < nlen + ndist) {
+                const int sym = inf_decode_w(in, st.lit);
+                if (sym < 0 || in.past_end()) return false;
+                if (sym < 16) {
+                    st.len[k++] = (uint8_t)sym;
+                    continue;
+                }
+                uint8_t v = 0;
+                int rep;
+                if (sym == 16) {
+                    if (k == 0) return false;
+                    v = (uint8_t)exr_uni(st.len[k - 1]);
+                    rep = 3 + (int)in.bits(2);
+                } else if (sym == 17) {
+                    rep = 3 + (int)in.bits(3);
+                } else {
+                    rep = 11 + (int)in.bits(7);
+                }
+                if (k + rep > nlen + ndist) return false;
+                while (rep--) st.len[k++] = v;
+            }
+            if (in.past_end()) return false;
+            if (!inf_build(st.lit, st.len, nlen) || !inf_build(st.dist, st.len + nlen, ndist)) return false;
+        }
+        for (;;) {
+            // (reading past the input makes past_end() true for good, and every path from there
+            // fails: it is tested at the block's end, at each match and before the trailer, not
+            // per literal)
+            const int sym = inf_decode_w(in, st.lit);
+            if (sym < 0) return false;
+            if (sym < 256) {
+                if (lane == 0) ring[out & (W - 1)] = (uint8_t)sym;
+                out = exr_uni(out + 1u);
+                if (out - fl >= kFlush) {
+                    flush1();
+                    if (over_cap || in.past_end()) return false;  // (also ends a run of literals past the input)
+                }
+                continue;
+            }
+            if (in.past_end() || over_cap) return false;
+            if (sym == 256) break;
+            const uint32_t li = (uint32_t)sym - 257u;
+            if (li >= 29u) return false;
+            const uint32_t len = len_base(li) + in.bits((int)len_ext(li));
+            const int di = inf_decode_w(in, st.dist);
+            if (di < 0 || di >= 30) return false;
+            const uint32_t dist = dist_base((uint32_t)di) + in.bits((int)dist_ext((uint32_t)di));
+            if (in.past_end() || dist > out) return false;
+            if (out + len > cap) return false;
+            // the match, 64 bytes per round: sources from before `out` only (see above); from the
+            // ring while none of them can have been overwritten by this match's own bytes, else
+            // from dst (dist > W - len >= kFlush + 258: every source byte is flushed)
+            const uint32_t q0 = out - dist;
+            if (dist + len <= (uint32_t)W) {
+                if (dist >= len) {
+                    for (uint32_t k = lane; k < len; k += 64u) ring[(out + k) & (W - 1)] = ring[(q0 + k) & (W - 1)];
+                } else {
+                    for (uint32_t k = lane; k < len; k += 64u) ring[(out + k) & (W - 1)] = ring[(q0 + k % dist) & (W - 1)];
+                }
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flushes' stores)
+                for (uint32_t k = lane; k < len; k += 64u) ring[(out + k) & (W - 1)] = dst[q0 + k];
+            }
+            out = exr_uni(out + len);
+            flush();
+        }
+    }
+    if (over_cap || out > cap) return false;
+    // the last bytes (fewer than kFlush): whole dwords, then the tail
+    const uint32_t o4 = out & ~3u;
+    for (uint32_t k = fl + 4u * lane; k < o4; k += 256u)
+        *reinterpret_cast<uint32_t*>(dst + k) = *reinterpret_cast<const uint32_t*>(ring + (k & (W - 1)));
+    if (o4 + lane < out) dst[o4 + lane] = ring[(o4 + lane) & (W - 1)];
+    in.bits(in.cnt & 7);  // to a byte boundary
+    uint32_t adler = 0;
+    for (int k = 0; k < 4; ++k) adler = (adler << 8) | in.bits(8);
+    if (in.past_end()) return false;
+    // Adler-32 of the output: a = 1 + sum b_i, b = out + sum (out - i) b_i (mod 65521)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint64_t s1 = 0, s2 = 0;
+    for (uint32_t i = 4u * lane; i < out; i += 256u) {
+        const bool whole = i + 4u <= out;
+        const uint32_t v = whole ? *reinterpret_cast<const uint32_t*>(dst + i) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t b = whole ? (v >> (8 * j)) & 255u : (i + j < out ? (uint32_t)dst[i + j] : 0u);
+            s1 += b;
+            s2 += (uint64_t)(out - (i + j)) * b;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+    }
+    const uint32_t a1 = (uint32_t)((1 + s1) % 65521u), a2 = (uint32_t)((s2 + (uint64_t)out) % 65521u);
+    if (exr_uni(adler) != exr_uni((a2 << 16) | a1)) return false;
+    *produced = out;
+    return true;
+}
+
 // Per compressed chunk (of any image of the call: `file` is the first file's device address, a
-// chunk's own at + c.base): decompress (lane 0), then the predictor as a workgroup prefix sum.
-// One wave per chunk, a 16 KiB LDS ring (exr_inflate<kExrWinDev>): ~20 KiB of LDS, so eight chunks
-// per CU inflate at once (four with the 32 KiB window and 256-thread workgroups: 375 MP/s at the
-// exr bench before).
-constexpr int kExrWinDev = 16384;
+// chunk's own at + c.base): decompress (the wave: exr_inflate_wave; RLE: lane 0), then the
+// predictor as a workgroup prefix sum. One wave per chunk and a W-byte LDS ring: ~20 KiB of LDS
+// with the 16 KiB ring, eight chunks per CU at once.
+#ifndef ICX_EXR_WIN
+#define ICX_EXR_WIN 16384
+#endif
+constexpr int kExrWinDev = ICX_EXR_WIN;
 constexpr int kUnpackThreads = 64;
 __global__ __launch_bounds__(kUnpackThreads) void k_exr_unpack(const uint8_t* __restrict__ file, ExrChunk* __restrict__ ch,
                                                     const int32_t* __restrict__ list, uint8_t* __restrict__ scratch,
                                                     int32_t* __restrict__ fail) {
     __shared__ InfState st;
-    __shared__ uint8_t win[kExrWinDev];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kExrWinDev];  // (dword reads: exr_inflate_wave's flush)
     __shared__ uint32_t part[kUnpackThreads];
     __shared__ int64_t produced;
     ExrChunk& c = ch[list[blockIdx.x]];
@@ -51,8 +335,8 @@ __global__ __launch_bounds__(kUnpackThreads) void k_exr_unpack(const uint8_t* __
     const uint8_t* f = file + c.base + c.src;
     bool ok = true;
     int64_t m = 0;
-    if (c.mode == 1) {  // (wave-uniform) the whole wave runs the inflate, lane 0 stores
-        ok = exr_inflate<kExrWinDev>(f, c.len, t, c.out_len, &m, st, win);
+    if (c.mode == 1) {  // (wave-uniform) the whole wave runs the inflate
+        ok = exr_inflate_wave<kExrWinDev>(f, c.len, t, c.out_len, &m, st, win);
     } else if (threadIdx.x == 0) {
         ok = exr_unrle(f, c.len, t, c.out_len);
         m = c.out_len;
@@ -68,24 +352,43 @@ __global__ __launch_bounds__(kUnpackThreads) void k_exr_unpack(const uint8_t* __
     __syncthreads();
     m = produced;
     if (m == 0) return;
-    // t'[i] = t[0] + sum_{k=1..i} (t[k] - 128) mod 256: each thread one contiguous segment
-    const int64_t seg = (m + kUnpackThreads - 1) / kUnpackThreads;
+#ifdef ICX_EXP_NOPRED  // timing experiment only: the inflate alone (output left predicted)
+    return;
+#endif
+    // t'[i] = t[0] + sum_{k=1..i} (t[k] - 128) mod 256: each thread one contiguous segment of whole
+    // dwords (t is 16-byte aligned), read and written a dword at a time
+    const int64_t seg = ((m + kUnpackThreads - 1) / kUnpackThreads + 3) & ~(int64_t)3;
     const int64_t a = min<int64_t>(m, (int64_t)threadIdx.x * seg), b = min<int64_t>(m, a + seg);
     uint32_t sum = 0;
-    for (int64_t k = a; k < b; ++k) sum += k == 0 ? t[0] : (uint32_t)t[k] - 128u;
+    int64_t k = a;
+    for (; k + 4 <= b; k += 4) sum = __builtin_amdgcn_sad_u8(*reinterpret_cast<const uint32_t*>(t + k), 0u, sum);
+    for (; k < b; ++k) sum += t[k];
+    sum -= 128u * (uint32_t)(b - a);
+    if (a == 0 && b > 0) sum += 128u;  // (t[0] enters as it is)
     part[threadIdx.x] = sum;
     __syncthreads();
     if (threadIdx.x == 0) {  // (64 partial sums: a serial scan is cheap next to the inflate)
         uint32_t run = 0;
-        for (int k = 0; k < kUnpackThreads; ++k) {
-            const uint32_t v = part[k];
-            part[k] = run;
+        for (int q = 0; q < kUnpackThreads; ++q) {
+            const uint32_t v = part[q];
+            part[q] = run;
             run += v;
         }
     }
     __syncthreads();
     uint32_t run = part[threadIdx.x];
-    for (int64_t k = a; k < b; ++k) {
+    for (k = a; k + 4 <= b; k += 4) {
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(t + k);
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t x = (v >> (8 * j)) & 255u;
+            run += k + j == 0 ? x : x - 128u;
+            o |= (run & 255u) << (8 * j);
+        }
+        *reinterpret_cast<uint32_t*>(t + k) = o;
+    }
+    for (; k < b; ++k) {
         run += k == 0 ? t[0] : (uint32_t)t[k] - 128u;
         t[k] = (uint8_t)run;
     }

@@ -56,6 +56,11 @@ struct InfTab {  // canonical code: number of codes per length, symbols in code 
     uint16_t count[16];
     uint16_t sym[288];
     uint16_t fast[1 << kInfFast];
+    // per length l: one past the last code (first + count) and the sym index of code c (off + c);
+    // the device inflate decodes codes longer than kInfFast bits from these (one round of LDS
+    // reads instead of one per length)
+    uint16_t lim[16];
+    int16_t off[16];
 };
 
 struct InfState {
@@ -110,6 +115,12 @@ ICX_HD bool inf_build(InfTab& h, const uint8_t* len, int n) {
     for (int l = 1; l < 15; ++l) offs[l + 1] = (uint16_t)(offs[l] + h.count[l]);
     next[1] = 0;
     for (int l = 1; l < 15; ++l) next[l + 1] = (uint16_t)((next[l] + h.count[l]) << 1);
+    h.lim[0] = 0;
+    h.off[0] = 0;
+    for (int l = 1; l < 16; ++l) {
+        h.lim[l] = (uint16_t)(next[l] + h.count[l]);
+        h.off[l] = (int16_t)(offs[l] - next[l]);
+    }
     for (int i = 0; i < (1 << kInfFast); ++i) h.fast[i] = 0;
     for (int s = 0; s < n; ++s) {
         const int l = len[s];
@@ -124,7 +135,8 @@ ICX_HD bool inf_build(InfTab& h, const uint8_t* len, int n) {
     return true;
 }
 
-ICX_HD int inf_decode(BitIn& in, const InfTab& h) {
+template <class In>  // (BitIn, or k_exr_unpack's register-window reader)
+ICX_HD int inf_decode(In& in, const InfTab& h) {
     in.fill(16);
     const uint32_t e = exr_uni(h.fast[in.buf & ((1u << kInfFast) - 1u)]);
     if (e) {
