@@ -80,17 +80,22 @@ struct InW {
         cnt = 0;
         over = 0;
     }
-    __device__ __forceinline__ void fill(int k) {  // k <= 32
-        if (cnt >= k) return;
-        const uint32_t p = pos + mis;
-        while (p >= wb + 256u) {  // (wave-uniform) the next window; its successor's load goes out now
+    // The window moves in one place only, adv(), which each decode loop calls once per iteration
+    // (an iteration consumes at most 16 input bytes, so fill() always finds its 4 bytes in
+    // [wb, wb + 512)): with the window's registers written at several inlined sites, the copies
+    // the compiler made to merge them waited for every load and store in flight, on every symbol.
+    __device__ __forceinline__ void adv() {
+        if (pos + mis >= wb + 256u) {  // (wave-uniform) the next window; its successor's load goes out now
             cur = nxt;
             wb += 256u;
             nxt = ld(wb + 256u);
         }
-        const uint32_t o = p - wb, i0 = o >> 2;
-        const uint32_t v0 = __builtin_amdgcn_readlane(cur, i0);
-        const uint32_t v1 = i0 == 63u ? __builtin_amdgcn_readlane(nxt, 0) : __builtin_amdgcn_readlane(cur, i0 + 1u);
+    }
+    __device__ __forceinline__ void fill(int k) {  // k <= 32
+        if (cnt >= k) return;
+        const uint32_t o = pos + mis - wb, i0 = o >> 2, i1 = i0 + 1u;  // (o < 512 - 4)
+        const uint32_t v0 = i0 < 64u ? __builtin_amdgcn_readlane(cur, i0) : __builtin_amdgcn_readlane(nxt, i0 - 64u);
+        const uint32_t v1 = i1 < 64u ? __builtin_amdgcn_readlane(cur, i1) : __builtin_amdgcn_readlane(nxt, i1 - 64u);
         const uint32_t w = __builtin_amdgcn_alignbyte(v1, v0, o & 3u);
         if (pos + 4u > n) over += 8u * (pos + 4u - max(pos, n));  // (bytes at or past n read as 0: ld does not load them)
         buf |= (uint64_t)w << cnt;
@@ -187,6 +192,7 @@ __device__ __forceinline__ bool exr_inflate_wave(const uint8_t* src, int64_t n64
     };
     int last = 0;
     while (!last) {
+        in.adv();
         last = (int)in.bits(1);
         const uint32_t type = in.bits(2);
         if (type == 0) {  // stored
@@ -195,6 +201,7 @@ __device__ __forceinline__ bool exr_inflate_wave(const uint8_t* src, int64_t n64
             if (in.past_end() || (len ^ 0xFFFFu) != nlen) return false;
             if (out + len > cap) return false;
             for (uint32_t k = 0; k < len; ++k) {
+                in.adv();
                 const uint32_t b = in.bits(8);
                 if (in.past_end()) return false;
                 lit(b);
@@ -210,10 +217,14 @@ __device__ __forceinline__ bool exr_inflate_wave(const uint8_t* src, int64_t n64
         } else {  // dynamic codes
             const int nlen = (int)in.bits(5) + 257, ndist = (int)in.bits(5) + 1, ncode = (int)in.bits(4) + 4;
             if (nlen > 286 || ndist > 30) return false;
-            for (int k = 0; k < 19; ++k) st.len[Deflate::kClOrder[k]] = k < ncode ? (uint8_t)in.bits(3) : 0;
+            for (int k = 0; k < 19; ++k) {
+                in.adv();
+                st.len[Deflate::kClOrder[k]] = k < ncode ? (uint8_t)in.bits(3) : 0;
+            }
             if (in.past_end() || !inf_build(st.lit, st.len, 19)) return false;
             int k = 0;
             while (k < nlen + ndist) {
+                in.adv();
                 const int sym = inf_decode_w(in, st.lit);
                 if (sym < 0 || in.past_end()) return false;
                 if (sym < 16) {
@@ -237,31 +248,37 @@ __device__ __forceinline__ bool exr_inflate_wave(const uint8_t* src, int64_t n64
             if (in.past_end()) return false;
             if (!inf_build(st.lit, st.len, nlen) || !inf_build(st.dist, st.len + nlen, ndist)) return false;
         }
+        // (every failure leaves the loop by one break with `bad` set: a single exit besides the
+        // block's end, so the compiler does not thread a state variable through every literal)
+        bool bad = false;
         for (;;) {
+            in.adv();
             // (reading past the input makes past_end() true for good, and every path from there
             // fails: it is tested at the block's end, at each match and before the trailer, not
             // per literal)
             const int sym = inf_decode_w(in, st.lit);
-            if (sym < 0) return false;
-            if (sym < 256) {
+            if ((uint32_t)sym < 256u) {
                 if (lane == 0) ring[out & (W - 1)] = (uint8_t)sym;
                 out = exr_uni(out + 1u);
                 if (out - fl >= kFlush) {
                     flush1();
-                    if (over_cap || in.past_end()) return false;  // (also ends a run of literals past the input)
+                    bad = over_cap || in.past_end();  // (also ends a run of literals past the input)
+                    if (bad) break;
                 }
                 continue;
             }
-            if (in.past_end() || over_cap) return false;
-            if (sym == 256) break;
+            bad = sym < 0 || in.past_end() || over_cap;
+            if (bad || sym == 256) break;
             const uint32_t li = (uint32_t)sym - 257u;
-            if (li >= 29u) return false;
-            const uint32_t len = len_base(li) + in.bits((int)len_ext(li));
+            bad = li >= 29u;
+            if (bad) break;
+            const uint32_t len = len_base(li) + in.bits((int)len_ext(li));  // (then the distance code)
             const int di = inf_decode_w(in, st.dist);
-            if (di < 0 || di >= 30) return false;
+            bad = di < 0 || di >= 30;
+            if (bad) break;
             const uint32_t dist = dist_base((uint32_t)di) + in.bits((int)dist_ext((uint32_t)di));
-            if (in.past_end() || dist > out) return false;
-            if (out + len > cap) return false;
+            bad = in.past_end() || dist > out || out + len > cap;
+            if (bad) break;
             // the match, 64 bytes per round: sources from before `out` only (see above); from the
             // ring while none of them can have been overwritten by this match's own bytes, else
             // from dst (dist > W - len >= kFlush + 258: every source byte is flushed)
@@ -279,6 +296,7 @@ __device__ __forceinline__ bool exr_inflate_wave(const uint8_t* src, int64_t n64
             out = exr_uni(out + len);
             flush();
         }
+        if (bad) return false;
     }
     if (over_cap || out > cap) return false;
     // the last bytes (fewer than kFlush): whole dwords, then the tail
@@ -286,6 +304,7 @@ __device__ __forceinline__ bool exr_inflate_wave(const uint8_t* src, int64_t n64
     for (uint32_t k = fl + 4u * lane; k < o4; k += 256u)
         *reinterpret_cast<uint32_t*>(dst + k) = *reinterpret_cast<const uint32_t*>(ring + (k & (W - 1)));
     if (o4 + lane < out) dst[o4 + lane] = ring[(o4 + lane) & (W - 1)];
+    in.adv();
     in.bits(in.cnt & 7);  // to a byte boundary
     uint32_t adler = 0;
     for (int k = 0; k < 4; ++k) adler = (adler << 8) | in.bits(8);
