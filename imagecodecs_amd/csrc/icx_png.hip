@@ -1210,6 +1210,73 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
     }
     if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
 }
+// emit_segment for the wave's LDS image (round 6): each lane takes kRun consecutive token slots,
+// one wave prefix sum of the lanes' bit totals places them, and each lane packs its slots into
+// whole words in a register -- the words it fills alone are plain stores, only its first and last
+// (shared with the neighbouring lanes) are atomicOr. (One slot per lane OR-ed every token into LDS
+// with up to three atomics, several lanes on each word.)
+constexpr int kRun = 8;
+__device__ __forceinline__ void emit_segment_runs(uint32_t* W, unsigned long long pos, const BlockCodes& B,
+                                                  const uint16_t* Hd, uint32_t nh, const uint16_t* T, uint32_t nt,
+                                                  bool head, bool eob, int lane) {
+    if (head) {  // the block header: its words, shifted into place
+        const uint32_t hb = B.hdr_bits;
+        for (uint32_t i = lane; i * 32 < hb; i += 64) {
+            const int n = (int)min(32u, hb - i * 32);
+            or_bits(W, pos + i * 32, n == 32 ? B.hdr[i] : (B.hdr[i] & ((1u << n) - 1u)), n);
+        }
+        pos += hb;
+    }
+    const uint32_t n = nh + nt;
+    auto slot = [&](uint32_t i) -> uint32_t { return i < nh ? (uint32_t)Hd[i] : (uint32_t)T[i - nh]; };
+    for (uint32_t i0 = 0; i0 < n; i0 += 64 * kRun) {
+        const uint32_t ib = i0 + (uint32_t)lane * kRun;
+        uint64_t v[kRun];
+        int nb[kRun];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int r = 0; r < kRun; ++r) {
+            const uint32_t i = ib + r;
+            nb[r] = 0;
+            v[r] = i < n ? token_code(B, slot(i), i + 1 < n ? slot(i + 1) : 0u, nb[r]) : 0;
+            tot += (uint32_t)nb[r];
+        }
+        uint32_t inc;  // inclusive scan of the lanes' bit totals (rocprim's DPP cross-lane scan)
+        using WScan = rocprim::warp_scan<uint32_t, 64>;
+        typename WScan::storage_type wst;
+        WScan().inclusive_scan(tot, inc, wst);
+        const unsigned long long s0 = pos + inc - tot;
+        uint32_t wi = (uint32_t)(s0 >> 5);
+        int an = (int)(s0 & 31);
+        uint64_t acc = 0;
+        bool first = true;
+        auto put = [&](uint32_t piece, int k) {  // k <= 32 bits; an < 32 before
+            acc |= (uint64_t)piece << an;
+            an += k;
+            if (an >= 32) {
+                if (first) atomicOr(W + wi, (uint32_t)acc);  // (shared with the lane before)
+                else W[wi] = (uint32_t)acc;
+                first = false;
+                ++wi;
+                acc >>= 32;
+                an -= 32;
+            }
+        };
+#pragma unroll
+        for (int r = 0; r < kRun; ++r) {
+            if (nb[r] > 32) {
+                put((uint32_t)v[r], 32);
+                put((uint32_t)(v[r] >> 32), nb[r] - 32);
+            } else if (nb[r] > 0) {
+                put((uint32_t)v[r], nb[r]);
+            }
+        }
+        if (tot && an > 0) atomicOr(W + wi, (uint32_t)acc);  // (shared with the lane after)
+        pos += __shfl(inc, 63);
+    }
+    if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
+}
+
 // The file's layout once the deflate stream's length is known, on the device (k_png_size): the
 // rest of the encode reads it there, so no host read-back sits between the deflate and the file.
 struct PngTail {
@@ -1249,7 +1316,7 @@ __global__ __launch_bounds__(256) void k_png_emit(int64_t nseg, const uint16_t* 
     uint32_t* W = img[wave];
     for (int i = lane; i < nw; i += 64) W[i] = 0;
     __builtin_amdgcn_wave_barrier();
-    emit_segment(W, o0 & 31, B, Hd, nh, T, nt, head, eob, lane);
+    emit_segment_runs(W, o0 & 31, B, Hd, nh, T, nt, head, eob, lane);
     __builtin_amdgcn_wave_barrier();
     for (int i = lane; i < nw; i += 64) {
         const uint32_t v = W[i];
