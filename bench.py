@@ -982,6 +982,10 @@ def main():
                 "avg_launch_ms": round(stages[dom] / launches, 3),
                 "stage_ms": {k: round(v, 3) for k, v in stages.items()},
                 "pipeline_frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+        if kname == "k_gw_lane":
+            roof["kernel_note"] = ("the write stage's events bracket both k_gw_lane instances on the stream: "
+                                   "<512,false> and the CHK instance <512,true> (128 workgroups; streams ending in "
+                                   "a syntax error); their rocprofv3 averages add up to avg_launch_ms")
         roof.update(pipeline_traffic(args.workload, n, alg_bytes))
     out = {
         "metric": f"megapixels/s JPEG decode, {W}x{H} RGB batch",
