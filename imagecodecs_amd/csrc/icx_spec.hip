@@ -1192,6 +1192,15 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 // gives the IDCT each block's pool block and DC offset (k_gw_scan, k_gw_map). The per-lane logic
 // is icx_spec_core.h's gw_* / gc_*, which tests/emu/spec_emu.cpp runs lane by lane on the CPU.
 
+// x + (this lane's bit of the mask m): one v_addc with the mask as its carry-in (a select of 0 / 1
+// and an add otherwise).
+__device__ __forceinline__ int32_t add_lane_bit(int32_t x, uint64_t m) {
+    int32_t r;
+    uint64_t c;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
+    return r;
+}
+
 // A pointer every lane of the wave holds, as the compiler's uniform (SGPR) value.
 __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
     const uint64_t v = reinterpret_cast<uint64_t>(p);
@@ -1331,7 +1340,9 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             live = live && !leave;
             const bool own_bs = live && bs;
             if (rec_on) {  // (wave-uniform: skipped once every lane has its kRecGw records)
-                const bool rc = own_bs && b == 0 && nrec < kRecGw;
+                int rc_b = own_bs && nrec < kRecGw ? b : 1;
+                asm volatile("" : "+v"(rc_b));
+                const bool rc = rc_b == 0;
                 if (wave_any(rc)) {  // MCU start: a splice point for the count lane
                     if (rc) {
                         RecState e;
@@ -1347,7 +1358,11 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                     rec_on = wave_any(live && nrec < kRecGw);
                 }
             }
-            const bool need = own_bs && left == 0;
+            // (the conditions wave_any / wave_ballot take are single compares of integers: a
+            // ballot of an AND of lane masks is lowered through a VGPR, two more VALU each)
+            int32_t left_own = own_bs ? left : 1;
+            asm volatile("" : "+v"(left_own));  // (kept opaque: else folded back into the AND)
+            const bool need = left_own == 0;
             if (wave_any(need)) {  // an overflow chunk from the pool's tail (flat regions)
                 if (need) {
                     const unsigned long long nb = atomicAdd(pool_next, (unsigned long long)kGwChunk);
@@ -1382,8 +1397,11 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             // block is a discarded speculative one or the image fails)
             sv[slot_cell(threadIdx.x, o.n2)] = (Cell)(o.w2 ? o.v2 : 0);
             sv[slot_cell(threadIdx.x, o.n1)] = (Cell)(bs ? cell : o.v1);
-            const bool done = live && z == 0;
-            k += done ? 1 : 0;
+            int z_live = live ? z : 1;
+            asm volatile("" : "+v"(z_live));
+            const bool done = z_live == 0;
+            const uint64_t m = wave_ballot(done);
+            k = add_lane_bit(k, m);  // k += done
             {  // the block ended: the next block's component (frozen once the lane left)
                 const bool rot = done && ((chgm >> bcur) & 1u) != 0u;
                 const int32_t t0 = dc0;
@@ -1391,7 +1409,6 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                 dc1 = rot ? dc2 : dc1;
                 dc2 = rot ? t0 : dc2;
             }
-            const uint64_t m = wave_ballot(done);
             if (m) {  // wave-uniform: flush the completed blocks, 8 per round
                 if (done) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
