@@ -1201,6 +1201,13 @@ __device__ __forceinline__ int32_t add_lane_bit(int32_t x, uint64_t m) {
     return r;
 }
 
+__device__ __forceinline__ int32_t sub_lane_bit(int32_t x, uint64_t m) {  // x - (this lane's bit of m)
+    int32_t r;
+    uint64_t c;
+    asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
+    return r;
+}
+
 // A pointer every lane of the wave holds, as the compiler's uniform (SGPR) value.
 __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
     const uint64_t v = reinterpret_cast<uint64_t>(p);
@@ -1326,6 +1333,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         int bl = 0;
         int32_t left = Sst, nxt = sbase;  // slots left in the current run (static, then chunks), the next one
         bool rec_on = true;  // some live lane of the wave still records MCU starts (wave-uniform)
+        bool any_over = false;  // some lane's pool ran out: its nxt stays at the scratch block (wave-uniform)
         (void)kFar;
         // 2. store every block from g0 on
         if (wave_any(live)) do {
@@ -1338,7 +1346,10 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             // updates, which costs a copy of each per iteration)
             asm volatile("" : "+v"(ul), "+v"(bl));
             live = live && !leave;
-            const bool own_bs = live && bs;
+            int z_own = live ? z : 1;  // (own_bs as one compare: its ballot is the carry of two counters below)
+            asm volatile("" : "+v"(z_own));
+            const bool own_bs = z_own == 0;  // live && bs
+            const uint64_t om = wave_ballot(own_bs);
             if (rec_on) {  // (wave-uniform: skipped once every lane has its kRecGw records)
                 int rc_b = own_bs && nrec < kRecGw ? b : 1;
                 asm volatile("" : "+v"(rc_b));
@@ -1378,10 +1389,11 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                     }
                     left = over ? INT32_MAX : kGwChunk;
                 }
+                any_over = any_over || wave_any(over != 0);
             }
             addr = own_bs ? nxt : addr;
-            nxt += own_bs && !over ? 1 : 0;
-            left -= own_bs ? 1 : 0;
+            nxt = add_lane_bit(nxt, any_over ? om & ~wave_ballot(over != 0) : om);  // nxt += own_bs && !over
+            left = sub_lane_bit(left, om);                                           // left -= own_bs
             // one lookup (every lane: the reader moves on idle lanes too, see k_spec_write)
             const uint32_t u0 = r.used;
             const int bcur = b;
