@@ -1902,6 +1902,9 @@ __global__ __launch_bounds__(256) void k_fused420(const Desc* __restrict__ desc,
 #ifndef ICX_F5_QV  // 1: the quantisation table in VGPRs (168 VGPRs, no v_readlane): C3 -1.1%
 #define ICX_F5_QV 0
 #endif
+#ifndef ICX_F5_QL  // 1: the table in LDS, into VGPRs per block (short-lived: no v_readlane of spilled SGPRs)
+#define ICX_F5_QL 1
+#endif
 constexpr int kFB5 = ICX_FB5;
 __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* __restrict__ desc, const int16_t* __restrict__ ac,
                                                    const int32_t* __restrict__ dcv, const uint2* __restrict__ map,
@@ -1914,10 +1917,16 @@ __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* 
     const int wave = wave_index(), lane = threadIdx.x & 63, mq = lane >> 2, k = lane & 3, sbx = k & 1, sby = k >> 1;
     uint32_t (*Yl)[64] = Yl_all[wave];
     uint32_t qw[16];
+#if ICX_F5_QL  // the table in LDS, read into VGPRs per block just before the dequantisation
+    __shared__ __attribute__((aligned(16))) uint32_t qlds[16];
+    if (threadIdx.x < 16) qlds[threadIdx.x] = reinterpret_cast<const uint32_t*>(d.q[d.c[0].tq])[threadIdx.x];
+    __syncthreads();
+#endif
     load_qw_g(d.q[d.c[0].tq], qw);
 #if ICX_F5_QV  // in vector registers, read by SDWA (in scalar registers they were spilled to VGPR lanes: 63 v_readlane per block)
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) asm volatile("" : "+v"(qw[k2]));
+#elif ICX_F5_QL
 #else
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) qw[k2] = __builtin_amdgcn_readfirstlane(qw[k2]);
@@ -1969,7 +1978,23 @@ __global__ __launch_bounds__(256, ICX_FUSED5_MINW) void k_fused420s(const Desc* 
                 p = blk_pend(d, map, nblk(mby + 1));
 #endif
                 uint32_t rowd[16];
+#if ICX_F5_QL
+                {
+                    asm volatile("" ::: "memory");  // (reloaded per block: not hoisted out of the loop)
+                    uint32_t qv[16];
+#pragma unroll
+                    for (int q4 = 0; q4 < 4; ++q4) {
+                        const uint4 t4 = reinterpret_cast<const uint4*>(qlds)[q4];
+                        qv[4 * q4] = t4.x;
+                        qv[4 * q4 + 1] = t4.y;
+                        qv[4 * q4 + 2] = t4.z;
+                        qv[4 * q4 + 3] = t4.w;
+                    }
+                    block_idct(c, qv, dcv, l, rowd);
+                }
+#else
                 block_idct(c, qw, dcv, l, rowd);
+#endif
                 uint2* dst = reinterpret_cast<uint2*>(&Yl[sby * 8][mq * 4 + sbx * 2]);
 #pragma unroll
                 for (int r = 0; r < 8; ++r) dst[r * 32] = make_uint2(rowd[2 * r], rowd[2 * r + 1]);
