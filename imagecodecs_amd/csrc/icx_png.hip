@@ -37,10 +37,13 @@ namespace icx {
 
 namespace png {
 
-constexpr int kSeg = 4096;            // LZ77 / emit segment (bytes of the filtered stream), one lane each
+#ifndef ICX_PNG_SEG
+#define ICX_PNG_SEG 4096
+#endif
+constexpr int kSeg = ICX_PNG_SEG;     // LZ77 / emit segment (bytes of the filtered stream), one lane each
 constexpr int kSlots = kSeg + 8;      // token slots per segment: up to kSeg - 1 literals + a match
                                       // overhanging the segment end (16-byte multiple)
-constexpr int kSegPerBlock = 64;      // 256 KiB deflate blocks (lodepng's size at this scale, :1830)
+constexpr int kSegPerBlock = 262144 / kSeg;  // 256 KiB deflate blocks (lodepng's size at this scale, :1830)
 constexpr int kNLL = 286, kND = 30;   // literal/length and distance alphabets
 constexpr int kHdrWords = 96;         // per-block header bit buffer (<= 3072 bits)
 constexpr int kCrcSeg = 1024;         // CRC-32 segment, one lane each
