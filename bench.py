@@ -541,6 +541,21 @@ def main_hdr(args, wl, world, rank, local):
 
     for _ in range(args.warmup):
         step()
+    if args.graph:  # one step captured (the library launches without host waits under capture), then replays
+        if M != 1:
+            raise SystemExit("--graph takes one batch (no --inflight)")
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out[0].data_ptr(), stride,
+                                d_st[0].data_ptr(), d_dims[0].data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+
+        def step():
+            graph.replay()
+            return 0
+        for _ in range(max(1, args.warmup)):
+            step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -686,6 +701,21 @@ def main_exr(args, wl, world, rank, local):
 
     for _ in range(args.warmup):
         step()
+    if args.graph:  # one step captured (the library launches without host waits under capture), then replays
+        if M != 1:
+            raise SystemExit("--graph takes one batch (no --inflight)")
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out[0].data_ptr(), stride,
+                                d_st[0].data_ptr(), d_dims[0].data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+
+        def step():
+            graph.replay()
+            return 0
+        for _ in range(max(1, args.warmup)):
+            step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -753,6 +783,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive sub-batch (decode workloads)")
     ap.add_argument("--png-single", action="store_true", help="C5: one encode call per image (no batch entry)")
+    ap.add_argument("--graph", action="store_true",
+                    help="decode workloads: capture one step (the whole batch call) in a HIP graph and replay it "
+                         "(every entropy round and every layout's back half are enqueued: no host waits)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="decode workloads: steps in flight (0 = the workload's default); step k runs on batch "
                          "k %% M with its own stream and output buffers, so one step's back half overlaps the "
@@ -858,6 +891,21 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if args.graph:  # one step captured (the library launches without host waits under capture), then replays
+        if M != 1:
+            raise SystemExit("--graph takes one batch (no --inflight)")
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            batch.decode_device(n, d_data.data_ptr(), d_off.data_ptr(), d_sz.data_ptr(), d_out[0].data_ptr(), stride,
+                                d_st[0].data_ptr(), d_dims[0].data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+
+        def step():
+            graph.replay()
+            return 0
+        for _ in range(max(1, args.warmup)):
+            step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -1001,6 +1049,7 @@ def main():
         "parity": {"all_status_ok": ok_all, "images_checked_vs_oracle": checked, "mismatches": mismatches},
         "entropy_paths": paths,
         "inflight": {"steps_in_flight": M, "group": group or "auto", "groups_per_call": batch.groups_per_call(n)},
+        "hip_graph": bool(args.graph),
         "records": records,
         "pcie_inclusive": pcie,
         "gen_seconds": round(gen_s, 1),
