@@ -980,6 +980,22 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
     }
 }
 
+// x + (this lane's bit of the mask m): one v_addc with the mask as its carry-in (a select of 0 / 1
+// and an add otherwise).
+__device__ __forceinline__ int32_t add_lane_bit(int32_t x, uint64_t m) {
+    int32_t r;
+    uint64_t c;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
+    return r;
+}
+
+__device__ __forceinline__ int32_t sub_lane_bit(int32_t x, uint64_t m) {  // x - (this lane's bit of m)
+    int32_t r;
+    uint64_t c;
+    asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
+    return r;
+}
+
 // One flat loop over lookups per lane (lanes of a wave never wait for each other at block
 // boundaries); each block is assembled in the lane's LDS slot and leaves as eight 16-byte
 // stores when it ends (scattered 2-byte global stores amplified HBM writes ~10x).
@@ -1032,16 +1048,17 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         const int64_t errbits = s.errpos == INT64_MAX ? INT64_MAX : s.errpos * 8;
         int4* A = reinterpret_cast<int4*>(ac + desc[i].acbase * 64);  // (in place: the image's pool region)
         int32_t* D = dcv + desc[i].acbase;
-        const int64_t total_blocks = s.total_blocks;
+        const int32_t total_blocks = (int32_t)s.total_blocks;  // (an image's blocks fit 31 bits: <= 65535^2 / 64 x 6)
         bool act = j < s.nsub && lane_ok;
         // every lane runs a reader (lanes past the image's last lane idle at position 0)
         const uint64_t entry = dri ? pack_state(start_byte * 8, 0, 0)
                                    : ((!act || j == 0) ? pack_state(0, 0, 0) : X[base + j - 1]);
         Reader r;
         r.init(U + s.uoff, s.ulen, st_pos(entry));
-        int b = st_b(entry), z = st_z(entry), ci = 0;
+        int b = st_b(entry), z = st_z(entry);
         int32_t pred[3] = {0, 0, 0};
-        int64_t bi = 0, limit = 0;
+        int32_t bi = 0;
+        int64_t limit = 0;
         bool bad = false;
         // the block in progress at entry belongs to the previous lane
         while (z != 0) (void)write_step(r, T, H, S, b, z, false);
@@ -1052,12 +1069,13 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         uint32_t lim_rel = kFar;
         // the loop's error-byte tests as one compare each: u0 + 16 > err_rel, u0 + 16 + kAcBits > err_rel
         const int32_t err_peek = (int32_t)err_rel - 16, err_pair = err_peek - WriteTab::kAcBits;
-        int64_t bend = total_blocks;  // block index the lane stops at
+        int32_t bend = total_blocks;  // block index the lane stops at
         uint32_t used_end = 0;        // bits consumed when the lane's last block completed
         if (act && dri) {
-            bi = j * iblocks;
-            bend = min(total_blocks, bi + iblocks);
-            act = bi < bend;
+            const int64_t b0 = j * iblocks;
+            act = b0 < total_blocks;
+            bi = act ? (int32_t)b0 : 0;
+            bend = (int32_t)min<int64_t>(total_blocks, b0 + iblocks);
         } else if (act) {
             limit = j == s.nsub - 1 ? INT64_MAX : st_pos(X[base + j]);
             if (limit != INT64_MAX) lim_rel = (uint32_t)min<int64_t>(kFar, max<int64_t>(0, limit - e0));
@@ -1065,13 +1083,22 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             pred[0] = le.p0;
             pred[1] = le.p1;
             pred[2] = le.p2;
-            bi = le.G;
-            act = bi < total_blocks;
+            act = le.G < total_blocks;
+            bi = act ? (int32_t)le.G : 0;
         }
+        // DC predictors rotated with the current block's component (as in k_gw_lane): dc0 is the
+        // predictor of block b's component, dc1 / dc2 those of the next two in MCU order (NanoJPEG
+        // has 1 or 3 components, in order in the MCU); a block end whose next block has another
+        // component rotates them by one, and a DC code reads and updates dc0 alone.
+        const int c0 = S.comp(b);
+        int32_t dc0 = c0 == 0 ? pred[0] : (c0 == 1 ? pred[1] : pred[2]);
+        int32_t dc1 = c0 == 0 ? pred[1] : (c0 == 1 ? pred[2] : pred[0]);
+        int32_t dc2 = c0 == 0 ? pred[2] : (c0 == 1 ? pred[0] : pred[1]);
+        const uint32_t chgm = S.chg_mask();
         // The predictors come from a load issued before the loop: without this the compiler
         // waits for them at their first use inside the loop with vmcnt(0) -- i.e. for every
         // coefficient store and prefetch in flight -- on every DC code.
-        asm volatile("" : "+v"(pred[0]), "+v"(pred[1]), "+v"(pred[2]));
+        asm volatile("" : "+v"(dc0), "+v"(dc1), "+v"(dc2));
         r.phase();  // the prelude above ran a lane-dependent number of lookups
 #ifdef ICX_EXP_CYC  // timing experiment only: per-wave loop cycles and iterations (printf)
         const uint64_t cyc0 = clock64();
@@ -1092,10 +1119,10 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             const bool dc = z == 0;
             // a block starts: stop at the next lane's territory
             act = act && !(dc && r.used >= lim_rel);
-            ci = dc ? S.comp(b) : ci;
             // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644); a second
             // symbol is only paired when its own peek stays clear of the error byte
             const uint32_t u0 = r.used;
+            const int bcur = b;
             const WriteOut o = write_step(r, T, H, S, b, z, (int32_t)u0 > err_pair);
             // Bookkeeping by selects, not per-lane branches (each divergent `if` cost its exec-mask
             // save / restore and a branch in every iteration).
@@ -1103,10 +1130,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             bad = bad || (act && fail);
             const bool ok = act && !fail;
             const bool okdc = ok && dc;
-            const int32_t pc = wadd(ci == 0 ? pred[0] : (ci == 1 ? pred[1] : pred[2]), o.v1);
-            pred[0] = okdc && ci == 0 ? pc : pred[0];
-            pred[1] = okdc && ci == 1 ? pc : pred[1];
-            pred[2] = okdc && ci == 2 ? pc : pred[2];
+            const int32_t pc = wadd(dc0, o.v1);
+            dc0 = okdc ? pc : dc0;
             const int32_t cell = dc_cell(pc);
             if (okdc && cell == kDcEscape) D[bi] = pc;  // DC outside int16 (corrupt streams only)
             // Both slot writes always issue (zig-zag order; k_idct reorders). A symbol that writes
@@ -1119,12 +1144,21 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             // is never stored)
             sv[slot_elem(threadIdx.x, o.n2)] = (int16_t)(o.w2 ? o.v2 : 0);
             sv[slot_elem(threadIdx.x, o.n1)] = (int16_t)(dc ? cell : o.v1);
-            const bool done = ok && z == 0;
-            const int64_t bdone = bi;
-            bi += done ? 1 : 0;
+            int z_ok = ok ? z : 1;  // (done as one compare: its ballot is the block counter's carry)
+            asm volatile("" : "+v"(z_ok));
+            const bool done = z_ok == 0;
+            const uint64_t m = wave_ballot(done);
+            const int32_t bdone = bi;
+            bi = add_lane_bit(bi, m);  // bi += done
             act = ok && (!done || bi < bend);
             used_end = done ? r.used : used_end;  // (the reader keeps moving once the lane is idle)
-            const uint64_t m = wave_ballot(done);
+            {  // the block ended: the next block's component (frozen once the lane stopped)
+                const bool rot = done && ((chgm >> bcur) & 1u) != 0u;
+                const int32_t t0 = dc0;
+                dc0 = rot ? dc1 : dc0;
+                dc1 = rot ? dc2 : dc1;
+                dc2 = rot ? t0 : dc2;
+            }
             if (m) {  // wave-uniform; every lane takes part
                 if (done) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -1136,7 +1170,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
                 for (int k0 = 0; k0 < cnt; k0 += 8) {
                     const int e = k0 + (lane >> 3), q = lane & 7;
                     const int src = done_lane[wave][min(e, cnt - 1)];
-                    const int bsrc = __shfl((int)bdone, src);  // block index of that lane's block
+                    const int bsrc = __shfl(bdone, src);  // block index of that lane's block
                     if (e < cnt) {
                         const int sl = (wave << 6) | src;
                         int4* sp = &slots[sl][0];
@@ -1191,22 +1225,6 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 // blocks are stored twice. The blocks land in the group's coefficient pool in lane order; a map
 // gives the IDCT each block's pool block and DC offset (k_gw_scan, k_gw_map). The per-lane logic
 // is icx_spec_core.h's gw_* / gc_*, which tests/emu/spec_emu.cpp runs lane by lane on the CPU.
-
-// x + (this lane's bit of the mask m): one v_addc with the mask as its carry-in (a select of 0 / 1
-// and an add otherwise).
-__device__ __forceinline__ int32_t add_lane_bit(int32_t x, uint64_t m) {
-    int32_t r;
-    uint64_t c;
-    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
-    return r;
-}
-
-__device__ __forceinline__ int32_t sub_lane_bit(int32_t x, uint64_t m) {  // x - (this lane's bit of m)
-    int32_t r;
-    uint64_t c;
-    asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
-    return r;
-}
 
 // A pointer every lane of the wave holds, as the compiler's uniform (SGPR) value.
 __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
