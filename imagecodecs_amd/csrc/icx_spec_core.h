@@ -530,13 +530,35 @@ ICX_HD WriteOut write_step(Reader& r, const Tab& T, const Huff* H, const Sel& S,
 // boundary at or after `end`. The lead lets the lane resynchronise before `start`, so its first
 // recorded state is (almost always) on the true path and the count lane splices at once; only
 // differences of the totals are ever used (tot - rec[m]), so the extra prefix cancels.
+// Per-component DC sums kept rotated with the current block's component (d0 is block b's, d1 / d2
+// the next two in MCU order: NanoJPEG has 1 or 3 components, in order in the MCU), so a DC code
+// updates d0 alone and a block end whose next block has another component rotates by one (the
+// k_gw_lane scheme; a 3-way select per DC code and per update otherwise). At an MCU start (b = 0)
+// they are in component order.
+struct DcRot {
+    int32_t d0 = 0, d1 = 0, d2 = 0;
+    ICX_HD void rotate_if(bool r) {
+        const int32_t t = d0;
+        d0 = r ? d1 : d0;
+        d1 = r ? d2 : d1;
+        d2 = r ? t : d2;
+    }
+    ICX_HD void out(int c, int32_t* s) const {  // component order, the rotation at component c
+        s[c] = d0;
+        s[c == 2 ? 0 : c + 1] = d1;
+        s[c == 0 ? 2 : c - 1] = d2;
+    }
+};
+
 ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const ScanTab& T, const Huff* H, const Sel& S, int64_t start,
                            int64_t end, int b0, RecState* rec, int32_t* nrec, int32_t* tot, int64_t lead = 0) {
     const int64_t s0 = start - lead > 0 ? start - lead : 0;
     Reader r;
     r.init(U, ulen, s0);
     int b = b0, z = 0;
-    int32_t val, cnt = 0, ds[3] = {0, 0, 0};
+    int32_t val, cnt = 0;
+    DcRot ds;
+    const uint32_t chgm = S.chg_mask();
     int nr = 0;
     const uint32_t pre = (uint32_t)(start - s0), span = (uint32_t)(end - s0);
     while (r.used < span) {
@@ -545,23 +567,20 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const ScanTab& T, con
             e.rel = r.used - pre;
             e.b = b;
             e.cnt = cnt;
-            e.ds[0] = ds[0];
-            e.ds[1] = ds[1];
-            e.ds[2] = ds[2];
+            e.ds[0] = ds.d0;  // (b = 0: the rotation is at component 0)
+            e.ds[1] = ds.d1;
+            e.ds[2] = ds.d2;
         }
-        const int ci = S.comp(b);
         const bool dc = z == 0;
+        const int bcur = b;
         scan_step(r, T, H, S, b, z, val);
-        if (dc) {
-            ++cnt;
-            ds[ci] = wadd(ds[ci], val);
-        }
+        cnt += dc ? 1 : 0;
+        ds.d0 = dc ? wadd(ds.d0, val) : ds.d0;
+        ds.rotate_if(z == 0 && ((chgm >> bcur) & 1u) != 0u);  // (z = 0: block bcur ended)
     }
     *nrec = nr;
     tot[0] = cnt;
-    tot[1] = ds[0];
-    tot[2] = ds[1];
-    tot[3] = ds[2];
+    ds.out(S.comp(b), tot + 1);
     return pack_state(r.pos(), b, z);
 }
 
@@ -575,7 +594,9 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const ScanTab& T, con
     Reader r;
     r.init(U, ulen, st_pos(entry));
     int b = st_b(entry), z = st_z(entry);
-    int32_t val, cnt = 0, ds[3] = {0, 0, 0};
+    int32_t val, cnt = 0;
+    DcRot ds;  // (all 0: the rotation starts at block b's component)
+    const uint32_t chgm = S.chg_mask();
     int m = 0;
     synced = false;
     const uint32_t off = (uint32_t)(st_pos(entry) - start), span = (uint32_t)(end - start);
@@ -584,30 +605,33 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const ScanTab& T, con
             const int64_t rel = off + r.used;
             while (m < nrec && (int64_t)rec[m].rel < rel) ++m;
             if (m < nrec && (int64_t)rec[m].rel == rel) {
+                int32_t d[3];
+                ds.out(0, d);  // (b = 0)
                 out.cnt = cnt + tot[0] - rec[m].cnt;
-                out.ds0 = wadd(ds[0], wsub(tot[1], rec[m].ds[0]));
-                out.ds1 = wadd(ds[1], wsub(tot[2], rec[m].ds[1]));
-                out.ds2 = wadd(ds[2], wsub(tot[3], rec[m].ds[2]));
+                out.ds0 = wadd(d[0], wsub(tot[1], rec[m].ds[0]));
+                out.ds1 = wadd(d[1], wsub(tot[2], rec[m].ds[1]));
+                out.ds2 = wadd(d[2], wsub(tot[3], rec[m].ds[2]));
                 out.mism = 0;
                 synced = true;
                 if (bits) *bits = r.used;
                 return guess_exit;
             }
         }
-        const int ci = S.comp(b);
         const bool dc = z == 0;
+        const int bcur = b;
         scan_step(r, T, H, S, b, z, val);
-        if (dc) {
-            ++cnt;
-            ds[ci] = wadd(ds[ci], val);
-        }
+        cnt += dc ? 1 : 0;
+        ds.d0 = dc ? wadd(ds.d0, val) : ds.d0;
+        ds.rotate_if(z == 0 && ((chgm >> bcur) & 1u) != 0u);
     }
     const uint64_t ex = pack_state(r.pos(), b, z);
     if (bits) *bits = r.used;
+    int32_t d[3];
+    ds.out(S.comp(b), d);
     out.cnt = cnt;
-    out.ds0 = ds[0];
-    out.ds1 = ds[1];
-    out.ds2 = ds[2];
+    out.ds0 = d[0];
+    out.ds1 = d[1];
+    out.ds2 = d[2];
     out.mism = ex != guess_exit;
     return ex;
 }
