@@ -61,6 +61,41 @@ def test_exr_large_vs_oracle(ctx, comp, tiles, levels):
     assert np.array_equal(img.view(np.uint32), oimg.view(np.uint32))
 
 
+@pytest.mark.parametrize("mode", ["stored", "fixed", "best", "flat"])
+def test_exr_zip_block_types_vs_oracle(ctx, monkeypatch, mode):
+    """Every deflate block type through the wave inflate (icx_exr.hip exr_inflate_wave): stored
+    blocks (zlib level 0), fixed-Huffman blocks (Z_FIXED), level 9, and a flat image whose chunks
+    are long repeats (distance < length, and matches reaching past the 16 KiB ring) -- each equal
+    to the oracle bit for bit."""
+    import zlib
+
+    class Z:  # (tools/exrwrite.py's compressor, replaced for this file)
+        @staticmethod
+        def compress(data, level=6):
+            if mode == "stored":
+                return zlib.compress(data, 0)
+            if mode == "fixed":
+                c = zlib.compressobj(6, zlib.DEFLATED, 15, 9, zlib.Z_FIXED)
+                return c.compress(data) + c.flush()
+            return zlib.compress(data, 9)
+
+    monkeypatch.setattr(W, "zlib", Z)
+    rng = np.random.default_rng(77)
+    h, w = 160, 1500
+    y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+    if mode == "flat":
+        chans = [(n, np.full((h, w), 0.25 * (k + 1), np.float16)) for k, n in enumerate("RGBA")]
+        chans[0] = ("R", (np.floor(x / 700) * 0.5).astype(np.float16))  # (a step every 700 columns)
+    else:
+        chans = [(n, (np.sin(x * (0.01 + 0.003 * k)) * np.cos(y * 0.013) * 50 + rng.normal(0, 0.05, (h, w))).astype(np.float16))
+                 for k, n in enumerate("RGBA")]
+    data = W.write_exr(chans, compression=W.ZIP)
+    oc, ow, oh, oimg = O.decode(data)
+    code, ww, hh, img = ctx.exr_decode(data)
+    assert (code, ww, hh) == (oc, ow, oh) == (0, w, h)
+    assert np.array_equal(img.view(np.uint32), oimg.view(np.uint32))
+
+
 def test_exr_random_damage(ctx):
     """Random byte damage to fixtures: the GPU's code equals the oracle's, and so do the bits of
     the files that still decode."""
