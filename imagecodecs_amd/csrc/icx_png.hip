@@ -481,6 +481,10 @@ __device__ __forceinline__ void stage_view(const uint8_t* __restrict__ F, int64_
         *reinterpret_cast<uint4*>(lds + 16 * k) = v;
     }
 }
+// A lane's value at a wave-uniform lane index: v_readlane into a scalar register (__shfl is an LDS
+// permute, and its round trip sat on the parse's serial chain)
+__device__ __forceinline__ int rdl(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+
 // Length of the match at p against p - dist, at most maxlen: four bytes per step, the first
 // differing byte from the lowest set bit of the XOR.
 __device__ __forceinline__ int match_len(const SegView& V, int64_t p, int64_t dist, int maxlen) {
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
                 int mi = m ? __ffsll((unsigned long long)m) - 1 : 64;
                 // lazy evaluation (zlib's deflate_slow): a match start whose successor has a
                 // longer match becomes a literal, and the successor is considered in turn
-                while (mi + 1 < wend && __shfl(best, mi + 1) > __shfl(best, mi)) {
+                while (mi + 1 < wend && rdl(best, mi + 1) > rdl(best, mi)) {
                     m &= m - 1;
                     mi = __ffsll((unsigned long long)m) - 1;
                 }
@@ -598,7 +602,7 @@ __global__ __launch_bounds__(256) void k_png_lz77(const uint8_t* __restrict__ F,
                 nt += (uint32_t)(le - li);
                 pos = p0 + le;
                 if (mi < wend) {  // the match at lane mi
-                    const int len = __shfl(best, mi), dist = __shfl(bd, mi);
+                    const int len = rdl(best, mi), dist = rdl(bd, mi);
                     if (lane == 0) {
                         T[nt] = (uint16_t)(0x4000u | (uint32_t)(len - 3));    // match: length slot,
                         T[nt + 1] = (uint16_t)(0x8000u | (uint32_t)(dist - 1));  // then distance slot
