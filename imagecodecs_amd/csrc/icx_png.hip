@@ -666,10 +666,10 @@ __device__ __forceinline__ void seam_score(const SegView& V, int64_t N, int64_t 
     }
     len0 = dist0 = len1 = 0;
     for (int k = 0; k < 6; ++k) {
-        const int a = __shfl(l, k), b = __shfl(l, 6 + k);
+        const int a = rdl(l, k), b = rdl(l, 6 + k);
         if (a > len0) {
             len0 = a;
-            dist0 = __shfl(d, k);
+            dist0 = rdl(d, k);
         }
         len1 = max(len1, b);
     }
@@ -1213,7 +1213,7 @@ __device__ __forceinline__ void emit_segment(uint32_t* W, unsigned long long pos
         typename WScan::storage_type wst;  // empty for the cross-lane implementation
         WScan().inclusive_scan((uint32_t)nb, inc, wst);
         or_bits(W, pos + inc - nb, v, nb);
-        pos += __shfl(inc, 63);
+        pos += (uint32_t)rdl((int)inc, 63);
     }
     if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
 }
@@ -1279,7 +1279,7 @@ __device__ __forceinline__ void emit_segment_runs(uint32_t* W, unsigned long lon
             }
         }
         if (tot && an > 0) atomicOr(W + wi, (uint32_t)acc);  // (shared with the lane after)
-        pos += __shfl(inc, 63);
+        pos += (uint32_t)rdl((int)inc, 63);
     }
     if (eob && lane == 0) or_bits(W, pos, B.ll_code[256], B.ll_len[256]);
 }
