@@ -1337,7 +1337,11 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         const int32_t sbase = (int32_t)(desc[i].acbase + j * Sst);
         RecState* R = rec + f * kRec;
         int nrec = 0;
-        bool live = act;  // storing; false from the exit on (and for lanes past the image's last)
+        // Lanes still storing (false from the exit on, and for lanes past the image's last), as a
+        // wave mask: every lane condition below is a ballot of one compare ANDed with lane masks
+        // in SGPRs, and a lane reads its bit by lane_in (round 6: 6 VALU per lookup fewer than
+        // per-lane bools, whose ballots and opaque selects cost two each).
+        uint64_t lm = wave_ballot(act);
         int32_t k = 0, err = INT32_MAX, chunk = -1, chunk0 = -1, over = 0, addr = 0;
         // Lane-local DC sums rotated with the current block's component: dc0 is the sum of block
         // b's component, dc1 / dc2 those of the next two in MCU order. An MCU runs through the
@@ -1353,27 +1357,27 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
         bool rec_on = true;  // some live lane of the wave still records MCU starts (wave-uniform)
         bool any_over = false;  // some lane's pool ran out: its nxt stays at the scratch block (wave-uniform)
         (void)kFar;
+        uint32_t span_o = span;
+        asm volatile("" : "+v"(span_o));  // (else `u >= span` is folded with `act` into an OR, whose ballot takes a VGPR)
         // 2. store every block from g0 on
-        if (wave_any(live)) do {
+        if (lm) do {
             const bool bs = z == 0;
+            const uint64_t bsm = wave_ballot(bs);
             const uint32_t u = r.used;
-            const bool leave = live && bs && u >= span && b <= bmax;
+            const uint64_t lvm = bsm & wave_ballot(u >= span_o) & wave_ballot(b <= bmax) & lm;
+            const bool leave = lane_in(lvm);
             ul = leave ? u : ul;
             bl = leave ? b : bl;
             // (here, not sunk to the latch: there they keep the old b / used alive past their
             // updates, which costs a copy of each per iteration)
             asm volatile("" : "+v"(ul), "+v"(bl));
-            live = live && !leave;
-            int z_own = live ? z : 1;  // (own_bs as one compare: its ballot is the carry of two counters below)
-            asm volatile("" : "+v"(z_own));
-            const bool own_bs = z_own == 0;  // live && bs
-            const uint64_t om = wave_ballot(own_bs);
+            lm &= ~lvm;
+            const uint64_t om = bsm & lm;  // live && bs: its lanes own a block start
+            const bool own_bs = lane_in(om);
             if (rec_on) {  // (wave-uniform: skipped once every lane has its kRecGw records)
-                int rc_b = own_bs && nrec < kRecGw ? b : 1;
-                asm volatile("" : "+v"(rc_b));
-                const bool rc = rc_b == 0;
-                if (wave_any(rc)) {  // MCU start: a splice point for the count lane
-                    if (rc) {
+                const uint64_t rcm = om & wave_ballot(b == 0) & wave_ballot(nrec < kRecGw);
+                if (rcm) {  // MCU start: a splice point for the count lane
+                    if (lane_in(rcm)) {
                         RecState e;
                         e.rel = u - pre;
                         e.b = 0;
@@ -1384,16 +1388,12 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                         R[nrec] = e;
                         ++nrec;
                     }
-                    rec_on = wave_any(live && nrec < kRecGw);
+                    rec_on = (lm & wave_ballot(nrec < kRecGw)) != 0;
                 }
             }
-            // (the conditions wave_any / wave_ballot take are single compares of integers: a
-            // ballot of an AND of lane masks is lowered through a VGPR, two more VALU each)
-            int32_t left_own = own_bs ? left : 1;
-            asm volatile("" : "+v"(left_own));  // (kept opaque: else folded back into the AND)
-            const bool need = left_own == 0;
-            if (wave_any(need)) {  // an overflow chunk from the pool's tail (flat regions)
-                if (need) {
+            const uint64_t nm = om & wave_ballot(left == 0);
+            if (nm) {  // an overflow chunk from the pool's tail (flat regions)
+                if (lane_in(nm)) {
                     const unsigned long long nb = atomicAdd(pool_next, (unsigned long long)kGwChunk);
                     if (nb + kGwChunk <= (unsigned long long)pool_cap) {
                         const int32_t c = (int32_t)(nb / kGwChunk);
@@ -1417,7 +1417,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             const int bcur = b;
             const WriteOut o = write_step(r, T, H, S, b, z, CHK ? eb.near(u0) : false);
             const bool fail = CHK ? eb.fail(u0, o.err, r.used) : o.err;
-            err = live && fail && err == INT32_MAX ? k : err;
+            err = lane_in(lm) && fail && err == INT32_MAX ? k : err;
             const bool owndc = own_bs;
             const int32_t pc = wadd(dc0, o.v1);
             dc0 = owndc ? pc : dc0;
@@ -1427,10 +1427,8 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             // block is a discarded speculative one or the image fails)
             sv[slot_cell(threadIdx.x, o.n2)] = (Cell)(o.w2 ? o.v2 : 0);
             sv[slot_cell(threadIdx.x, o.n1)] = (Cell)(bs ? cell : o.v1);
-            int z_live = live ? z : 1;
-            asm volatile("" : "+v"(z_live));
-            const bool done = z_live == 0;
-            const uint64_t m = wave_ballot(done);
+            const uint64_t m = wave_ballot(z == 0) & lm;
+            const bool done = lane_in(m);
             k = add_lane_bit(k, m);  // k += done
             {  // the block ended: the next block's component (frozen once the lane left)
                 const bool rot = done && ((chgm >> bcur) & 1u) != 0u;
@@ -1466,7 +1464,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
                 }
                 __builtin_amdgcn_wave_barrier();
             }
-        } while (wave_any(live));
+        } while (lm);
         if (act) {
             X[f] = pack_state(s0 + ul, bl, 0);
             GwOut g;

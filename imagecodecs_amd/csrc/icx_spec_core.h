@@ -297,7 +297,20 @@ ICX_HD uint64_t wave_ballot(bool p) {
     return p ? 1u : 0u;
 #endif
 }
+// The lane's bit of a wave-uniform mask as a lane condition: the mask's SGPR pair is the condition
+// (no VALU). Lane masks kept as ballots and combined with scalar ANDs stay in SGPRs; a ballot of an
+// AND of lane bools is lowered through a VGPR (two VALU).
+ICX_HD bool lane_in(uint64_t m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_inverse_ballot_w64(m);
+#else
+    return m != 0;
+#endif
+}
 
+#ifndef ICX_RD_SUBB
+#define ICX_RD_SUBB 1
+#endif
 // MSB-first reader over U (padded as above).
 // Latency hiding at the WAVE level: a wave's vmcnt counts every lane's loads in issue order, so a
 // lane cannot wait for "its own" older load while a neighbour's newer one is in flight. Loads
@@ -344,7 +357,16 @@ struct Reader {
         const uint64_t w = (a0 >> 32) << ((32 - nb) & 63);
         buf |= need ? w : 0ull;
         nb += need ? 32 : 0;
+#if defined(__HIP_DEVICE_COMPILE__) && ICX_RD_SUBB
+        {  // na -= need: the compare's lane mask as the borrow (one VALU, not a select and a subtract)
+            int32_t r;
+            uint64_t c;
+            asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(na), "s"(wave_ballot(need)));
+            na = r;
+        }
+#else
         na -= need ? 1 : 0;
+#endif
         const bool take = na == 0;
         const uint64_t s0 = (a0 << 32) | (a1 >> 32), s1 = a1 << 32;
         a0 = take ? b0 : (need ? s0 : a0);
