@@ -980,6 +980,12 @@ __global__ __launch_bounds__(256) void k_spec_scan(int n, SpecImg* __restrict__ 
     }
 }
 
+// A pointer every lane of the wave holds, as the compiler's uniform (SGPR) value.
+__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo);
+}
 // x + (this lane's bit of the mask m): one v_addc with the mask as its carry-in (a select of 0 / 1
 // and an add otherwise).
 __device__ __forceinline__ int32_t add_lane_bit(int32_t x, uint64_t m) {
@@ -1055,6 +1061,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
                                    : ((!act || j == 0) ? pack_state(0, 0, 0) : X[base + j - 1]);
         Reader r;
         r.init(U + s.uoff, s.ulen, st_pos(entry));
+        r.u = uniform_ptr(r.u);  // (one image per workgroup: the stream base and end chunk stay in SGPRs)
+        r.cmax = __builtin_amdgcn_readfirstlane(r.cmax);
         int b = st_b(entry), z = st_z(entry);
         int32_t pred[3] = {0, 0, 0};
         int32_t bi = 0;
@@ -1108,7 +1116,10 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
         // then the wave flushes the blocks its lanes completed together -- eight 128-byte blocks
         // per round, each lane moving one 16-byte chunk LDS -> HBM and zeroing it (coalesced
         // full-line stores, no divergent per-lane flush).
-        while (__any(act)) {
+        // Active lanes as a wave mask (as in k_gw_lane): the loop test and the block counter's
+        // carry are scalar ANDs of single-compare ballots.
+        uint64_t am = wave_ballot(act);
+        while (am) {
 #ifdef ICX_EXP_CYC
             ++it_w;
 #endif
@@ -1118,7 +1129,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             // copies, which made every iteration wait for the newest load and all stores.
             const bool dc = z == 0;
             // a block starts: stop at the next lane's territory
-            act = act && !(dc && r.used >= lim_rel);
+            am &= ~(wave_ballot(dc) & wave_ballot(r.used >= lim_rel));
+            const bool act = lane_in(am);
             // NanoJPEG fetches bytes to cover a 16-bit peek before each code (:644); a second
             // symbol is only paired when its own peek stays clear of the error byte
             const uint32_t u0 = r.used;
@@ -1128,7 +1140,8 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             // save / restore and a branch in every iteration).
             const bool fail = (int32_t)u0 > err_peek || o.err || r.used > err_rel;
             bad = bad || (act && fail);
-            const bool ok = act && !fail;
+            const uint64_t okm = am & ~wave_ballot(fail);
+            const bool ok = lane_in(okm);
             const bool okdc = ok && dc;
             const int32_t pc = wadd(dc0, o.v1);
             dc0 = okdc ? pc : dc0;
@@ -1144,13 +1157,11 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             // is never stored)
             sv[slot_elem(threadIdx.x, o.n2)] = (int16_t)(o.w2 ? o.v2 : 0);
             sv[slot_elem(threadIdx.x, o.n1)] = (int16_t)(dc ? cell : o.v1);
-            int z_ok = ok ? z : 1;  // (done as one compare: its ballot is the block counter's carry)
-            asm volatile("" : "+v"(z_ok));
-            const bool done = z_ok == 0;
-            const uint64_t m = wave_ballot(done);
+            const uint64_t m = wave_ballot(z == 0) & okm;
+            const bool done = lane_in(m);
             const int32_t bdone = bi;
             bi = add_lane_bit(bi, m);  // bi += done
-            act = ok && (!done || bi < bend);
+            am = okm & ~(m & ~wave_ballot(bi < bend));  // act = ok && (!done || bi < bend)
             used_end = done ? r.used : used_end;  // (the reader keeps moving once the lane is idle)
             {  // the block ended: the next block's component (frozen once the lane stopped)
                 const bool rot = done && ((chgm >> bcur) & 1u) != 0u;
@@ -1226,12 +1237,6 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
 // gives the IDCT each block's pool block and DC offset (k_gw_scan, k_gw_map). The per-lane logic
 // is icx_spec_core.h's gw_* / gc_*, which tests/emu/spec_emu.cpp runs lane by lane on the CPU.
 
-// A pointer every lane of the wave holds, as the compiler's uniform (SGPR) value.
-__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo);
-}
 
 // NL lanes per workgroup (the wg2pre numbering: kWriteLanesBig). Two loops per lane:
 //  1. the lead: from `lead` bits before the lane's start to its first block start at or after
