@@ -1145,8 +1145,9 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             const bool okdc = ok && dc;
             const int32_t pc = wadd(dc0, o.v1);
             dc0 = okdc ? pc : dc0;
-            const int32_t cell = dc_cell(pc);
-            if (okdc && cell == kDcEscape) D[bi] = pc;  // DC outside int16 (corrupt streams only)
+            const bool dc_in = (uint32_t)pc + 32767u < 65535u;  // dc_cell's range test, reused for the escape
+            const int32_t cell = dc_in ? pc : kDcEscape;
+            if (okdc && !dc_in) D[bi] = pc;  // DC outside int16 (corrupt streams only)
             // Both slot writes always issue (zig-zag order; k_idct reorders). A symbol that writes
             // nothing stores 0 at a coefficient the block has not reached: the cursor (EOB), or
             // the one after the first symbol (no pair) -- which is that symbol's own cell when it
@@ -1164,7 +1165,7 @@ __global__ __launch_bounds__(NL) void k_spec_write(int want, int n, const Desc* 
             am = okm & ~(m & ~wave_ballot(bi < bend));  // act = ok && (!done || bi < bend)
             used_end = done ? r.used : used_end;  // (the reader keeps moving once the lane is idle)
             {  // the block ended: the next block's component (frozen once the lane stopped)
-                const bool rot = done && ((chgm >> bcur) & 1u) != 0u;
+                const bool rot = done && ubfe(chgm, (uint32_t)bcur, 1u) != 0u;
                 const int32_t t0 = dc0;
                 dc0 = rot ? dc1 : dc0;
                 dc1 = rot ? dc2 : dc1;
@@ -1426,8 +1427,9 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             const bool owndc = own_bs;
             const int32_t pc = wadd(dc0, o.v1);
             dc0 = owndc ? pc : dc0;
-            const int32_t cell = dc_cell(pc);
-            if (owndc && cell == kDcEscape) dcv[addr] = pc;  // lane-local DC outside int16 (rare)
+            const bool dc_in = (uint32_t)pc + 32767u < 65535u;  // dc_cell's range test, reused for the escape
+            const int32_t cell = dc_in ? pc : kDcEscape;
+            if (owndc && !dc_in) dcv[addr] = pc;  // lane-local DC outside int16 (rare)
             // (v1 is 0 for EOB and invalid codes; an invalid DC code is a decode error, so that
             // block is a discarded speculative one or the image fails)
             sv[slot_cell(threadIdx.x, o.n2)] = (Cell)(o.w2 ? o.v2 : 0);
@@ -1436,7 +1438,7 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             const bool done = lane_in(m);
             k = add_lane_bit(k, m);  // k += done
             {  // the block ended: the next block's component (frozen once the lane left)
-                const bool rot = done && ((chgm >> bcur) & 1u) != 0u;
+                const bool rot = done && ubfe(chgm, (uint32_t)bcur, 1u) != 0u;
                 const int32_t t0 = dc0;
                 dc0 = rot ? dc1 : dc0;
                 dc1 = rot ? dc2 : dc1;

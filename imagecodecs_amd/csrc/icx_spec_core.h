@@ -507,9 +507,9 @@ struct WriteOut {
     bool err;
     // Slot cells for a block assembled in place (k_gw_lane, k_spec_write): v1 goes to n1, then
     // (v2 if w2, else 0) to n2, n2 written first. n1 = c1 when w1, else the unreached cursor z;
-    // n2 = c2 when w2, else the first cell past symbol 1 (when that is 64, cell 63, which the
-    // n1 write then overwrites). Clamped to 63 where c1 would pass it, which only a decode
-    // error does (the block is then garbage: a discarded speculative one, or a failing image).
+    // n2 = c2 when w2, else n1 (the 0 lands where the n1 write then overwrites it). n1 is taken
+    // mod 64 where c1 would pass 63, which only a decode error does (the block is then garbage:
+    // a discarded speculative one, or a failing image).
     int n1, n2;
 };
 template <class Tab>
@@ -530,9 +530,9 @@ ICX_HD WriteOut write_step(Reader& r, const Tab& T, const Huff* H, const Sel& S,
     o.w2 = pair && !eob2;
     {  // (zad1 = 0 exactly for EOB / invalid codes, and a pair's second symbol has zad2 >= 1)
         const int zn1 = z + (int)zad1;
-        const int n1 = zn1 - (zad1 != 0u ? 1 : 0), n2 = zn1 + (o.w2 ? (int)zad2 - 1 : 0);
-        o.n1 = n1 < 63 ? n1 : 63;
-        o.n2 = n2 < 63 ? n2 : 63;
+        const int n1 = zn1 - (zad1 != 0u ? 1 : 0);
+        o.n1 = n1 & 63;                                  // (past 63 only on a decode error: kept in the slot)
+        o.n2 = o.w2 ? zn1 + (int)zad2 - 1 : o.n1;        // (a pair's cell is <= 63 by the pair test)
     }
     const bool eob = pair ? eob2 != 0 : st_eob1(e) != 0;
     const int zn = z + (int)zad1 + (pair ? (int)zad2 : 0);
@@ -598,7 +598,7 @@ ICX_HD uint64_t lane_guess(const uint8_t* U, int64_t ulen, const ScanTab& T, con
         scan_step(r, T, H, S, b, z, val);
         cnt += dc ? 1 : 0;
         ds.d0 = dc ? wadd(ds.d0, val) : ds.d0;
-        ds.rotate_if(z == 0 && ((chgm >> bcur) & 1u) != 0u);  // (z = 0: block bcur ended)
+        ds.rotate_if(z == 0 && ubfe(chgm, (uint32_t)bcur, 1u) != 0u);  // (z = 0: block bcur ended)
     }
     *nrec = nr;
     tot[0] = cnt;
@@ -644,7 +644,7 @@ ICX_HD uint64_t lane_count(const uint8_t* U, int64_t ulen, const ScanTab& T, con
         scan_step(r, T, H, S, b, z, val);
         cnt += dc ? 1 : 0;
         ds.d0 = dc ? wadd(ds.d0, val) : ds.d0;
-        ds.rotate_if(z == 0 && ((chgm >> bcur) & 1u) != 0u);
+        ds.rotate_if(z == 0 && ubfe(chgm, (uint32_t)bcur, 1u) != 0u);
     }
     const uint64_t ex = pack_state(r.pos(), b, z);
     if (bits) *bits = r.used;
