@@ -1371,12 +1371,11 @@ __global__ __launch_bounds__(NL, ICX_GW_MINW) void k_gw_lane(int n, const Desc* 
             const uint64_t bsm = wave_ballot(bs);
             const uint32_t u = r.used;
             const uint64_t lvm = bsm & wave_ballot(u >= span_o) & wave_ballot(b <= bmax) & lm;
-            const bool leave = lane_in(lvm);
-            ul = leave ? u : ul;
-            bl = leave ? b : bl;
-            // (here, not sunk to the latch: there they keep the old b / used alive past their
-            // updates, which costs a copy of each per iteration)
-            asm volatile("" : "+v"(ul), "+v"(bl));
+            if (lvm) {  // (wave-uniform: a lane leaves once, so the exit state's selects run rarely)
+                const bool leave = lane_in(lvm);
+                ul = leave ? u : ul;
+                bl = leave ? b : bl;
+            }
             lm &= ~lvm;
             const uint64_t om = bsm & lm;  // live && bs: its lanes own a block start
             const bool own_bs = lane_in(om);
